@@ -1,0 +1,66 @@
+// dgraph_amd — host launcher API of the gfx950 kernels.
+//
+// Launchers take raw device pointers plus the caller's hipStream_t (always the
+// PyTorch current stream, never the legacy default stream: the reference's
+// launchers ignored the stream they fetched, torch_local_kernels.cu:60,105,159,228).
+// They return the launch status; the torch binding layer turns errors into c10::Error.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dgraph {
+
+enum class DType : int { F32 = 0, BF16 = 1 };
+enum class IType : int { I32 = 0, I64 = 1 };
+
+// ---------------------------------------------------------------------------
+// CSR SpMM / segment reduction (K-new-2).
+//   out[r, f] = row_scale[r] * sum_{j in [rowptr[r], rowptr[r+1])}
+//                 ew[j, h(f)] * col_scale[col[j]] * x[col[j], f]
+//               + beta * out[r, f]
+// Any of ew / col_scale / row_scale may be null (== 1). h(f) = f / head_dim.
+// Deterministic: one wavefront owns an output row, fixed summation order.
+// ---------------------------------------------------------------------------
+hipError_t spmm_csr(DType dt, IType it, const int64_t* rowptr, const void* col,
+                    const float* ew, int heads, int head_dim, const float* col_scale,
+                    const float* row_scale, const void* x, int64_t ldx, void* out,
+                    int64_t ldo, int64_t nrows, int F, float beta, hipStream_t stream);
+
+// ---------------------------------------------------------------------------
+// Row copy with optional source and destination index (K4/K7/K8 replacement, K-new-1).
+//   out[dst(i)] (+)= x[src(i)]   for i in [0, n)
+// src/dst null == identity. src(i) < 0 writes zeros; dst(i) < 0 skips the row.
+// accumulate uses fp32 atomics and requires an fp32 output.
+// ---------------------------------------------------------------------------
+hipError_t copy_rows(DType dt, IType it, const void* x, int64_t ldx, const void* src_idx,
+                     const void* dst_idx, void* out, int64_t ldo, int64_t n, int F,
+                     bool accumulate, hipStream_t stream);
+
+// Masked row gather: out[i] = x[idx[i]] where mask[i] == value, else untouched.
+hipError_t masked_gather_rows(DType dt, const void* x, int64_t ldx, const int64_t* idx,
+                              const int64_t* mask, int64_t value, void* out, int64_t ldo,
+                              int64_t n, int F, hipStream_t stream);
+
+// ---------------------------------------------------------------------------
+// Edge softmax over CSR segments (K-new-3), numerically stable (max-subtracted;
+// the reference omitted it, RGAT.py:154).
+//   alpha[j, h] = exp(s[j,h] - max_seg) / sum_seg exp(.)
+// backward: ds[j,h] = alpha[j,h] * (g[j,h] - sum_seg alpha*g)
+// Scores are fp32 [E, H] in CSR edge order.
+// ---------------------------------------------------------------------------
+hipError_t edge_softmax_fwd(const int64_t* rowptr, const float* s, float* alpha,
+                            int64_t nrows, int H, hipStream_t stream);
+hipError_t edge_softmax_bwd(const int64_t* rowptr, const float* alpha, const float* g,
+                            float* ds, int64_t nrows, int H, hipStream_t stream);
+
+// ---------------------------------------------------------------------------
+// Fused epilogues (elementwise.hip). numel and F must be multiples of 32.
+//   bias_relu_pack: y = act(y + bias) in place; bits (may be null) = keep mask.
+//   relu_mask_bwd : g = bit ? g : 0 in place.
+// ---------------------------------------------------------------------------
+hipError_t bias_relu_pack(DType dt, void* y, const float* bias, uint32_t* bits, int64_t numel,
+                          int F, bool relu, hipStream_t stream);
+hipError_t relu_mask_bwd(DType dt, void* g, const uint32_t* bits, int64_t numel,
+                         hipStream_t stream);
+
+}  // namespace dgraph

@@ -1,0 +1,169 @@
+// dgraph_amd — CSR SpMM / segment-sum aggregation for gfx950 (K-new-2).
+//
+// Replaces the reference's scatter_add-based aggregation (GCN.py:57-65,
+// _torch_func_impl.py:222-227, RankLocalOps.py:148-206 with its atomic float4 path)
+// by a destination-sorted, atomic-free segment reduction:
+//   * one wavefront (64 lanes) owns an output row; the wave is split into
+//     G = 64/LPR lane groups, each group streams every G-th neighbour row with
+//     VEC-wide (up to 16 B) loads, so a wave keeps 4*G neighbour rows in flight;
+//   * accumulation is fp32 in VGPRs, the G partial sums are combined with
+//     cross-lane xor shuffles (fixed order => bitwise deterministic);
+//   * the result is written once with a row scale (mean = 1/deg) and optional
+//     beta*out accumulate (used to add the halo part after the interior part).
+// The kernel is HBM/Infinity-Cache bandwidth bound (random row gathers), so the
+// target is bytes/s, not FLOP/s (see profiles/).
+#include "../common.h"
+#include "kernels.h"
+
+namespace dgraph {
+namespace {
+
+template <typename T, typename IdxT, int VEC, int LPR>
+__global__ __launch_bounds__(256) void spmm_csr_kernel(
+    const int64_t* __restrict__ rowptr, const IdxT* __restrict__ col,
+    const float* __restrict__ ew, int heads, int head_dim,
+    const float* __restrict__ col_scale, const float* __restrict__ row_scale,
+    const T* __restrict__ x, int64_t ldx, T* __restrict__ out, int64_t ldo,
+    int64_t nrows, int F, float beta) {
+  constexpr int G = kWave / LPR;  // lane groups per wave = neighbour rows per step
+  const int lane = threadIdx.x & (kWave - 1);
+  const int g = lane / LPR;
+  const int l = lane % LPR;
+  const int64_t wave = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
+
+  for (int64_t r = wave; r < nrows; r += nwaves) {
+    const int64_t s = rowptr[r];
+    const int64_t e = rowptr[r + 1];
+    for (int fc = 0; fc < F; fc += LPR * VEC) {
+      const int f = fc + l * VEC;
+      const bool active = f < F;
+      const int h = (heads > 1) ? (f / head_dim) : 0;
+      float acc[VEC];
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) acc[i] = 0.f;
+
+      int64_t j = s + g;
+      // Main loop: 4 neighbour rows per lane group in flight.
+      for (; j + 3 * G < e; j += 4 * G) {
+        int64_t c[4];
+        float w[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) c[u] = static_cast<int64_t>(col[j + u * G]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          float wu = ew ? ew[(j + u * G) * heads + h] : 1.f;
+          if (col_scale) wu *= col_scale[c[u]];
+          w[u] = wu;
+        }
+        if (active) {
+          float v[4][VEC];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) load_vec_f32<T, VEC>(x + c[u] * ldx + f, v[u]);
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int i = 0; i < VEC; ++i) acc[i] = fmaf(w[u], v[u][i], acc[i]);
+        }
+      }
+      for (; j < e; j += G) {
+        const int64_t c0 = static_cast<int64_t>(col[j]);
+        float w0 = ew ? ew[j * heads + h] : 1.f;
+        if (col_scale) w0 *= col_scale[c0];
+        if (active) {
+          float v[VEC];
+          load_vec_f32<T, VEC>(x + c0 * ldx + f, v);
+#pragma unroll
+          for (int i = 0; i < VEC; ++i) acc[i] = fmaf(w0, v[i], acc[i]);
+        }
+      }
+      // Combine the G lane groups (xor butterfly over the group index bits).
+#pragma unroll
+      for (int off = LPR; off < kWave; off <<= 1)
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) acc[i] += __shfl_xor(acc[i], off, kWave);
+
+      if (g == 0 && active) {
+        const float rs = row_scale ? row_scale[r] : 1.f;
+        T* o = out + r * ldo + f;
+        if (beta != 0.f) {
+          float old[VEC];
+          load_vec_f32<T, VEC>(o, old);
+#pragma unroll
+          for (int i = 0; i < VEC; ++i) acc[i] = fmaf(acc[i], rs, beta * old[i]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < VEC; ++i) acc[i] *= rs;
+        }
+        store_vec_f32<T, VEC>(o, acc);
+      }
+    }
+  }
+}
+
+template <typename T, typename IdxT, int VEC>
+hipError_t launch_lpr(const int64_t* rowptr, const IdxT* col, const float* ew, int heads,
+                      int head_dim, const float* cs, const float* rs, const T* x, int64_t ldx,
+                      T* out, int64_t ldo, int64_t nrows, int F, float beta, hipStream_t st) {
+  const int lanes_needed = (F + VEC - 1) / VEC;
+  const int64_t blocks = cap_blocks((nrows + 3) / 4, 256 * 32);
+  dim3 grid(static_cast<unsigned>(blocks)), block(256);
+#define DG_SPMM_CASE(LPR_)                                                               \
+  hipLaunchKernelGGL((spmm_csr_kernel<T, IdxT, VEC, LPR_>), grid, block, 0, st, rowptr, \
+                     col, ew, heads, head_dim, cs, rs, x, ldx, out, ldo, nrows, F, beta); \
+  return hipGetLastError();
+  if (lanes_needed <= 4) { DG_SPMM_CASE(4) }
+  if (lanes_needed <= 8) { DG_SPMM_CASE(8) }
+  if (lanes_needed <= 16) { DG_SPMM_CASE(16) }
+  if (lanes_needed <= 32) { DG_SPMM_CASE(32) }
+  DG_SPMM_CASE(64)
+#undef DG_SPMM_CASE
+}
+
+inline bool aligned(const void* p, int bytes) {
+  return (reinterpret_cast<uintptr_t>(p) % bytes) == 0;
+}
+
+template <typename T, typename IdxT>
+hipError_t launch_vec(const int64_t* rowptr, const IdxT* col, const float* ew, int heads,
+                      int head_dim, const float* cs, const float* rs, const T* x, int64_t ldx,
+                      T* out, int64_t ldo, int64_t nrows, int F, float beta, hipStream_t st) {
+  // Widest vector that divides the row, both leading dimensions, the head
+  // size and both base pointers.
+  constexpr int kMaxVec = 16 / sizeof(T);
+  auto ok = [&](int v) {
+    return F % v == 0 && ldx % v == 0 && ldo % v == 0 && (heads <= 1 || head_dim % v == 0) &&
+           aligned(x, v * sizeof(T)) && aligned(out, v * sizeof(T));
+  };
+  if (ok(kMaxVec))
+    return launch_lpr<T, IdxT, kMaxVec>(rowptr, col, ew, heads, head_dim, cs, rs, x, ldx, out,
+                                        ldo, nrows, F, beta, st);
+  if (ok(4))
+    return launch_lpr<T, IdxT, 4>(rowptr, col, ew, heads, head_dim, cs, rs, x, ldx, out, ldo,
+                                  nrows, F, beta, st);
+  return launch_lpr<T, IdxT, 1>(rowptr, col, ew, heads, head_dim, cs, rs, x, ldx, out, ldo,
+                                nrows, F, beta, st);
+}
+
+}  // namespace
+
+hipError_t spmm_csr(DType dt, IType it, const int64_t* rowptr, const void* col,
+                    const float* ew, int heads, int head_dim, const float* col_scale,
+                    const float* row_scale, const void* x, int64_t ldx, void* out,
+                    int64_t ldo, int64_t nrows, int F, float beta, hipStream_t stream) {
+  if (nrows <= 0 || F <= 0) return hipSuccess;
+  if (heads < 1) heads = 1;
+  if (head_dim < 1) head_dim = F;
+#define DG_ARGS(T, I)                                                                   \
+  rowptr, static_cast<const I*>(col), ew, heads, head_dim, col_scale, row_scale,        \
+      static_cast<const T*>(x), ldx, static_cast<T*>(out), ldo, nrows, F, beta, stream
+  if (dt == DType::F32) {
+    if (it == IType::I32) return launch_vec<float, int32_t>(DG_ARGS(float, int32_t));
+    return launch_vec<float, int64_t>(DG_ARGS(float, int64_t));
+  }
+  if (it == IType::I32) return launch_vec<uint16_t, int32_t>(DG_ARGS(uint16_t, int32_t));
+  return launch_vec<uint16_t, int64_t>(DG_ARGS(uint16_t, int64_t));
+#undef DG_ARGS
+}
+
+}  // namespace dgraph

@@ -1,0 +1,91 @@
+"""All-to-all-v executor with host-cached split vectors.
+
+The reference recomputes split lists from device tensors on every call
+(``_get_splits`` ``.tolist()`` x2 at NCCLBackendEngine.py:257-274, one device sync per
+halo exchange). Plans here are static (I6), so the splits are turned into Python lists
+once and the exchange is a single stream-ordered RCCL all-to-all-v: every peer pair
+(i -> j) rides its own xGMI link, all 7 links concurrently. ``async_op=True`` returns a
+handle whose ``wait()`` only makes the *current stream* wait (no host sync), which is
+what the interior/boundary overlap in :mod:`dgraph_amd.parallel.dist_graph` builds on.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+
+def offsets_to_splits(offsets) -> List[int]:
+    if isinstance(offsets, torch.Tensor):
+        o = offsets.detach().cpu().tolist()
+    else:
+        o = list(offsets)
+    return [int(o[i + 1] - o[i]) for i in range(len(o) - 1)]
+
+
+class _Done:
+    def wait(self):
+        return None
+
+    def is_completed(self):
+        return True
+
+
+class CommStats:
+    """Process-wide byte counters (plan statistics / metrics stream)."""
+
+    calls = 0
+    bytes_sent = 0
+    bytes_recv = 0
+
+    @classmethod
+    def reset(cls):
+        cls.calls = cls.bytes_sent = cls.bytes_recv = 0
+
+
+class AllToAllV:
+    """Exchange rows: rank r sends ``send[send_off[p]:send_off[p+1]]`` to peer p and
+    receives peer q's segment into ``recv[recv_off[q]:recv_off[q+1]]``."""
+
+    def __init__(self, send_splits: Sequence[int], recv_splits: Sequence[int],
+                 group: Optional[dist.ProcessGroup] = None):
+        self.send_splits = [int(s) for s in send_splits]
+        self.recv_splits = [int(s) for s in recv_splits]
+        self.group = group
+        self.total_send = sum(self.send_splits)
+        self.total_recv = sum(self.recv_splits)
+        self._world = len(self.send_splits)
+
+    def reversed(self) -> "AllToAllV":
+        return AllToAllV(self.recv_splits, self.send_splits, self.group)
+
+    def __call__(self, send: torch.Tensor, out: Optional[torch.Tensor] = None,
+                 async_op: bool = False):
+        if send.shape[0] != self.total_send:
+            raise ValueError(f"send has {send.shape[0]} rows, plan expects {self.total_send}")
+        if out is None:
+            out = torch.empty((self.total_recv,) + tuple(send.shape[1:]), dtype=send.dtype,
+                              device=send.device)
+        row_bytes = send[0:1].numel() * send.element_size() if send.dim() > 0 else send.element_size()
+        CommStats.calls += 1
+        CommStats.bytes_sent += self.total_send * row_bytes
+        CommStats.bytes_recv += self.total_recv * row_bytes
+        if self._world <= 1 or not dist.is_initialized() or dist.get_world_size(self.group) == 1:
+            if self.total_send:
+                out.copy_(send)
+            return (out, _Done()) if async_op else out
+        if self.total_send == 0 and self.total_recv == 0:
+            # everyone must still enter the collective
+            pass
+        send_c = send.contiguous()
+        work = dist.all_to_all_single(
+            out, send_c,
+            output_split_sizes=self.recv_splits,
+            input_split_sizes=self.send_splits,
+            group=self.group,
+            async_op=async_op,
+        )
+        if async_op:
+            return out, work
+        return out

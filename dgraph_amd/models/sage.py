@@ -1,0 +1,287 @@
+"""GraphSAGE (mean aggregator) for vertex-partitioned full-graph training.
+
+The north-star model of BASELINE.json (ogbn-papers100M-shaped 3-layer GraphSAGE). The
+reference has no GraphSAGE; this is built on the library's
+distributed aggregation (:mod:`dgraph_amd.parallel.dist_graph`).
+
+Each layer is ONE autograd node, designed for the 288 GB HBM budget of a single MI355X
+holding a 111M-vertex / 3.2B-edge graph:
+
+    y = act(x @ W_self + mean_{j in N(i)} x_j @ W_neigh + b)
+
+* aggregation runs at ``min(F_in, F_out)`` features: aggregate-then-project when
+  F_in <= F_out, project-then-aggregate otherwise (linearity);
+* the aggregate is *not* stored for backward unless memory allows (``save_agg``); it is
+  recomputed by one more SpMM, so a layer saves nothing beyond its input and output,
+  which the neighbouring layers hold anyway;
+* weights are fp32 masters, compute is bf16 with fp32 accumulation; weight gradients are
+  produced in fp32 directly by the GEMM (``out_dtype``) where supported.
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as Fn
+from torch.autograd import Function
+
+from ..ops import kernels as K
+from ..parallel.dist_graph import DistGraph
+
+
+def mm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """``a @ b`` with an fp32 result (bf16 operands, fp32 accumulate)."""
+    if a.is_cuda and a.dtype != torch.float32:
+        try:
+            return torch.mm(a, b, out_dtype=torch.float32)
+        except (RuntimeError, TypeError):
+            pass
+    return torch.mm(a, b).float()
+
+
+class SAGELayerFn(Function):
+    @staticmethod
+    def forward(ctx, x, w_self, w_neigh, bias, graph: DistGraph, relu: bool,
+                project_first: bool, save_agg: bool):
+        dt = x.dtype
+        ws, wn = w_self.to(dt), w_neigh.to(dt)
+        a_saved = None
+        if project_first:
+            z = x @ wn
+            y = graph.aggregate(z, mean=True)
+            del z
+            if bias is not None:
+                y.add_(bias.to(dt))
+            y.addmm_(x, ws)
+        else:
+            a = graph.aggregate(x, mean=True)
+            y = torch.addmm(bias.to(dt), x, ws) if bias is not None else x @ ws
+            y.addmm_(a, wn)
+            if save_agg:
+                a_saved = a
+            del a
+        if relu:
+            y.relu_()
+        ctx.graph, ctx.relu, ctx.project_first = graph, relu, project_first
+        ctx.has_bias = bias is not None
+        ctx.save_for_backward(x, y if relu else None, ws, wn, a_saved)
+        ctx.w_dtype = w_self.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, y, ws, wn, a = ctx.saved_tensors
+        graph: DistGraph = ctx.graph
+        g = gy.to(x.dtype)
+        if ctx.relu:
+            g = torch.where(y > 0, g, torch.zeros((), dtype=g.dtype, device=g.device))
+        g = g.contiguous()
+        dws = mm_f32(x.t(), g).to(ctx.w_dtype) if ctx.needs_input_grad[1] else None
+        db = g.float().sum(0).to(ctx.w_dtype) if ctx.has_bias and ctx.needs_input_grad[3] else None
+        dx = dwn = None
+        if ctx.project_first:
+            dz = graph.aggregate_T(g, mean=True)
+            if ctx.needs_input_grad[2]:
+                dwn = mm_f32(x.t(), dz).to(ctx.w_dtype)
+            if ctx.needs_input_grad[0]:
+                dx = g @ ws.t()
+                dx.addmm_(dz, wn.t())
+            del dz
+        else:
+            if ctx.needs_input_grad[2]:
+                if a is None:
+                    a = graph.aggregate(x, mean=True)
+                dwn = mm_f32(a.t(), g).to(ctx.w_dtype)
+                del a
+            if ctx.needs_input_grad[0]:
+                t = g @ wn.t()
+                dx = graph.aggregate_T(t, mean=True)
+                del t
+                dx.addmm_(g, ws.t())
+        return dx, dws, dwn, db, None, None, None, None
+
+
+class SAGEConv(nn.Module):
+    """One GraphSAGE-mean layer over a :class:`DistGraph`."""
+
+    def __init__(self, in_dim: int, out_dim: int, bias: bool = True, relu: bool = True,
+                 order: str = "auto", save_agg: Optional[bool] = None):
+        super().__init__()
+        self.in_dim, self.out_dim, self.relu = in_dim, out_dim, relu
+        self.w_self = nn.Parameter(torch.empty(in_dim, out_dim))
+        self.w_neigh = nn.Parameter(torch.empty(in_dim, out_dim))
+        self.bias = nn.Parameter(torch.zeros(out_dim)) if bias else None
+        if order not in ("auto", "aggregate_first", "project_first"):
+            raise ValueError(order)
+        self.order = order
+        self.save_agg = save_agg
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        nn.init.xavier_uniform_(self.w_self)
+        nn.init.xavier_uniform_(self.w_neigh)
+        if self.bias is not None:
+            nn.init.zeros_(self.bias)
+
+    def project_first(self) -> bool:
+        if self.order == "auto":
+            return self.out_dim < self.in_dim
+        return self.order == "project_first"
+
+    def forward(self, x: torch.Tensor, graph: DistGraph) -> torch.Tensor:
+        save = self.save_agg
+        if save is None:
+            save = _auto_save_agg(x, graph)
+        return SAGELayerFn.apply(x, self.w_self, self.w_neigh, self.bias, graph, self.relu,
+                                 self.project_first(), bool(save))
+
+
+def _auto_save_agg(x: torch.Tensor, graph: DistGraph) -> bool:
+    """Store the aggregate for backward only if it costs < 15% of free device memory."""
+    if not x.is_cuda:
+        return True
+    free, _ = torch.cuda.mem_get_info(x.device)
+    return x.numel() * x.element_size() < 0.15 * free
+
+
+class SAGEStackFn(Function):
+    """The whole layer stack as ONE autograd node (memory-lean training path).
+
+    Owning every hidden activation lets backward *recycle* buffers: after layer i's weight
+    gradients are formed from its input ``h_i``, ``h_i``'s storage receives ``dh_i``; ReLU
+    layers keep a 1-bit mask instead of their output. Peak memory for the papers100M
+    shape (111M x 256 bf16 hidden) drops from ~330 GB (per-layer autograd) to ~240 GB, so
+    the 1-GPU point of the scaling curve fits in one MI355X's 288 GB.
+    """
+
+    @staticmethod
+    def forward(ctx, x0, graph: DistGraph, specs, *params):
+        acts = [x0]
+        masks = []
+        h = x0
+        dt = x0.dtype
+        for i, (relu, pf) in enumerate(specs):
+            ws, wn, b = params[3 * i], params[3 * i + 1], params[3 * i + 2]
+            ws_, wn_ = ws.to(dt), wn.to(dt)
+            if pf:
+                z = h @ wn_
+                y = graph.aggregate(z, mean=True)
+                del z
+                y.addmm_(h, ws_)
+            else:
+                a = graph.aggregate(h, mean=True)
+                y = h @ ws_
+                y.addmm_(a, wn_)
+                del a
+            F = y.shape[1]
+            if relu and F % 32 == 0 and y.numel() % 32 == 0:
+                bits = torch.empty(K.mask_words(y.numel()), dtype=torch.int32, device=y.device)
+                K.bias_relu_pack(y, b, bits, relu=True)
+                masks.append(bits)
+            else:
+                if b is not None:
+                    y.add_(b.to(dt))
+                if relu:
+                    y.relu_()
+                masks.append(y if relu else None)
+            if i + 1 < len(specs):
+                acts.append(y)
+            h = y
+        ctx.graph, ctx.specs = graph, specs
+        ctx.acts, ctx.masks = acts, masks
+        ctx.x0_requires_grad = x0.requires_grad
+        ctx.save_for_backward(*params)
+        return h
+
+    @staticmethod
+    def backward(ctx, gy):
+        params = ctx.saved_tensors
+        graph: DistGraph = ctx.graph
+        acts, masks, specs = ctx.acts, ctx.masks, ctx.specs
+        ctx.acts = ctx.masks = None
+        dt = acts[0].dtype
+        g = gy.to(dt).contiguous()
+        grads = [None] * len(params)
+        dx0 = None
+        for i in reversed(range(len(specs))):
+            relu, pf = specs[i]
+            ws, wn, b = params[3 * i], params[3 * i + 1], params[3 * i + 2]
+            ws_, wn_ = ws.to(dt), wn.to(dt)
+            m = masks[i]
+            masks[i] = None
+            if relu:
+                if m.dtype == torch.int32:
+                    if g is gy:  # never modify the caller's gradient in place
+                        g = g.clone()
+                    K.relu_mask_bwd(g, m)
+                else:
+                    g = torch.where(m > 0, g, torch.zeros((), dtype=g.dtype, device=g.device))
+            del m
+            x = acts[i]
+            acts[i] = None
+            recyclable = i > 0  # hidden activations are private to this node
+            need_dx = i > 0 or ctx.x0_requires_grad
+            grads[3 * i] = mm_f32(x.t(), g).to(ws.dtype)
+            if b is not None:
+                grads[3 * i + 2] = g.float().sum(0).to(b.dtype)
+            dx = None
+            if pf:
+                dz = graph.aggregate_T(g, mean=True)
+                grads[3 * i + 1] = mm_f32(x.t(), dz).to(wn.dtype)
+                if need_dx:
+                    dx = torch.mm(g, ws_.t(), out=x) if recyclable else g @ ws_.t()
+                    dx.addmm_(dz, wn_.t())
+                del dz
+            else:
+                a = graph.aggregate(x, mean=True)
+                grads[3 * i + 1] = mm_f32(a.t(), g).to(wn.dtype)
+                if need_dx:
+                    t = torch.mm(g, wn_.t(), out=a)
+                    dx = graph.aggregate_T(t, mean=True, out=x if recyclable else None)
+                    del t
+                    dx.addmm_(g, ws_.t())
+                del a
+            del x
+            g = dx
+            if i == 0:
+                dx0 = dx
+        return (dx0, None, None, *grads)
+
+
+class GraphSAGE(nn.Module):
+    """``num_layers`` SAGE-mean layers (ReLU between, none after the last) -> logits.
+
+    With ``dropout == 0`` the forward runs as one :class:`SAGEStackFn` node (buffer
+    recycling, bit masks); otherwise as per-layer :class:`SAGEConv` nodes.
+    """
+
+    def __init__(self, in_dim: int, hidden: int, out_dim: int, num_layers: int = 3,
+                 dropout: float = 0.0, save_agg: Optional[bool] = None):
+        super().__init__()
+        dims = [in_dim] + [hidden] * (num_layers - 1) + [out_dim]
+        self.layers = nn.ModuleList(
+            SAGEConv(dims[i], dims[i + 1], relu=(i < num_layers - 1), save_agg=save_agg)
+            for i in range(num_layers)
+        )
+        self.dropout = dropout
+
+    def forward(self, x: torch.Tensor, graph: DistGraph) -> torch.Tensor:
+        if self.dropout == 0 or not self.training:
+            specs = tuple((l.relu, l.project_first()) for l in self.layers)
+            params = []
+            for l in self.layers:
+                params += [l.w_self, l.w_neigh, l.bias]
+            return SAGEStackFn.apply(x, graph, specs, *params)
+        for i, layer in enumerate(self.layers):
+            x = layer(x, graph)
+            if self.dropout > 0 and self.training and i < len(self.layers) - 1:
+                x = Fn.dropout(x, self.dropout, training=True)
+        return x
+
+    def num_message_edges(self, graph: DistGraph) -> int:
+        """Directed message edges aggregated per layer on this rank (``E_msg``)."""
+        n = graph.interior.nnz
+        if graph.halo is not None:
+            n += graph.halo.nnz
+        return n

@@ -1,0 +1,136 @@
+"""Functional entry points of the native op library (device dispatch).
+
+GPU tensors -> hand-written HIP kernels in ``csrc/kernels`` (via ``torch.ops.dgraph_amd``);
+CPU tensors -> :mod:`dgraph_amd.ops.reference`. There is no GPU fallback: a missing
+native library raises (see :func:`dgraph_amd._native.ops`).
+
+Native-kernel counterparts of the reference's ``torch_local`` module
+(DGraph/distributed/csrc/torch_local_kernels.cu:28-254), generalised to bf16/fp32,
+int32/int64 indices and wave64.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from .. import _native
+from . import reference as _ref
+
+
+def _native_ok(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+def _f32(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+    if t is None:
+        return None
+    if t.dtype != torch.float32 or not t.is_contiguous():
+        t = t.float().contiguous()
+    return t
+
+
+def spmm(
+    rowptr: torch.Tensor,
+    col: torch.Tensor,
+    x: torch.Tensor,
+    out: Optional[torch.Tensor] = None,
+    *,
+    edge_weight: Optional[torch.Tensor] = None,
+    col_scale: Optional[torch.Tensor] = None,
+    row_scale: Optional[torch.Tensor] = None,
+    heads: int = 1,
+    beta: float = 0.0,
+) -> torch.Tensor:
+    """CSR aggregation ``out[r] = row_scale[r]*sum_j w_j*col_scale[c_j]*x[c_j] + beta*out[r]``."""
+    R = rowptr.numel() - 1
+    F = x.shape[1]
+    if out is None:
+        out = torch.empty(R, F, dtype=x.dtype, device=x.device)
+        beta = 0.0
+    heads = max(int(heads), 1)
+    if _native_ok(x):
+        _native.ops().spmm(
+            rowptr, col, _f32(edge_weight), _f32(col_scale), _f32(row_scale), x, out,
+            heads, F // heads, float(beta),
+        )
+        return out
+    return _ref.spmm(rowptr, col, x, out, edge_weight, col_scale, row_scale, heads, beta)
+
+
+def copy_rows(
+    x: torch.Tensor,
+    src_idx: Optional[torch.Tensor] = None,
+    dst_idx: Optional[torch.Tensor] = None,
+    out: Optional[torch.Tensor] = None,
+    *,
+    num_out_rows: Optional[int] = None,
+    accumulate: bool = False,
+) -> torch.Tensor:
+    """``out[dst[i]] (+)= x[src[i]]`` (identity when an index is None)."""
+    if out is None:
+        n = (src_idx.numel() if src_idx is not None else x.shape[0])
+        rows = num_out_rows if num_out_rows is not None else n
+        alloc = torch.zeros if (accumulate or dst_idx is not None) else torch.empty
+        out = alloc(rows, x.shape[1], dtype=torch.float32 if accumulate else x.dtype,
+                    device=x.device)
+    if src_idx is not None and dst_idx is not None and src_idx.dtype != dst_idx.dtype:
+        src_idx, dst_idx = src_idx.long(), dst_idx.long()
+    if _native_ok(x):
+        xin = x.float() if (accumulate and x.dtype != torch.float32) else x
+        _native.ops().copy_rows(xin, src_idx, dst_idx, out, bool(accumulate))
+        return out
+    return _ref.copy_rows(x, src_idx, dst_idx, out, accumulate)
+
+
+def gather_rows(x: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
+    """``out[i] = x[idx[i]]`` (zeros where idx < 0)."""
+    out = torch.empty(idx.numel(), x.shape[1], dtype=x.dtype, device=x.device)
+    return copy_rows(x, src_idx=idx, out=out)
+
+
+def masked_gather_rows(x, idx, mask, value, out):
+    if _native_ok(x):
+        _native.ops().masked_gather_rows(x, idx.long(), mask.long(), int(value), out)
+        return out
+    return _ref.masked_gather_rows(x, idx, mask, value, out)
+
+
+def edge_softmax_fwd(rowptr: torch.Tensor, scores: torch.Tensor) -> torch.Tensor:
+    if _native_ok(scores):
+        s = scores.float().contiguous()
+        alpha = torch.empty_like(s)
+        _native.ops().edge_softmax_fwd(rowptr, s, alpha)
+        return alpha
+    return _ref.edge_softmax_fwd(rowptr, scores)
+
+
+def edge_softmax_bwd(rowptr: torch.Tensor, alpha: torch.Tensor, grad: torch.Tensor) -> torch.Tensor:
+    if _native_ok(alpha):
+        a = alpha.float().contiguous()
+        g = grad.float().contiguous()
+        ds = torch.empty_like(a)
+        _native.ops().edge_softmax_bwd(rowptr, a, g, ds)
+        return ds
+    return _ref.edge_softmax_bwd(rowptr, alpha, grad)
+
+
+def mask_words(numel: int) -> int:
+    return (numel + 31) // 32
+
+
+def bias_relu_pack(y: torch.Tensor, bias: Optional[torch.Tensor] = None,
+                   bits: Optional[torch.Tensor] = None, relu: bool = True) -> None:
+    """In place ``y = act(y + bias)``; optional 1-bit keep mask (int32 words)."""
+    if _native_ok(y):
+        _native.ops().bias_relu_pack(y, _f32(bias), bits, bool(relu))
+        return
+    _ref.bias_relu_pack(y, bias, bits, relu)
+
+
+def relu_mask_bwd(g: torch.Tensor, bits: torch.Tensor) -> None:
+    """In place ``g = keep ? g : 0`` from a mask written by :func:`bias_relu_pack`."""
+    if _native_ok(g):
+        _native.ops().relu_mask_bwd(g, bits)
+        return
+    _ref.relu_mask_bwd(g, bits)

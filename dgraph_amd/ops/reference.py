@@ -1,0 +1,125 @@
+"""Pure-PyTorch fp32 reference implementations of the native ops.
+
+Used (a) for CPU tensors, so the whole framework runs and is tested without a GPU, and
+(b) as the numerics oracle the HIP kernels are compared against in ``tests/``.
+Semantics match :mod:`dgraph_amd.ops.kernels` exactly (see csrc/kernels/kernels.h).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+
+def _row_ids(rowptr: torch.Tensor) -> torch.Tensor:
+    deg = rowptr[1:] - rowptr[:-1]
+    return torch.repeat_interleave(torch.arange(deg.numel(), device=rowptr.device), deg)
+
+
+def spmm(
+    rowptr: torch.Tensor,
+    col: torch.Tensor,
+    x: torch.Tensor,
+    out: torch.Tensor,
+    edge_weight: Optional[torch.Tensor] = None,
+    col_scale: Optional[torch.Tensor] = None,
+    row_scale: Optional[torch.Tensor] = None,
+    heads: int = 1,
+    beta: float = 0.0,
+) -> torch.Tensor:
+    R = rowptr.numel() - 1
+    F = x.shape[1]
+    col = col.long()
+    rows = _row_ids(rowptr)
+    vals = x.float()[col]
+    if edge_weight is not None:
+        w = edge_weight.float().reshape(col.numel(), max(heads, 1))
+        hd = F // max(heads, 1)
+        vals = (vals.view(-1, max(heads, 1), hd) * w.unsqueeze(-1)).view(-1, F)
+    if col_scale is not None:
+        vals = vals * col_scale.float()[col].unsqueeze(1)
+    acc = torch.zeros(R, F, dtype=torch.float32, device=x.device)
+    acc.index_add_(0, rows, vals)
+    if row_scale is not None:
+        acc = acc * row_scale.float().unsqueeze(1)
+    if beta != 0.0:
+        acc = acc + beta * out[:R].float()
+    out[:R].copy_(acc.to(out.dtype))
+    return out
+
+
+def copy_rows(
+    x: torch.Tensor,
+    src_idx: Optional[torch.Tensor],
+    dst_idx: Optional[torch.Tensor],
+    out: torch.Tensor,
+    accumulate: bool = False,
+) -> torch.Tensor:
+    n = (src_idx.numel() if src_idx is not None else
+         dst_idx.numel() if dst_idx is not None else x.shape[0])
+    if src_idx is not None:
+        s = src_idx.long()
+        vals = torch.zeros(n, x.shape[1], dtype=x.dtype, device=x.device)
+        ok = s >= 0
+        vals[ok] = x[s[ok]]
+    else:
+        vals = x[:n]
+    if dst_idx is not None:
+        d = dst_idx.long()
+        keep = d >= 0
+        d, vals = d[keep], vals[keep]
+    else:
+        d = torch.arange(n, device=x.device)
+    if accumulate:
+        out.index_add_(0, d, vals.to(out.dtype))
+    else:
+        out[d] = vals.to(out.dtype)
+    return out
+
+
+def masked_gather_rows(x, idx, mask, value, out):
+    sel = mask == value
+    out[sel] = x[idx[sel]]
+    return out
+
+
+def edge_softmax_fwd(rowptr: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
+    s2 = s.float().reshape(s.shape[0], -1)
+    rows = _row_ids(rowptr)
+    R = rowptr.numel() - 1
+    H = s2.shape[1]
+    m = torch.full((R, H), float("-inf"), device=s.device)
+    m = m.scatter_reduce(0, rows.unsqueeze(1).expand(-1, H), s2, reduce="amax")
+    e = torch.exp(s2 - m[rows])
+    den = torch.zeros(R, H, device=s.device).index_add_(0, rows, e)
+    return (e / den[rows]).reshape(s.shape)
+
+
+def edge_softmax_bwd(rowptr: torch.Tensor, alpha: torch.Tensor, g: torch.Tensor) -> torch.Tensor:
+    a2 = alpha.float().reshape(alpha.shape[0], -1)
+    g2 = g.float().reshape(a2.shape)
+    rows = _row_ids(rowptr)
+    R = rowptr.numel() - 1
+    dot = torch.zeros(R, a2.shape[1], device=alpha.device).index_add_(0, rows, a2 * g2)
+    return (a2 * (g2 - dot[rows])).reshape(alpha.shape)
+
+
+def bias_relu_pack(y: torch.Tensor, bias, bits, relu: bool) -> None:
+    t = y.float()
+    if bias is not None:
+        t = t + bias.float()
+    if relu:
+        keep = t > 0
+        t = torch.where(keep, t, torch.zeros((), device=t.device))
+        if bits is not None:
+            kb = keep.reshape(-1, 32).to(torch.int64)
+            w = (kb << torch.arange(32, device=y.device)).sum(1)
+            w = torch.where(w >= 2**31, w - 2**32, w)
+            bits.view(-1)[: w.numel()] = w.to(torch.int32)
+    y.copy_(t.to(y.dtype))
+
+
+def relu_mask_bwd(g: torch.Tensor, bits: torch.Tensor) -> None:
+    w = bits.view(-1)[: g.numel() // 32].to(torch.int64) & 0xFFFFFFFF
+    keep = ((w.unsqueeze(1) >> torch.arange(32, device=g.device)) & 1).bool().reshape(g.shape)
+    g.masked_fill_(~keep, 0)

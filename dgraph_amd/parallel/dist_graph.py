@@ -1,0 +1,145 @@
+"""Per-rank partitioned graph with halo-overlapped aggregation.
+
+This is the hot path of vertex-partitioned full-graph training (P1-P3, §5.7 design 1).
+The local CSR (rows = owned vertices, columns = owned vertices ++ halo rows) is split
+once into an *interior* part (columns < L) and a *halo* part (columns >= L). Then
+
+    aggregate(x):   pack send rows (native gather) -> RCCL all-to-all-v on the comm stream
+                    || interior SpMM on the compute stream -> wait -> halo SpMM (beta=1)
+    aggregate_T(g): halo^T SpMM -> reverse all-to-all-v || interior^T SpMM -> wait ->
+                    segment-sum of the received rows into their owners (beta=1)
+
+so the interior aggregation hides the exchange, and there is no host sync and no float
+atomic anywhere. ``aggregate_T`` is the exact adjoint of ``aggregate``. The reference
+serialised every exchange with compute and synced the host per exchange (§3.2 notes).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional
+
+import torch
+from torch.autograd import Function
+
+from ..comm.alltoallv import AllToAllV
+from ..ops import kernels as K
+from ..ops.csr import CSR, IndexMap
+
+
+class DistGraph:
+    def __init__(
+        self,
+        csr: CSR,
+        num_local: int,
+        num_halo: int,
+        send_local_idx: Optional[torch.Tensor] = None,
+        send_splits: Optional[List[int]] = None,
+        recv_splits: Optional[List[int]] = None,
+        group=None,
+        symmetric: bool = False,
+        overlap: bool = True,
+    ):
+        assert csr.num_rows == num_local, "CSR rows must be the local vertices"
+        assert csr.num_cols == num_local + num_halo
+        self.L, self.H = int(num_local), int(num_halo)
+        self.csr = csr
+        self.inv_deg = csr.inv_degree()
+        self.symmetric = symmetric
+        self.overlap = overlap
+        if self.H > 0 or (send_local_idx is not None and send_local_idx.numel() > 0):
+            self.interior, self.halo = csr.split_columns(self.L)
+            self.interior.symmetric = symmetric
+            self.send_map = IndexMap(send_local_idx.to(csr.device), self.L)
+            self.a2a = AllToAllV(send_splits, recv_splits, group)
+            self.a2a_rev = self.a2a.reversed()
+            if self.a2a.total_recv != self.H:
+                raise ValueError(f"recv splits sum {self.a2a.total_recv} != halo {self.H}")
+        else:
+            self.interior, self.halo = csr, None
+            self.interior.symmetric = symmetric
+            self.send_map = None
+            self.a2a = self.a2a_rev = None
+        # drop the un-split copy's column array when split (memory: 288 GB budget)
+        if self.halo is not None:
+            self.csr = None
+
+    @property
+    def device(self):
+        return self.interior.device
+
+    @staticmethod
+    def from_pattern(cp, num_nbr_rows: Optional[int] = None, group=None,
+                     symmetric: bool = False) -> "DistGraph":
+        """From a :class:`CommunicationPattern` (its local_edge_list = (central, nbr))."""
+        le = cp.local_edge_list
+        L_n = cp.num_local_neighbor_vertices or cp.num_local_vertices
+        if L_n != cp.num_local_vertices:
+            raise ValueError("DistGraph needs a homogeneous pattern (use plan ops for bipartite)")
+        csr = CSR.from_coo(le[:, 0], le[:, 1], cp.num_local_vertices,
+                           cp.num_local_vertices + cp.num_halo_vertices)
+        return DistGraph(csr, cp.num_local_vertices, cp.num_halo_vertices, cp.send_local_idx,
+                         cp.send_splits(), cp.recv_splits(), group, symmetric)
+
+    # ------------------------------------------------------------------ non-autograd
+    def aggregate(self, x: torch.Tensor, mean: bool = True,
+                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        rs = self.inv_deg if mean else None
+        if self.halo is None:
+            return K.spmm(self.interior.rowptr, self.interior.col, x, out, row_scale=rs)
+        send = K.gather_rows(x, self.send_map.idx)
+        recv, work = self.a2a(send, async_op=True)
+        if not self.overlap:
+            work.wait()
+        out = K.spmm(self.interior.rowptr, self.interior.col, x, out, row_scale=rs)
+        work.wait()
+        K.spmm(self.halo.rowptr, self.halo.col, recv, out, row_scale=rs, beta=1.0)
+        return out
+
+    def aggregate_T(self, g: torch.Tensor, mean: bool = True,
+                    out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        cs = self.inv_deg if mean else None
+        g = g.contiguous()
+        it = self.interior if self.interior.symmetric else self.interior.transpose()
+        if self.halo is None:
+            return K.spmm(it.rowptr, it.col, g, out, col_scale=cs)
+        ht = self.halo.transpose()
+        hg = K.spmm(ht.rowptr, ht.col, g, col_scale=cs)
+        sg, work = self.a2a_rev(hg, async_op=True)
+        if not self.overlap:
+            work.wait()
+        out = K.spmm(it.rowptr, it.col, g, out, col_scale=cs)
+        work.wait()
+        st = self.send_map.transpose_csr()
+        K.spmm(st.rowptr, st.col, sg, out, beta=1.0)
+        return out
+
+    def prepare_backward(self):
+        """Build the cached transposes eagerly (outside any timed region)."""
+        if not self.interior.symmetric:
+            self.interior.transpose()
+        if self.halo is not None:
+            self.halo.transpose()
+            self.send_map.transpose_csr()
+        return self
+
+    def memory_bytes(self) -> int:
+        n = self.interior.memory_bytes()
+        if self.halo is not None:
+            n += self.halo.memory_bytes()
+        return n
+
+
+class _DistAggregateFn(Function):
+    @staticmethod
+    def forward(ctx, x, graph: DistGraph, mean: bool):
+        ctx.graph, ctx.mean = graph, mean
+        return graph.aggregate(x.contiguous(), mean)
+
+    @staticmethod
+    def backward(ctx, g):
+        return ctx.graph.aggregate_T(g, ctx.mean), None, None
+
+
+def dist_aggregate(x: torch.Tensor, graph: DistGraph, mean: bool = True) -> torch.Tensor:
+    """Autograd-aware distributed neighbourhood aggregation (sum or mean)."""
+    return _DistAggregateFn.apply(x, graph, mean)
