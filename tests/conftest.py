@@ -1,0 +1,88 @@
+"""Shared pytest configuration.
+
+* ``gpu`` marker: tests that need a real MI355X (run with ``-m gpu`` on the GPU box);
+  everything else runs on CPU.
+* ``run_ranks(fn, world_size)``: spawn a CPU/gloo process group of ``world_size`` ranks
+  on 127.0.0.1 and run ``fn(rank, world_size, *args)`` in each (the reference tested
+  distribution only with torchrun on GPUs; this runs the same test bodies
+  anywhere).
+"""
+from __future__ import annotations
+
+import os
+import socket
+import sys
+import traceback
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an AMD GPU (MI355X) and the native library")
+    config.addinivalue_line("markers", "slow: long-running test")
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world_size, port, fn, args, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world_size), LOCAL_RANK=str(rank))
+    try:
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo", rank=rank, world_size=world_size)
+        torch.manual_seed(0)
+        fn(rank, world_size, *args)
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, None))
+    except BaseException:
+        q.put((rank, traceback.format_exc()))
+
+
+def run_ranks(fn, world_size: int, *args, timeout: float = 240.0):
+    """Run ``fn(rank, world_size, *args)`` in ``world_size`` gloo processes; re-raise the
+    first failure with its traceback."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world_size, port, fn, args, q))
+             for r in range(world_size)]
+    for p in procs:
+        p.start()
+    errors = []
+    for _ in procs:
+        try:
+            rank, err = q.get(timeout=timeout)
+        except Exception:
+            errors.append("timeout waiting for ranks")
+            break
+        if err:
+            errors.append(f"rank {rank}:\n{err}")
+    for p in procs:
+        p.join(timeout=10)
+        if p.is_alive():
+            p.kill()
+    if errors:
+        raise AssertionError("\n".join(errors))
+
+
+@pytest.fixture
+def ranks():
+    return run_ranks
+
+
+def gpu_available() -> bool:
+    return torch.cuda.is_available()
