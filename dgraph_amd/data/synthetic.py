@@ -170,21 +170,28 @@ def localize_columns(csr: CSR, rank: int, offsets: List[int]):
     (csr_local, halo_gids, halo_counts_per_owner)."""
     lo, hi = offsets[rank], offsets[rank + 1]
     L = hi - lo
-    col = csr.col.long()
-    remote = (col < lo) | (col >= hi)
-    halo = torch.unique(col[remote])
+    step = 1 << 28  # chunked: bounded temporaries, no >2^31-element masks
+    n = csr.col.numel()
+    parts = []
+    for a in range(0, n, step):
+        c = csr.col[a:a + step].long()
+        parts.append(torch.unique(c[(c < lo) | (c >= hi)]))
+    halo = torch.unique(torch.cat(parts)) if parts else csr.col.new_zeros(0).long()
+    del parts
     H = halo.numel()
-    new = torch.empty_like(col)
-    new[~remote] = col[~remote] - lo
-    if H:
-        new[remote] = L + torch.searchsorted(halo, col[remote])
-    del col, remote
+    new = torch.empty(n, dtype=index_dtype_for(L + H), device=csr.col.device)
+    for a in range(0, n, step):
+        c = csr.col[a:a + step].long()
+        remote = (c < lo) | (c >= hi)
+        loc = c - lo
+        if H:
+            loc = torch.where(remote, L + torch.searchsorted(halo, c), loc)
+        new[a:a + step] = loc.to(new.dtype)
     W = len(offsets) - 1
     off_t = torch.tensor(offsets, device=halo.device, dtype=torch.int64)
     owners = torch.bucketize(halo, off_t, right=True) - 1
     counts = torch.bincount(owners, minlength=W).tolist() if H else [0] * W
-    out = CSR(csr.rowptr, new.to(index_dtype_for(L + H)).contiguous(), L + H, None,
-              symmetric=False)
+    out = CSR(csr.rowptr, new, L + H, None, symmetric=False)
     return out, halo, counts
 
 
@@ -199,6 +206,11 @@ def build_partition(shape: GraphShape, rank: int, world_size: int, device, seed:
 
     csr_g, L, offsets = build_local_csr(shape, rank, world_size, device, seed, global_frac,
                                         window)
+    if world_size == 1:  # every column is local already
+        csr_g.num_cols = L
+        return dict(csr=csr_g, L=L, H=0, halo_gids=csr_g.col[:0].long(),
+                    send_local_idx=torch.zeros(0, dtype=torch.int32, device=device),
+                    send_splits=[0], recv_splits=[0], offsets=offsets)
     csr, halo, recv_splits = localize_columns(csr_g, rank, offsets)
     del csr_g
     if world_size > 1:

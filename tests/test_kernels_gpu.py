@@ -153,12 +153,14 @@ def test_sage_stack_gpu_matches_cpu():
 
     shape = SHAPES["ogbn-arxiv"].scaled(0.02)
     outs = {}
+    # generate once on the CPU (device RNG streams differ), then copy
+    p = build_partition(shape, 0, 1, "cpu")
+    x_cpu, _, _ = node_data(shape, 0, p["offsets"], "cpu", dtype=torch.float32)
     for dev in ("cpu", DEV):
-        p = build_partition(shape, 0, 1, dev)
-        csr = p["csr"]
+        csr = p["csr"].to(dev)
         csr.num_cols = p["L"]
         g = DistGraph(csr, p["L"], 0, symmetric=True)
-        x, y, tr = node_data(shape, 0, p["offsets"], dev, dtype=torch.float32)
+        x = x_cpu.to(dev)
         torch.manual_seed(0)
         m = GraphSAGE(shape.num_features, 64, shape.num_classes, 3).to(dev)
         out = m(x, g)
