@@ -23,6 +23,11 @@ import os
 import sys
 import time
 
+# large, long-lived activations + transient SpMM buffers: avoid allocator fragmentation
+# (expandable segments are unsupported on ROCm; forbid splitting huge cached blocks so a
+#  freed 57 GB activation block is never carved up by a 38 GB request)
+os.environ.setdefault("PYTORCH_ALLOC_CONF", "max_split_size_mb:512")
+
 import torch
 import torch.distributed as dist
 
@@ -102,9 +107,8 @@ def main():
     inv_n = 1.0 / max(n_train, 1)
 
     def step():
-        out = model(x, graph)
-        logits = out.index_select(0, train_idx).float()
-        del out
+        # all-vertex forward; logits of the train split leave the fused stack
+        logits = model(x, graph, out_rows=train_idx).float()
         loss = torch.nn.functional.cross_entropy(logits, y_train, reduction="sum") * inv_n
         loss.backward()
         if sync is not None:

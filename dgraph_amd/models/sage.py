@@ -40,6 +40,12 @@ def mm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     return torch.mm(a, b).float()
 
 
+def col_sum_f32(g: torch.Tensor) -> torch.Tensor:
+    """Column sums in fp32 without materialising an fp32 copy of ``g`` (the reduction
+    casts on the fly; a [111M, 172] fp32 copy would be 71 GB)."""
+    return torch.sum(g, dim=0, dtype=torch.float32)
+
+
 class SAGELayerFn(Function):
     @staticmethod
     def forward(ctx, x, w_self, w_neigh, bias, graph: DistGraph, relu: bool,
@@ -78,7 +84,7 @@ class SAGELayerFn(Function):
             g = torch.where(y > 0, g, torch.zeros((), dtype=g.dtype, device=g.device))
         g = g.contiguous()
         dws = mm_f32(x.t(), g).to(ctx.w_dtype) if ctx.needs_input_grad[1] else None
-        db = g.float().sum(0).to(ctx.w_dtype) if ctx.has_bias and ctx.needs_input_grad[3] else None
+        db = col_sum_f32(g).to(ctx.w_dtype) if ctx.has_bias and ctx.needs_input_grad[3] else None
         dx = dwn = None
         if ctx.project_first:
             dz = graph.aggregate_T(g, mean=True)
@@ -156,7 +162,7 @@ class SAGEStackFn(Function):
     """
 
     @staticmethod
-    def forward(ctx, x0, graph: DistGraph, specs, *params):
+    def forward(ctx, x0, graph: DistGraph, specs, out_rows, *params):
         acts = [x0]
         masks = []
         h = x0
@@ -192,6 +198,11 @@ class SAGEStackFn(Function):
         ctx.acts, ctx.masks = acts, masks
         ctx.x0_requires_grad = x0.requires_grad
         ctx.save_for_backward(*params)
+        ctx.out_rows, ctx.out_shape = out_rows, tuple(h.shape)
+        if out_rows is not None:
+            # the last layer is computed for every vertex; only the requested rows leave
+            # the node, so autograd never holds a dense [V, C] output gradient
+            return h.index_select(0, out_rows)
         return h
 
     @staticmethod
@@ -201,7 +212,11 @@ class SAGEStackFn(Function):
         acts, masks, specs = ctx.acts, ctx.masks, ctx.specs
         ctx.acts = ctx.masks = None
         dt = acts[0].dtype
-        g = gy.to(dt).contiguous()
+        if ctx.out_rows is not None:
+            g = torch.zeros(ctx.out_shape, dtype=dt, device=gy.device)
+            g.index_copy_(0, ctx.out_rows, gy.to(dt))
+        else:
+            g = gy.to(dt).contiguous()
         grads = [None] * len(params)
         dx0 = None
         for i in reversed(range(len(specs))):
@@ -224,7 +239,7 @@ class SAGEStackFn(Function):
             need_dx = i > 0 or ctx.x0_requires_grad
             grads[3 * i] = mm_f32(x.t(), g).to(ws.dtype)
             if b is not None:
-                grads[3 * i + 2] = g.float().sum(0).to(b.dtype)
+                grads[3 * i + 2] = col_sum_f32(g).to(b.dtype)
             dx = None
             if pf:
                 dz = graph.aggregate_T(g, mean=True)
@@ -246,7 +261,7 @@ class SAGEStackFn(Function):
             g = dx
             if i == 0:
                 dx0 = dx
-        return (dx0, None, None, *grads)
+        return (dx0, None, None, None, *grads)
 
 
 class GraphSAGE(nn.Module):
@@ -266,18 +281,21 @@ class GraphSAGE(nn.Module):
         )
         self.dropout = dropout
 
-    def forward(self, x: torch.Tensor, graph: DistGraph) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, graph: DistGraph,
+                out_rows: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Logits for all local vertices, or only for ``out_rows`` (e.g. the train split:
+        the full last layer is still computed, but no dense [V, C] gradient is held)."""
         if self.dropout == 0 or not self.training:
             specs = tuple((l.relu, l.project_first()) for l in self.layers)
             params = []
             for l in self.layers:
                 params += [l.w_self, l.w_neigh, l.bias]
-            return SAGEStackFn.apply(x, graph, specs, *params)
+            return SAGEStackFn.apply(x, graph, specs, out_rows, *params)
         for i, layer in enumerate(self.layers):
             x = layer(x, graph)
             if self.dropout > 0 and self.training and i < len(self.layers) - 1:
                 x = Fn.dropout(x, self.dropout, training=True)
-        return x
+        return x if out_rows is None else x.index_select(0, out_rows)
 
     def num_message_edges(self, graph: DistGraph) -> int:
         """Directed message edges aggregated per layer on this rank (``E_msg``)."""
