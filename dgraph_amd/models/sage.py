@@ -151,37 +151,89 @@ def _auto_save_agg(x: torch.Tensor, graph: DistGraph) -> bool:
     return x.numel() * x.element_size() < 0.15 * free
 
 
+class SageWorkspace:
+    """Preplanned activation slots for :class:`SAGEStackFn` (no per-step allocation).
+
+    Slot plan for dims ``d_0..d_n`` over ``L`` rows (bf16):
+      act[i]  (i = 1..n-1): hidden activation h_i, later its gradient dh_i (recycled)
+      tmp_a               : aggregate / projection temp of every layer (fwd) and the
+                            dense output gradient + aggregate recompute (bwd)
+      tmp_b               : last-layer output (fwd) and aggregate_T temp (bwd)
+    For the papers100M shape this is 209 GB of slots + 28 GB of features + 14 GB of CSR:
+    the steady state performs no device allocation at all. (The caching allocator freed
+    and re-mapped tens-of-GB blocks every step — 1.6 s of hipFree/hipMalloc per block on
+    MI355X — measured with rocprofv3, profiles/.)
+    """
+
+    def __init__(self):
+        self.key = None
+        self.slots = {}
+        self.generation = 0
+
+    def prepare(self, L: int, dims, pf_flags, dtype, device):
+        key = (L, tuple(dims), tuple(pf_flags), dtype, str(device))
+        if key == self.key:
+            return
+        self.slots = {}
+        n = len(dims) - 1
+        C = dims[-1]
+        wa = max([C] + [(dims[i + 1] if pf_flags[i] else dims[i]) for i in range(n)])
+        wb = max([C] + [dims[i + 1] for i in range(n) if pf_flags[i]])
+        for i in range(1, n):
+            self.slots[f"act{i}"] = torch.empty(L * dims[i], dtype=dtype, device=device)
+        self.slots["tmp_a"] = torch.empty(L * wa, dtype=dtype, device=device)
+        self.slots["tmp_b"] = torch.empty(L * wb, dtype=dtype, device=device)
+        self.key = key
+
+    def view(self, name: str, L: int, F: int) -> torch.Tensor:
+        return self.slots[name][: L * F].view(L, F)
+
+
 class SAGEStackFn(Function):
     """The whole layer stack as ONE autograd node (memory-lean training path).
 
     Owning every hidden activation lets backward *recycle* buffers: after layer i's weight
     gradients are formed from its input ``h_i``, ``h_i``'s storage receives ``dh_i``; ReLU
-    layers keep a 1-bit mask instead of their output. Peak memory for the papers100M
-    shape (111M x 256 bf16 hidden) drops from ~330 GB (per-layer autograd) to ~240 GB, so
-    the 1-GPU point of the scaling curve fits in one MI355X's 288 GB.
+    layers keep a 1-bit mask instead of their output; all large tensors live in the
+    preplanned :class:`SageWorkspace` slots. Peak for the papers100M shape on one GPU:
+    ~251 GB of 288 GB (per-layer autograd would need ~330 GB).
     """
 
     @staticmethod
-    def forward(ctx, x0, graph: DistGraph, specs, out_rows, *params):
+    def forward(ctx, x0, graph: DistGraph, specs, out_rows, ws_obj, *params):
+        # workspace slots are used on the training path (row-subset output); a full
+        # output must own its storage, so that path allocates
+        use_ws = ws_obj is not None and out_rows is not None
+        n = len(specs)
+        L = x0.shape[0]
+        dt = x0.dtype
+        dims = [x0.shape[1]] + [params[3 * i].shape[1] for i in range(n)]
+        pf_flags = [pf for (_, pf) in specs]
+        if use_ws:
+            ws_obj.prepare(L, dims, pf_flags, dt, x0.device)
+            ws_obj.generation += 1
+        V = (lambda name, F: ws_obj.view(name, L, F)) if use_ws else \
+            (lambda name, F: torch.empty(L, F, dtype=dt, device=x0.device))
         acts = [x0]
         masks = []
         h = x0
-        dt = x0.dtype
         for i, (relu, pf) in enumerate(specs):
             ws, wn, b = params[3 * i], params[3 * i + 1], params[3 * i + 2]
             ws_, wn_ = ws.to(dt), wn.to(dt)
+            last = i == n - 1
+            Fo = dims[i + 1]
+            y = V("tmp_b" if last else f"act{i + 1}", Fo)
             if pf:
-                z = h @ wn_
-                y = graph.aggregate(z, mean=True)
+                z = torch.mm(h, wn_, out=V("tmp_a", Fo))
+                graph.aggregate(z, mean=True, out=y)
                 del z
                 y.addmm_(h, ws_)
             else:
-                a = graph.aggregate(h, mean=True)
-                y = h @ ws_
+                a = graph.aggregate(h, mean=True, out=V("tmp_a", dims[i]))
+                torch.mm(h, ws_, out=y)
                 y.addmm_(a, wn_)
                 del a
-            F = y.shape[1]
-            if relu and F % 32 == 0 and y.numel() % 32 == 0:
+            if relu and Fo % 32 == 0 and y.numel() % 32 == 0:
                 bits = torch.empty(K.mask_words(y.numel()), dtype=torch.int32, device=y.device)
                 K.bias_relu_pack(y, b, bits, relu=True)
                 masks.append(bits)
@@ -191,14 +243,16 @@ class SAGEStackFn(Function):
                 if relu:
                     y.relu_()
                 masks.append(y if relu else None)
-            if i + 1 < len(specs):
+            if not last:
                 acts.append(y)
             h = y
-        ctx.graph, ctx.specs = graph, specs
+        ctx.graph, ctx.specs, ctx.dims = graph, specs, dims
         ctx.acts, ctx.masks = acts, masks
         ctx.x0_requires_grad = x0.requires_grad
+        ctx.ws, ctx.use_ws = ws_obj, use_ws
+        ctx.gen = ws_obj.generation if use_ws else None
         ctx.save_for_backward(*params)
-        ctx.out_rows, ctx.out_shape = out_rows, tuple(h.shape)
+        ctx.out_rows = out_rows
         if out_rows is not None:
             # the last layer is computed for every vertex; only the requested rows leave
             # the node, so autograd never holds a dense [V, C] output gradient
@@ -209,17 +263,28 @@ class SAGEStackFn(Function):
     def backward(ctx, gy):
         params = ctx.saved_tensors
         graph: DistGraph = ctx.graph
-        acts, masks, specs = ctx.acts, ctx.masks, ctx.specs
+        acts, masks, specs, dims = ctx.acts, ctx.masks, ctx.specs, ctx.dims
         ctx.acts = ctx.masks = None
-        dt = acts[0].dtype
+        ws_obj, use_ws = ctx.ws, ctx.use_ws
+        if use_ws and ws_obj.generation != ctx.gen:
+            raise RuntimeError("SAGEStackFn: workspace reused by another forward before "
+                               "this backward; run backward before the next forward")
+        n = len(specs)
+        x0 = acts[0]
+        L, dt = x0.shape[0], x0.dtype
+        V = (lambda name, F: ws_obj.view(name, L, F)) if use_ws else \
+            (lambda name, F: torch.empty(L, F, dtype=dt, device=x0.device))
         if ctx.out_rows is not None:
-            g = torch.zeros(ctx.out_shape, dtype=dt, device=gy.device)
+            g = V("tmp_a", dims[-1])
+            g.zero_()
             g.index_copy_(0, ctx.out_rows, gy.to(dt))
         else:
             g = gy.to(dt).contiguous()
+            if g is gy:
+                g = g.clone()  # never modify the caller's gradient in place
         grads = [None] * len(params)
         dx0 = None
-        for i in reversed(range(len(specs))):
+        for i in reversed(range(n)):
             relu, pf = specs[i]
             ws, wn, b = params[3 * i], params[3 * i + 1], params[3 * i + 2]
             ws_, wn_ = ws.to(dt), wn.to(dt)
@@ -227,8 +292,6 @@ class SAGEStackFn(Function):
             masks[i] = None
             if relu:
                 if m.dtype == torch.int32:
-                    if g is gy:  # never modify the caller's gradient in place
-                        g = g.clone()
                     K.relu_mask_bwd(g, m)
                 else:
                     g = torch.where(m > 0, g, torch.zeros((), dtype=g.dtype, device=g.device))
@@ -242,26 +305,32 @@ class SAGEStackFn(Function):
                 grads[3 * i + 2] = col_sum_f32(g).to(b.dtype)
             dx = None
             if pf:
-                dz = graph.aggregate_T(g, mean=True)
+                dz = graph.aggregate_T(g, mean=True, out=V("tmp_b", dims[i + 1]))
                 grads[3 * i + 1] = mm_f32(x.t(), dz).to(wn.dtype)
                 if need_dx:
                     dx = torch.mm(g, ws_.t(), out=x) if recyclable else g @ ws_.t()
                     dx.addmm_(dz, wn_.t())
                 del dz
             else:
-                a = graph.aggregate(x, mean=True)
+                # tmp_a may still hold g for the last layer: recompute into tmp_b then
+                a_name = "tmp_b" if (i == n - 1 and ctx.out_rows is not None) else "tmp_a"
+                if i == n - 1 and ctx.out_rows is not None and dims[i] > dims[-1]:
+                    a_buf = torch.empty(L, dims[i], dtype=dt, device=x.device)
+                else:
+                    a_buf = V(a_name, dims[i])
+                a = graph.aggregate(x, mean=True, out=a_buf)
                 grads[3 * i + 1] = mm_f32(a.t(), g).to(wn.dtype)
                 if need_dx:
                     t = torch.mm(g, wn_.t(), out=a)
                     dx = graph.aggregate_T(t, mean=True, out=x if recyclable else None)
                     del t
                     dx.addmm_(g, ws_.t())
-                del a
+                del a, a_buf
             del x
             g = dx
             if i == 0:
                 dx0 = dx
-        return (dx0, None, None, None, *grads)
+        return (dx0, None, None, None, None, *grads)
 
 
 class GraphSAGE(nn.Module):
@@ -280,6 +349,7 @@ class GraphSAGE(nn.Module):
             for i in range(num_layers)
         )
         self.dropout = dropout
+        self._workspace = SageWorkspace()
 
     def forward(self, x: torch.Tensor, graph: DistGraph,
                 out_rows: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -290,7 +360,8 @@ class GraphSAGE(nn.Module):
             params = []
             for l in self.layers:
                 params += [l.w_self, l.w_neigh, l.bias]
-            return SAGEStackFn.apply(x, graph, specs, out_rows, *params)
+            ws = self._workspace if (self.training and torch.is_grad_enabled()) else None
+            return SAGEStackFn.apply(x, graph, specs, out_rows, ws, *params)
         for i, layer in enumerate(self.layers):
             x = layer(x, graph)
             if self.dropout > 0 and self.training and i < len(self.layers) - 1:
