@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""Micro-benchmark of the CSR SpMM aggregation kernel variants on a synthetic graph.
+
+Interleaved A/B rounds in one process (cdna_hip_programming.md §5.4 rule 24); reports
+median ms and effective bytes/s (gathered neighbour rows + indices + output rows).
+Example: python benchmarks/bench_spmm.py --shape ogbn-papers100M --feats 128,172,256
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shape", default="ogbn-products")
+    ap.add_argument("--scale", type=float, default=1.0)
+    ap.add_argument("--feats", default="128,172,256")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--global-frac", type=float, default=0.05)
+    ap.add_argument("--variants", default="1:0,2:0,2:1")
+    a = ap.parse_args()
+    from dgraph_amd import _native
+    from dgraph_amd.data.synthetic import SHAPES, build_partition
+    from dgraph_amd.ops import kernels as K
+
+    ops = _native.ops()
+    dev = torch.device("cuda", 0)
+    shape = SHAPES[a.shape] if a.scale == 1.0 else SHAPES[a.shape].scaled(a.scale)
+    p = build_partition(shape, 0, 1, dev, global_frac=a.global_frac)
+    csr = p["csr"]
+    inv = csr.inv_degree()
+    variants = [tuple(int(v) for v in s.split(":")) for s in a.variants.split(",")]
+    res = {}
+    for F in [int(f) for f in a.feats.split(",")]:
+        x = torch.randn(p["L"], F, device=dev, dtype=torch.bfloat16)
+        out = torch.empty_like(x)
+        times = {v: [] for v in variants}
+        ref = None
+        for r in range(a.rounds + 1):
+            for v in variants:
+                ops.set_spmm_config(*v)
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                torch.cuda.synchronize()
+                s.record()
+                K.spmm(csr.rowptr, csr.col, x, out, row_scale=inv)
+                e.record()
+                torch.cuda.synchronize()
+                if r > 0:
+                    times[v].append(s.elapsed_time(e))
+                if ref is None:
+                    ref = out.clone()
+                else:
+                    assert torch.equal(out, ref), f"variant {v} differs"
+        nbytes = csr.nnz * (F * 2 + csr.col.element_size()) + p["L"] * F * 2
+        for v in variants:
+            ms = statistics.median(times[v])
+            res[f"F{F}_v{v[0]}_xcd{v[1]}"] = {"ms": round(ms, 3),
+                                              "TBps": round(nbytes / ms / 1e9, 3)}
+            print(f"F={F:4d} variant={v[0]} xcd={v[1]}: {ms:8.2f} ms  "
+                  f"{nbytes / ms / 1e9:6.2f} TB/s effective", flush=True)
+        del x, out, ref
+    ops.set_spmm_config(2, 1)
+    print(json.dumps({"shape": shape.name, "nnz": csr.nnz, "rows": p["L"], "results": res}))
+
+
+if __name__ == "__main__":
+    main()

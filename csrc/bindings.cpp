@@ -207,7 +207,12 @@ void relu_mask_bwd_op(const at::Tensor& g, const at::Tensor& bits) {
 }  // namespace
 }  // namespace dgraph
 
+void set_spmm_config_op(int64_t variant, int64_t xcd) {
+  dgraph::set_spmm_config(static_cast<int>(variant), static_cast<int>(xcd));
+}
+
 TORCH_LIBRARY(dgraph_amd, m) {
+  m.def("set_spmm_config(int variant, int xcd) -> ()", &set_spmm_config_op);
   m.def("bias_relu_pack(Tensor(a!) y, Tensor? bias, Tensor(b!)? bits, bool relu) -> ()");
   m.def("relu_mask_bwd(Tensor(a!) g, Tensor bits) -> ()");
   m.def(

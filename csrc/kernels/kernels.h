@@ -21,6 +21,10 @@ enum class IType : int { I32 = 0, I64 = 1 };
 // Any of ew / col_scale / row_scale may be null (== 1). h(f) = f / head_dim.
 // Deterministic: one wavefront owns an output row, fixed summation order.
 // ---------------------------------------------------------------------------
+// Kernel selection (tuning / A-B measurement): variant 1 = per-group index loads,
+// 2 = cooperative index load + shuffles (default); xcd = XCD-aware row chunking.
+void set_spmm_config(int variant, int xcd);
+
 hipError_t spmm_csr(DType dt, IType it, const int64_t* rowptr, const void* col,
                     const float* ew, int heads, int head_dim, const float* col_scale,
                     const float* row_scale, const void* x, int64_t ldx, void* out,

@@ -101,13 +101,138 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(
   }
 }
 
+// v2: the wave loads up to 64 (col, weight) pairs of its row with ONE coalesced load
+// (lane j <- slot base+j) and broadcasts them to the lane groups with ds_bpermute
+// shuffles, so the neighbour-row loads no longer wait on a per-group dependent index
+// load; U neighbour rows per lane group in flight. Optional XCD-aware row mapping: the
+// rows are cut into 8 contiguous chunks, chunk x served by the blocks that share XCD x
+// (blockIdx % 8), so each XCD's L2 sees one contiguous row window (speed only).
+template <typename T, typename IdxT, int VEC, int LPR, int U, bool XCD>
+__global__ __launch_bounds__(256) void spmm_csr_v2_kernel(
+    const int64_t* __restrict__ rowptr, const IdxT* __restrict__ col,
+    const float* __restrict__ ew, int heads, int head_dim,
+    const float* __restrict__ col_scale, const float* __restrict__ row_scale,
+    const T* __restrict__ x, int64_t ldx, T* __restrict__ out, int64_t ldo,
+    int64_t nrows, int F, float beta) {
+  constexpr int G = kWave / LPR;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int g = lane / LPR;
+  const int l = lane % LPR;
+  const int wpb = blockDim.x >> 6;
+  int64_t r0, rstep, rend;
+  if constexpr (XCD) {
+    const int nx = 8;
+    const int64_t bx = blockIdx.x % nx;
+    const int64_t bpx = gridDim.x / nx;  // host guarantees gridDim.x % 8 == 0
+    const int64_t chunk = (nrows + nx - 1) / nx;
+    const int64_t lo = bx * chunk;
+    rend = lo + chunk < nrows ? lo + chunk : nrows;
+    r0 = lo + (blockIdx.x / nx) * wpb + (threadIdx.x >> 6);
+    rstep = bpx * wpb;
+  } else {
+    r0 = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+    rstep = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
+    rend = nrows;
+  }
+  const bool multi_head = heads > 1;
+  for (int64_t r = r0; r < rend; r += rstep) {
+    const int64_t s = rowptr[r];
+    const int64_t e = rowptr[r + 1];
+    for (int fc = 0; fc < F; fc += LPR * VEC) {
+      const int f = fc + l * VEC;
+      const bool active = f < F;
+      const int h = multi_head ? (f / head_dim) : 0;
+      float acc[VEC];
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) acc[i] = 0.f;
+      for (int64_t base = s; base < e; base += kWave) {
+        const int n = (e - base) < kWave ? static_cast<int>(e - base) : kWave;
+        // cooperative index/weight load: lane j owns slot base + j
+        IdxT my_c = 0;
+        float my_w = 1.f;
+        if (lane < n) {
+          my_c = col[base + lane];
+          if (col_scale) my_w = col_scale[my_c];
+        }
+        using R = typename RawVec<VEC * sizeof(T)>::type;
+        for (int k = g; k < n; k += G * U) {
+          R v[U];  // raw (packed bf16) rows: half the VGPRs of an fp32 staging copy
+          float w[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const int kk = k + u * G;
+            const int src = kk < n ? kk : 0;
+            const int64_t c = static_cast<int64_t>(__shfl(my_c, src, kWave));
+            float wu = __shfl(my_w, src, kWave);
+            if (ew) wu *= ew[(base + src) * heads + h];
+            w[u] = kk < n ? wu : 0.f;
+            if (active && kk < n) {
+              v[u] = *reinterpret_cast<const R*>(x + c * ldx + f);
+            } else {
+              v[u] = R{};
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const T* e = reinterpret_cast<const T*>(&v[u]);
+#pragma unroll
+            for (int i = 0; i < VEC; ++i) acc[i] = fmaf(w[u], Elem<T>::to_f32(e[i]), acc[i]);
+          }
+        }
+      }
+#pragma unroll
+      for (int off = LPR; off < kWave; off <<= 1)
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) acc[i] += __shfl_xor(acc[i], off, kWave);
+      if (g == 0 && active) {
+        const float rs = row_scale ? row_scale[r] : 1.f;
+        T* o = out + r * ldo + f;
+        if (beta != 0.f) {
+          float old[VEC];
+          load_vec_f32<T, VEC>(o, old);
+#pragma unroll
+          for (int i = 0; i < VEC; ++i) acc[i] = fmaf(acc[i], rs, beta * old[i]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < VEC; ++i) acc[i] *= rs;
+        }
+        store_vec_f32<T, VEC>(o, acc);
+      }
+    }
+  }
+}
+
+int g_spmm_variant = 2;  // 1 = per-group index loads, 2 = cooperative + shuffles
+int g_spmm_xcd = 1;
+
 template <typename T, typename IdxT, int VEC>
 hipError_t launch_lpr(const int64_t* rowptr, const IdxT* col, const float* ew, int heads,
                       int head_dim, const float* cs, const float* rs, const T* x, int64_t ldx,
                       T* out, int64_t ldo, int64_t nrows, int F, float beta, hipStream_t st) {
   const int lanes_needed = (F + VEC - 1) / VEC;
-  const int64_t blocks = cap_blocks((nrows + 3) / 4, 256 * 32);
+  int64_t blocks = cap_blocks((nrows + 3) / 4, 256 * 32);
+  const bool xcd = g_spmm_xcd && blocks >= 64;
+  if (xcd) blocks = (blocks / 8) * 8;
   dim3 grid(static_cast<unsigned>(blocks)), block(256);
+  if (g_spmm_variant == 2) {
+    // U rows in flight per lane group: ~16 neighbour rows per wave
+#define DG_V2(LPR_, U_)                                                                    \
+  if (xcd)                                                                                 \
+    hipLaunchKernelGGL((spmm_csr_v2_kernel<T, IdxT, VEC, LPR_, U_, true>), grid, block, 0, \
+                       st, rowptr, col, ew, heads, head_dim, cs, rs, x, ldx, out, ldo,     \
+                       nrows, F, beta);                                                    \
+  else                                                                                     \
+    hipLaunchKernelGGL((spmm_csr_v2_kernel<T, IdxT, VEC, LPR_, U_, false>), grid, block,   \
+                       0, st, rowptr, col, ew, heads, head_dim, cs, rs, x, ldx, out, ldo,  \
+                       nrows, F, beta);                                                    \
+  return hipGetLastError();
+    if (lanes_needed <= 4) { DG_V2(4, 2) }
+    if (lanes_needed <= 8) { DG_V2(8, 2) }
+    if (lanes_needed <= 16) { DG_V2(16, 4) }
+    if (lanes_needed <= 32) { DG_V2(32, 8) }
+    DG_V2(64, 8)
+#undef DG_V2
+  }
 #define DG_SPMM_CASE(LPR_)                                                               \
   hipLaunchKernelGGL((spmm_csr_kernel<T, IdxT, VEC, LPR_>), grid, block, 0, st, rowptr, \
                      col, ew, heads, head_dim, cs, rs, x, ldx, out, ldo, nrows, F, beta); \
@@ -146,6 +271,11 @@ hipError_t launch_vec(const int64_t* rowptr, const IdxT* col, const float* ew, i
 }
 
 }  // namespace
+
+void set_spmm_config(int variant, int xcd) {
+  if (variant == 1 || variant == 2) g_spmm_variant = variant;
+  if (xcd == 0 || xcd == 1) g_spmm_xcd = xcd;
+}
 
 hipError_t spmm_csr(DType dt, IType it, const int64_t* rowptr, const void* col,
                     const float* ew, int heads, int head_dim, const float* col_scale,
