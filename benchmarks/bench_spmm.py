@@ -55,8 +55,9 @@ def main():
                     times[v].append(s.elapsed_time(e))
                 if ref is None:
                     ref = out.clone()
-                else:
-                    assert torch.equal(out, ref), f"variant {v} differs"
+                else:  # variants sum in different orders: compare to rounding
+                    err = (out.float() - ref.float()).abs().max().item()
+                    assert err < 5e-2, f"variant {v} differs by {err}"
         nbytes = csr.nnz * (F * 2 + csr.col.element_size()) + p["L"] * F * 2
         for v in variants:
             ms = statistics.median(times[v])

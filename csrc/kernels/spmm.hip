@@ -155,12 +155,14 @@ __global__ __launch_bounds__(256) void spmm_csr_v2_kernel(
           if (col_scale) my_w = col_scale[my_c];
         }
         using R = typename RawVec<VEC * sizeof(T)>::type;
-        for (int k = g; k < n; k += G * U) {
+        // wave-uniform trip count: every lane stays active through the shuffles
+        // (ds_bpermute cannot read a lane that has left the loop)
+        for (int k0 = 0; k0 < n; k0 += G * U) {
           R v[U];  // raw (packed bf16) rows: half the VGPRs of an fp32 staging copy
           float w[U];
 #pragma unroll
           for (int u = 0; u < U; ++u) {
-            const int kk = k + u * G;
+            const int kk = k0 + g + u * G;
             const int src = kk < n ? kk : 0;
             const int64_t c = static_cast<int64_t>(__shfl(my_c, src, kWave));
             float wu = __shfl(my_w, src, kWave);

@@ -72,6 +72,29 @@ def test_spmm_strided_and_empty():
     torch.testing.assert_close(out.cpu(), ref, atol=1e-4, rtol=1e-4)
 
 
+@pytest.mark.parametrize("variant,xcd", [(1, 0), (2, 0), (2, 1)])
+@pytest.mark.parametrize("F", [16, 40, 64, 128, 256])
+def test_spmm_variants_agree_ragged_rows(variant, xcd, F):
+    """Rows whose degrees are not multiples of the lane-group count and exceed one
+    64-edge chunk (exercises every group finishing at a different slot)."""
+    from dgraph_amd import _native
+
+    g = torch.Generator().manual_seed(F)
+    deg = torch.randint(0, 200, (700,), generator=g)
+    rowptr = torch.zeros(701, dtype=torch.long)
+    rowptr[1:] = torch.cumsum(deg, 0)
+    col = torch.randint(0, 500, (int(rowptr[-1]),), generator=g, dtype=torch.int32)
+    x = torch.randn(500, F, device=DEV)
+    ref = R.spmm(rowptr, col, x.cpu(), torch.empty(700, F))
+    ops = _native.ops()
+    try:
+        ops.set_spmm_config(variant, xcd)
+        out = K.spmm(rowptr.to(DEV), col.to(DEV), x)
+    finally:
+        ops.set_spmm_config(2, 1)
+    torch.testing.assert_close(out.cpu(), ref, atol=1e-4, rtol=1e-4)
+
+
 def test_spmm_deterministic():
     csr = _rand_csr(1000, 1000, 30, torch.int32, DEV, skew=True)
     x = torch.randn(1000, 128, device=DEV, dtype=torch.bfloat16)
