@@ -168,17 +168,20 @@ __global__ __launch_bounds__(256) void spmm_csr_v2_kernel(
             float wu = __shfl(my_w, src, kWave);
             if (ew) wu *= ew[(base + src) * heads + h];
             w[u] = kk < n ? wu : 0.f;
-            if (active && kk < n) {
-              v[u] = *reinterpret_cast<const R*>(x + c * ldx + f);
-            } else {
-              v[u] = R{};
-            }
+            // unconditional load (padding slots re-read slot 0 with weight 0; lanes past
+            // F read column 0): a per-slot "load or zero" select makes hipcc branch
+            // around each load and drain vmcnt per slot (guide §5 trap (c))
+            v[u] = *reinterpret_cast<const R*>(x + c * ldx + (active ? f : 0));
           }
 #pragma unroll
           for (int u = 0; u < U; ++u) {
             const T* e = reinterpret_cast<const T*>(&v[u]);
+            const bool ok = k0 + g + u * G < n;  // select, not a branch (inf*0 safe)
 #pragma unroll
-            for (int i = 0; i < VEC; ++i) acc[i] = fmaf(w[u], Elem<T>::to_f32(e[i]), acc[i]);
+            for (int i = 0; i < VEC; ++i) {
+              const float t = fmaf(w[u], Elem<T>::to_f32(e[i]), acc[i]);
+              acc[i] = ok ? t : acc[i];
+            }
           }
         }
       }
