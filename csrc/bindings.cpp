@@ -177,15 +177,15 @@ void bias_relu_pack_op(const at::Tensor& y, const c10::optional<at::Tensor>& bia
   check_dev(y, y, "y");
   TORCH_CHECK(y.is_contiguous() && y.dim() == 2, "y must be contiguous 2-D");
   const int64_t F = y.size(1);
-  TORCH_CHECK(F % 32 == 0, "bias_relu_pack needs F % 32 == 0");
+  TORCH_CHECK(F % 8 == 0, "bias_relu_pack needs F % 8 == 0");
   const float* bp = opt_f32(bias, y, "bias");
   if (bp) TORCH_CHECK(bias->numel() == F, "bias must have F elements");
   uint32_t* bitp = nullptr;
   if (bits.has_value() && bits->defined()) {
     check_dev(*bits, y, "bits");
     TORCH_CHECK(bits->scalar_type() == at::kInt && bits->is_contiguous() &&
-                    bits->numel() * 32 >= y.numel(),
-                "bits must be contiguous int32 with numel/32 words");
+                    bits->numel() >= (y.numel() + 511) / 512 * 16,
+                "bits must be contiguous int32 with ceil(numel/512)*16 words");
     bitp = reinterpret_cast<uint32_t*>(bits->data_ptr<int32_t>());
   }
   c10::DeviceGuard g(y.device());
@@ -196,12 +196,26 @@ void bias_relu_pack_op(const at::Tensor& y, const c10::optional<at::Tensor>& bia
 void relu_mask_bwd_op(const at::Tensor& g, const at::Tensor& bits) {
   check_dev(g, g, "g");
   check_dev(bits, g, "bits");
-  TORCH_CHECK(g.is_contiguous() && g.numel() % 32 == 0, "g must be contiguous, numel%32==0");
-  TORCH_CHECK(bits.scalar_type() == at::kInt && bits.numel() * 32 >= g.numel(), "bad bits");
+  TORCH_CHECK(g.is_contiguous() && g.numel() % 8 == 0, "g must be contiguous, numel%8==0");
+  TORCH_CHECK(bits.scalar_type() == at::kInt && bits.numel() >= (g.numel() + 511) / 512 * 16,
+              "bad bits");
   c10::DeviceGuard gd(g.device());
   DG_HIP_CHECK(relu_mask_bwd(dtype_of(g), g.data_ptr(),
                              reinterpret_cast<const uint32_t*>(bits.data_ptr<int32_t>()),
                              g.numel(), cur_stream(g)));
+}
+
+at::Tensor col_sum_op(const at::Tensor& g) {
+  check_dev(g, g, "g");
+  check_rows(g, "g");
+  const int64_t L = g.size(0), F = g.size(1);
+  const int64_t nb = std::max<int64_t>(1, std::min<int64_t>(1024, (L + 255) / 256));
+  auto partial = at::empty({nb, F}, g.options().dtype(at::kFloat));
+  c10::DeviceGuard gd(g.device());
+  DG_HIP_CHECK(col_sum_partial(dtype_of(g), g.data_ptr(), g.stride(0), L,
+                               static_cast<int>(F), partial.data_ptr<float>(),
+                               static_cast<int>(nb), cur_stream(g)));
+  return partial.sum(0);
 }
 
 }  // namespace
@@ -215,6 +229,7 @@ TORCH_LIBRARY(dgraph_amd, m) {
   m.def("set_spmm_config(int variant, int xcd) -> ()", &set_spmm_config_op);
   m.def("bias_relu_pack(Tensor(a!) y, Tensor? bias, Tensor(b!)? bits, bool relu) -> ()");
   m.def("relu_mask_bwd(Tensor(a!) g, Tensor bits) -> ()");
+  m.def("col_sum(Tensor g) -> Tensor");
   m.def(
       "spmm(Tensor rowptr, Tensor col, Tensor? edge_weight, Tensor? col_scale, "
       "Tensor? row_scale, Tensor x, Tensor(a!) out, int heads, int head_dim, float beta) -> ()");
@@ -233,4 +248,5 @@ TORCH_LIBRARY_IMPL(dgraph_amd, CUDA, m) {
   m.impl("edge_softmax_bwd", &dgraph::edge_softmax_bwd_op);
   m.impl("bias_relu_pack", &dgraph::bias_relu_pack_op);
   m.impl("relu_mask_bwd", &dgraph::relu_mask_bwd_op);
+  m.impl("col_sum", &dgraph::col_sum_op);
 }

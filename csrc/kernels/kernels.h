@@ -58,13 +58,17 @@ hipError_t edge_softmax_bwd(const int64_t* rowptr, const float* alpha, const flo
                             float* ds, int64_t nrows, int H, hipStream_t stream);
 
 // ---------------------------------------------------------------------------
-// Fused epilogues (elementwise.hip). numel and F must be multiples of 32.
-//   bias_relu_pack: y = act(y + bias) in place; bits (may be null) = keep mask.
+// Fused epilogues (elementwise.hip). numel and F must be multiples of 8.
+//   bias_relu_pack: y = act(y + bias) in place; bits (may be null) = keep mask,
+//                   ceil(numel/512)*16 32-bit words (layout: see elementwise.hip).
 //   relu_mask_bwd : g = bit ? g : 0 in place.
+//   col_sum_partial: partial[b, :] = column sums of rows of block b (fp32).
 // ---------------------------------------------------------------------------
 hipError_t bias_relu_pack(DType dt, void* y, const float* bias, uint32_t* bits, int64_t numel,
                           int F, bool relu, hipStream_t stream);
 hipError_t relu_mask_bwd(DType dt, void* g, const uint32_t* bits, int64_t numel,
                          hipStream_t stream);
+hipError_t col_sum_partial(DType dt, const void* g, int64_t ld, int64_t L, int F,
+                           float* partial, int nblocks, hipStream_t stream);
 
 }  // namespace dgraph

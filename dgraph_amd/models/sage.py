@@ -30,20 +30,7 @@ from ..ops import kernels as K
 from ..parallel.dist_graph import DistGraph
 
 
-def mm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    """``a @ b`` with an fp32 result (bf16 operands, fp32 accumulate)."""
-    if a.is_cuda and a.dtype != torch.float32:
-        try:
-            return torch.mm(a, b, out_dtype=torch.float32)
-        except (RuntimeError, TypeError):
-            pass
-    return torch.mm(a, b).float()
-
-
-def col_sum_f32(g: torch.Tensor) -> torch.Tensor:
-    """Column sums in fp32 without materialising an fp32 copy of ``g`` (the reduction
-    casts on the fly; a [111M, 172] fp32 copy would be 71 GB)."""
-    return torch.sum(g, dim=0, dtype=torch.float32)
+from ..ops.dense import col_sum_f32, mm_f32, wgrad  # noqa: F401  (re-exported)
 
 
 class SAGELayerFn(Function):
@@ -83,13 +70,13 @@ class SAGELayerFn(Function):
         if ctx.relu:
             g = torch.where(y > 0, g, torch.zeros((), dtype=g.dtype, device=g.device))
         g = g.contiguous()
-        dws = mm_f32(x.t(), g).to(ctx.w_dtype) if ctx.needs_input_grad[1] else None
+        dws = wgrad(x, g).to(ctx.w_dtype) if ctx.needs_input_grad[1] else None
         db = col_sum_f32(g).to(ctx.w_dtype) if ctx.has_bias and ctx.needs_input_grad[3] else None
         dx = dwn = None
         if ctx.project_first:
             dz = graph.aggregate_T(g, mean=True)
             if ctx.needs_input_grad[2]:
-                dwn = mm_f32(x.t(), dz).to(ctx.w_dtype)
+                dwn = wgrad(x, dz).to(ctx.w_dtype)
             if ctx.needs_input_grad[0]:
                 dx = g @ ws.t()
                 dx.addmm_(dz, wn.t())
@@ -98,7 +85,7 @@ class SAGELayerFn(Function):
             if ctx.needs_input_grad[2]:
                 if a is None:
                     a = graph.aggregate(x, mean=True)
-                dwn = mm_f32(a.t(), g).to(ctx.w_dtype)
+                dwn = wgrad(a, g).to(ctx.w_dtype)
                 del a
             if ctx.needs_input_grad[0]:
                 t = g @ wn.t()
@@ -300,13 +287,13 @@ class SAGEStackFn(Function):
             acts[i] = None
             recyclable = i > 0  # hidden activations are private to this node
             need_dx = i > 0 or ctx.x0_requires_grad
-            grads[3 * i] = mm_f32(x.t(), g).to(ws.dtype)
+            grads[3 * i] = wgrad(x, g).to(ws.dtype)
             if b is not None:
                 grads[3 * i + 2] = col_sum_f32(g).to(b.dtype)
             dx = None
             if pf:
                 dz = graph.aggregate_T(g, mean=True, out=V("tmp_b", dims[i + 1]))
-                grads[3 * i + 1] = mm_f32(x.t(), dz).to(wn.dtype)
+                grads[3 * i + 1] = wgrad(x, dz).to(wn.dtype)
                 if need_dx:
                     dx = torch.mm(g, ws_.t(), out=x) if recyclable else g @ ws_.t()
                     dx.addmm_(dz, wn_.t())
@@ -319,7 +306,7 @@ class SAGEStackFn(Function):
                 else:
                     a_buf = V(a_name, dims[i])
                 a = graph.aggregate(x, mean=True, out=a_buf)
-                grads[3 * i + 1] = mm_f32(a.t(), g).to(wn.dtype)
+                grads[3 * i + 1] = wgrad(a, g).to(wn.dtype)
                 if need_dx:
                     t = torch.mm(g, wn_.t(), out=a)
                     dx = graph.aggregate_T(t, mean=True, out=x if recyclable else None)

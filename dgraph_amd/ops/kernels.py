@@ -116,7 +116,18 @@ def edge_softmax_bwd(rowptr: torch.Tensor, alpha: torch.Tensor, grad: torch.Tens
 
 
 def mask_words(numel: int) -> int:
-    return (numel + 31) // 32
+    """int32 words of a keep mask for ``numel`` elements (512-element chunks x 16)."""
+    return (numel + 511) // 512 * 16
+
+
+def col_sum(g: torch.Tensor) -> torch.Tensor:
+    """fp32 column sums of a 2-D tensor (bias gradients), deterministic."""
+    if _native_ok(g) and g.dim() == 2 and g.stride(1) == 1:
+        vec = 4 if g.dtype == torch.float32 else 8
+        if g.shape[1] % vec == 0 and g.shape[1] // vec <= 256 and g.stride(0) % vec == 0:
+            return _native.ops().col_sum(g)
+        return torch.sum(g, dim=0, dtype=torch.float32)
+    return _ref.col_sum(g)
 
 
 def bias_relu_pack(y: torch.Tensor, bias: Optional[torch.Tensor] = None,

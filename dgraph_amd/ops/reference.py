@@ -104,6 +104,33 @@ def edge_softmax_bwd(rowptr: torch.Tensor, alpha: torch.Tensor, g: torch.Tensor)
     return (a2 * (g2 - dot[rows])).reshape(alpha.shape)
 
 
+def _mask_to_words(keep: torch.Tensor) -> torch.Tensor:
+    """Keep-mask -> int32 words in the kernels' layout: 512-element chunks, word j (64
+    bit, little-endian int32 pair) of a chunk holds bit l = keep(8*l + j)."""
+    flat = keep.reshape(-1)
+    n = flat.numel()
+    nch = (n + 511) // 512
+    pad = torch.zeros(nch * 512, dtype=torch.bool, device=flat.device)
+    pad[:n] = flat
+    k = pad.view(nch, 64, 8).permute(0, 2, 1).to(torch.int64)  # [chunk, j, lane]
+    lo = (k[:, :, :32] << torch.arange(32, device=k.device)).sum(-1)
+    hi = (k[:, :, 32:] << torch.arange(32, device=k.device)).sum(-1)
+    w = torch.stack([lo, hi], -1).reshape(-1)
+    w = torch.where(w >= 2**31, w - 2**32, w)
+    return w.to(torch.int32)
+
+
+def _words_to_mask(bits: torch.Tensor, numel: int) -> torch.Tensor:
+    nch = (numel + 511) // 512
+    w = bits.reshape(-1)[: nch * 16].to(torch.int64) & 0xFFFFFFFF
+    w = w.view(nch, 8, 2)
+    lanes = torch.arange(32, device=w.device)
+    lo = (w[:, :, 0:1] >> lanes) & 1
+    hi = (w[:, :, 1:2] >> lanes) & 1
+    k = torch.cat([lo, hi], -1)  # [chunk, j, lane]
+    return k.permute(0, 2, 1).reshape(-1)[:numel].bool()
+
+
 def bias_relu_pack(y: torch.Tensor, bias, bits, relu: bool) -> None:
     t = y.float()
     if bias is not None:
@@ -112,14 +139,15 @@ def bias_relu_pack(y: torch.Tensor, bias, bits, relu: bool) -> None:
         keep = t > 0
         t = torch.where(keep, t, torch.zeros((), device=t.device))
         if bits is not None:
-            kb = keep.reshape(-1, 32).to(torch.int64)
-            w = (kb << torch.arange(32, device=y.device)).sum(1)
-            w = torch.where(w >= 2**31, w - 2**32, w)
-            bits.view(-1)[: w.numel()] = w.to(torch.int32)
+            w = _mask_to_words(keep)
+            bits.view(-1)[: w.numel()] = w
     y.copy_(t.to(y.dtype))
 
 
 def relu_mask_bwd(g: torch.Tensor, bits: torch.Tensor) -> None:
-    w = bits.view(-1)[: g.numel() // 32].to(torch.int64) & 0xFFFFFFFF
-    keep = ((w.unsqueeze(1) >> torch.arange(32, device=g.device)) & 1).bool().reshape(g.shape)
+    keep = _words_to_mask(bits, g.numel()).reshape(g.shape)
     g.masked_fill_(~keep, 0)
+
+
+def col_sum(g: torch.Tensor) -> torch.Tensor:
+    return g.float().sum(0)

@@ -169,6 +169,36 @@ def test_bias_relu_pack_and_mask(dtype):
     torch.testing.assert_close(g.cpu(), gc)
 
 
+@pytest.mark.parametrize("shape", [(1000, 64), (3, 256), (777, 40), (5000, 172)])
+def test_bias_relu_pack_shapes(shape):
+    y = torch.randn(*shape, device=DEV).to(torch.bfloat16)
+    yc = y.cpu().clone()
+    bits = torch.empty(K.mask_words(y.numel()), dtype=torch.int32, device=DEV)
+    K.bias_relu_pack(y, None, bits, relu=True)
+    bref = torch.empty(bits.numel(), dtype=torch.int32)
+    R.bias_relu_pack(yc, None, bref, True)
+    assert torch.equal(y.cpu(), yc)
+    assert torch.equal(bits.cpu(), bref)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("F", [8, 64, 172, 256])
+def test_col_sum(dtype, F):
+    g = torch.randn(70001, F, device=DEV).to(dtype)
+    torch.testing.assert_close(K.col_sum(g).cpu(), g.float().sum(0).cpu(), atol=5e-2, rtol=1e-3)
+
+
+def test_wgrad_split_k():
+    from dgraph_amd.ops.dense import wgrad
+
+    x = torch.randn(600_001, 128, device=DEV).to(torch.bfloat16)
+    g = torch.randn(600_001, 96, device=DEV).to(torch.bfloat16)
+    ref = x.float().t() @ g.float()
+    out = wgrad(x, g, rows_per_chunk=1 << 16)
+    assert out.dtype == torch.float32
+    torch.testing.assert_close(out, ref, atol=0.5, rtol=1e-2)
+
+
 def test_sage_stack_gpu_matches_cpu():
     from dgraph_amd.data.synthetic import SHAPES, build_partition, node_data
     from dgraph_amd.models.sage import GraphSAGE
