@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--global-frac", type=float, default=0.05)
     ap.add_argument("--variants", default="1:0,2:0,2:1")
+    ap.add_argument("--slices", default="1")
     a = ap.parse_args()
     from dgraph_amd import _native
     from dgraph_amd.data.synthetic import SHAPES, build_partition
@@ -60,6 +61,25 @@ def main():
                     err = (out[rows].float() - ref[rows].float()).abs().max().item()
                     assert err < 5e-2, f"variant {v} differs by {err}"
         nbytes = csr.nnz * (F * 2 + csr.col.element_size()) + p["L"] * F * 2
+        # feature-sliced execution (narrower gathered rows -> smaller per-XCD working set)
+        for s in [int(v) for v in a.slices.split(",") if int(v) > 1 and F % int(v) == 0]:
+            ts = []
+            w = F // s
+            for r in range(a.rounds + 1):
+                st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                torch.cuda.synchronize()
+                st.record()
+                for j in range(s):
+                    K.spmm(csr.rowptr, csr.col, x[:, j * w:(j + 1) * w],
+                           out[:, j * w:(j + 1) * w], row_scale=inv)
+                en.record()
+                torch.cuda.synchronize()
+                if r > 0:
+                    ts.append(st.elapsed_time(en))
+            ms = statistics.median(ts)
+            res[f"F{F}_slices{s}"] = {"ms": round(ms, 3), "TBps": round(nbytes / ms / 1e9, 3)}
+            print(f"F={F:4d} slices={s}: {ms:8.2f} ms  {nbytes / ms / 1e9:6.2f} TB/s effective",
+                  flush=True)
         for v in variants:
             ms = statistics.median(times[v])
             res[f"F{F}_v{v[0]}_xcd{v[1]}"] = {"ms": round(ms, 3),

@@ -18,7 +18,10 @@
 namespace dgraph {
 namespace {
 
-template <typename T>
+// One 512-element chunk per wave-iteration step; CH chunks are loaded before any is
+// processed so each wave keeps CH x 1 KiB of loads in flight (a single chunk per
+// iteration left the kernel latency-bound at ~2.2 TB/s, profiles/).
+template <typename T, int CH>
 __global__ __launch_bounds__(256) void bias_relu_pack_kernel(
     T* __restrict__ y, const float* __restrict__ bias, uint64_t* __restrict__ bits,
     int64_t numel, int F, bool relu) {
@@ -27,49 +30,59 @@ __global__ __launch_bounds__(256) void bias_relu_pack_kernel(
   const int64_t nchunks = (numel + 511) / 512;
   const int64_t wave = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
-  for (int64_t ch = wave; ch < nchunks; ch += nwaves) {
-    const int64_t e0 = ch * 512 + lane * VEC;
-    const bool valid = e0 < numel;  // numel % 8 == 0 (host check)
-    float x[VEC];
-    if (valid) {
-      if constexpr (sizeof(T) == 2) {
-        load_vec_f32<T, 8>(y + e0, x);
+  for (int64_t ch0 = wave * CH; ch0 < nchunks; ch0 += nwaves * CH) {
+    float x[CH][VEC];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int64_t e0 = (ch0 + c) * 512 + lane * VEC;
+      if (e0 < numel) {  // numel % 8 == 0 (host check)
+        if constexpr (sizeof(T) == 2) {
+          load_vec_f32<T, 8>(y + e0, x[c]);
+        } else {
+          float a[4], b[4];
+          load_vec_f32<T, 4>(y + e0, a);
+          load_vec_f32<T, 4>(y + e0 + 4, b);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) { x[c][i] = a[i]; x[c][i + 4] = b[i]; }
+        }
       } else {
-        float a[4], b[4];
-        load_vec_f32<T, 4>(y + e0, a);
-        load_vec_f32<T, 4>(y + e0 + 4, b);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) { x[i] = a[i]; x[i + 4] = b[i]; }
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < VEC; ++i) x[i] = 0.f;
-    }
-    const int c0 = static_cast<int>(e0 % F);  // F % 8 == 0: one row per lane slot
-    uint64_t my_word = 0;
-#pragma unroll
-    for (int j = 0; j < VEC; ++j) {
-      float t = x[j] + ((bias && valid) ? bias[c0 + j] : 0.f);
-      bool keep = t > 0.f;
-      if (relu) t = keep ? t : 0.f;
-      x[j] = t;
-      const uint64_t b = __ballot(valid && keep);
-      if (lane == j) my_word = b;
-    }
-    if (valid) {
-      if constexpr (sizeof(T) == 2) {
-        store_vec_f32<T, 8>(y + e0, x);
-      } else {
-        float a[4] = {x[0], x[1], x[2], x[3]}, b[4] = {x[4], x[5], x[6], x[7]};
-        store_vec_f32<T, 4>(y + e0, a);
-        store_vec_f32<T, 4>(y + e0 + 4, b);
+        for (int i = 0; i < VEC; ++i) x[c][i] = 0.f;
       }
     }
-    if (bits && relu && lane < VEC) bits[ch * 8 + lane] = my_word;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int64_t ch = ch0 + c;
+      if (ch >= nchunks) break;  // wave-uniform
+      const int64_t e0 = ch * 512 + lane * VEC;
+      const bool valid = e0 < numel;
+      const int c0 = static_cast<int>(e0 % F);  // F % 8 == 0: one row per lane slot
+      uint64_t my_word = 0;
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        float t = x[c][j] + ((bias && valid) ? bias[c0 + j] : 0.f);
+        const bool keep = t > 0.f;
+        if (relu) t = keep ? t : 0.f;
+        x[c][j] = t;
+        const uint64_t b = __ballot(valid && keep);
+        if (lane == j) my_word = b;
+      }
+      if (valid) {
+        if constexpr (sizeof(T) == 2) {
+          store_vec_f32<T, 8>(y + e0, x[c]);
+        } else {
+          float a[4] = {x[c][0], x[c][1], x[c][2], x[c][3]};
+          float b[4] = {x[c][4], x[c][5], x[c][6], x[c][7]};
+          store_vec_f32<T, 4>(y + e0, a);
+          store_vec_f32<T, 4>(y + e0 + 4, b);
+        }
+      }
+      if (bits && relu && lane < VEC) bits[ch * 8 + lane] = my_word;
+    }
   }
 }
 
-template <typename T>
+template <typename T, int CH>
 __global__ __launch_bounds__(256) void relu_mask_bwd_kernel(
     T* __restrict__ g, const uint64_t* __restrict__ bits, int64_t numel) {
   constexpr int VEC = 8;
@@ -77,29 +90,41 @@ __global__ __launch_bounds__(256) void relu_mask_bwd_kernel(
   const int64_t nchunks = (numel + 511) / 512;
   const int64_t wave = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
-  for (int64_t ch = wave; ch < nchunks; ch += nwaves) {
-    const int64_t e0 = ch * 512 + lane * VEC;
-    // lane j < 8 loads word j; broadcast through shuffles (64-bit: two halves)
-    uint64_t w = lane < VEC ? bits[ch * 8 + lane] : 0;
-    uint32_t m = 0;
+  for (int64_t ch0 = wave * CH; ch0 < nchunks; ch0 += nwaves * CH) {
+    uint64_t w[CH];
+    T v[CH][VEC];
 #pragma unroll
-    for (int j = 0; j < VEC; ++j) {
-      const uint32_t lo = __shfl(static_cast<uint32_t>(w), j, 64);
-      const uint32_t hi = __shfl(static_cast<uint32_t>(w >> 32), j, 64);
-      const uint32_t bit = lane < 32 ? (lo >> lane) & 1u : (hi >> (lane - 32)) & 1u;
-      m |= bit << j;
+    for (int c = 0; c < CH; ++c) {  // issue every load of the group first
+      const int64_t ch = ch0 + c;
+      const int64_t e0 = ch * 512 + lane * VEC;
+      w[c] = (lane < VEC && ch < nchunks) ? bits[ch * 8 + lane] : 0;
+      if (e0 < numel) {
+#pragma unroll
+        for (int k = 0; k < VEC * static_cast<int>(sizeof(T)) / 16; ++k)
+          reinterpret_cast<uint4*>(v[c])[k] = reinterpret_cast<const uint4*>(g + e0)[k];
+      }
     }
-    if (e0 >= numel || m == 0xFFu) continue;
-    if constexpr (sizeof(T) == 2) {
-      float x[8];
-      load_vec_f32<T, 8>(g + e0, x);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) x[j] = ((m >> j) & 1u) ? x[j] : 0.f;
-      store_vec_f32<T, 8>(g + e0, x);
-    } else {
+    for (int c = 0; c < CH; ++c) {
+      const int64_t ch = ch0 + c;
+      if (ch >= nchunks) break;  // wave-uniform
+      const int64_t e0 = ch * 512 + lane * VEC;
+      // lane j < 8 holds word j; broadcast through shuffles (64-bit: two halves)
+      uint32_t m = 0;
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (!((m >> j) & 1u)) g[e0 + j] = 0.f;
+      for (int j = 0; j < VEC; ++j) {
+        const uint32_t lo = __shfl(static_cast<uint32_t>(w[c]), j, 64);
+        const uint32_t hi = __shfl(static_cast<uint32_t>(w[c] >> 32), j, 64);
+        const uint32_t bit = lane < 32 ? (lo >> lane) & 1u : (hi >> (lane - 32)) & 1u;
+        m |= bit << j;
+      }
+      if (e0 >= numel || m == 0xFFu) continue;
+#pragma unroll
+      for (int j = 0; j < VEC; ++j)
+        if (!((m >> j) & 1u)) v[c][j] = T(0);
+#pragma unroll
+      for (int k = 0; k < VEC * static_cast<int>(sizeof(T)) / 16; ++k)
+        reinterpret_cast<uint4*>(g + e0)[k] = reinterpret_cast<const uint4*>(v[c])[k];
     }
   }
 }
@@ -147,13 +172,15 @@ hipError_t bias_relu_pack(DType dt, void* y, const float* bias, uint32_t* bits, 
   if (numel <= 0) return hipSuccess;
   if (numel % 8 != 0 || F % 8 != 0) return hipErrorInvalidValue;
   const int64_t nchunks = (numel + 511) / 512;
-  dim3 block(256), grid(static_cast<unsigned>(cap_blocks((nchunks + 3) / 4, 256 * 16)));
+  constexpr int CH = 4;
+  dim3 block(256),
+      grid(static_cast<unsigned>(cap_blocks((nchunks + 4 * CH - 1) / (4 * CH), 256 * 8)));
   auto* b64 = reinterpret_cast<uint64_t*>(bits);
   if (dt == DType::F32)
-    hipLaunchKernelGGL(bias_relu_pack_kernel<float>, grid, block, 0, st,
+    hipLaunchKernelGGL((bias_relu_pack_kernel<float, CH>), grid, block, 0, st,
                        static_cast<float*>(y), bias, b64, numel, F, relu);
   else
-    hipLaunchKernelGGL(bias_relu_pack_kernel<uint16_t>, grid, block, 0, st,
+    hipLaunchKernelGGL((bias_relu_pack_kernel<uint16_t, CH>), grid, block, 0, st,
                        static_cast<uint16_t*>(y), bias, b64, numel, F, relu);
   return hipGetLastError();
 }
@@ -163,13 +190,15 @@ hipError_t relu_mask_bwd(DType dt, void* g, const uint32_t* bits, int64_t numel,
   if (numel <= 0) return hipSuccess;
   if (numel % 8 != 0) return hipErrorInvalidValue;
   const int64_t nchunks = (numel + 511) / 512;
-  dim3 block(256), grid(static_cast<unsigned>(cap_blocks((nchunks + 3) / 4, 256 * 16)));
+  constexpr int CH = 4;
+  dim3 block(256),
+      grid(static_cast<unsigned>(cap_blocks((nchunks + 4 * CH - 1) / (4 * CH), 256 * 8)));
   const auto* b64 = reinterpret_cast<const uint64_t*>(bits);
   if (dt == DType::F32)
-    hipLaunchKernelGGL(relu_mask_bwd_kernel<float>, grid, block, 0, st,
+    hipLaunchKernelGGL((relu_mask_bwd_kernel<float, CH>), grid, block, 0, st,
                        static_cast<float*>(g), b64, numel);
   else
-    hipLaunchKernelGGL(relu_mask_bwd_kernel<uint16_t>, grid, block, 0, st,
+    hipLaunchKernelGGL((relu_mask_bwd_kernel<uint16_t, CH>), grid, block, 0, st,
                        static_cast<uint16_t*>(g), b64, numel);
   return hipGetLastError();
 }

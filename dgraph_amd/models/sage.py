@@ -138,6 +138,23 @@ def _auto_save_agg(x: torch.Tensor, graph: DistGraph) -> bool:
     return x.numel() * x.element_size() < 0.15 * free
 
 
+def _pad8(n: int) -> int:
+    return (n + 7) // 8 * 8
+
+
+def _padded(params, i, dims_p, dt):
+    """Layer i's (W_self, W_neigh, bias) cast to ``dt`` and zero-padded to
+    ``[dims_p[i], dims_p[i+1]]`` (bias stays fp32 for the fused epilogue)."""
+    ws, wn, b = params[3 * i], params[3 * i + 1], params[3 * i + 2]
+    ri, ro = dims_p[i] - ws.shape[0], dims_p[i + 1] - ws.shape[1]
+    if ri or ro:
+        ws = Fn.pad(ws, (0, ro, 0, ri))
+        wn = Fn.pad(wn, (0, ro, 0, ri))
+        if b is not None:
+            b = Fn.pad(b, (0, ro))
+    return ws.to(dt), wn.to(dt), b
+
+
 class SageWorkspace:
     """Preplanned activation slots for :class:`SAGEStackFn` (no per-step allocation).
 
@@ -195,9 +212,12 @@ class SAGEStackFn(Function):
         L = x0.shape[0]
         dt = x0.dtype
         dims = [x0.shape[1]] + [params[3 * i].shape[1] for i in range(n)]
+        # hidden/output widths padded to multiples of 8 (16-B bf16 rows: full-width
+        # vector loads in the SpMM and the ReLU-mask kernels); pads stay exactly zero
+        dims_p = [dims[0]] + [_pad8(d) for d in dims[1:]]
         pf_flags = [pf for (_, pf) in specs]
         if use_ws:
-            ws_obj.prepare(L, dims, pf_flags, dt, x0.device)
+            ws_obj.prepare(L, dims_p, pf_flags, dt, x0.device)
             ws_obj.generation += 1
         V = (lambda name, F: ws_obj.view(name, L, F)) if use_ws else \
             (lambda name, F: torch.empty(L, F, dtype=dt, device=x0.device))
@@ -205,10 +225,10 @@ class SAGEStackFn(Function):
         masks = []
         h = x0
         for i, (relu, pf) in enumerate(specs):
-            ws, wn, b = params[3 * i], params[3 * i + 1], params[3 * i + 2]
-            ws_, wn_ = ws.to(dt), wn.to(dt)
+            ws, wn, b = _padded(params, i, dims_p, dt)
+            ws_, wn_ = ws, wn
             last = i == n - 1
-            Fo = dims[i + 1]
+            Fo = dims_p[i + 1]
             y = V("tmp_b" if last else f"act{i + 1}", Fo)
             if pf:
                 z = torch.mm(h, wn_, out=V("tmp_a", Fo))
@@ -216,11 +236,11 @@ class SAGEStackFn(Function):
                 del z
                 y.addmm_(h, ws_)
             else:
-                a = graph.aggregate(h, mean=True, out=V("tmp_a", dims[i]))
+                a = graph.aggregate(h, mean=True, out=V("tmp_a", dims_p[i]))
                 torch.mm(h, ws_, out=y)
                 y.addmm_(a, wn_)
                 del a
-            if relu and Fo % 32 == 0 and y.numel() % 32 == 0:
+            if relu and Fo % 8 == 0 and y.is_contiguous():
                 bits = torch.empty(K.mask_words(y.numel()), dtype=torch.int32, device=y.device)
                 K.bias_relu_pack(y, b, bits, relu=True)
                 masks.append(bits)
@@ -233,24 +253,26 @@ class SAGEStackFn(Function):
             if not last:
                 acts.append(y)
             h = y
-        ctx.graph, ctx.specs, ctx.dims = graph, specs, dims
+        ctx.graph, ctx.specs, ctx.dims, ctx.dims_p = graph, specs, dims, dims_p
         ctx.acts, ctx.masks = acts, masks
         ctx.x0_requires_grad = x0.requires_grad
         ctx.ws, ctx.use_ws = ws_obj, use_ws
         ctx.gen = ws_obj.generation if use_ws else None
         ctx.save_for_backward(*params)
         ctx.out_rows = out_rows
+        C = dims[-1]
         if out_rows is not None:
             # the last layer is computed for every vertex; only the requested rows leave
             # the node, so autograd never holds a dense [V, C] output gradient
-            return h.index_select(0, out_rows)
-        return h
+            return h.index_select(0, out_rows)[:, :C].contiguous()
+        return h[:, :C] if C != h.shape[1] else h
 
     @staticmethod
     def backward(ctx, gy):
         params = ctx.saved_tensors
         graph: DistGraph = ctx.graph
-        acts, masks, specs, dims = ctx.acts, ctx.masks, ctx.specs, ctx.dims
+        acts, masks, specs, dims_true = ctx.acts, ctx.masks, ctx.specs, ctx.dims
+        dims = ctx.dims_p  # everything below runs at the padded widths
         ctx.acts = ctx.masks = None
         ws_obj, use_ws = ctx.ws, ctx.use_ws
         if use_ws and ws_obj.generation != ctx.gen:
@@ -261,12 +283,16 @@ class SAGEStackFn(Function):
         L, dt = x0.shape[0], x0.dtype
         V = (lambda name, F: ws_obj.view(name, L, F)) if use_ws else \
             (lambda name, F: torch.empty(L, F, dtype=dt, device=x0.device))
+        C, Cp = dims_true[-1], dims[-1]
+        gyp = gy.to(dt)
+        if Cp != C:
+            gyp = Fn.pad(gyp, (0, Cp - C))
         if ctx.out_rows is not None:
-            g = V("tmp_a", dims[-1])
+            g = V("tmp_a", Cp)
             g.zero_()
-            g.index_copy_(0, ctx.out_rows, gy.to(dt))
+            g.index_copy_(0, ctx.out_rows, gyp)
         else:
-            g = gy.to(dt).contiguous()
+            g = gyp.contiguous()
             if g is gy:
                 g = g.clone()  # never modify the caller's gradient in place
         grads = [None] * len(params)
@@ -274,7 +300,8 @@ class SAGEStackFn(Function):
         for i in reversed(range(n)):
             relu, pf = specs[i]
             ws, wn, b = params[3 * i], params[3 * i + 1], params[3 * i + 2]
-            ws_, wn_ = ws.to(dt), wn.to(dt)
+            ws_, wn_, _ = _padded(params, i, dims, dt)
+            r_in, r_out = dims_true[i], dims_true[i + 1]
             m = masks[i]
             masks[i] = None
             if relu:
@@ -287,13 +314,13 @@ class SAGEStackFn(Function):
             acts[i] = None
             recyclable = i > 0  # hidden activations are private to this node
             need_dx = i > 0 or ctx.x0_requires_grad
-            grads[3 * i] = wgrad(x, g).to(ws.dtype)
+            grads[3 * i] = wgrad(x, g)[:r_in, :r_out].to(ws.dtype)
             if b is not None:
-                grads[3 * i + 2] = col_sum_f32(g).to(b.dtype)
+                grads[3 * i + 2] = col_sum_f32(g)[:r_out].to(b.dtype)
             dx = None
             if pf:
                 dz = graph.aggregate_T(g, mean=True, out=V("tmp_b", dims[i + 1]))
-                grads[3 * i + 1] = wgrad(x, dz).to(wn.dtype)
+                grads[3 * i + 1] = wgrad(x, dz)[:r_in, :r_out].to(wn.dtype)
                 if need_dx:
                     dx = torch.mm(g, ws_.t(), out=x) if recyclable else g @ ws_.t()
                     dx.addmm_(dz, wn_.t())
@@ -306,7 +333,7 @@ class SAGEStackFn(Function):
                 else:
                     a_buf = V(a_name, dims[i])
                 a = graph.aggregate(x, mean=True, out=a_buf)
-                grads[3 * i + 1] = wgrad(a, g).to(wn.dtype)
+                grads[3 * i + 1] = wgrad(a, g)[:r_in, :r_out].to(wn.dtype)
                 if need_dx:
                     t = torch.mm(g, wn_.t(), out=a)
                     dx = graph.aggregate_T(t, mean=True, out=x if recyclable else None)

@@ -169,7 +169,14 @@ def test_bias_relu_pack_and_mask(dtype):
     torch.testing.assert_close(g.cpu(), gc)
 
 
-@pytest.mark.parametrize("shape", [(1000, 64), (3, 256), (777, 40), (5000, 172)])
+def test_bias_relu_pack_rejects_unaligned_rows():
+    y = torch.randn(10, 172, device=DEV).to(torch.bfloat16)
+    bits = torch.empty(K.mask_words(y.numel()), dtype=torch.int32, device=DEV)
+    with pytest.raises(RuntimeError):
+        K.bias_relu_pack(y, None, bits, relu=True)
+
+
+@pytest.mark.parametrize("shape", [(1000, 64), (3, 256), (777, 40), (5000, 168), (9, 8)])
 def test_bias_relu_pack_shapes(shape):
     y = torch.randn(*shape, device=DEV).to(torch.bfloat16)
     yc = y.cpu().clone()
