@@ -81,6 +81,14 @@ class SAGELayerFn(Function):
                 dx = g @ ws.t()
                 dx.addmm_(dz, wn.t())
             del dz
+        elif ctx.needs_input_grad[0] and a is None and wn.shape[1] <= 2 * wn.shape[0]:
+            # one SpMM at F_out: u = A^T g -> dW_neigh = x^T u, dx = g Ws^T + u Wn^T
+            u = graph.aggregate_T(g, mean=True)
+            if ctx.needs_input_grad[2]:
+                dwn = wgrad(x, u).to(ctx.w_dtype)
+            dx = g @ ws.t()
+            dx.addmm_(u, wn.t())
+            del u
         else:
             if ctx.needs_input_grad[2]:
                 if a is None:
@@ -325,6 +333,16 @@ class SAGEStackFn(Function):
                     dx = torch.mm(g, ws_.t(), out=x) if recyclable else g @ ws_.t()
                     dx.addmm_(dz, wn_.t())
                 del dz
+            elif need_dx and dims[i + 1] <= 2 * dims[i]:
+                # u = A^T g gives both gradients with ONE SpMM at F_out:
+                #   dW_neigh = (A h)^T g = h^T u,   dh = g W_self^T + u W_neigh^T
+                # (instead of recomputing A h AND aggregating A^T (g W_neigh^T))
+                u_name = "tmp_b" if (i == n - 1 and ctx.out_rows is not None) else "tmp_a"
+                u = graph.aggregate_T(g, mean=True, out=V(u_name, dims[i + 1]))
+                grads[3 * i + 1] = wgrad(x, u)[:r_in, :r_out].to(wn.dtype)
+                dx = torch.mm(g, ws_.t(), out=x) if recyclable else g @ ws_.t()
+                dx.addmm_(u, wn_.t())
+                del u
             else:
                 # tmp_a may still hold g for the last layer: recompute into tmp_b then
                 a_name = "tmp_b" if (i == n - 1 and ctx.out_rows is not None) else "tmp_a"
