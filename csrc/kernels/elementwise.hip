@@ -26,9 +26,16 @@ __global__ __launch_bounds__(256) void bias_relu_pack_kernel(
     T* __restrict__ y, const float* __restrict__ bias, uint64_t* __restrict__ bits,
     int64_t numel, int F, bool relu) {
   constexpr int VEC = 8;  // elements per lane (16 B bf16, 32 B fp32)
+  // the bias is staged once per block in LDS (the per-element global bias loads made the
+  // first version VMEM-issue bound: 8 loads per 16 B of data)
+  extern __shared__ __attribute__((aligned(16))) float sbias[];
+  if (bias)
+    for (int c = threadIdx.x; c < F; c += blockDim.x) sbias[c] = bias[c];
+  __syncthreads();
   const int lane = threadIdx.x & 63;
   const int64_t nchunks = (numel + 511) / 512;
-  const int64_t wave = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t wave =
+      __builtin_amdgcn_readfirstlane((static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6);
   const int64_t nwaves = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
   for (int64_t ch0 = wave * CH; ch0 < nchunks; ch0 += nwaves * CH) {
     float x[CH][VEC];
@@ -56,11 +63,14 @@ __global__ __launch_bounds__(256) void bias_relu_pack_kernel(
       if (ch >= nchunks) break;  // wave-uniform
       const int64_t e0 = ch * 512 + lane * VEC;
       const bool valid = e0 < numel;
-      const int c0 = static_cast<int>(e0 % F);  // F % 8 == 0: one row per lane slot
+      // column of this lane's first element: one 64-bit modulo per chunk (scalar), then
+      // 32-bit math per lane; F % 8 == 0 keeps a lane's 8 elements in one row
+      const int cbase = static_cast<int>((ch * 512) % F);
+      const int c0 = (cbase + lane * VEC) % F;
       uint64_t my_word = 0;
 #pragma unroll
       for (int j = 0; j < VEC; ++j) {
-        float t = x[c][j] + ((bias && valid) ? bias[c0 + j] : 0.f);
+        float t = x[c][j] + (bias ? sbias[c0 + j] : 0.f);
         const bool keep = t > 0.f;
         if (relu) t = keep ? t : 0.f;
         x[c][j] = t;
@@ -88,16 +98,14 @@ __global__ __launch_bounds__(256) void relu_mask_bwd_kernel(
   constexpr int VEC = 8;
   const int lane = threadIdx.x & 63;
   const int64_t nchunks = (numel + 511) / 512;
-  const int64_t wave = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t wave =
+      __builtin_amdgcn_readfirstlane((static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6);
   const int64_t nwaves = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
   for (int64_t ch0 = wave * CH; ch0 < nchunks; ch0 += nwaves * CH) {
-    uint64_t w[CH];
     T v[CH][VEC];
 #pragma unroll
-    for (int c = 0; c < CH; ++c) {  // issue every load of the group first
-      const int64_t ch = ch0 + c;
-      const int64_t e0 = ch * 512 + lane * VEC;
-      w[c] = (lane < VEC && ch < nchunks) ? bits[ch * 8 + lane] : 0;
+    for (int c = 0; c < CH; ++c) {  // issue every data load of the group first
+      const int64_t e0 = (ch0 + c) * 512 + lane * VEC;
       if (e0 < numel) {
 #pragma unroll
         for (int k = 0; k < VEC * static_cast<int>(sizeof(T)) / 16; ++k)
@@ -109,15 +117,12 @@ __global__ __launch_bounds__(256) void relu_mask_bwd_kernel(
       const int64_t ch = ch0 + c;
       if (ch >= nchunks) break;  // wave-uniform
       const int64_t e0 = ch * 512 + lane * VEC;
-      // lane j < 8 holds word j; broadcast through shuffles (64-bit: two halves)
+      // the chunk's 8 mask words are wave-uniform: scalar loads (s_load), then each lane
+      // extracts its bit of word j with one 64-bit shift
+      const uint64_t* wp = bits + ch * 8;
       uint32_t m = 0;
 #pragma unroll
-      for (int j = 0; j < VEC; ++j) {
-        const uint32_t lo = __shfl(static_cast<uint32_t>(w[c]), j, 64);
-        const uint32_t hi = __shfl(static_cast<uint32_t>(w[c] >> 32), j, 64);
-        const uint32_t bit = lane < 32 ? (lo >> lane) & 1u : (hi >> (lane - 32)) & 1u;
-        m |= bit << j;
-      }
+      for (int j = 0; j < VEC; ++j) m |= static_cast<uint32_t>((wp[j] >> lane) & 1u) << j;
       if (e0 >= numel || m == 0xFFu) continue;
 #pragma unroll
       for (int j = 0; j < VEC; ++j)
@@ -176,11 +181,13 @@ hipError_t bias_relu_pack(DType dt, void* y, const float* bias, uint32_t* bits, 
   dim3 block(256),
       grid(static_cast<unsigned>(cap_blocks((nchunks + 4 * CH - 1) / (4 * CH), 256 * 8)));
   auto* b64 = reinterpret_cast<uint64_t*>(bits);
+  const size_t lds = bias ? static_cast<size_t>(F) * sizeof(float) : 0;
+  if (lds > 64 * 1024) return hipErrorInvalidValue;
   if (dt == DType::F32)
-    hipLaunchKernelGGL((bias_relu_pack_kernel<float, CH>), grid, block, 0, st,
+    hipLaunchKernelGGL((bias_relu_pack_kernel<float, CH>), grid, block, lds, st,
                        static_cast<float*>(y), bias, b64, numel, F, relu);
   else
-    hipLaunchKernelGGL((bias_relu_pack_kernel<uint16_t, CH>), grid, block, 0, st,
+    hipLaunchKernelGGL((bias_relu_pack_kernel<uint16_t, CH>), grid, block, lds, st,
                        static_cast<uint16_t*>(y), bias, b64, numel, F, relu);
   return hipGetLastError();
 }
