@@ -108,6 +108,8 @@ class NCCLBackendEngine(BackendEngine):
 
         if comm_plan is not None:
             return plan_gather(x, comm_plan, self.group)
+        if kw.get("cache") is not None:  # NCCLGatherCache from the G1 cache generators
+            return plan_gather(x, kw["cache"].plan, self.group)
         if indices is None or rank_mappings is None:
             raise ValueError("gather needs comm_plan= or (indices, rank_mappings)")
         return index_ops.g1_gather_global(x, indices, rank_mappings, self.get_local_rank(),
@@ -121,6 +123,8 @@ class NCCLBackendEngine(BackendEngine):
 
         if comm_plan is not None:
             return plan_scatter(x, comm_plan, self.group)
+        if kw.get("cache") is not None:  # NCCLScatterCache
+            return plan_scatter(x, kw["cache"].plan, self.group)
         if indices is None or rank_mappings is None or output_size is None:
             raise ValueError("scatter needs comm_plan= or (indices, rank_mappings, output_size)")
         return index_ops.g1_scatter_global(x, indices, rank_mappings, output_size,

@@ -19,12 +19,6 @@ from . import kernels as K
 from .csr import CSR, IndexMap
 
 
-def _edge_weight_in_csr_order(csr: CSR, ew: Optional[torch.Tensor], heads: int):
-    if ew is None:
-        return None
-    return ew.reshape(csr.nnz, heads).float().contiguous()
-
-
 class _AggregateFn(Function):
     @staticmethod
     def forward(ctx, x, csr: CSR, edge_weight, mean: bool, heads: int):
@@ -55,8 +49,9 @@ class _AggregateFn(Function):
             # d w[j,h] = row_scale[r] * <g[r, h-slice], x[c_j, h-slice]>  (SDDMM)
             rows = csr.row_ids()
             H = ctx.heads
-            gr = g.float()[rows].view(csr.nnz, H, -1)
-            xc = x_saved.float()[csr.col.long()].view(csr.nnz, H, -1)
+            cdt = torch.float64 if ew.dtype == torch.float64 else torch.float32
+            gr = g.to(cdt)[rows].view(csr.nnz, H, -1)
+            xc = x_saved.to(cdt)[csr.col.long()].view(csr.nnz, H, -1)
             gw = (gr * xc).sum(-1)
             if ctx.mean:
                 gw = gw * csr.inv_degree()[rows].unsqueeze(1)
@@ -78,10 +73,10 @@ def aggregate(
     """
     if reduce not in ("sum", "mean"):
         raise ValueError(f"unsupported reduce {reduce!r}")
-    ew = _edge_weight_in_csr_order(csr, edge_weight, heads)
-    if ew is not None and edge_weight.requires_grad:
-        ew = edge_weight.reshape(csr.nnz, heads)
-        if ew.dtype != torch.float32:
+    ew = None
+    if edge_weight is not None:
+        ew = edge_weight.reshape(csr.nnz, heads)  # native path casts to fp32 itself
+        if ew.dtype not in (torch.float32, torch.float64):
             ew = ew.float()
     return _AggregateFn.apply(x.contiguous(), csr, ew, reduce == "mean", heads)
 

@@ -31,19 +31,20 @@ def spmm(
     F = x.shape[1]
     col = col.long()
     rows = _row_ids(rowptr)
-    vals = x.float()[col]
+    adt = torch.float64 if x.dtype == torch.float64 else torch.float32
+    vals = x.to(adt)[col]
     if edge_weight is not None:
-        w = edge_weight.float().reshape(col.numel(), max(heads, 1))
+        w = edge_weight.to(adt).reshape(col.numel(), max(heads, 1))
         hd = F // max(heads, 1)
         vals = (vals.view(-1, max(heads, 1), hd) * w.unsqueeze(-1)).view(-1, F)
     if col_scale is not None:
-        vals = vals * col_scale.float()[col].unsqueeze(1)
-    acc = torch.zeros(R, F, dtype=torch.float32, device=x.device)
+        vals = vals * col_scale.to(adt)[col].unsqueeze(1)
+    acc = torch.zeros(R, F, dtype=adt, device=x.device)
     acc.index_add_(0, rows, vals)
     if row_scale is not None:
-        acc = acc * row_scale.float().unsqueeze(1)
+        acc = acc * row_scale.to(adt).unsqueeze(1)
     if beta != 0.0:
-        acc = acc + beta * out[:R].float()
+        acc = acc + beta * out[:R].to(adt)
     out[:R].copy_(acc.to(out.dtype))
     return out
 
