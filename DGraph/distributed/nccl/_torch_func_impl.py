@@ -1,0 +1,3 @@
+"""API-compatibility module: reference path ``DGraph/distributed/nccl/_torch_func_impl.py`` re-exported from ``dgraph_amd.parallel.plan_ops``
+(dgraph_amd is the implementation; this tree only preserves DGraph import paths)."""
+from dgraph_amd.parallel.plan_ops import CommPlan_GatherFunction, CommPlan_ScatterFunction  # noqa: F401

@@ -1,0 +1,5 @@
+"""API-compatibility module: reference path ``DGraph.torch_local (native extension)`` re-exported from ``dgraph_amd.ops.local``
+(dgraph_amd is the implementation; this tree only preserves DGraph import paths)."""
+from dgraph_amd.ops.local import (  # noqa: F401
+    local_masked_gather, local_masked_scatter, local_masked_scatter_add_gather,
+    local_masked_scatter_gather)

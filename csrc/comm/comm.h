@@ -1,0 +1,20 @@
+// dgraph_amd — native communication runtime (symmetric heap kernels, RCCL plan executor).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../kernels/kernels.h"
+
+namespace dgraph {
+
+// out[i, :F] = *(T*)(peer_base[owner[i]] + base_off)[row[i] * ld_src, +F)
+hipError_t heap_get_rows(DType dt, const uint64_t* peer_base, int64_t base_off,
+                         const int64_t* owner, const int64_t* row, void* out, int64_t ld_src,
+                         int64_t ld_out, int64_t n, int F, hipStream_t st);
+
+// *(T*)(peer_base[row_peer[i]] + dst_off)[row_dst[i] * ld_dst, +F) = src[i, :F]
+hipError_t heap_put_rows(DType dt, const uint64_t* peer_base, int64_t dst_off,
+                         const int64_t* row_peer, const int64_t* row_dst, const void* src,
+                         int64_t ld_src, int64_t ld_dst, int64_t n, int F, hipStream_t st);
+
+}  // namespace dgraph

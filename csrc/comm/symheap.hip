@@ -1,0 +1,145 @@
+// dgraph_amd — one-sided symmetric heap over HIP IPC (the NVSHMEM replacement, N3/N4).
+//
+// rocSHMEM is not installed, so every rank hipMalloc's a heap of the SAME size (the max
+// over ranks: the reference's collective nvshmem_malloc had mismatched sizes, D4),
+// exports an IPC handle (dmabuf under HSA_ENABLE_IPC_MODE_LEGACY=0), and maps every peer's
+// heap into its address space. Kernels then read/write peer memory directly over xGMI:
+//
+//   heap_get_rows : out[i] = heap_of(owner[i])[base_off + row[i]*ld, +F)   (K15: remote get)
+//   heap_put_rows : heap_of(peer)[dst_off + (remote_off[peer] + j)*ld] = src[send_off[peer] + j]
+//                   for every peer segment (one-sided put at remote_offsets, HaloExchange)
+//
+// One wavefront moves G = 64/LPR rows per step with 16-B loads/stores; the peer table is a
+// small device array of base pointers. Completion: the host drains the stream and joins a
+// process-group barrier (writes from a peer are visible to a rank once the peer's kernel
+// has completed and both have passed the barrier; stores to peer memory are made visible
+// with a system-scope release at kernel end).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../common.h"
+#include "comm.h"
+
+namespace dgraph {
+namespace {
+
+template <typename T, int VEC, int LPR>
+__global__ __launch_bounds__(256) void heap_get_rows_kernel(
+    const uint64_t* __restrict__ peer_base, int64_t base_off, const int64_t* __restrict__ owner,
+    const int64_t* __restrict__ row, T* __restrict__ out, int64_t ld_src, int64_t ld_out,
+    int64_t n, int F) {
+  constexpr int G = kWave / LPR;
+  const int lane = threadIdx.x & 63;
+  const int g = lane / LPR, l = lane % LPR;
+  const int64_t wave = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
+  for (int64_t base = wave * G; base < n; base += nwaves * G) {
+    const int64_t i = base + g;
+    if (i >= n) continue;
+    const T* src = reinterpret_cast<const T*>(peer_base[owner[i]] + base_off) + row[i] * ld_src;
+    for (int f = l * VEC; f < F; f += LPR * VEC) {
+      float v[VEC];
+      load_vec_f32<T, VEC>(src + f, v);
+      store_vec_f32<T, VEC>(out + i * ld_out + f, v);
+    }
+  }
+}
+
+template <typename T, int VEC, int LPR>
+__global__ __launch_bounds__(256) void heap_put_rows_kernel(
+    const uint64_t* __restrict__ peer_base, int64_t dst_off, const int64_t* __restrict__ row_peer,
+    const int64_t* __restrict__ row_dst, const T* __restrict__ src, int64_t ld_src,
+    int64_t ld_dst, int64_t n, int F) {
+  constexpr int G = kWave / LPR;
+  const int lane = threadIdx.x & 63;
+  const int g = lane / LPR, l = lane % LPR;
+  const int64_t wave = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
+  for (int64_t base = wave * G; base < n; base += nwaves * G) {
+    const int64_t i = base + g;
+    if (i >= n) continue;
+    T* dst = reinterpret_cast<T*>(peer_base[row_peer[i]] + dst_off) + row_dst[i] * ld_dst;
+    for (int f = l * VEC; f < F; f += LPR * VEC) {
+      float v[VEC];
+      load_vec_f32<T, VEC>(src + i * ld_src + f, v);
+      store_vec_f32<T, VEC>(dst + f, v);
+    }
+  }
+  // make this block's peer stores visible system-wide before the kernel retires
+  __threadfence_system();
+}
+
+inline int pick_lpr(int lanes) {
+  return lanes <= 4 ? 4 : lanes <= 8 ? 8 : lanes <= 16 ? 16 : lanes <= 32 ? 32 : 64;
+}
+
+template <typename T>
+hipError_t launch_get(const uint64_t* pb, int64_t off, const int64_t* own, const int64_t* row,
+                      void* out, int64_t lds, int64_t ldo, int64_t n, int F, hipStream_t st) {
+  dim3 block(256), grid(static_cast<unsigned>(cap_blocks((n + 15) / 16, 256 * 16)));
+  constexpr int V = 16 / sizeof(T);
+  const bool vec = F % V == 0 && lds % V == 0 && ldo % V == 0;
+  const int lpr = pick_lpr(vec ? F / V : F);
+#define DG_GET(VV, L)                                                                        \
+  hipLaunchKernelGGL((heap_get_rows_kernel<T, VV, L>), grid, block, 0, st, pb, off, own, row, \
+                     static_cast<T*>(out), lds, ldo, n, F)
+#define DG_GET_ALL(VV)                                        \
+  switch (lpr) {                                              \
+    case 4: DG_GET(VV, 4); break;                             \
+    case 8: DG_GET(VV, 8); break;                             \
+    case 16: DG_GET(VV, 16); break;                           \
+    case 32: DG_GET(VV, 32); break;                           \
+    default: DG_GET(VV, 64); break;                           \
+  }
+  if (vec) { DG_GET_ALL(V) } else { DG_GET_ALL(1) }
+#undef DG_GET_ALL
+#undef DG_GET
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_put(const uint64_t* pb, int64_t off, const int64_t* rp, const int64_t* rd,
+                      const void* src, int64_t lds, int64_t ldd, int64_t n, int F, hipStream_t st) {
+  dim3 block(256), grid(static_cast<unsigned>(cap_blocks((n + 15) / 16, 256 * 16)));
+  constexpr int V = 16 / sizeof(T);
+  const bool vec = F % V == 0 && lds % V == 0 && ldd % V == 0;
+  const int lpr = pick_lpr(vec ? F / V : F);
+#define DG_PUT(VV, L)                                                                       \
+  hipLaunchKernelGGL((heap_put_rows_kernel<T, VV, L>), grid, block, 0, st, pb, off, rp, rd, \
+                     static_cast<const T*>(src), lds, ldd, n, F)
+#define DG_PUT_ALL(VV)                                        \
+  switch (lpr) {                                              \
+    case 4: DG_PUT(VV, 4); break;                             \
+    case 8: DG_PUT(VV, 8); break;                             \
+    case 16: DG_PUT(VV, 16); break;                           \
+    case 32: DG_PUT(VV, 32); break;                           \
+    default: DG_PUT(VV, 64); break;                           \
+  }
+  if (vec) { DG_PUT_ALL(V) } else { DG_PUT_ALL(1) }
+#undef DG_PUT_ALL
+#undef DG_PUT
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t heap_get_rows(DType dt, const uint64_t* peer_base, int64_t base_off,
+                         const int64_t* owner, const int64_t* row, void* out, int64_t ld_src,
+                         int64_t ld_out, int64_t n, int F, hipStream_t st) {
+  if (n <= 0 || F <= 0) return hipSuccess;
+  if (dt == DType::F32)
+    return launch_get<float>(peer_base, base_off, owner, row, out, ld_src, ld_out, n, F, st);
+  return launch_get<uint16_t>(peer_base, base_off, owner, row, out, ld_src, ld_out, n, F, st);
+}
+
+hipError_t heap_put_rows(DType dt, const uint64_t* peer_base, int64_t dst_off,
+                         const int64_t* row_peer, const int64_t* row_dst, const void* src,
+                         int64_t ld_src, int64_t ld_dst, int64_t n, int F, hipStream_t st) {
+  if (n <= 0 || F <= 0) return hipSuccess;
+  if (dt == DType::F32)
+    return launch_put<float>(peer_base, dst_off, row_peer, row_dst, src, ld_src, ld_dst, n, F, st);
+  return launch_put<uint16_t>(peer_base, dst_off, row_peer, row_dst, src, ld_src, ld_dst, n, F,
+                              st);
+}
+
+}  // namespace dgraph

@@ -10,10 +10,15 @@ what the interior/boundary overlap in :mod:`dgraph_amd.parallel.dist_graph` buil
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Sequence
 
 import torch
 import torch.distributed as dist
+
+# "torch": ProcessGroupNCCL (RCCL through torch.distributed); "native": the C++ RCCL
+# plan executor (comm/rccl_exec.py). Both are RCCL over xGMI; GPU tensors only.
+A2A_IMPL = os.environ.get("DGRAPH_A2A_IMPL", "torch")
 
 
 def offsets_to_splits(offsets) -> List[int]:
@@ -75,10 +80,13 @@ class AllToAllV:
             if self.total_send:
                 out.copy_(send)
             return (out, _Done()) if async_op else out
-        if self.total_send == 0 and self.total_recv == 0:
-            # everyone must still enter the collective
-            pass
         send_c = send.contiguous()
+        if A2A_IMPL == "native" and send_c.is_cuda:
+            from .rccl_exec import RCCLExecutor
+
+            work = RCCLExecutor.for_group(self.group).alltoallv(
+                [send_c], [out], self.send_splits, self.recv_splits, async_op=async_op)
+            return (out, work) if async_op else out
         work = dist.all_to_all_single(
             out, send_c,
             output_split_sizes=self.recv_splits,

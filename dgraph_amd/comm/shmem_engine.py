@@ -3,10 +3,10 @@
 Counterpart of the reference's ``NVSHMEMBackendEngine`` + ``torch_nvshmem_p2p``
 (nvshmem/NVSHMEMBackendEngine.py:163-315, csrc/torch_nvshmem_p2p.cu:32-376).
 rocSHMEM is not installed in this image, so the symmetric heap is the native HIP-IPC
-heap in ``csrc/comm/symmetric_heap.hip`` (:class:`dgraph_amd.comm.symheap.SymmetricHeap`):
+heap in ``csrc/comm/symheap.hip`` (:class:`dgraph_amd.comm.symheap.SymmetricHeap`):
 every rank maps every peer's heap over xGMI, remote rows are read with wave64 16-byte
 peer loads (the K15 remote get) and written with peer stores at ``remote_offsets`` (put),
-completion is a device-side flag barrier. Sizes are agreed as the max over ranks
+completion is a stream drain plus a group barrier. Sizes are agreed as the max over ranks
 (fixing the reference's mismatched collective ``nvshmem_malloc`` sizes, D4).
 
 When the heap cannot be used (host tensors, a single process spanning several nodes, or
