@@ -218,6 +218,97 @@ at::Tensor col_sum_op(const at::Tensor& g) {
   return partial.sum(0);
 }
 
+// mode 0 (agg): out[r] = sum_c relu(rowterm[r] + gat[c]); mode 1 (cnt): out[r] = rowmul[r] *
+// #{c : rowterm[r] + gat[c] > 0}; mode 2 (tgrad): out[r] = sum_c gat2[c] * [rowterm[r]+gat[c]>0]
+void pair_relu_op(const at::Tensor& rowptr, const at::Tensor& col, int64_t mode,
+                  const at::Tensor& rowterm, const at::Tensor& gat,
+                  const c10::optional<at::Tensor>& gat2, const c10::optional<at::Tensor>& rowmul,
+                  const at::Tensor& out) {
+  check_dev(rowterm, rowterm, "rowterm");
+  for (const at::Tensor* t : {&rowptr, &col, &gat, &out}) check_dev(*t, rowterm, "operand");
+  check_rows(rowterm, "rowterm");
+  check_rows(gat, "gat");
+  check_rows(out, "out");
+  TORCH_CHECK(mode >= 0 && mode <= 2, "pair_relu: mode must be 0, 1 or 2");
+  TORCH_CHECK(rowptr.scalar_type() == at::kLong && rowptr.is_contiguous() && col.is_contiguous(),
+              "rowptr must be contiguous int64, col contiguous");
+  const int64_t nrows = rowptr.numel() - 1;
+  const int64_t F = out.size(1);
+  TORCH_CHECK(rowterm.size(0) >= nrows && out.size(0) >= nrows && rowterm.size(1) == F &&
+                  gat.size(1) == F,
+              "pair_relu: shape mismatch");
+  TORCH_CHECK(rowterm.scalar_type() == gat.scalar_type() &&
+                  out.scalar_type() == gat.scalar_type(),
+              "pair_relu: dtype mismatch");
+  const void* g2 = nullptr;
+  int64_t ldg2 = 0;
+  if (mode == 2) {
+    TORCH_CHECK(gat2.has_value() && gat2->defined(), "pair_relu mode 2 needs gat2");
+    check_dev(*gat2, rowterm, "gat2");
+    check_rows(*gat2, "gat2");
+    TORCH_CHECK(gat2->size(1) == F && gat2->scalar_type() == gat.scalar_type(), "gat2 mismatch");
+    g2 = gat2->data_ptr();
+    ldg2 = gat2->stride(0);
+  }
+  const void* m = nullptr;
+  int64_t ldm = 0;
+  if (mode == 1) {
+    TORCH_CHECK(rowmul.has_value() && rowmul->defined(), "pair_relu mode 1 needs rowmul");
+    check_dev(*rowmul, rowterm, "rowmul");
+    check_rows(*rowmul, "rowmul");
+    TORCH_CHECK(rowmul->size(1) == F && rowmul->size(0) >= nrows &&
+                    rowmul->scalar_type() == gat.scalar_type(),
+                "rowmul mismatch");
+    m = rowmul->data_ptr();
+    ldm = rowmul->stride(0);
+  }
+  c10::DeviceGuard g(out.device());
+  DG_HIP_CHECK(pair_relu(dtype_of(out), itype_of(col), static_cast<int>(mode),
+                         rowptr.data_ptr<int64_t>(), col.data_ptr(), rowterm.data_ptr(),
+                         rowterm.stride(0), gat.data_ptr(), gat.stride(0), g2, ldg2, m, ldm,
+                         out.data_ptr(), out.stride(0), nrows, static_cast<int>(F),
+                         cur_stream(out)));
+}
+
+// out[e] = act(Y[e] + P[src[e]] + Q[dst[e]]) ; with gin: out[e] = gin[e] * act'(...)
+void gather_add_act_op(const c10::optional<at::Tensor>& Y, const c10::optional<at::Tensor>& P,
+                       const c10::optional<at::Tensor>& src, const c10::optional<at::Tensor>& Q,
+                       const c10::optional<at::Tensor>& dst, const c10::optional<at::Tensor>& gin,
+                       const at::Tensor& out, int64_t act) {
+  check_dev(out, out, "out");
+  check_rows(out, "out");
+  TORCH_CHECK(act >= 0 && act <= 2, "act must be 0 (none), 1 (relu) or 2 (silu)");
+  const int64_t E = out.size(0), F = out.size(1);
+  auto opt_rows = [&](const c10::optional<at::Tensor>& t, const char* name, bool per_edge,
+                      int64_t& ld) -> const void* {
+    if (!t.has_value() || !t->defined()) return nullptr;
+    check_dev(*t, out, name);
+    check_rows(*t, name);
+    TORCH_CHECK(t->size(1) == F && t->scalar_type() == out.scalar_type(), name, " mismatch");
+    if (per_edge) TORCH_CHECK(t->size(0) >= E, name, " has too few rows");
+    ld = t->stride(0);
+    return t->data_ptr();
+  };
+  auto opt_idx = [&](const c10::optional<at::Tensor>& t, const char* name) -> const int64_t* {
+    TORCH_CHECK(t.has_value() && t->defined(), name, " index required");
+    check_dev(*t, out, name);
+    TORCH_CHECK(t->scalar_type() == at::kLong && t->is_contiguous() && t->numel() >= E, name,
+                " must be contiguous int64 with E entries");
+    return t->data_ptr<int64_t>();
+  };
+  int64_t ldy = 0, ldp = 0, ldq = 0, ldg = 0;
+  const void* y = opt_rows(Y, "Y", true, ldy);
+  const void* p = opt_rows(P, "P", false, ldp);
+  const void* q = opt_rows(Q, "Q", false, ldq);
+  const void* gi = opt_rows(gin, "gin", true, ldg);
+  const int64_t* sp = p ? opt_idx(src, "src") : nullptr;
+  const int64_t* dp = q ? opt_idx(dst, "dst") : nullptr;
+  c10::DeviceGuard g(out.device());
+  DG_HIP_CHECK(gather_add_act(dtype_of(out), gi != nullptr, y, ldy, p, ldp, sp, q, ldq, dp, gi,
+                              ldg, out.data_ptr(), out.stride(0), E, static_cast<int>(F),
+                              static_cast<int>(act), cur_stream(out)));
+}
+
 }  // namespace
 }  // namespace dgraph
 
@@ -230,6 +321,10 @@ TORCH_LIBRARY(dgraph_amd, m) {
   m.def("bias_relu_pack(Tensor(a!) y, Tensor? bias, Tensor(b!)? bits, bool relu) -> ()");
   m.def("relu_mask_bwd(Tensor(a!) g, Tensor bits) -> ()");
   m.def("col_sum(Tensor g) -> Tensor");
+  m.def("pair_relu(Tensor rowptr, Tensor col, int mode, Tensor rowterm, Tensor gat, Tensor? gat2, "
+        "Tensor? rowmul, Tensor(a!) out) -> ()");
+  m.def("gather_add_act(Tensor? Y, Tensor? P, Tensor? src, Tensor? Q, Tensor? dst, Tensor? gin, "
+        "Tensor(a!) out, int act) -> ()");
   m.def(
       "spmm(Tensor rowptr, Tensor col, Tensor? edge_weight, Tensor? col_scale, "
       "Tensor? row_scale, Tensor x, Tensor(a!) out, int heads, int head_dim, float beta) -> ()");
@@ -249,4 +344,6 @@ TORCH_LIBRARY_IMPL(dgraph_amd, CUDA, m) {
   m.impl("bias_relu_pack", &dgraph::bias_relu_pack_op);
   m.impl("relu_mask_bwd", &dgraph::relu_mask_bwd_op);
   m.impl("col_sum", &dgraph::col_sum_op);
+  m.impl("pair_relu", &dgraph::pair_relu_op);
+  m.impl("gather_add_act", &dgraph::gather_add_act_op);
 }

@@ -71,4 +71,19 @@ hipError_t relu_mask_bwd(DType dt, void* g, const uint32_t* bits, int64_t numel,
 hipError_t col_sum_partial(DType dt, const void* g, int64_t ld, int64_t L, int F,
                            float* partial, int nblocks, hipStream_t stream);
 
+// ---------------------------------------------------------------------------
+// Fused edge-MLP kernels (edge_fused.hip, K-new-6). mode 0: out[r] = sum relu(R[r]+X[c]);
+// mode 1: out[r] = M[r] * #{c : R[r]+X[c] > 0}; mode 2: out[r] = sum X2[c]*[R[r]+X[c] > 0].
+// gather_add_act: out[e] = act(Y[e] + P[src[e]] + Q[dst[e]]) (any of Y/P/Q null), act
+// 0 none / 1 relu / 2 silu; bwd: out[e] = gin[e] * act'(same pre-activation).
+// ---------------------------------------------------------------------------
+hipError_t pair_relu(DType dt, IType it, int mode, const int64_t* rowptr, const void* col,
+                     const void* rowterm, int64_t ldr, const void* gat, int64_t ldg,
+                     const void* gat2, int64_t ldg2, const void* rowmul, int64_t ldm, void* out,
+                     int64_t ldo, int64_t nrows, int F, hipStream_t st);
+hipError_t gather_add_act(DType dt, bool bwd, const void* Y, int64_t ldy, const void* P,
+                          int64_t ldp, const int64_t* src, const void* Q, int64_t ldq,
+                          const int64_t* dst, const void* gin, int64_t ldgi, void* out,
+                          int64_t ldo, int64_t E, int F, int act, hipStream_t st);
+
 }  // namespace dgraph

@@ -145,3 +145,35 @@ def relu_mask_bwd(g: torch.Tensor, bits: torch.Tensor) -> None:
         _native.ops().relu_mask_bwd(g, bits)
         return
     _ref.relu_mask_bwd(g, bits)
+
+
+def pair_relu(rowptr: torch.Tensor, col: torch.Tensor, mode: int, rowterm: torch.Tensor,
+              gat: torch.Tensor, gat2: Optional[torch.Tensor] = None,
+              rowmul: Optional[torch.Tensor] = None,
+              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Fused edge-MLP aggregation (edge_fused.hip). mode 0: ``sum_c relu(R[r]+X[c])``;
+    1: ``M[r] * #{R[r]+X[c] > 0}``; 2: ``sum_c X2[c] [R[r]+X[c] > 0]``."""
+    R = rowptr.numel() - 1
+    if out is None:
+        out = torch.empty(R, gat.shape[1], dtype=gat.dtype, device=gat.device)
+    if _native_ok(gat):
+        _native.ops().pair_relu(rowptr, col, int(mode), rowterm, gat, gat2, rowmul, out)
+        return out
+    return _ref.pair_relu(rowptr, col, mode, rowterm, gat, gat2, rowmul, out)
+
+
+ACT_IDS = {None: 0, "none": 0, "identity": 0, "relu": 1, "silu": 2}
+
+
+def gather_add_act(E: int, F: int, *, Y=None, P=None, src=None, Q=None, dst=None, gin=None,
+                   act="none", out: Optional[torch.Tensor] = None,
+                   dtype=None, device=None) -> torch.Tensor:
+    """``out[e] = act(Y[e] + P[src[e]] + Q[dst[e]])``; with ``gin``: ``gin[e] * act'(...)``."""
+    ref = next(t for t in (Y, P, Q, gin, out) if t is not None)
+    if out is None:
+        out = torch.empty(E, F, dtype=dtype or ref.dtype, device=device or ref.device)
+    a = ACT_IDS[act]
+    if _native_ok(out):
+        _native.ops().gather_add_act(Y, P, src, Q, dst, gin, out, a)
+        return out
+    return _ref.gather_add_act(Y, P, src, Q, dst, gin, out, a)

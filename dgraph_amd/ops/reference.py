@@ -152,3 +152,59 @@ def relu_mask_bwd(g: torch.Tensor, bits: torch.Tensor) -> None:
 
 def col_sum(g: torch.Tensor) -> torch.Tensor:
     return g.float().sum(0)
+
+
+def pair_relu(rowptr, col, mode: int, rowterm, gat, gat2=None, rowmul=None, out=None):
+    """CPU reference of the fused edge-MLP aggregation (csrc/kernels/edge_fused.hip)."""
+    cdt = torch.float64 if gat.dtype == torch.float64 else torch.float32
+    R = rowptr.numel() - 1
+    rows = _row_ids(rowptr)
+    c = col.long()
+    pre = rowterm.to(cdt)[rows] + gat.to(cdt)[c]
+    if mode == 0:
+        val = pre.clamp_min(0)
+    elif mode == 1:
+        val = (pre > 0).to(cdt)
+    else:
+        val = torch.where(pre > 0, gat2.to(cdt)[c], torch.zeros((), dtype=cdt))
+    acc = torch.zeros(R, gat.shape[1], dtype=cdt).index_add_(0, rows, val)
+    if mode == 1:
+        acc = acc * rowmul.to(cdt)[:R]
+    if out is None:
+        return acc.to(gat.dtype)
+    out[:R].copy_(acc)
+    return out
+
+
+def _act(x, act: int):
+    if act == 1:
+        return x.clamp_min(0)
+    if act == 2:
+        return x * torch.sigmoid(x)
+    return x
+
+
+def _act_grad(x, act: int):
+    if act == 1:
+        return (x > 0).to(x.dtype)
+    if act == 2:
+        s = torch.sigmoid(x)
+        return s * (1 + x * (1 - s))
+    return torch.ones_like(x)
+
+
+def gather_add_act(Y, P, src, Q, dst, gin, out, act: int):
+    cdt = torch.float64 if out.dtype == torch.float64 else torch.float32
+    E, F = out.shape
+    pre = torch.zeros(E, F, dtype=cdt)
+    if Y is not None:
+        pre += Y[:E].to(cdt)
+    if P is not None:
+        pre += P.to(cdt)[src[:E].long()]
+    if Q is not None:
+        pre += Q.to(cdt)[dst[:E].long()]
+    if gin is None:
+        out.copy_(_act(pre, act))
+    else:
+        out.copy_(gin[:E].to(cdt) * _act_grad(pre, act))
+    return out

@@ -142,3 +142,25 @@ class TimingReport:
                 for k, lst in TimingReport.resolve().items()}
         with open(path, "w") as f:
             json.dump(data, f)
+
+
+class region:
+    """``with region("name"):`` — a TimingReport region when TimingReport is initialised,
+    otherwise a no-op (so models can be instrumented unconditionally)."""
+
+    __slots__ = ("name", "on")
+
+    def __init__(self, name: str):
+        self.name = name
+        self.on = False
+
+    def __enter__(self):
+        self.on = TimingReport._is_initialized
+        if self.on:
+            TimingReport.start(self.name)
+        return self
+
+    def __exit__(self, exc_type, exc_val, exc_tb):
+        if self.on:
+            TimingReport.stop(self.name)
+        return False

@@ -229,3 +229,76 @@ def test_sage_stack_gpu_matches_cpu():
     torch.testing.assert_close(outs[DEV][0], outs["cpu"][0], atol=1e-3, rtol=1e-3)
     for a, b in zip(outs[DEV][1], outs["cpu"][1]):
         torch.testing.assert_close(a, b, atol=1e-3, rtol=1e-2)
+
+
+@pytest.mark.parametrize("F", [1, 5, 8, 16, 64, 100, 256])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("idx", [torch.int32, torch.int64])
+def test_pair_relu_modes(F, dtype, idx):
+    csr = _rand_csr(200, 333, 9, idx, DEV, skew=True, seed=F + 7)
+    P = torch.randn(200, F, device=DEV).to(dtype)
+    Q = torch.randn(333, F, device=DEV).to(dtype)
+    g = torch.randn(200, F, device=DEV).to(dtype)
+    rc = CSR(csr.rowptr.cpu(), csr.col.cpu(), 333)
+    for mode in (0, 1):
+        out = K.pair_relu(csr.rowptr, csr.col, mode, P, Q, rowmul=g if mode == 1 else None)
+        ref = R.pair_relu(rc.rowptr, rc.col, mode, P.cpu().float(), Q.cpu().float(),
+                          rowmul=g.cpu().float() if mode == 1 else None)
+        torch.testing.assert_close(out.cpu().float(), ref, **_tol(dtype))
+    t = CSR(csr.rowptr, csr.col, 333).transpose()
+    out = K.pair_relu(t.rowptr, t.col, 2, Q, P, gat2=g)
+    tc = CSR(t.rowptr.cpu(), t.col.cpu(), 200)
+    ref = R.pair_relu(tc.rowptr, tc.col, 2, Q.cpu().float(), P.cpu().float(),
+                      gat2=g.cpu().float())
+    torch.testing.assert_close(out.cpu().float(), ref, **_tol(dtype))
+
+
+@pytest.mark.parametrize("F", [3, 8, 64, 200])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("act", ["none", "relu", "silu"])
+def test_gather_add_act(F, dtype, act):
+    E, Vs, Vd = 3000, 150, 170
+    gen = torch.Generator().manual_seed(F)
+    Y = torch.randn(E, F, generator=gen).to(dtype)
+    P = torch.randn(Vs, F, generator=gen).to(dtype)
+    Q = torch.randn(Vd, F, generator=gen).to(dtype)
+    gin = torch.randn(E, F, generator=gen).to(dtype)
+    src = torch.randint(0, Vs, (E,), generator=gen)
+    dst = torch.randint(0, Vd, (E,), generator=gen)
+    d = lambda t: t.to(DEV)  # noqa: E731
+    for use_y, use_p, use_q in [(1, 1, 1), (0, 1, 1), (1, 0, 1), (1, 1, 0)]:
+        kw = dict(Y=Y if use_y else None, P=P if use_p else None, src=src if use_p else None,
+                  Q=Q if use_q else None, dst=dst if use_q else None)
+        kwd = {k: (None if v is None else d(v)) for k, v in kw.items()}
+        kwf = {k: (None if v is None else (v.float() if v.is_floating_point() else v))
+               for k, v in kw.items()}
+        out = K.gather_add_act(E, F, act=act, **kwd)
+        ref = K.gather_add_act(E, F, act=act, **kwf)
+        torch.testing.assert_close(out.cpu().float(), ref, **_tol(dtype))
+        outb = K.gather_add_act(E, F, act=act, gin=d(gin), **kwd)
+        refb = K.gather_add_act(E, F, act=act, gin=gin.float(), **kwf)
+        torch.testing.assert_close(outb.cpu().float(), refb, **_tol(dtype))
+
+
+def test_gcn_layer_gpu_matches_cpu():
+    from dgraph_amd.models.gcn import GraphConvLayer
+
+    torch.manual_seed(0)
+    L, T, E, C, H = 500, 700, 6000, 32, 64
+    g = torch.Generator().manual_seed(1)
+    edges = torch.stack([torch.randint(0, L, (E,), generator=g),
+                         torch.randint(0, T, (E,), generator=g)], 1)
+    x = torch.randn(T, C, generator=g)
+    layer = GraphConvLayer(2 * C, H)
+    out_c = layer(x.requires_grad_(True), edges, L)
+    w = torch.randn(out_c.shape, generator=g)
+    (out_c * w).sum().backward()
+    gx_c, gw_c = x.grad.clone(), layer.conv.weight.grad.clone()
+    layer.zero_grad()
+    lg = layer.to(DEV)
+    xg = x.detach().to(DEV).requires_grad_(True)
+    out_g = lg(xg, edges.to(DEV), L)
+    (out_g * w.to(DEV)).sum().backward()
+    torch.testing.assert_close(out_g.cpu(), out_c.detach(), atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(xg.grad.cpu(), gx_c, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(lg.conv.weight.grad.cpu(), gw_c, atol=1e-3, rtol=1e-4)
