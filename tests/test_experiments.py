@@ -1,0 +1,38 @@
+"""End-to-end trainer runs on CPU/gloo (synthetic data when ogb is absent): the OGB GCN
+experiment at W=1 and W=2 gives the same loss trajectory and writes the reference's log
+files."""
+import os
+
+import numpy as np
+import pytest
+
+
+def _ogb_gcn(rank, world, log_dir, out_path):
+    import torch
+
+    from dgraph_amd import Communicator
+    from dgraph_amd.experiments import ogb_gcn
+    from dgraph_amd.utils.timing import TimingReport
+
+    torch.set_num_threads(2)
+    tr, vl, va = ogb_gcn.main(backend="nccl", dataset="arxiv", epochs=4, lr=1e-2,
+                              hidden_dims=32, log_dir=log_dir, synthetic_scale=0.01)
+    if rank == 0:
+        np.save(out_path, tr)
+    TimingReport.reset()
+    Communicator.instance().destroy()
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_ogb_gcn_trainer(ranks, tmp_path, world):
+    ranks(_ogb_gcn, world, str(tmp_path / "logs"), str(tmp_path / "loss.npy"))
+    tr = np.load(tmp_path / "loss.npy")
+    assert tr.shape == (1, 4) and np.isfinite(tr).all() and tr[0, -1] < tr[0, 0]
+    for k in ("training_loss", "validation_accuracy", "test_results", "runtime_experiment"):
+        assert os.path.exists(tmp_path / "logs" / f"arxiv_world{world}_run0_{k}.log")
+    assert os.path.exists(tmp_path / "logs" / f"arxiv_timing_report_world{world}.json")
+    ref = tmp_path.parent / f"gcn_loss_w{world}.npy"
+    np.save(ref, tr)
+    other = tmp_path.parent / f"gcn_loss_w{3 - world}.npy"
+    if other.exists():  # W=1 and W=2 train the same model on the same data
+        np.testing.assert_allclose(tr, np.load(other), rtol=1e-4, atol=1e-5)
