@@ -277,7 +277,7 @@ void gather_add_act_op(const c10::optional<at::Tensor>& Y, const c10::optional<a
                        const at::Tensor& out, int64_t act) {
   check_dev(out, out, "out");
   check_rows(out, "out");
-  TORCH_CHECK(act >= 0 && act <= 2, "act must be 0 (none), 1 (relu) or 2 (silu)");
+  TORCH_CHECK(act >= 0 && act <= 3, "act must be 0 (none), 1 (relu), 2 (silu), 3 (leaky 0.2)");
   const int64_t E = out.size(0), F = out.size(1);
   auto opt_rows = [&](const c10::optional<at::Tensor>& t, const char* name, bool per_edge,
                       int64_t& ld) -> const void* {

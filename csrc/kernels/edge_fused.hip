@@ -15,7 +15,7 @@
 //   pair_relu_tgrad (transposed CSR: row j, neighbours i)
 //       dQ[j]  = sum_{i : j in N(i)} g[i] * [P[i] + Q[j] > 0]          (backward, dQ)
 //   gather_add_act  (edge-parallel, for MLPs with more layers)
-//       h[e]   = act(Y[e] + P[src[e]] + Q[dst[e]])          act in {none, relu, silu}
+//       h[e]   = act(Y[e] + P[src[e]] + Q[dst[e]])  act in {none, relu, silu, leaky 0.2}
 //   gather_add_act_bwd
 //       d[e]   = g[e] * act'(Y[e] + P[src[e]] + Q[dst[e]])  (pre-activation recomputed)
 //
@@ -122,11 +122,13 @@ __global__ __launch_bounds__(256) void pair_relu_kernel(
 
 __device__ __forceinline__ float act_fwd(float x, int act) {
   if (act == 1) return fmaxf(x, 0.f);
+  if (act == 3) return x > 0.f ? x : 0.2f * x;
   if (act == 2) return x / (1.f + __expf(-x));
   return x;
 }
 __device__ __forceinline__ float act_grad(float x, int act) {
   if (act == 1) return x > 0.f ? 1.f : 0.f;
+  if (act == 3) return x > 0.f ? 1.f : 0.2f;
   if (act == 2) {
     const float s = 1.f / (1.f + __expf(-x));
     return s * (1.f + x * (1.f - s));

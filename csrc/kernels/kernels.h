@@ -75,7 +75,7 @@ hipError_t col_sum_partial(DType dt, const void* g, int64_t ld, int64_t L, int F
 // Fused edge-MLP kernels (edge_fused.hip, K-new-6). mode 0: out[r] = sum relu(R[r]+X[c]);
 // mode 1: out[r] = M[r] * #{c : R[r]+X[c] > 0}; mode 2: out[r] = sum X2[c]*[R[r]+X[c] > 0].
 // gather_add_act: out[e] = act(Y[e] + P[src[e]] + Q[dst[e]]) (any of Y/P/Q null), act
-// 0 none / 1 relu / 2 silu; bwd: out[e] = gin[e] * act'(same pre-activation).
+// 0 none / 1 relu / 2 silu / 3 leaky-relu(0.2); bwd: out[e] = gin[e] * act'(same pre-activation).
 // ---------------------------------------------------------------------------
 hipError_t pair_relu(DType dt, IType it, int mode, const int64_t* rowptr, const void* col,
                      const void* rowterm, int64_t ldr, const void* gat, int64_t ldg,

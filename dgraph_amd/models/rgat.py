@@ -1,0 +1,222 @@
+"""Graph attention for heterogeneous graphs (experiments/OGB-LSC/RGAT.py:44-382).
+
+``CommAwareGAT`` computes, for every destination vertex ``i`` of one relation,
+``out_i = sum_j alpha_ij h_j (+ W_res x_i) (+ b)`` with ``h = W x`` and
+``alpha_ij = softmax_j(leaky_relu(a . [h_i || h_j] + c))``.
+
+MI355X formulation (``_forward_graph``, used with a :class:`RelationGraph`):
+
+* the attention logit is split over the concatenation, ``a . [h_i || h_j] =
+  s_dst[i] + s_src[j]`` — two vertex-level reductions instead of an ``E x 2F`` concat and
+  an ``E``-row GEMV;
+* ONE halo exchange per relation moves ``[h_j || s_src_j]`` rows of remote sources;
+* per-edge work is three native kernels: logits (``gather_add_act``, leaky-ReLU), a
+  max-subtracted edge softmax over each destination's CSR segment (the reference's
+  ``exp`` had no max subtraction, RGAT.py:154) and the edge-weighted multi-head SpMM;
+  no atomics, no per-edge feature tensors.
+
+``heads`` splits the channels into ``heads`` attention heads (the reference accepted and
+ignored it). The reference's plan-based (G2, ``NCCLEdgeConditionedGraphCommPlan``) and
+index-based (G1 COO) forwards are kept for API parity.
+
+``CommAwareRGAT`` runs ALL relations of every layer (the reference broke out after the
+first relation, RGAT.py:357-358; ``relations="first"`` restores that behaviour).
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from ..ops.aggregate import aggregate, edge_softmax
+from ..ops.edge_mlp import edge_pre_activation
+from .norm import DistributedBatchNorm1D
+
+
+def _world(comm) -> int:
+    if comm is not None:
+        return comm.get_world_size()
+    return dist.get_world_size() if dist.is_initialized() else 1
+
+
+class ConvLayer(nn.Module):
+    def __init__(self, in_channels, out_channels):
+        super().__init__()
+        self.conv = nn.Linear(in_channels, out_channels)
+        self.act = nn.ReLU(inplace=True)
+
+    def forward(self, x):
+        return self.act(self.conv(x))
+
+
+class CommAwareGAT(nn.Module):
+    def __init__(self, in_channels: int, out_channels: int, comm=None, heads: int = 1,
+                 bias: bool = True, residual: bool = False, hetero: bool = False):
+        super().__init__()
+        if out_channels % heads:
+            raise ValueError("out_channels must be divisible by heads")
+        self.conv1 = nn.Linear(in_channels, out_channels, bias=False)
+        self.comm = comm
+        self.project_message = nn.Linear(2 * out_channels, heads)
+        self.leaky_relu = nn.LeakyReLU(0.2, inplace=False)
+        self.residual = residual
+        self.heads = heads
+        self.hetero = hetero
+        self.out_channels = out_channels
+        if residual:
+            self.res_net = nn.Linear(in_channels, out_channels, bias=False)
+        if bias:
+            self.bias = nn.Parameter(torch.zeros(out_channels))
+        else:
+            self.register_parameter("bias", None)
+        self._halo = None
+
+    # ------------------------------------------------------------------ dispatch
+    def forward(self, x, comm_plan=None, *, x_j=None, graph=None, edge_index=None,
+                rank_mapping=None, src_gather_cache=None, dest_gather_cache=None,
+                dest_scatter_cache=None):
+        from ..data.hetero import RelationGraph
+
+        if isinstance(comm_plan, RelationGraph):
+            graph, comm_plan = comm_plan, None
+        if graph is not None:
+            return self._forward_graph(x, graph, x_j)
+        if comm_plan is not None:
+            return self._forward_comm_plan(x, comm_plan, x_j=x_j)
+        return self._forward_coo(x, edge_index, rank_mapping, x_j, src_gather_cache,
+                                 dest_gather_cache, dest_scatter_cache)
+
+    def _head_scores(self, h: torch.Tensor, part: int) -> torch.Tensor:
+        """``s[:, k] = h[:, head k] . a_k`` with ``a_k`` the head-k block of the
+        destination (part 0) or source (part 1) half of ``project_message``."""
+        H, C = self.heads, self.out_channels
+        D = C // H
+        W = self.project_message.weight[:, part * C:(part + 1) * C]  # [H, C]
+        if H == 1:
+            return h @ W.t()
+        blocks = torch.stack([W[k, k * D:(k + 1) * D] for k in range(H)])  # [H, D]
+        return (h.view(-1, H, D) * blocks.to(h.dtype)).sum(-1)
+
+    def _apply_res_and_bias(self, out, x):
+        if self.residual:
+            out = out + self.res_net(x)
+        if self.bias is not None:
+            out = out + self.bias
+        return out
+
+    # ------------------------------------------------------------------ fast path
+    def _forward_graph(self, x, graph, x_j=None):
+        C, H = self.out_channels, self.heads
+        h = self.conv1(x)
+        hj = self.conv1(x_j) if (self.hetero and x_j is not None) else h
+        s_dst = self._head_scores(h, 0) + self.project_message.bias.to(h.dtype)
+        s_src = self._head_scores(hj, 1)
+        payload = torch.cat([hj, s_src.to(hj.dtype)], dim=1)
+        if _world(self.comm) > 1:  # collective on every rank of the relation's group
+            from ..parallel.halo import HaloExchange
+
+            if self._halo is None:
+                self._halo = HaloExchange(self.comm)
+            halo = self._halo(payload, graph.pattern)
+            payload = torch.cat([payload, halo], dim=0)
+        hj_all, ssrc_all = payload[:, :C], payload[:, C:]
+        logits = edge_pre_activation(None, s_dst.to(payload.dtype), ssrc_all,
+                                     graph.row_map(), graph.col_map(), act="leaky_relu")
+        # softmax statistics in fp32 (fp64 inputs stay fp64)
+        alpha = edge_softmax(logits if logits.dtype == torch.float64 else logits.float(),
+                             graph.csr)
+        out = aggregate(hj_all, graph.csr, edge_weight=alpha, heads=H)
+        return self._apply_res_and_bias(out, x)
+
+    # ------------------------------------------------------------------ reference paths
+    def _process_messages(self, h, h_j):
+        scores = self.leaky_relu(self.project_message(torch.cat([h, h_j], dim=-1)))
+        return torch.exp(scores)
+
+    def _calc_attention_messages(self, neighbor_features, numerator, denominator):
+        alpha = numerator / (denominator + 1e-16)
+        H = self.heads
+        nf = neighbor_features.reshape(*neighbor_features.shape[:-1], H, -1)
+        return (nf * alpha.unsqueeze(-1)).reshape(neighbor_features.shape)
+
+    def _forward_comm_plan(self, x, comm_plan, x_j=None):
+        """G2 plan path (RGAT.py:171-201): per-edge tensors through plan gathers."""
+        h = self.conv1(x)
+        src_plan = comm_plan.source_graph_plan
+        if self.hetero:
+            h_j = self.conv1(x_j)
+            dst_plan = comm_plan.dest_graph_plan
+        else:
+            h_j, dst_plan = h, src_plan
+        h_i = self.comm.gather(h, comm_plan=dst_plan)
+        h_j = self.comm.gather(h_j, comm_plan=src_plan)
+        num = self._process_messages(h_i, h_j)
+        den = self.comm.gather(self.comm.scatter(num, comm_plan=dst_plan), comm_plan=dst_plan)
+        out = self.comm.scatter(self._calc_attention_messages(h_j, num, den),
+                                comm_plan=dst_plan)
+        return self._apply_res_and_bias(out, x)
+
+    def _forward_coo(self, x, edge_index, rank_mapping, x_j=None, src_gather_cache=None,
+                     dest_gather_cache=None, dest_scatter_cache=None):
+        """G1 index path (RGAT.py:208-268)."""
+        h = self.conv1(x)
+        h_j = self.conv1(x_j) if self.hetero else h
+        src_idx, dst_idx = edge_index[:, 0, :], edge_index[:, 1, :]
+        src_rm = torch.cat([rank_mapping[0].unsqueeze(0), rank_mapping[0].unsqueeze(0)], 0)
+        dst_rm = torch.cat([rank_mapping[0].unsqueeze(0), rank_mapping[1].unsqueeze(0)], 0)
+        h_i = self.comm.gather(h, dst_idx, dst_rm, cache=dest_gather_cache)
+        h_j = self.comm.gather(h_j, src_idx, src_rm, cache=src_gather_cache)
+        num = self._process_messages(h_i, h_j)
+        den = self.comm.scatter(num, dst_idx, dst_rm, h.size(-2), cache=dest_scatter_cache)
+        den = self.comm.gather(den, src_idx, src_rm, cache=dest_gather_cache)
+        out = self.comm.scatter(self._calc_attention_messages(h_j, num, den), dst_idx, dst_rm,
+                                h.size(-2), cache=dest_scatter_cache)
+        return self._apply_res_and_bias(out, x)
+
+
+class CommAwareRGAT(nn.Module):
+    def __init__(self, in_channels, out_channels, hidden_channels, num_relations, num_layers,
+                 heads, comm=None, dropout: float = 0.5, relations: str = "all",
+                 num_node_types: int = 3, bn_group=None):
+        super().__init__()
+        self.num_layers, self.dropout, self.comm = num_layers, dropout, comm
+        self.num_relations = num_relations
+        self.relations = relations
+        self.layers = nn.ModuleList()
+        for i in range(num_layers):
+            cin = in_channels if i == 0 else hidden_channels
+            self.layers.append(nn.ModuleList([
+                CommAwareGAT(cin, hidden_channels, heads=heads, bias=True, residual=True,
+                             comm=comm, hetero=True) for _ in range(num_relations)]))
+        self.bn_layers = nn.ModuleList([
+            DistributedBatchNorm1D(hidden_channels, recompute=True, group=bn_group)
+            for _ in range(num_layers)])
+        self.skip_layers = nn.ModuleList(
+            [nn.Linear(in_channels, hidden_channels)]
+            + [nn.Linear(hidden_channels, hidden_channels) for _ in range(num_layers - 1)])
+        self.num_node_types = num_node_types
+        self.mlp = nn.Sequential(
+            nn.Linear(hidden_channels, hidden_channels),
+            DistributedBatchNorm1D(hidden_channels, recompute=True, group=bn_group),
+            nn.ReLU(inplace=True),
+            nn.Dropout(dropout),
+            nn.Linear(hidden_channels, out_channels),
+        )
+
+    def forward(self, xs: List[torch.Tensor], edge_types, graphs) -> torch.Tensor:
+        assert len(edge_types) == len(graphs)
+        outs = list(xs)
+        for i in range(self.num_layers):
+            tmp = [self.skip_layers[i](o) for o in outs]
+            for j, (et, g) in enumerate(zip(edge_types, graphs)):
+                if self.relations == "first" and j > 0:
+                    break
+                s, d = et
+                tmp[d] = tmp[d] + self.layers[i][j](outs[d], g, x_j=outs[s])
+            outs = []
+            for t in tmp:
+                t = torch.relu(self.bn_layers[i](t))
+                outs.append(nn.functional.dropout(t, self.dropout, self.training))
+        return self.mlp(outs[0])

@@ -162,7 +162,7 @@ def pair_relu(rowptr: torch.Tensor, col: torch.Tensor, mode: int, rowterm: torch
     return _ref.pair_relu(rowptr, col, mode, rowterm, gat, gat2, rowmul, out)
 
 
-ACT_IDS = {None: 0, "none": 0, "identity": 0, "relu": 1, "silu": 2}
+ACT_IDS = {None: 0, "none": 0, "identity": 0, "relu": 1, "silu": 2, "leaky_relu": 3}
 
 
 def gather_add_act(E: int, F: int, *, Y=None, P=None, src=None, Q=None, dst=None, gin=None,

@@ -85,23 +85,26 @@ def masked_gather_rows(x, idx, mask, value, out):
 
 
 def edge_softmax_fwd(rowptr: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
-    s2 = s.float().reshape(s.shape[0], -1)
+    cdt = torch.float64 if s.dtype == torch.float64 else torch.float32
+    s2 = s.to(cdt).reshape(s.shape[0], -1)
     rows = _row_ids(rowptr)
     R = rowptr.numel() - 1
     H = s2.shape[1]
-    m = torch.full((R, H), float("-inf"), device=s.device)
+    m = torch.full((R, H), float("-inf"), device=s.device, dtype=cdt)
     m = m.scatter_reduce(0, rows.unsqueeze(1).expand(-1, H), s2, reduce="amax")
     e = torch.exp(s2 - m[rows])
-    den = torch.zeros(R, H, device=s.device).index_add_(0, rows, e)
+    den = torch.zeros(R, H, device=s.device, dtype=cdt).index_add_(0, rows, e)
     return (e / den[rows]).reshape(s.shape)
 
 
 def edge_softmax_bwd(rowptr: torch.Tensor, alpha: torch.Tensor, g: torch.Tensor) -> torch.Tensor:
-    a2 = alpha.float().reshape(alpha.shape[0], -1)
-    g2 = g.float().reshape(a2.shape)
+    cdt = torch.float64 if alpha.dtype == torch.float64 else torch.float32
+    a2 = alpha.to(cdt).reshape(alpha.shape[0], -1)
+    g2 = g.to(cdt).reshape(a2.shape)
     rows = _row_ids(rowptr)
     R = rowptr.numel() - 1
-    dot = torch.zeros(R, a2.shape[1], device=alpha.device).index_add_(0, rows, a2 * g2)
+    dot = torch.zeros(R, a2.shape[1], device=alpha.device, dtype=cdt).index_add_(0, rows,
+                                                                              a2 * g2)
     return (a2 * (g2 - dot[rows])).reshape(alpha.shape)
 
 
@@ -181,6 +184,8 @@ def _act(x, act: int):
         return x.clamp_min(0)
     if act == 2:
         return x * torch.sigmoid(x)
+    if act == 3:
+        return torch.where(x > 0, x, 0.2 * x)
     return x
 
 
@@ -190,6 +195,8 @@ def _act_grad(x, act: int):
     if act == 2:
         s = torch.sigmoid(x)
         return s * (1 + x * (1 - s))
+    if act == 3:
+        return torch.where(x > 0, torch.ones_like(x), torch.full_like(x, 0.2))
     return torch.ones_like(x)
 
 

@@ -28,8 +28,10 @@ class GradSync:
         ps = [p for p in self.params]
         numel = sum(p.numel() for p in ps)
         dev = ps[0].device
-        if self._flat is None or self._flat.numel() != numel or self._flat.device != dev:
-            self._flat = torch.empty(numel, dtype=torch.float32, device=dev)
+        fdt = torch.float64 if any(p.dtype == torch.float64 for p in ps) else torch.float32
+        if (self._flat is None or self._flat.numel() != numel or self._flat.device != dev
+                or self._flat.dtype != fdt):
+            self._flat = torch.empty(numel, dtype=fdt, device=dev)
         off = 0
         for p in ps:
             n = p.numel()
@@ -46,7 +48,7 @@ class GradSync:
             n = p.numel()
             v = self._flat[off:off + n].view_as(p)
             if p.grad is None:
-                p.grad = v.clone()
+                p.grad = v.to(p.dtype, copy=True)
             else:
                 p.grad.copy_(v)
             off += n
