@@ -1,0 +1,178 @@
+"""OGB-LSC (MAG240M-like) RGAT experiment (experiments/OGB-LSC/{main,Trainer,config}.py).
+
+Full-graph training of :class:`~dgraph_amd.models.rgat.CommAwareRGAT` on a heterogeneous
+paper/author/institution graph: Adam (lr 1e-4, weight decay 5e-4) with a StepLR schedule,
+cross-entropy summed over the local training papers and divided by the global target
+count, global train/val/test accuracy in ``evaluate``. Replicated weights are synchronised
+with one flat all-reduce (:class:`GradSync`) — unused relation parameters get zero
+gradients, so no ``find_unused_parameters`` machinery is needed. Differences from the
+reference: every relation is used (``relations="all"``), attention heads are real, the
+per-epoch ``empty_cache()`` + device sync is gone (the caching allocator keeps the
+steady-state buffers resident).
+
+CLI: ``python -m dgraph_amd.experiments.ogb_lsc --dataset synthetic --num_papers 32768``.
+"""
+from __future__ import annotations
+
+import argparse
+import time
+from dataclasses import dataclass
+
+import torch
+import torch.nn.functional as F
+
+from .. import Communicator
+from ..data.hetero import (DGraph_MAG240M_Dataset, SyntheticHeteroConfig,
+                           SyntheticHeterogeneousDataset)
+from ..models.norm import GetGlobalVal
+from ..models.rgat import CommAwareRGAT
+from ..parallel.grad_sync import GradSync
+from ..utils.metrics import print_on_rank_zero
+
+
+@dataclass
+class ModelConfig:
+    hidden_channels: int = 2
+    dropout: float = 0.5
+    num_layers: int = 2
+    heads: int = 1          # reference default 4 was unused; must divide hidden_channels
+    use_cache: bool = True
+    relations: str = "all"
+
+
+@dataclass
+class TrainingConfig:
+    epochs: int = 100
+    lr: float = 1e-4
+    lr_step_size: int = 25
+    lr_gamma: float = 0.25
+    weight_decay: float = 5e-4
+
+
+@dataclass
+class SyntheticDatasetConfig(SyntheticHeteroConfig):
+    num_papers: int = 2048 * 16
+    num_authors: int = 1024 * 16
+    num_institutions: int = 16 * 16
+    num_features: int = 16
+    num_classes: int = 153
+
+
+def _device() -> torch.device:
+    if torch.cuda.is_available():
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+class Trainer:
+    def __init__(self, dataset, comm, model_config: ModelConfig = None,
+                 training_config: TrainingConfig = None, device=None, seed: int = 0):
+        self.dataset = dataset
+        self.comm = comm
+        self.model_config = model_config or ModelConfig()
+        self.training_config = training_config or TrainingConfig()
+        self.device = device or _device()
+        mc, tc = self.model_config, self.training_config
+        torch.manual_seed(seed)
+        self.model = CommAwareRGAT(
+            in_channels=dataset.num_features, out_channels=dataset.num_classes,
+            hidden_channels=mc.hidden_channels, num_relations=dataset.num_relations,
+            num_layers=mc.num_layers, heads=mc.heads, comm=comm, dropout=mc.dropout,
+            relations=mc.relations, bn_group=comm.group).to(self.device)
+        self.sync = GradSync(self.model.parameters(), group=comm.group)
+        self.optimizer = torch.optim.Adam(self.model.parameters(), lr=tc.lr,
+                                          weight_decay=tc.weight_decay)
+        self.scheduler = torch.optim.lr_scheduler.StepLR(self.optimizer, tc.lr_step_size,
+                                                         tc.lr_gamma)
+        self.history = []
+
+    def prepare_data(self):
+        self.dataset = self.dataset.to(self.device)
+        return self
+
+    def _forward(self):
+        xs, ets, rels = self.dataset[0]
+        return self.model(xs, ets, rels)
+
+    def train(self, epochs: int = None) -> float:
+        self.model.train()
+        tm = self.dataset.get_mask("train").to(self.device)
+        target = self.dataset.get_target("train").to(self.device)
+        n_glob = GetGlobalVal(target.numel(), self.comm.group, self.device)
+        loss_val = 0.0
+        for epoch in range(1, (epochs or self.training_config.epochs) + 1):
+            t0 = time.perf_counter()
+            self.optimizer.zero_grad(set_to_none=True)
+            out = self._forward()
+            loss = F.cross_entropy(out[tm].float(), target, reduction="sum") / n_glob
+            loss.backward()
+            self.sync.all_reduce()
+            self.optimizer.step()
+            self.scheduler.step()
+            loss_val = GetGlobalVal(float(loss.detach()), self.comm.group, self.device)
+            ms = (time.perf_counter() - t0) * 1e3
+            self.history.append({"epoch": epoch, "loss": loss_val, "ms": ms})
+            print_on_rank_zero(f"Epoch {epoch:03d} | loss {loss_val:.4f} | {ms:.1f} ms")
+        return loss_val
+
+    @torch.no_grad()
+    def evaluate(self):
+        self.model.eval()
+        pred = self._forward().argmax(-1)
+        accs = []
+        for split in ("train", "val", "test"):
+            m = self.dataset.get_mask(split).to(self.device)
+            y = self.dataset.get_target(split).to(self.device)
+            correct = GetGlobalVal(int((pred[m] == y).sum()), self.comm.group, self.device)
+            total = GetGlobalVal(int(m.numel()), self.comm.group, self.device)
+            accs.append(correct / max(total, 1.0))
+        self.model.train()
+        return tuple(accs)
+
+
+def main(comm_type: str = "nccl", dataset: str = "synthetic", num_papers: int = 2048,
+         num_authors: int = 512, num_institutions: int = 16, num_features: int = 16,
+         num_classes: int = 153, epochs: int = 100, hidden_channels: int = 2,
+         num_layers: int = 2, heads: int = 1, dropout: float = 0.5, lr: float = 1e-4,
+         data_dir: str = "data/MAG240M", cache_dir: str = None):
+    if dataset not in ("synthetic", "mag240m"):
+        raise ValueError(f"Invalid dataset: {dataset}")
+    if comm_type not in ("nccl", "nvshmem", "rocshmem", "gloo", "mpi"):
+        raise ValueError(f"Invalid comm_type: {comm_type}")
+    comm = Communicator.init_process_group(comm_type)
+    if dataset == "synthetic":
+        cfg = SyntheticDatasetConfig(num_papers=num_papers, num_authors=num_authors,
+                                     num_institutions=num_institutions,
+                                     num_features=num_features, num_classes=num_classes)
+        ds = SyntheticHeterogeneousDataset(cfg, comm, cache_dir=cache_dir)
+    else:
+        ds = DGraph_MAG240M_Dataset(comm, data_dir=data_dir)
+    trainer = Trainer(ds, comm, ModelConfig(hidden_channels=hidden_channels,
+                                            num_layers=num_layers, heads=heads,
+                                            dropout=dropout),
+                      TrainingConfig(epochs=epochs, lr=lr))
+    trainer.prepare_data()
+    final = trainer.train()
+    accs = trainer.evaluate()
+    print_on_rank_zero(f"final loss {final:.4f} | acc train/val/test "
+                       f"{accs[0]:.4f}/{accs[1]:.4f}/{accs[2]:.4f}")
+    return trainer, final, accs
+
+
+def cli(argv=None):
+    p = argparse.ArgumentParser(description="RGAT on OGB-LSC-like heterogeneous graphs")
+    for name, typ, default in [("comm_type", str, "nccl"), ("dataset", str, "synthetic"),
+                               ("num_papers", int, 2048), ("num_authors", int, 512),
+                               ("num_institutions", int, 16), ("num_features", int, 16),
+                               ("num_classes", int, 153), ("epochs", int, 100),
+                               ("hidden_channels", int, 2), ("num_layers", int, 2),
+                               ("heads", int, 1), ("dropout", float, 0.5),
+                               ("lr", float, 1e-4), ("data_dir", str, "data/MAG240M"),
+                               ("cache_dir", str, None)]:
+        p.add_argument(f"--{name}", type=typ, default=default)
+    main(**vars(p.parse_args(argv)))
+    Communicator.instance().destroy()
+
+
+if __name__ == "__main__":
+    cli()

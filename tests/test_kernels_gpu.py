@@ -302,3 +302,34 @@ def test_gcn_layer_gpu_matches_cpu():
     torch.testing.assert_close(out_g.cpu(), out_c.detach(), atol=1e-4, rtol=1e-4)
     torch.testing.assert_close(xg.grad.cpu(), gx_c, atol=1e-4, rtol=1e-4)
     torch.testing.assert_close(lg.conv.weight.grad.cpu(), gw_c, atol=1e-3, rtol=1e-4)
+
+
+def test_gat_layer_gpu_matches_cpu():
+    from dgraph_amd.data.hetero import build_relation_graph, get_vertex_offsets
+    from dgraph_amd.models.rgat import CommAwareGAT
+
+    torch.manual_seed(0)
+    Ns, Nd, E, Cin, C = 900, 700, 9000, 24, 64
+    g = torch.Generator().manual_seed(3)
+    edges = torch.unique(torch.stack([torch.randint(0, Ns, (E,), generator=g),
+                                      torch.randint(0, Nd, (E,), generator=g)]), dim=1)
+    offs = {0: get_vertex_offsets(Nd, 1), 1: get_vertex_offsets(Ns, 1)}
+    rel = build_relation_graph(edges, 1, 0, offs, 0, 1)
+    layer = CommAwareGAT(Cin, C, heads=4, residual=True, hetero=True)
+    xd = torch.randn(Nd, Cin, generator=g)
+    xs = torch.randn(Ns, Cin, generator=g)
+    w = torch.randn(Nd, C, generator=g)
+    xdc, xsc = xd.clone().requires_grad_(True), xs.clone().requires_grad_(True)
+    out_c = layer(xdc, rel, x_j=xsc)
+    (out_c * w).sum().backward()
+    grads_c = [p.grad.clone() for p in layer.parameters()]
+    layer.zero_grad()
+    lg = layer.to(DEV)
+    rel = rel.to(DEV)
+    xdg, xsg = xd.to(DEV).requires_grad_(True), xs.to(DEV).requires_grad_(True)
+    out_g = lg(xdg, rel, x_j=xsg)
+    (out_g * w.to(DEV)).sum().backward()
+    torch.testing.assert_close(out_g.cpu(), out_c.detach(), atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(xsg.grad.cpu(), xsc.grad, atol=1e-4, rtol=1e-3)
+    for a, b in zip(lg.parameters(), grads_c):
+        torch.testing.assert_close(a.grad.cpu(), b, atol=1e-3, rtol=1e-3)
