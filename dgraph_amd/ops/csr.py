@@ -78,17 +78,28 @@ class CSR:
     def permute_edges(self, edge_values: torch.Tensor) -> torch.Tensor:
         return edge_values if self.perm is None else edge_values[self.perm]
 
-    def to(self, device) -> "CSR":
-        t = None if self._transpose is None else self._transpose.to(device)
+    def _moved(self, device) -> "CSR":
         return CSR(
             self.rowptr.to(device),
             self.col.to(device),
             self.num_cols,
             None if self.perm is None else self.perm.to(device),
             self.symmetric,
-            t,
+            None,
             None if self._inv_deg is None else self._inv_deg.to(device),
         )
+
+    def to(self, device) -> "CSR":
+        """Move to ``device``, keeping the cached transpose (and its back link)."""
+        new = self._moved(device)
+        t = self._transpose
+        if t is self:
+            new._transpose = new
+        elif t is not None:
+            nt = t._moved(device)
+            nt._transpose = new
+            new._transpose = nt
+        return new
 
     @staticmethod
     def from_coo(
