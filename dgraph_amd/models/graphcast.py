@@ -1,0 +1,313 @@
+"""GraphCast encoder-processor-decoder (experiments/GraphCast/{layers,model}.py).
+
+Layer structure and parameter names follow the reference (``MeshGraphMLP._model`` =
+Linear, SiLU, [Linear, SiLU]*, Linear, LayerNorm), so state dicts are interchangeable.
+The MI355X formulation of the hot blocks:
+
+* ``MeshEdgeBlock``: ``e' = MLP([x_src[s] || x_dst[d] || e]) + e``. The first Linear is
+  distributed over the concatenation: vertex-level GEMMs ``P = x_src W_s^T``,
+  ``Q = x_dst W_d^T`` plus the edge GEMM ``Y = e W_e^T + b``, fused with the gathers and the
+  SiLU in ONE edge kernel (``gather_add_act``; the pre-activation is recomputed in backward,
+  never stored). No ``E x 3F`` concatenation is ever built.
+* ``MeshNodeBlock``: ``x' = MLP([x || sum_{e -> x} e]) + x`` with the edge sum a
+  destination-sorted CSR segment reduction (deterministic, no atomics) and the first Linear
+  split over ``[x || agg]`` (no concat).
+* Distribution: each edge set lives with the rank that aggregates it (see
+  :mod:`dgraph_amd.data.graphcast_graph`), so the only communication is one halo exchange
+  of the non-aggregating endpoint's features per edge block, through the set's
+  :class:`CommunicationPattern` (RCCL all-to-all-v on GPUs).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Optional, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..ops.aggregate import scatter_sum
+from ..ops.csr import IndexMap
+from ..ops.edge_mlp import edge_pre_activation
+from ..utils.timing import region
+
+
+@dataclass
+class TrainingConfig:
+    """graphcast_config.py:17-30."""
+
+    lr: float = 1e-3
+    lr_step3: float = 3e-7
+    num_iters_step1: int = 1000
+    num_iters_step2: int = 299000
+    num_iters_step3: int = 11000
+    step_change_freq: int = 1000
+    save_freq: int = 1
+    grad_clip_norm: float = 32.0
+    val_freq: int = 5
+
+
+@dataclass
+class DataConfig:
+    latlon_res: Tuple[int, int] = (721, 1440)
+    num_samples_per_year_train: int = 4
+    num_channels_climate: int = 73
+    num_channels_static: int = 5
+    num_history: int = 0
+    use_cos_zenith: bool = True
+    dt: float = 6.0
+    start_year: int = 1980
+    use_time_of_year_index: bool = True
+    stride: int = 1
+
+
+@dataclass
+class ModelConfig:
+    processor_layers: int = 4
+    hidden_dim: int = 128
+    mesh_level: int = 6
+    multimesh: bool = True
+    input_grid_dim: int = 73
+    input_mesh_dim: int = 3
+    input_edge_dim: int = 4
+    output_grid_dim: int = 73
+
+
+@dataclass
+class Config:
+    training: TrainingConfig = field(default_factory=TrainingConfig)
+    data: DataConfig = field(default_factory=DataConfig)
+    model: ModelConfig = field(default_factory=ModelConfig)
+
+
+class MeshGraphMLP(nn.Module):
+    def __init__(self, input_dim: int, output_dim: int, hidden_dim: int = 512,
+                 hidden_layers: int = 1, activation_fn: Optional[nn.Module] = None,
+                 norm_type: Optional[str] = "LayerNorm"):
+        super().__init__()
+        self.input_dim, self.output_dim = input_dim, output_dim
+        act = activation_fn if activation_fn is not None else nn.SiLU()
+        layers = [nn.Linear(input_dim, hidden_dim), act]
+        for _ in range(hidden_layers - 1):
+            layers += [nn.Linear(hidden_dim, hidden_dim), act]
+        layers.append(nn.Linear(hidden_dim, output_dim))
+        if norm_type is not None:
+            layers.append(getattr(nn, norm_type)(output_dim))
+        self._model = nn.Sequential(*layers)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return self._model(x)
+
+    def tail(self, h: torch.Tensor) -> torch.Tensor:
+        """Everything after the first Linear + activation."""
+        for m in list(self._model)[2:]:
+            h = m(h)
+        return h
+
+    def first_act_name(self) -> str:
+        act = self._model[1]
+        if isinstance(act, nn.SiLU):
+            return "silu"
+        if isinstance(act, nn.ReLU):
+            return "relu"
+        raise NotImplementedError(f"fused first layer supports SiLU/ReLU, got {act}")
+
+
+class MeshEdgeBlock(nn.Module):
+    def __init__(self, input_src_node_dim: int, input_dst_node_dim: int, input_edge_dim: int,
+                 output_edge_dim: int, comm=None, hidden_dim: int = 512,
+                 num_hidden_layers: int = 1, aggregation_type: str = "sum"):
+        super().__init__()
+        assert aggregation_type == "sum", "Only sum aggregation is supported."
+        self.comm = comm
+        self.dims = (input_src_node_dim, input_dst_node_dim, input_edge_dim)
+        self.mesh_mlp = MeshGraphMLP(input_src_node_dim + input_dst_node_dim + input_edge_dim,
+                                     output_edge_dim, hidden_dim, num_hidden_layers)
+        self._maps: dict = {}
+
+    def _split_first(self):
+        lin = self.mesh_mlp._model[0]
+        a, b, _ = self.dims
+        W = lin.weight
+        return W[:, :a], W[:, a:a + b], W[:, a + b:], lin.bias
+
+    def fused(self, src_feats: torch.Tensor, dst_feats: torch.Tensor, edge_feats: torch.Tensor,
+              src_map: IndexMap, dst_map: IndexMap) -> torch.Tensor:
+        """Edge update with index maps over the rows of ``src_feats`` / ``dst_feats``."""
+        Ws, Wd, We, b = self._split_first()
+        P = F.linear(src_feats, Ws)
+        Q = F.linear(dst_feats, Wd)
+        Y = F.linear(edge_feats, We, b)
+        h = edge_pre_activation(Y, P, Q, src_map, dst_map, self.mesh_mlp.first_act_name())
+        return self.mesh_mlp.tail(h) + edge_feats
+
+    def forward(self, src_node_features, dst_node_features, edge_features, src_indices,
+                dst_indices, src_rank_mapping=None, dst_rank_mapping=None):
+        """Reference signature (single process, global indices)."""
+        key = (src_indices.data_ptr(), dst_indices.data_ptr(), src_indices.numel(),
+               src_node_features.shape[0], dst_node_features.shape[0])
+        maps = self._maps.get(key)
+        if maps is None:
+            maps = (IndexMap(src_indices.reshape(-1).long(), src_node_features.shape[0]),
+                    IndexMap(dst_indices.reshape(-1).long(), dst_node_features.shape[0]))
+            self._maps = {key: maps}
+        return self.fused(src_node_features, dst_node_features, edge_features, *maps)
+
+
+class MeshNodeBlock(nn.Module):
+    def __init__(self, input_node_dim: int, input_edge_dim: int, output_node_dim: int,
+                 comm=None, hidden_dim: int = 512, num_hidden_layers: int = 1,
+                 aggregation_type: str = "sum"):
+        super().__init__()
+        assert aggregation_type == "sum", "Only sum aggregation is supported."
+        self.comm = comm
+        self.node_dim = input_node_dim
+        self.mesh_mlp = MeshGraphMLP(input_node_dim + input_edge_dim, output_node_dim,
+                                     hidden_dim, num_hidden_layers)
+        self._maps: dict = {}
+
+    def fused(self, node_features: torch.Tensor, edge_features: torch.Tensor,
+              agg_map: IndexMap) -> torch.Tensor:
+        agg = scatter_sum(edge_features, agg_map)
+        lin = self.mesh_mlp._model[0]
+        n = self.node_dim
+        h = F.linear(node_features, lin.weight[:, :n], lin.bias)
+        h = h + F.linear(agg.to(h.dtype), lin.weight[:, n:])
+        h = self.mesh_mlp._model[1](h)
+        return self.mesh_mlp.tail(h) + node_features
+
+    def forward(self, node_features, edge_features, src_indices, rank_mapping=None):
+        """Reference signature: edges are summed into ``node_features`` rows
+        ``src_indices[e]``."""
+        key = (src_indices.data_ptr(), src_indices.numel(), node_features.shape[0])
+        m = self._maps.get(key)
+        if m is None:
+            m = IndexMap(src_indices.reshape(-1).long(), node_features.shape[0])
+            self._maps = {key: m}
+        return self.fused(node_features, edge_features, m)
+
+
+# ----------------------------------------------------------------------------- model
+class _Halo:
+    """Halo-exchanged ``[local | halo]`` rows for an edge set (identity when single)."""
+
+    def __init__(self, comm):
+        self.comm = comm
+        self._ex = None
+
+    def __call__(self, x: torch.Tensor, es) -> torch.Tensor:
+        if es.pattern is None:
+            return x
+        if self._ex is None:
+            from ..parallel.halo import HaloExchange
+
+            self._ex = HaloExchange(self.comm)
+        return torch.cat([x, self._ex(x, es.pattern)], dim=0)
+
+
+class GraphCastEmbedder(nn.Module):
+    def __init__(self, cfg, *args, **kwargs):
+        super().__init__()
+        m = cfg.model
+        H = m.hidden_dim
+        self.grid_input_dim, self.mesh_input_dim, self.hidden_dim = (m.input_grid_dim,
+                                                                     m.input_mesh_dim, H)
+        self.grid_feature_embedder = MeshGraphMLP(m.input_grid_dim, H, H, 1)
+        self.mesh_feature_embedder = MeshGraphMLP(m.input_mesh_dim, H, H, 1)
+        self.grid2mesh_edge_embedder = MeshGraphMLP(m.input_edge_dim, H, H, 1)
+        self.mesh2grid_edge_embedder = MeshGraphMLP(m.input_edge_dim, H, H, 1)
+        self.mesh2mesh_edge_embedder = MeshGraphMLP(m.input_edge_dim, H, H, 1)
+
+    def forward(self, grid_features, mesh_features, mesh2mesh_edge_features,
+                grid2mesh_edge_features, mesh2grid_edge_features):
+        return (self.grid_feature_embedder(grid_features),
+                self.mesh_feature_embedder(mesh_features),
+                self.mesh2mesh_edge_embedder(mesh2mesh_edge_features),
+                self.grid2mesh_edge_embedder(grid2mesh_edge_features),
+                self.mesh2grid_edge_embedder(mesh2grid_edge_features))
+
+
+class GraphCastEncoder(nn.Module):
+    def __init__(self, cfg, comm=None, *args, **kwargs):
+        super().__init__()
+        H = cfg.model.hidden_dim
+        self.edge_mlp = MeshEdgeBlock(H, H, H, H, comm, H)
+        self.mesh_node_mlp = MeshNodeBlock(H, H, H, comm, H)
+        self.grid_node_mlp = MeshGraphMLP(H, H)
+        self.halo = _Halo(comm)
+
+    def forward(self, grid_node_features, mesh_node_features, g2m_edge_features, g2m) -> Tuple:
+        grid_all = self.halo(grid_node_features, g2m)       # senders: grid (local|halo)
+        e = self.edge_mlp.fused(grid_all, mesh_node_features, g2m_edge_features,
+                                g2m.other_map(), g2m.agg_map())
+        n = self.mesh_node_mlp.fused(mesh_node_features, e, g2m.agg_map())
+        mesh_node_features = mesh_node_features + n
+        grid_node_features = grid_node_features + self.grid_node_mlp(grid_node_features)
+        return grid_node_features, mesh_node_features
+
+
+class GraphCastProcessor(nn.Module):
+    def __init__(self, cfg, comm=None, *args, **kwargs):
+        super().__init__()
+        H = cfg.model.hidden_dim
+        L = cfg.model.processor_layers
+        self.edge_processors = nn.ModuleList([MeshEdgeBlock(H, H, H, H, comm, H)
+                                              for _ in range(L)])
+        self.node_processors = nn.ModuleList([MeshNodeBlock(H, H, H, comm, H)
+                                              for _ in range(L)])
+        self.halo = _Halo(comm)
+
+    def forward(self, mesh_features, m2m_edge_features, m2m) -> Tuple:
+        e, n = m2m_edge_features, mesh_features
+        for i, (el, nl) in enumerate(zip(self.edge_processors, self.node_processors)):
+            with region(f"processor-{i}"):
+                n_all = self.halo(n, m2m)            # receivers (dst) may be remote
+                e = el.fused(n, n_all, e, m2m.agg_map(), m2m.other_map())
+                n = nl.fused(n, e, m2m.agg_map())    # aggregate at the source
+        return n, e
+
+
+class GraphCastDecoder(nn.Module):
+    def __init__(self, cfg, comm=None, *args, **kwargs):
+        super().__init__()
+        H = cfg.model.hidden_dim
+        self.comm = comm
+        self.edge_mlp = MeshEdgeBlock(H, H, H, H, comm, H)
+        self.node_mlp = MeshNodeBlock(H, H, H, comm, H, 1)
+        self.halo = _Halo(comm)
+
+    def forward(self, m2g_edge_features, grid_node_features, mesh_node_features, m2g):
+        mesh_all = self.halo(mesh_node_features, m2g)     # senders: mesh (local|halo)
+        e = self.edge_mlp.fused(mesh_all, grid_node_features, m2g_edge_features,
+                                m2g.other_map(), m2g.agg_map())
+        n = self.node_mlp.fused(grid_node_features, e, m2g.agg_map())
+        return grid_node_features + n
+
+
+class DGraphCast(nn.Module):
+    def __init__(self, cfg, comm=None, *args, **kwargs):
+        super().__init__()
+        self.hidden_dim = cfg.model.hidden_dim
+        self.output_grid_dim = cfg.model.output_grid_dim
+        self.comm = comm
+        self.embedder = GraphCastEmbedder(cfg)
+        self.encoder = GraphCastEncoder(cfg, comm)
+        self.processor = GraphCastProcessor(cfg, comm)
+        self.decoder = GraphCastDecoder(cfg, comm)
+        self.final_prediction = MeshGraphMLP(self.hidden_dim, self.output_grid_dim)
+
+    def forward(self, input_grid_features: torch.Tensor, static_graph) -> torch.Tensor:
+        g = static_graph
+        x = input_grid_features.reshape(-1, input_grid_features.shape[-1])
+        with region("embedder"):
+            grid, mesh, e_m2m, e_g2m, e_m2g = self.embedder(
+                x, g.mesh_node_features.to(x.dtype), g.m2m.features.to(x.dtype),
+                g.g2m.features.to(x.dtype), g.m2g.features.to(x.dtype))
+        with region("encoder"):
+            grid, mesh = self.encoder(grid, mesh, e_g2m, g.g2m)
+        with region("processor"):
+            mesh, _ = self.processor(mesh, e_m2m, g.m2m)
+        with region("decoder"):
+            grid = self.decoder(e_m2g, grid, mesh, g.m2g)
+        with region("final"):
+            return self.final_prediction(grid)

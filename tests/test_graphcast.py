@@ -1,0 +1,140 @@
+"""GraphCast (experiments/GraphCast): mesh / graph construction, fused edge and node
+blocks vs the reference's concat formulation, and distributed (W=2,3 latitude-band
+partition with halo exchanges) vs single-process equivalence of the whole model."""
+import numpy as np
+import pytest
+import torch
+
+from dgraph_amd.data.graphcast_graph import (build_global_graph, edge_features, mesh_hierarchy,
+                                             multimesh_edges, partition_graphcast_graph)
+from dgraph_amd.models.graphcast import (Config, DGraphCast, MeshEdgeBlock, MeshGraphMLP,
+                                         MeshNodeBlock)
+
+
+@pytest.mark.parametrize("level", [0, 1, 2, 3])
+def test_icosahedral_hierarchy_counts(level):
+    v, faces = mesh_hierarchy(level)
+    assert v.shape == (10 * 4 ** level + 2, 3)
+    np.testing.assert_allclose(np.linalg.norm(v, axis=1), 1.0, atol=1e-12)
+    assert [f.shape[0] for f in faces] == [20 * 4 ** k for k in range(level + 1)]
+    s, d = multimesh_edges(faces)
+    assert s.size == 3 * sum(20 * 4 ** k for k in range(level + 1))
+    # closed, consistently oriented mesh: every directed edge has its reverse
+    fwd = set(zip(s.tolist(), d.tolist()))
+    assert all((b, a) in fwd for a, b in fwd)
+    # faces are outward oriented
+    f = faces[-1]
+    a, b, c = v[f[:, 0]], v[f[:, 1]], v[f[:, 2]]
+    assert (np.einsum("ij,ij->i", np.cross(b - a, c - a), a) > 0).all()
+
+
+def test_edge_features_local_frame():
+    rng = np.random.default_rng(0)
+    p = rng.normal(size=(50, 3))
+    p /= np.linalg.norm(p, axis=1, keepdims=True)
+    q = rng.normal(size=(50, 3))
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    f = edge_features(p, q)
+    # rotation preserves distances
+    d = np.linalg.norm(p - q, axis=1)
+    np.testing.assert_allclose(f[:, 3], d / d.max(), rtol=1e-5)
+    np.testing.assert_allclose(np.linalg.norm(f[:, :3], axis=1), f[:, 3], rtol=1e-5)
+
+
+def test_graph_sizes_small():
+    g = build_global_graph(2, (19, 36))
+    N = 19 * 36
+    assert g.m2g[0].size == 3 * N and g.grid_xyz.shape == (N, 3)
+    assert 0 < g.g2m[0].size <= 4 * N
+    pg = partition_graphcast_graph(g, 0, 1)
+    assert pg.num_local_grid == N and pg.num_local_mesh == 162
+    assert pg.m2m.num_edges == g.m2m[0].size
+
+
+def _ref_edge(block, xs, xd, e, s, d):
+    return block.mesh_mlp(torch.cat([xs[s], xd[d], e], 1)) + e
+
+
+def test_edge_and_node_blocks_match_reference():
+    torch.manual_seed(0)
+    H, Ns, Nd, E = 8, 13, 11, 60
+    eb = MeshEdgeBlock(H, H, H, H, hidden_dim=16).double()
+    nb = MeshNodeBlock(H, H, H, hidden_dim=16).double()
+    xs = torch.randn(Ns, H, dtype=torch.float64, requires_grad=True)
+    xd = torch.randn(Nd, H, dtype=torch.float64, requires_grad=True)
+    e = torch.randn(E, H, dtype=torch.float64, requires_grad=True)
+    s, d = torch.randint(0, Ns, (E,)), torch.randint(0, Nd, (E,))
+    out = eb(xs, xd, e, s, d)
+    ref = _ref_edge(eb, xs, xd, e, s, d)
+    torch.testing.assert_close(out, ref)
+    n = nb(xd, out, d)
+    agg = torch.zeros(Nd, H, dtype=torch.float64).index_add(0, d, ref)
+    nref = nb.mesh_mlp(torch.cat([xd, agg], 1)) + xd
+    torch.testing.assert_close(n, nref)
+    w = torch.randn_like(n)
+    params = [xs, xd, e] + list(eb.parameters()) + list(nb.parameters())
+    ga = torch.autograd.grad((n * w).sum(), params)
+    gb = torch.autograd.grad((nref * w).sum(), params)
+    for a, b in zip(ga, gb):
+        torch.testing.assert_close(a, b)
+
+
+def _small_cfg():
+    cfg = Config()
+    cfg.model.hidden_dim = 16
+    cfg.model.processor_layers = 2
+    cfg.model.input_grid_dim = cfg.model.output_grid_dim = 5
+    return cfg
+
+
+def _gc_dist(rank, world, out_dir):
+    import torch.distributed as dist
+
+    from dgraph_amd import Communicator
+    from dgraph_amd.data.weather import SyntheticWeatherDataset
+    from dgraph_amd.parallel.grad_sync import GradSync
+
+    comm = Communicator.init_process_group("nccl")
+    try:
+        g = build_global_graph(2, (19, 36))
+        pg = partition_graphcast_graph(g, rank, world, group=comm.group)
+        ds = SyntheticWeatherDataset(pg, num_channels=5, num_samples_per_year=3)
+        x, y = ds[0]
+        torch.manual_seed(0)
+        model = DGraphCast(_small_cfg(), comm).double()
+        out = model(x.double(), pg)
+        n = torch.tensor([float(out.numel())], dtype=torch.float64)
+        dist.all_reduce(n)
+        loss = ((out - y.double()) ** 2).sum() / n
+        loss.backward()
+        GradSync(model.parameters()).all_reduce()
+        gl = loss.detach().clone()
+        dist.all_reduce(gl)
+        full = torch.zeros(19 * 36, 5, dtype=torch.float64)
+        full[pg.grid_global_ids] = out.detach()
+        dist.all_reduce(full)
+        gn = torch.stack([p.grad.norm() if p.grad is not None else torch.zeros((), dtype=torch.float64)
+                          for p in model.parameters()])
+        if rank == 0:
+            torch.save({"out": full, "loss": gl, "gn": gn}, f"{out_dir}/gc_w{world}.pt")
+    finally:
+        comm.destroy()
+
+
+def test_graphcast_distributed_equivalence(ranks, tmp_path):
+    d = str(tmp_path)
+    for w in (1, 2, 3):
+        ranks(_gc_dist, w, d)
+    r1 = torch.load(f"{d}/gc_w1.pt", weights_only=True)
+    for w in (2, 3):
+        rw = torch.load(f"{d}/gc_w{w}.pt", weights_only=True)
+        torch.testing.assert_close(rw["out"], r1["out"])
+        torch.testing.assert_close(rw["loss"], r1["loss"])
+        torch.testing.assert_close(rw["gn"], r1["gn"])
+
+
+def test_mlp_reference_layout():
+    m = MeshGraphMLP(7, 5, hidden_dim=9, hidden_layers=2)
+    names = [k for k, _ in m.named_parameters()]
+    assert names == ["_model.0.weight", "_model.0.bias", "_model.2.weight", "_model.2.bias",
+                     "_model.4.weight", "_model.4.bias", "_model.5.weight", "_model.5.bias"]
