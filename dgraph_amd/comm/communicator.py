@@ -72,6 +72,21 @@ class Communicator(CommunicatorBase):
     def group(self):
         return getattr(self._engine, "group", None)
 
+    @property
+    def partition(self):
+        """:class:`~dgraph_amd.comm.groups.PartitionGroups` (graph group x replica group),
+        or None for engines without ``ranks_per_graph`` support."""
+        return getattr(self._engine, "_groups", None)
+
+    def partition_rank(self) -> int:
+        """Rank inside this process's graph group (== get_rank() without replicas)."""
+        p = self.partition
+        return p.partition_rank if p is not None else self.get_rank()
+
+    def partition_size(self) -> int:
+        p = self.partition
+        return p.ranks_per_graph if p is not None else self.get_world_size()
+
     def _check(self):
         assert Communicator._is_initialized, "Communicator not initialized"
 

@@ -60,3 +60,33 @@ def test_ogb_lsc_trainer_two_ranks(ranks, tmp_path):
     losses, accs = r[:6], r[6:]
     assert np.isfinite(losses).all() and losses[-1] < losses[0]
     assert ((accs >= 0) & (accs <= 1)).all()
+
+
+def _gc_train(rank, world, rpg, out_path, ckpt):
+    import torch
+
+    from dgraph_amd import Communicator
+    from dgraph_amd.experiments import graphcast
+
+    torch.set_num_threads(2)
+    tr, last = graphcast.main(backend="nccl", procs_per_graph=rpg, iters=3, mesh_level=1,
+                              grid="9x18", hidden_dim=8, processor_layers=1, channels=3,
+                              checkpoint_dir=ckpt)
+    if rank == 0:
+        np.save(out_path, np.array([h["loss"] for h in tr.history]))
+    Communicator.instance().destroy()
+
+
+@pytest.mark.parametrize("world,rpg", [(1, -1), (2, -1), (2, 1)])
+def test_graphcast_trainer(ranks, tmp_path, world, rpg):
+    out = tmp_path / "gc.npy"
+    ranks(_gc_train, world, rpg, str(out), str(tmp_path / "ck"))
+    losses = np.load(out)
+    assert losses.shape == (3,) and np.isfinite(losses).all()
+    assert os.path.exists(tmp_path / "ck" / "model_3.pth")
+    if rpg == -1:  # graph-parallel: identical trajectory to single process
+        ref = tmp_path.parent / "gc_ref.npy"
+        if world == 1:
+            np.save(ref, losses)
+        elif ref.exists():
+            np.testing.assert_allclose(losses, np.load(ref), rtol=1e-4)
