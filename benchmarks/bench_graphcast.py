@@ -1,0 +1,130 @@
+#!/usr/bin/env python3
+"""GraphCast training-step and MeshEdgeBlock micro-benchmark
+(experiments/GraphCast/microbenchmark_graphcast.py behaviour).
+
+* ``--mode step``: full DGraphCast forward + backward + Adam on the 721 x 1440 grid with
+  the level-6 multimesh (1.04 M grid nodes, 40 962 mesh nodes, 327 660 mesh edges,
+  ~1.6 M grid2mesh and 3.1 M mesh2grid edges); reports ms/step and edge updates/s.
+* ``--mode edge``: one processor MeshEdgeBlock (halo exchange + fused edge MLP) at
+  ``--hidden`` (reference: F=512), timing the communication and compute parts separately
+  with HIP events.
+
+Runs single-process or under torchrun (latitude-band graph partition, RCCL halos); rank 0
+prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mode", default="step", choices=["step", "edge"])
+    ap.add_argument("--mesh-level", type=int, default=6)
+    ap.add_argument("--grid", default="721x1440")
+    ap.add_argument("--hidden", type=int, default=128)
+    ap.add_argument("--layers", type=int, default=4)
+    ap.add_argument("--channels", type=int, default=73)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    a = ap.parse_args()
+
+    import torch.distributed as dist
+
+    from dgraph_amd import Communicator
+    from dgraph_amd.data.graphcast_graph import build_global_graph, partition_graphcast_graph
+    from dgraph_amd.data.weather import SyntheticWeatherDataset
+    from dgraph_amd.models.graphcast import Config, DGraphCast, MeshEdgeBlock
+    from dgraph_amd.parallel.grad_sync import GradSync
+
+    comm = Communicator.init_process_group("nccl")
+    rank, W = comm.get_rank(), comm.get_world_size()
+    dev = torch.device("cuda", torch.cuda.current_device())
+    dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
+    t0 = time.perf_counter()
+    g = build_global_graph(a.mesh_level, tuple(int(v) for v in a.grid.split("x")))
+    pg = partition_graphcast_graph(g, rank, W, group=comm.group).to(dev)
+    build_s = time.perf_counter() - t0
+    cfg = Config()
+    cfg.model.hidden_dim = a.hidden
+    cfg.model.processor_layers = a.layers
+    cfg.model.input_grid_dim = cfg.model.output_grid_dim = a.channels
+    torch.manual_seed(0)
+
+    def sync():
+        torch.cuda.synchronize()
+        if W > 1:
+            dist.barrier()
+
+    result = {}
+    if a.mode == "step":
+        ds = SyntheticWeatherDataset(pg, a.channels, 3)
+        x, y = (t.to(dev, dt) for t in ds[0])
+        model = DGraphCast(cfg, comm).to(dev, dt)
+        gs = GradSync(model.parameters())
+        opt = torch.optim.Adam(model.parameters(), lr=1e-4, fused=True)
+
+        def step():
+            opt.zero_grad(set_to_none=True)
+            out = model(x, pg)
+            loss = ((out.float() - y.float()) ** 2).mean()
+            loss.backward()
+            gs.all_reduce()
+            opt.step()
+            return loss
+
+        for _ in range(a.warmup):
+            step()
+        sync()
+        t = time.perf_counter()
+        for _ in range(a.steps):
+            loss = step()
+        sync()
+        ms = (time.perf_counter() - t) * 1e3 / a.steps
+        edges = a.layers * g.m2m[0].size + g.g2m[0].size + g.m2g[0].size
+        result = {"metric": "graphcast_step_ms", "ms_per_step": ms,
+                  "edge_updates_per_s": edges / (ms / 1e3), "loss": float(loss),
+                  "peak_mem_gb": torch.cuda.max_memory_allocated() / 1e9}
+    else:
+        H = a.hidden
+        blk = MeshEdgeBlock(H, H, H, H, comm, H).to(dev, dt)
+        n = torch.randn(pg.num_local_mesh, H, device=dev, dtype=dt)
+        e = torch.randn(pg.m2m.num_edges, H, device=dev, dtype=dt)
+        from dgraph_amd.parallel.halo import HaloExchange
+
+        hx = HaloExchange(comm)
+        comm_ms, comp_ms = [], []
+        for it in range(a.warmup + a.steps):
+            s0, s1, s2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+            s0.record()
+            n_all = torch.cat([n, hx(n, pg.m2m.pattern)]) if pg.m2m.pattern is not None else n
+            s1.record()
+            out = blk.fused(n, n_all, e, pg.m2m.agg_map(), pg.m2m.other_map())
+            s2.record()
+            torch.cuda.synchronize()
+            if it >= a.warmup:
+                comm_ms.append(s0.elapsed_time(s1))
+                comp_ms.append(s1.elapsed_time(s2))
+        del out
+        result = {"metric": "mesh_edge_block_ms", "comm_ms": sum(comm_ms) / len(comm_ms),
+                  "compute_ms": sum(comp_ms) / len(comp_ms), "edges": pg.m2m.num_edges}
+    t = torch.tensor([result.get("ms_per_step", result.get("compute_ms", 0.0))], device=dev)
+    if W > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        result.update({"n_gpus": W, "dtype": a.dtype, "hidden": a.hidden, "layers": a.layers,
+                       "grid": a.grid, "mesh_level": a.mesh_level, "graph_build_s": build_s,
+                       "max_over_ranks_ms": float(t)})
+        print(json.dumps(result), flush=True)
+    comm.destroy()
+
+
+if __name__ == "__main__":
+    main()
