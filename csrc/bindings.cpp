@@ -309,6 +309,68 @@ void gather_add_act_op(const c10::optional<at::Tensor>& Y, const c10::optional<a
                               static_cast<int>(act), cur_stream(out)));
 }
 
+bool ln_shape_ok(const at::Tensor& x) {
+  const int64_t F = x.size(1);
+  const int V = x.scalar_type() == at::kFloat ? 4 : 8;
+  const int64_t per = (F % V == 0) ? F / V : F;
+  return (per + 63) / 64 <= 8;
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> layer_norm_fwd_op(
+    const at::Tensor& x, const c10::optional<at::Tensor>& gamma,
+    const c10::optional<at::Tensor>& beta, const c10::optional<at::Tensor>& res, double eps) {
+  check_dev(x, x, "x");
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous(), "layer_norm: x must be contiguous [N, F]");
+  TORCH_CHECK(ln_shape_ok(x), "layer_norm: feature width too large for the kernel");
+  const int64_t N = x.size(0), F = x.size(1);
+  const float* gp = opt_f32(gamma, x, "gamma");
+  const float* bp = opt_f32(beta, x, "beta");
+  TORCH_CHECK((gp == nullptr) == (bp == nullptr), "gamma and beta must both be given or not");
+  if (gp) TORCH_CHECK(gamma->numel() == F && beta->numel() == F, "gamma/beta must have F elems");
+  const void* rp = nullptr;
+  if (res.has_value() && res->defined()) {
+    check_dev(*res, x, "res");
+    TORCH_CHECK(res->sizes() == x.sizes() && res->is_contiguous() &&
+                    res->scalar_type() == x.scalar_type(),
+                "res must match x");
+    rp = res->data_ptr();
+  }
+  auto y = at::empty_like(x);
+  auto opts = x.options().dtype(at::kFloat);
+  auto mean = at::empty({N}, opts);
+  auto rstd = at::empty({N}, opts);
+  c10::DeviceGuard g(x.device());
+  DG_HIP_CHECK(layer_norm_fwd(dtype_of(x), x.data_ptr(), gp, bp, rp, y.data_ptr(),
+                              mean.data_ptr<float>(), rstd.data_ptr<float>(), N,
+                              static_cast<int>(F), static_cast<float>(eps), cur_stream(x)));
+  return {y, mean, rstd};
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> layer_norm_bwd_op(
+    const at::Tensor& dy, const at::Tensor& x, const at::Tensor& mean, const at::Tensor& rstd,
+    const c10::optional<at::Tensor>& gamma) {
+  check_dev(x, x, "x");
+  check_dev(dy, x, "dy");
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && dy.is_contiguous() &&
+                  dy.sizes() == x.sizes() && dy.scalar_type() == x.scalar_type(),
+              "layer_norm_bwd: dy/x must be contiguous [N, F] of one dtype");
+  TORCH_CHECK(ln_shape_ok(x), "layer_norm: feature width too large for the kernel");
+  const int64_t N = x.size(0), F = x.size(1);
+  TORCH_CHECK(mean.numel() == N && rstd.numel() == N && mean.scalar_type() == at::kFloat &&
+                  rstd.scalar_type() == at::kFloat,
+              "mean/rstd must be fp32 [N]");
+  const float* gp = opt_f32(gamma, x, "gamma");
+  auto dx = at::empty_like(x);
+  const int64_t nb = std::max<int64_t>(1, std::min<int64_t>(1024, (N + 255) / 256));
+  auto partial = at::empty({nb, 2, F}, x.options().dtype(at::kFloat));
+  c10::DeviceGuard g(x.device());
+  DG_HIP_CHECK(layer_norm_bwd(dtype_of(x), dy.data_ptr(), x.data_ptr(), mean.data_ptr<float>(),
+                              rstd.data_ptr<float>(), gp, dx.data_ptr(), partial.data_ptr<float>(),
+                              static_cast<int>(nb), N, static_cast<int>(F), cur_stream(x)));
+  auto sums = partial.sum(0);
+  return {dx, sums[0], sums[1]};
+}
+
 }  // namespace
 }  // namespace dgraph
 
@@ -323,6 +385,10 @@ TORCH_LIBRARY(dgraph_amd, m) {
   m.def("col_sum(Tensor g) -> Tensor");
   m.def("pair_relu(Tensor rowptr, Tensor col, int mode, Tensor rowterm, Tensor gat, Tensor? gat2, "
         "Tensor? rowmul, Tensor(a!) out) -> ()");
+  m.def("layer_norm_fwd(Tensor x, Tensor? gamma, Tensor? beta, Tensor? res, float eps) -> "
+        "(Tensor, Tensor, Tensor)");
+  m.def("layer_norm_bwd(Tensor dy, Tensor x, Tensor mean, Tensor rstd, Tensor? gamma) -> "
+        "(Tensor, Tensor, Tensor)");
   m.def("gather_add_act(Tensor? Y, Tensor? P, Tensor? src, Tensor? Q, Tensor? dst, Tensor? gin, "
         "Tensor(a!) out, int act) -> ()");
   m.def(
@@ -346,4 +412,6 @@ TORCH_LIBRARY_IMPL(dgraph_amd, CUDA, m) {
   m.impl("col_sum", &dgraph::col_sum_op);
   m.impl("pair_relu", &dgraph::pair_relu_op);
   m.impl("gather_add_act", &dgraph::gather_add_act_op);
+  m.impl("layer_norm_fwd", &dgraph::layer_norm_fwd_op);
+  m.impl("layer_norm_bwd", &dgraph::layer_norm_bwd_op);
 }

@@ -86,4 +86,16 @@ hipError_t gather_add_act(DType dt, bool bwd, const void* Y, int64_t ldy, const 
                           const int64_t* dst, const void* gin, int64_t ldgi, void* out,
                           int64_t ldo, int64_t E, int F, int act, hipStream_t st);
 
+// ---------------------------------------------------------------------------
+// Row LayerNorm (layernorm.hip). y = (x - mean) * rstd * gamma + beta (+ res); gamma/beta
+// fp32 or both null; mean/rstd fp32 [N]. Backward writes dx and per-block fp32 partials
+// partial[b][0][:] = sum dy * x_hat, partial[b][1][:] = sum dy (b < nblocks).
+// ---------------------------------------------------------------------------
+hipError_t layer_norm_fwd(DType dt, const void* x, const float* gamma, const float* beta,
+                          const void* res, void* y, float* mean, float* rstd, int64_t N, int F,
+                          float eps, hipStream_t st);
+hipError_t layer_norm_bwd(DType dt, const void* dy, const void* x, const float* mean,
+                          const float* rstd, const float* gamma, void* dx, float* partial,
+                          int nblocks, int64_t N, int F, hipStream_t st);
+
 }  // namespace dgraph

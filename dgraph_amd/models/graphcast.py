@@ -27,6 +27,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.aggregate import scatter_sum
+from ..ops.dense import linear
+from ..ops.norm import layer_norm
 from ..ops.csr import IndexMap
 from ..ops.edge_mlp import edge_pre_activation
 from ..utils.timing import region
@@ -95,14 +97,24 @@ class MeshGraphMLP(nn.Module):
             layers.append(getattr(nn, norm_type)(output_dim))
         self._model = nn.Sequential(*layers)
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
-        return self._model(x)
+    def _run(self, h: torch.Tensor, start: int, residual=None) -> torch.Tensor:
+        mods = list(self._model)[start:]
+        for i, m in enumerate(mods):
+            if isinstance(m, nn.Linear):
+                h = linear(h, m.weight, m.bias)
+            elif isinstance(m, nn.LayerNorm) and i == len(mods) - 1:
+                h = layer_norm(h, m.weight, m.bias, m.eps, residual)  # residual fused
+                residual = None
+            else:
+                h = m(h)
+        return h if residual is None else h + residual
 
-    def tail(self, h: torch.Tensor) -> torch.Tensor:
-        """Everything after the first Linear + activation."""
-        for m in list(self._model)[2:]:
-            h = m(h)
-        return h
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+        return self._run(x, 0, residual)
+
+    def tail(self, h: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Everything after the first Linear + activation (``+ residual``)."""
+        return self._run(h, 2, residual)
 
     def first_act_name(self) -> str:
         act = self._model[1]
@@ -135,11 +147,11 @@ class MeshEdgeBlock(nn.Module):
               src_map: IndexMap, dst_map: IndexMap) -> torch.Tensor:
         """Edge update with index maps over the rows of ``src_feats`` / ``dst_feats``."""
         Ws, Wd, We, b = self._split_first()
-        P = F.linear(src_feats, Ws)
-        Q = F.linear(dst_feats, Wd)
-        Y = F.linear(edge_feats, We, b)
+        P = linear(src_feats, Ws)
+        Q = linear(dst_feats, Wd)
+        Y = linear(edge_feats, We, b)
         h = edge_pre_activation(Y, P, Q, src_map, dst_map, self.mesh_mlp.first_act_name())
-        return self.mesh_mlp.tail(h) + edge_feats
+        return self.mesh_mlp.tail(h, residual=edge_feats)
 
     def forward(self, src_node_features, dst_node_features, edge_features, src_indices,
                 dst_indices, src_rank_mapping=None, dst_rank_mapping=None):
@@ -171,10 +183,10 @@ class MeshNodeBlock(nn.Module):
         agg = scatter_sum(edge_features, agg_map)
         lin = self.mesh_mlp._model[0]
         n = self.node_dim
-        h = F.linear(node_features, lin.weight[:, :n], lin.bias)
-        h = h + F.linear(agg.to(h.dtype), lin.weight[:, n:])
+        h = linear(node_features, lin.weight[:, :n], lin.bias)
+        h = h + linear(agg.to(h.dtype), lin.weight[:, n:])
         h = self.mesh_mlp._model[1](h)
-        return self.mesh_mlp.tail(h) + node_features
+        return self.mesh_mlp.tail(h, residual=node_features)
 
     def forward(self, node_features, edge_features, src_indices, rank_mapping=None):
         """Reference signature: edges are summed into ``node_features`` rows
@@ -242,7 +254,7 @@ class GraphCastEncoder(nn.Module):
                                 g2m.other_map(), g2m.agg_map())
         n = self.mesh_node_mlp.fused(mesh_node_features, e, g2m.agg_map())
         mesh_node_features = mesh_node_features + n
-        grid_node_features = grid_node_features + self.grid_node_mlp(grid_node_features)
+        grid_node_features = self.grid_node_mlp(grid_node_features, residual=grid_node_features)
         return grid_node_features, mesh_node_features
 
 

@@ -53,3 +53,53 @@ def wgrad(x: torch.Tensor, g: torch.Tensor, rows_per_chunk: int = 1 << 18) -> to
 def col_sum_f32(g: torch.Tensor) -> torch.Tensor:
     """fp32 column sums without an fp32 copy of ``g``."""
     return K.col_sum(g)
+
+
+def _auto_rows_per_chunk(L: int) -> int:
+    """Chunk so the batched wgrad has >= ~128 independent output tiles (256 CUs), but
+    keeps chunks >= 4096 rows."""
+    c = 4096
+    while L // c > 128:
+        c *= 2
+    return c
+
+
+class _LinearFn(torch.autograd.Function):
+    """``y = x W^T + b`` whose backward computes dW with the split-K batched GEMM and
+    db with the native column sum (the library GEMM for a 128x128 weight gradient over
+    10^6 rows runs on 2 workgroups; profiles/graphcast_1gpu_kernel_stats.txt)."""
+
+    @staticmethod
+    def forward(ctx, x, W, b):
+        ctx.save_for_backward(x, W)
+        ctx.has_b = b is not None
+        return torch.nn.functional.linear(x, W, b)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, W = ctx.saved_tensors
+        N = W.shape[0]
+        g2 = g.reshape(-1, N).contiguous()
+        x2 = x.reshape(-1, W.shape[1])
+        dx = dW = db = None
+        if ctx.needs_input_grad[0]:
+            dx = (g2 @ W.to(g2.dtype)).reshape(x.shape)
+        if ctx.needs_input_grad[1]:
+            if g2.is_cuda:
+                dW = wgrad(g2, x2.contiguous(), _auto_rows_per_chunk(g2.shape[0]))
+            else:
+                dW = g2.t().to(torch.float64 if g2.dtype == torch.float64 else torch.float32) @ \
+                    x2.to(torch.float64 if g2.dtype == torch.float64 else torch.float32)
+            dW = dW.to(W.dtype)
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = (col_sum_f32(g2) if g2.is_cuda else g2.sum(0)).to(W.dtype)
+        return dx, dW, db
+
+
+def linear(x: torch.Tensor, W: torch.Tensor, b=None) -> torch.Tensor:
+    """Drop-in for ``F.linear`` with a tall-skinny-aware backward."""
+    if torch.is_autocast_enabled() and x.is_cuda:
+        dt = torch.get_autocast_gpu_dtype()
+        x, W = x.to(dt), W.to(dt)
+        b = None if b is None else b.to(dt)
+    return _LinearFn.apply(x, W, b)

@@ -6,7 +6,7 @@ OUT=$R/gpurun_out/prof_${TAG:-run}
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 ${TMO:-900} rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT" -o run \
-  -- python3 "$R/bench.py" ${BENCH_ARGS:---steps 2 --warmup 1} > "$OUT/stdout.log" 2>&1
+  -- python3 "$R/${SCRIPT:-bench.py}" ${BENCH_ARGS:---steps 2 --warmup 1} > "$OUT/stdout.log" 2>&1
 rc=$?
 echo "rocprof rc=$rc"
 find "$OUT" -name "*kernel_stats.csv" | head -3

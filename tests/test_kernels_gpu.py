@@ -333,3 +333,59 @@ def test_gat_layer_gpu_matches_cpu():
     torch.testing.assert_close(xsg.grad.cpu(), xsc.grad, atol=1e-4, rtol=1e-3)
     for a, b in zip(lg.parameters(), grads_c):
         torch.testing.assert_close(a.grad.cpu(), b, atol=1e-3, rtol=1e-3)
+
+
+@pytest.mark.parametrize("shape", [(1000, 128), (777, 73), (50, 512), (3, 1024), (4097, 8)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("affine,res", [(True, False), (True, True), (False, False)])
+def test_layer_norm_native(shape, dtype, affine, res):
+    from dgraph_amd.ops.norm import layer_norm
+
+    g = torch.Generator().manual_seed(shape[0])
+    x = (torch.randn(shape, generator=g) * 3 + 1).to(dtype)
+    r = torch.randn(shape, generator=g).to(dtype) if res else None
+    w = torch.randn(shape[1], generator=g) if affine else None
+    b = torch.randn(shape[1], generator=g) if affine else None
+    dy = torch.randn(shape, generator=g).to(dtype)
+    # fp32 reference
+    xr = x.float().requires_grad_(True)
+    wr = w.clone().requires_grad_(True) if affine else None
+    br = b.clone().requires_grad_(True) if affine else None
+    yr = torch.nn.functional.layer_norm(xr, (shape[1],), wr, br, 1e-5)
+    if res:
+        yr = yr + r.float()
+    (yr * dy.float()).sum().backward()
+    xg = x.to(DEV).requires_grad_(True)
+    wg = w.to(DEV).requires_grad_(True) if affine else None
+    bg = b.to(DEV).requires_grad_(True) if affine else None
+    rg = r.to(DEV).requires_grad_(True) if res else None
+    y = layer_norm(xg, wg, bg, 1e-5, rg)
+    (y * dy.to(DEV)).sum().backward()
+    tol = _tol(dtype)
+    torch.testing.assert_close(y.float().cpu(), yr.detach(), **tol)
+    torch.testing.assert_close(xg.grad.float().cpu(), xr.grad, **tol)
+    if affine:
+        torch.testing.assert_close(wg.grad.cpu(), wr.grad, atol=5e-2 * shape[0] ** 0.5, rtol=2e-2)
+        torch.testing.assert_close(bg.grad.cpu(), br.grad, atol=5e-2 * shape[0] ** 0.5, rtol=2e-2)
+    if res:
+        torch.testing.assert_close(rg.grad.float().cpu(), dy.float())
+
+
+@pytest.mark.parametrize("rows", [100, 5000, 300000])
+def test_linear_split_k_grads(rows):
+    from dgraph_amd.ops.dense import linear
+
+    g = torch.Generator().manual_seed(rows)
+    x = torch.randn(rows, 64, generator=g).to(DEV).requires_grad_(True)
+    W = torch.randn(48, 64, generator=g).to(DEV).requires_grad_(True)
+    b = torch.randn(48, generator=g).to(DEV).requires_grad_(True)
+    dy = torch.randn(rows, 48, generator=g).to(DEV)
+    y = linear(x, W, b)
+    (y * dy).sum().backward()
+    x2, W2, b2 = (t.detach().double().requires_grad_(True) for t in (x, W, b))
+    y2 = torch.nn.functional.linear(x2, W2, b2)
+    (y2 * dy.double()).sum().backward()
+    torch.testing.assert_close(y.double(), y2, atol=1e-3, rtol=1e-3)
+    torch.testing.assert_close(W.grad.double(), W2.grad, atol=1e-2 * rows ** 0.5 / 10, rtol=1e-3)
+    torch.testing.assert_close(b.grad.double(), b2.grad, atol=1e-3 * rows ** 0.5, rtol=1e-3)
+    torch.testing.assert_close(x.grad.double(), x2.grad, atol=1e-3, rtol=1e-3)
