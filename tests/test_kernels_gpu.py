@@ -348,14 +348,14 @@ def test_layer_norm_native(shape, dtype, affine, res):
     b = torch.randn(shape[1], generator=g) if affine else None
     dy = torch.randn(shape, generator=g).to(dtype)
     # fp32 reference
-    xr = x.float().requires_grad_(True)
+    xr = x.float().clone().requires_grad_(True)
     wr = w.clone().requires_grad_(True) if affine else None
     br = b.clone().requires_grad_(True) if affine else None
     yr = torch.nn.functional.layer_norm(xr, (shape[1],), wr, br, 1e-5)
     if res:
         yr = yr + r.float()
     (yr * dy.float()).sum().backward()
-    xg = x.to(DEV).requires_grad_(True)
+    xg = x.detach().to(DEV).requires_grad_(True)
     wg = w.to(DEV).requires_grad_(True) if affine else None
     bg = b.to(DEV).requires_grad_(True) if affine else None
     rg = r.to(DEV).requires_grad_(True) if res else None
