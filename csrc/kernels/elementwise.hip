@@ -213,19 +213,31 @@ hipError_t relu_mask_bwd(DType dt, void* g, const uint32_t* bits, int64_t numel,
 hipError_t col_sum_partial(DType dt, const void* g, int64_t ld, int64_t L, int F,
                            float* partial, int nblocks, hipStream_t st) {
   if (L <= 0 || F <= 0) return hipSuccess;
-  const int vec = dt == DType::F32 ? 4 : 8;
-  if (F % vec != 0 || F / vec > 256 || ld % vec != 0) return hipErrorInvalidValue;
+  int vec = dt == DType::F32 ? 4 : 8;
+  if (F % vec != 0 || ld % vec != 0) vec = 1;  // scalar lanes for odd widths (e.g. 73)
+  if (F / vec > 256) return hipErrorInvalidValue;
   const int64_t rpb = (L + nblocks - 1) / nblocks;
   const int tpr = F / vec;
   const int rpi = 256 / tpr;
   const size_t lds = static_cast<size_t>(rpi) * F * sizeof(float);
   dim3 block(256), grid(nblocks);
-  if (dt == DType::F32)
-    hipLaunchKernelGGL((col_sum_partial_kernel<float, 4>), grid, block, lds, st,
-                       static_cast<const float*>(g), ld, L, F, rpb, partial);
-  else
-    hipLaunchKernelGGL((col_sum_partial_kernel<uint16_t, 8>), grid, block, lds, st,
-                       static_cast<const uint16_t*>(g), ld, L, F, rpb, partial);
+  if (dt == DType::F32) {
+    auto gp = static_cast<const float*>(g);
+    if (vec == 4)
+      hipLaunchKernelGGL((col_sum_partial_kernel<float, 4>), grid, block, lds, st, gp, ld, L,
+                         F, rpb, partial);
+    else
+      hipLaunchKernelGGL((col_sum_partial_kernel<float, 1>), grid, block, lds, st, gp, ld, L,
+                         F, rpb, partial);
+  } else {
+    auto gp = static_cast<const uint16_t*>(g);
+    if (vec == 8)
+      hipLaunchKernelGGL((col_sum_partial_kernel<uint16_t, 8>), grid, block, lds, st, gp, ld,
+                         L, F, rpb, partial);
+    else
+      hipLaunchKernelGGL((col_sum_partial_kernel<uint16_t, 1>), grid, block, lds, st, gp, ld,
+                         L, F, rpb, partial);
+  }
   return hipGetLastError();
 }
 

@@ -124,7 +124,9 @@ def col_sum(g: torch.Tensor) -> torch.Tensor:
     """fp32 column sums of a 2-D tensor (bias gradients), deterministic."""
     if _native_ok(g) and g.dim() == 2 and g.stride(1) == 1:
         vec = 4 if g.dtype == torch.float32 else 8
-        if g.shape[1] % vec == 0 and g.shape[1] // vec <= 256 and g.stride(0) % vec == 0:
+        if g.shape[1] % vec != 0 or g.stride(0) % vec != 0:
+            vec = 1  # scalar-lane kernel variant
+        if g.shape[1] // vec <= 256:
             return _native.ops().col_sum(g)
         return torch.sum(g, dim=0, dtype=torch.float32)
     return _ref.col_sum(g)

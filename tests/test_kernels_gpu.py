@@ -189,7 +189,7 @@ def test_bias_relu_pack_shapes(shape):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("F", [8, 64, 172, 256])
+@pytest.mark.parametrize("F", [1, 5, 8, 64, 73, 172, 256])
 def test_col_sum(dtype, F):
     g = torch.randn(70001, F, device=DEV).to(dtype)
     torch.testing.assert_close(K.col_sum(g).cpu(), g.float().sum(0).cpu(), atol=5e-2, rtol=1e-3)
