@@ -124,6 +124,8 @@ def main():
                        "max_over_ranks_ms": float(t)})
         print(json.dumps(result), flush=True)
     comm.destroy()
+    if dist.is_initialized():
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -97,3 +97,44 @@ class AllToAllV:
         if async_op:
             return out, work
         return out
+
+
+def torch_alltoallv_with_comm_map(contiguous_send_tensor: torch.Tensor,
+                                  contiguous_recv_tensor: torch.Tensor,
+                                  send_comm_map: torch.Tensor, recv_comm_map: torch.Tensor,
+                                  rank: int, world_size: int, group=None):
+    """Per-peer split exchange along dim 1 of ``[B, rows, F]`` buffers
+    (alltoallv_impl.py:164-181); one all-to-all-v instead of a list-form all_to_all."""
+    ss = [int(v) for v in send_comm_map.tolist()]
+    rs = [int(v) for v in recv_comm_map.tolist()]
+    assert len(ss) == world_size and len(rs) == world_size
+    send = contiguous_send_tensor.transpose(0, 1).reshape(sum(ss), -1)
+    out = AllToAllV(ss, rs, group)(send)
+    contiguous_recv_tensor.copy_(out.reshape(sum(rs), contiguous_recv_tensor.shape[0],
+                                             -1).transpose(0, 1))
+    return list(torch.split(contiguous_recv_tensor, rs, dim=1))
+
+
+def _nccl_alltoallv_with_dict(send_buffer_dict, recv_buffer_dict, rank: int, world_size: int,
+                              group=None):
+    """Exchange per-peer buffers keyed by peer rank (alltoallv_impl.py:134-161) with one
+    all-to-all-v over their concatenation (received rows keep the sender's dtype; the
+    reference forced ``.float()``)."""
+    peers = range(world_size)
+    ref = next(iter(send_buffer_dict.values()), None)
+    if ref is None:
+        ref = next(iter(recv_buffer_dict.values()))
+    F = ref.shape[-1]
+    ss = [send_buffer_dict[p].numel() // F if p in send_buffer_dict and p != rank else 0
+          for p in peers]
+    rs = [recv_buffer_dict[p].numel() // F if p in recv_buffer_dict and p != rank else 0
+          for p in peers]
+    send = torch.cat([send_buffer_dict[p].reshape(-1, F) for p in peers if ss[p]] or
+                     [ref.new_zeros(0, F)])
+    out = AllToAllV(ss, rs, group)(send)
+    off = 0
+    for p in peers:
+        if rs[p]:
+            recv_buffer_dict[p].copy_(out[off:off + rs[p]].reshape(recv_buffer_dict[p].shape))
+            off += rs[p]
+    return recv_buffer_dict

@@ -154,3 +154,34 @@ def g1_scatter_global(x, indices, rank_mappings, output_size, rank, world_size, 
         plan = lower_local_form(idx, own, int(output_size), rank, world_size, group)
         cache.put(key, plan)
     return plan_scatter(_as_batched(x), plan, group)
+
+
+_LEGACY_CACHE = G1PlanCache()
+
+
+class GatherFunction:
+    """Reference-signature G1 gather (nccl/_torch_func_impl.py:355-579):
+    ``GatherFunction.apply(local_send_tensor[1,N,F], indices[1,E], edge_rank_loc[E],
+    edge_dest_ranks[E], rank, world_size)`` -> rows of the edges placed on ``rank``.
+    Lowered once to a static plan (cached by content), then executed by the plan gather
+    (autograd: the plan scatter), instead of re-deriving P2P send lists per call."""
+
+    @staticmethod
+    def apply(local_send_tensor, indices, edge_rank_loc, edge_dest_ranks, rank: int,
+              world_size: int, group=None):
+        rm = torch.stack([edge_rank_loc.reshape(-1), edge_dest_ranks.reshape(-1)])
+        return g1_gather_global(local_send_tensor, indices, rm, rank, world_size,
+                                _LEGACY_CACHE, group)
+
+
+class ScatterFunction:
+    """Reference-signature G1 scatter-sum (nccl/_torch_func_impl.py:582-782):
+    ``ScatterFunction.apply(send_tensor[1,E_r,F], indices, edge_src_ranks, edge_dest_ranks,
+    num_local_output_rows, rank, world_size)``."""
+
+    @staticmethod
+    def apply(send_tensor, indices, edge_src_ranks, edge_dest_ranks,
+              num_local_output_rows: int, rank: int, world_size: int, group=None):
+        rm = torch.stack([edge_src_ranks.reshape(-1), edge_dest_ranks.reshape(-1)])
+        return g1_scatter_global(send_tensor, indices, rm, int(num_local_output_rows), rank,
+                                 world_size, _LEGACY_CACHE, group)

@@ -213,3 +213,44 @@ def _offline_vs_collective(rank, world):
         save_cache(cache, p)
         c2 = load_cache(p)
         assert torch.equal(c2.plan.boundary_vertex_idx, cache.plan.boundary_vertex_idx)
+
+
+def _legacy_fns(rank, world):
+    import torch.distributed as dist
+
+    from dgraph_amd.comm.alltoallv import _nccl_alltoallv_with_dict, torch_alltoallv_with_comm_map
+    from dgraph_amd.parallel.index_ops import GatherFunction, ScatterFunction
+
+    dist_ok = dist.is_initialized()
+    assert dist_ok
+    torch.manual_seed(0)
+    X = torch.randn(1, 4, 2)
+    coo = torch.tensor([[0, 0, 0, 1, 2, 2, 2, 3], [1, 2, 3, 0, 3, 0, 3, 0]])
+    rm = torch.tensor([[0, 0, 0, 0, 1, 1, 1, 1], [0, 1, 1, 0, 1, 0, 1, 0]])
+    xl = X[:, 2 * rank:2 * rank + 2].clone().requires_grad_(True)
+    got = GatherFunction.apply(xl, coo[[1]], rm[0], rm[1], rank, world)
+    torch.testing.assert_close(got[0], X[0, coo[1]][rm[0] == rank])
+    got.sum().backward()
+    deg = torch.bincount(coo[1], minlength=4).float()
+    torch.testing.assert_close(xl.grad[0], deg[2 * rank:2 * rank + 2].unsqueeze(1).expand(2, 2))
+    Y = torch.arange(16.0).reshape(1, 8, 2)
+    yl = Y[:, rm[0] == rank]
+    s = ScatterFunction.apply(yl, coo[[1]], rm[0], rm[1], 2, rank, world)
+    exp = torch.zeros(4, 2).index_add_(0, coo[1], Y[0])
+    torch.testing.assert_close(s[0], exp[2 * rank:2 * rank + 2])
+    # comm-map exchange: rank r sends (p + 1) rows to peer p
+    send = torch.full((1, sum(p + 1 for p in range(world)), 3), float(rank))
+    recv = torch.empty(1, world * (rank + 1), 3)
+    parts = torch_alltoallv_with_comm_map(send, recv, torch.arange(1, world + 1),
+                                          torch.full((world,), rank + 1), rank, world)
+    for p, t in enumerate(parts):
+        assert torch.all(t == p)
+    sd = {p: torch.full((p + 2, 3), float(rank)) for p in range(world) if p != rank}
+    rd = {p: torch.empty(rank + 2, 3) for p in range(world) if p != rank}
+    _nccl_alltoallv_with_dict(sd, rd, rank, world)
+    for p, t in rd.items():
+        assert torch.all(t == p)
+
+
+def test_legacy_g1_functions(ranks):
+    ranks(_legacy_fns, 2)
