@@ -83,7 +83,9 @@ def main():
     if world == 1:
         csr.num_cols = part["L"]
     graph = DistGraph(csr, part["L"], part["H"], part["send_local_idx"], part["send_splits"],
-                      part["recv_splits"], comm.group, symmetric=(world == 1),
+                      # the synthetic graph is symmetrised, so the interior (local x local)
+                      # block is symmetric at every W: its transpose is never materialised
+                      part["recv_splits"], comm.group, symmetric=True,
                       overlap=not args.no_overlap)
     graph.prepare_backward()
     dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
