@@ -182,8 +182,12 @@ class SageWorkspace:
         self.slots = {}
         self.generation = 0
 
-    def prepare(self, L: int, dims, pf_flags, dtype, device):
-        key = (L, tuple(dims), tuple(pf_flags), dtype, str(device))
+    # device memory that must stay free after the optional ``agg0`` slot (RCCL buffers,
+    # masks, weight-gradient partials and allocator slack)
+    AGG0_HEADROOM = 24 << 30
+
+    def prepare(self, L: int, dims, pf_flags, dtype, device, keep_agg0: bool = False):
+        key = (L, tuple(dims), tuple(pf_flags), dtype, str(device), keep_agg0)
         if key == self.key:
             return
         self.slots = {}
@@ -195,7 +199,19 @@ class SageWorkspace:
             self.slots[f"act{i}"] = torch.empty(L * dims[i], dtype=dtype, device=device)
         self.slots["tmp_a"] = torch.empty(L * wa, dtype=dtype, device=device)
         self.slots["tmp_b"] = torch.empty(L * wb, dtype=dtype, device=device)
+        if keep_agg0 and not pf_flags[0]:
+            # layer 0's aggregate A x0 kept for its weight gradient (saves one SpMM per
+            # step) when it fits next to the other slots (multi-GPU shards; not 1-GPU
+            # papers100M, which needs ~263 GB without it)
+            need = L * dims[0] * torch.empty((), dtype=dtype).element_size()
+            free = torch.cuda.mem_get_info(device)[0] if torch.device(device).type == "cuda" \
+                else need + (64 << 30)  # host memory: treated as ample
+            if free - need >= self.AGG0_HEADROOM:
+                self.slots["agg0"] = torch.empty(L * dims[0], dtype=dtype, device=device)
         self.key = key
+
+    def has(self, name: str) -> bool:
+        return name in self.slots
 
     def view(self, name: str, L: int, F: int) -> torch.Tensor:
         return self.slots[name][: L * F].view(L, F)
@@ -225,8 +241,10 @@ class SAGEStackFn(Function):
         dims_p = [dims[0]] + [_pad8(d) for d in dims[1:]]
         pf_flags = [pf for (_, pf) in specs]
         if use_ws:
-            ws_obj.prepare(L, dims_p, pf_flags, dt, x0.device)
+            ws_obj.prepare(L, dims_p, pf_flags, dt, x0.device,
+                           keep_agg0=not x0.requires_grad)
             ws_obj.generation += 1
+        keep0 = use_ws and ws_obj.has("agg0") and not pf_flags[0] and not x0.requires_grad
         V = (lambda name, F: ws_obj.view(name, L, F)) if use_ws else \
             (lambda name, F: torch.empty(L, F, dtype=dt, device=x0.device))
         acts = [x0]
@@ -244,7 +262,8 @@ class SAGEStackFn(Function):
                 del z
                 y.addmm_(h, ws_)
             else:
-                a = graph.aggregate(h, mean=True, out=V("tmp_a", dims_p[i]))
+                slot = "agg0" if (i == 0 and keep0) else "tmp_a"
+                a = graph.aggregate(h, mean=True, out=V(slot, dims_p[i]))
                 torch.mm(h, ws_, out=y)
                 y.addmm_(a, wn_)
                 del a
@@ -264,7 +283,7 @@ class SAGEStackFn(Function):
         ctx.graph, ctx.specs, ctx.dims, ctx.dims_p = graph, specs, dims, dims_p
         ctx.acts, ctx.masks = acts, masks
         ctx.x0_requires_grad = x0.requires_grad
-        ctx.ws, ctx.use_ws = ws_obj, use_ws
+        ctx.ws, ctx.use_ws, ctx.keep0 = ws_obj, use_ws, keep0
         ctx.gen = ws_obj.generation if use_ws else None
         ctx.save_for_backward(*params)
         ctx.out_rows = out_rows
@@ -346,11 +365,14 @@ class SAGEStackFn(Function):
             else:
                 # tmp_a may still hold g for the last layer: recompute into tmp_b then
                 a_name = "tmp_b" if (i == n - 1 and ctx.out_rows is not None) else "tmp_a"
-                if i == n - 1 and ctx.out_rows is not None and dims[i] > dims[-1]:
+                if i == 0 and ctx.keep0:
+                    a_buf = a = V("agg0", dims[0])  # kept by forward: no recompute
+                elif i == n - 1 and ctx.out_rows is not None and dims[i] > dims[-1]:
                     a_buf = torch.empty(L, dims[i], dtype=dt, device=x.device)
                 else:
                     a_buf = V(a_name, dims[i])
-                a = graph.aggregate(x, mean=True, out=a_buf)
+                if not (i == 0 and ctx.keep0):
+                    a = graph.aggregate(x, mean=True, out=a_buf)
                 grads[3 * i + 1] = wgrad(a, g)[:r_in, :r_out].to(wn.dtype)
                 if need_dx:
                     t = torch.mm(g, wn_.t(), out=a)

@@ -117,3 +117,23 @@ def test_distributed_training_matches_single_rank(ranks, tmp_path, world):
     a = torch.load(tmp_path / "w1.pt", weights_only=True)
     b = torch.load(tmp_path / "wn.pt", weights_only=True)
     torch.testing.assert_close(a, b, atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize("keep_agg0", [True, False])
+def test_layer0_aggregate_kept_or_recomputed(monkeypatch, keep_agg0):
+    from dgraph_amd.models.sage import SageWorkspace
+
+    if not keep_agg0:  # no room for the slot: backward recomputes A x0
+        monkeypatch.setattr(SageWorkspace, "AGG0_HEADROOM", 1 << 62)
+    p, g, A = _graph()
+    x, _, tr = node_data(SHAPE, 0, p["offsets"], "cpu", dtype=torch.float32)
+    torch.manual_seed(0)
+    m = GraphSAGE(SHAPE.num_features, 256, 40, 3)  # layer 0 aggregates first
+    rows = torch.nonzero(tr).squeeze(1)
+    m(x, g, out_rows=rows).square().mean().backward()
+    assert m._workspace.has("agg0") == keep_agg0
+    grads = [q.grad.clone() for q in m.parameters()]
+    m.zero_grad()
+    _dense_forward(m, x, A)[rows].square().mean().backward()
+    for a, q in zip(grads, m.parameters()):
+        torch.testing.assert_close(a, q.grad, atol=1e-6, rtol=1e-4)
