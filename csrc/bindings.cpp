@@ -371,8 +371,73 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> layer_norm_bwd_op(
   return {dx, sums[0], sums[1]};
 }
 
+int64_t tile32_mask_words(int64_t M, int64_t N) { return (M + 255) / 256 * 8 * (N / 32) * 16; }
+
+void dual_gemm_op(const at::Tensor& A1, const at::Tensor& B1t, const c10::optional<at::Tensor>& A2,
+                  const c10::optional<at::Tensor>& B2t, const c10::optional<at::Tensor>& bias,
+                  const c10::optional<at::Tensor>& cin, const at::Tensor& out,
+                  const c10::optional<at::Tensor>& mask_out,
+                  const c10::optional<at::Tensor>& mask_in, bool relu) {
+  auto chk_bf16 = [&](const at::Tensor& t, const char* name) {
+    check_dev(t, out, name);
+    TORCH_CHECK(t.scalar_type() == at::kBFloat16, "dual_gemm: ", name, " must be bfloat16");
+    TORCH_CHECK(t.dim() == 2 && t.stride(1) == 1, "dual_gemm: ", name,
+                " must be 2-D with unit inner stride");
+  };
+  chk_bf16(out, "out");
+  chk_bf16(A1, "A1");
+  chk_bf16(B1t, "B1t");
+  const int64_t M = A1.size(0), K1 = A1.size(1), N = B1t.size(0);
+  TORCH_CHECK(B1t.size(1) == K1 && B1t.is_contiguous(), "B1t must be contiguous [N, K1]");
+  TORCH_CHECK(out.size(0) == M && out.size(1) == N, "out must be [M, N]");
+  TORCH_CHECK(A1.stride(0) % 8 == 0 && out.stride(0) % 1 == 0, "A1 row stride % 8");
+  const void* a2 = nullptr;
+  const void* b2 = nullptr;
+  int64_t K2 = 0, lda2 = 0;
+  if (A2.has_value() && A2->defined()) {
+    chk_bf16(*A2, "A2");
+    TORCH_CHECK(B2t.has_value() && B2t->defined(), "A2 needs B2t");
+    chk_bf16(*B2t, "B2t");
+    K2 = A2->size(1);
+    TORCH_CHECK(A2->size(0) == M && B2t->size(0) == N && B2t->size(1) == K2 &&
+                    B2t->is_contiguous() && A2->stride(0) % 8 == 0,
+                "A2/B2t shape mismatch");
+    a2 = A2->data_ptr();
+    b2 = B2t->data_ptr();
+    lda2 = A2->stride(0);
+  }
+  TORCH_CHECK(dual_gemm_supported(N, K1, K2), "dual_gemm: unsupported shape N=", N, " K1=", K1,
+              " K2=", K2);
+  const float* bp = opt_f32(bias, out, "bias");
+  if (bp) TORCH_CHECK(bias->numel() == N, "bias must have N elements");
+  const void* cp = nullptr;
+  int64_t ldc = 0;
+  if (cin.has_value() && cin->defined()) {
+    chk_bf16(*cin, "cin");
+    TORCH_CHECK(cin->size(0) == M && cin->size(1) == N, "cin must be [M, N]");
+    cp = cin->data_ptr();
+    ldc = cin->stride(0);
+  }
+  auto mask_ptr = [&](const c10::optional<at::Tensor>& m, const char* name) -> void* {
+    if (!m.has_value() || !m->defined()) return nullptr;
+    check_dev(*m, out, name);
+    TORCH_CHECK(m->scalar_type() == at::kLong && m->is_contiguous() &&
+                    m->numel() >= tile32_mask_words(M, N),
+                name, " must be contiguous int64 with ", tile32_mask_words(M, N), " words");
+    return m->data_ptr();
+  };
+  auto* mo = static_cast<uint64_t*>(mask_ptr(mask_out, "mask_out"));
+  auto* mi = static_cast<const uint64_t*>(mask_ptr(mask_in, "mask_in"));
+  c10::DeviceGuard g(out.device());
+  DG_HIP_CHECK(dual_gemm(A1.data_ptr(), A1.stride(0), B1t.data_ptr(), K1, a2, lda2, b2, K2, bp,
+                         cp, ldc, out.data_ptr(), out.stride(0), M, N, mo, mi, relu,
+                         cur_stream(out)));
+}
+
 }  // namespace
 }  // namespace dgraph
+
+int64_t tile32_mask_words_op(int64_t M, int64_t N) { return dgraph::tile32_mask_words(M, N); }
 
 void set_spmm_config_op(int64_t variant, int64_t xcd) {
   dgraph::set_spmm_config(static_cast<int>(variant), static_cast<int>(xcd));
@@ -389,6 +454,9 @@ TORCH_LIBRARY(dgraph_amd, m) {
         "(Tensor, Tensor, Tensor)");
   m.def("layer_norm_bwd(Tensor dy, Tensor x, Tensor mean, Tensor rstd, Tensor? gamma) -> "
         "(Tensor, Tensor, Tensor)");
+  m.def("dual_gemm(Tensor A1, Tensor B1t, Tensor? A2, Tensor? B2t, Tensor? bias, Tensor? cin, "
+        "Tensor(a!) out, Tensor(b!)? mask_out, Tensor? mask_in, bool relu) -> ()");
+  m.def("tile32_mask_words(int M, int N) -> int", &tile32_mask_words_op);
   m.def("gather_add_act(Tensor? Y, Tensor? P, Tensor? src, Tensor? Q, Tensor? dst, Tensor? gin, "
         "Tensor(a!) out, int act) -> ()");
   m.def(
@@ -413,5 +481,6 @@ TORCH_LIBRARY_IMPL(dgraph_amd, CUDA, m) {
   m.impl("pair_relu", &dgraph::pair_relu_op);
   m.impl("gather_add_act", &dgraph::gather_add_act_op);
   m.impl("layer_norm_fwd", &dgraph::layer_norm_fwd_op);
+  m.impl("dual_gemm", &dgraph::dual_gemm_op);
   m.impl("layer_norm_bwd", &dgraph::layer_norm_bwd_op);
 }

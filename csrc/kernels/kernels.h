@@ -98,4 +98,18 @@ hipError_t layer_norm_bwd(DType dt, const void* dy, const void* x, const float* 
                           const float* rstd, const float* gamma, void* dx, float* partial,
                           int nblocks, int64_t N, int F, hipStream_t st);
 
+// ---------------------------------------------------------------------------
+// Fused tall-skinny MFMA dual GEMM (dual_gemm.hip), bf16 in / fp32 accumulate:
+//   out = epi(A1 @ B1 (+ A2 @ B2) (+ bias) (+ cin)); B given transposed (Bt[N][K]).
+// N in {128,192,256}; K1, K2 in {128,192,256} (K2 = 0: single GEMM); lda % 8 == 0.
+// relu: writes keep bits to mask_out ("tile32" layout, see dual_gemm.hip);
+// mask_in: zeroes elements whose keep bit is 0. Mask arrays hold
+// ceil(M/256) * 8 * (N/32) * 16 uint64 words.
+// ---------------------------------------------------------------------------
+bool dual_gemm_supported(int64_t N, int64_t K1, int64_t K2);
+hipError_t dual_gemm(const void* A1, int64_t lda1, const void* B1t, int64_t K1, const void* A2,
+                     int64_t lda2, const void* B2t, int64_t K2, const float* bias,
+                     const void* cin, int64_t ldc, void* out, int64_t ldo, int64_t M, int64_t N,
+                     uint64_t* mask_out, const uint64_t* mask_in, bool relu, hipStream_t st);
+
 }  // namespace dgraph

@@ -103,3 +103,29 @@ def linear(x: torch.Tensor, W: torch.Tensor, b=None) -> torch.Tensor:
         x, W = x.to(dt), W.to(dt)
         b = None if b is None else b.to(dt)
     return _LinearFn.apply(x, W, b)
+
+
+def tile32_mask_words(M: int, N: int) -> int:
+    """int64 words of a dual-GEMM keep mask for an [M, N] output."""
+    return (M + 255) // 256 * 8 * (N // 32) * 16
+
+
+def dual_gemm_supported(A1: torch.Tensor, N: int, K2: int = 0) -> bool:
+    ks = (128, 192, 256)
+    return (A1.is_cuda and A1.dtype == torch.bfloat16 and N in ks and A1.shape[1] in ks
+            and (K2 == 0 or K2 in ks) and A1.stride(1) == 1 and A1.stride(0) % 8 == 0)
+
+
+def dual_gemm(A1: torch.Tensor, B1t: torch.Tensor, A2=None, B2t=None, bias=None, cin=None,
+              out=None, relu: bool = False, mask_out=None, mask_in=None) -> torch.Tensor:
+    """``out = epi(A1 B1 (+ A2 B2) (+ bias) (+ cin))`` on the native MFMA kernel
+    (csrc/kernels/dual_gemm.hip); ``B*t`` are the transposed right operands ``[N, K]``."""
+    from .. import _native
+
+    if out is None:
+        out = torch.empty(A1.shape[0], B1t.shape[0], dtype=A1.dtype, device=A1.device)
+    b = None if bias is None else bias.float().contiguous()
+    _native.ops().dual_gemm(A1, B1t.contiguous(), A2,
+                            None if B2t is None else B2t.contiguous(), b, cin, out, mask_out,
+                            mask_in, bool(relu))
+    return out

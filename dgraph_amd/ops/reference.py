@@ -215,3 +215,38 @@ def gather_add_act(Y, P, src, Q, dst, gin, out, act: int):
     else:
         out.copy_(gin[:E].to(cdt) * _act_grad(pre, act))
     return out
+
+
+def tile32_encode(keep: torch.Tensor) -> torch.Tensor:
+    """Keep mask [M, N] -> int64 words in the dual-GEMM "tile32" layout
+    (csrc/kernels/dual_gemm.hip): word[(rb * NT + t) * 16 + r] bit l = keep of
+    (32 rb + (r & 3) + 8 (r >> 2) + 4 (l >> 5), 32 t + (l & 31)); rows padded to 256."""
+    M, N = keep.shape
+    NT = N // 32
+    Mp = (M + 255) // 256 * 256
+    k = torch.zeros(Mp, N, dtype=torch.bool)
+    k[:M] = keep.cpu()
+    lane = torch.arange(64)
+    r = torch.arange(16)
+    rows = (r.unsqueeze(1) & 3) + 8 * (r.unsqueeze(1) >> 2) + 4 * (lane.unsqueeze(0) >> 5)  # [16, 64]
+    cols = lane & 31
+    kt = k.view(Mp // 32, 32, NT, 32)                      # [rb, rr, t, cc]
+    # non-adjacent advanced indices: the broadcast index dims come first -> [16, 64, rb, t]
+    bits = kt[:, rows, :, cols.unsqueeze(0).expand(16, 64)]
+    bits = bits.permute(2, 3, 0, 1).to(torch.int64)        # [rb, t, 16, 64]
+    w = (bits << torch.arange(64, dtype=torch.int64)).sum(-1)  # wraps like uint64
+    return w.reshape(-1)
+
+
+def tile32_decode(words: torch.Tensor, M: int, N: int) -> torch.Tensor:
+    NT = N // 32
+    Mp = (M + 255) // 256 * 256
+    w = words.cpu()[: Mp // 32 * NT * 16].view(Mp // 32, NT, 16, 1)
+    bits = ((w >> torch.arange(64, dtype=torch.int64)) & 1).bool()  # [rb, t, 16, 64]
+    lane = torch.arange(64)
+    r = torch.arange(16)
+    rows = (r.unsqueeze(1) & 3) + 8 * (r.unsqueeze(1) >> 2) + 4 * (lane.unsqueeze(0) >> 5)
+    cols = (lane & 31).unsqueeze(0).expand(16, 64)
+    out = torch.zeros(Mp // 32, 32, NT, 32, dtype=torch.bool)
+    out[:, rows, :, cols] = bits.permute(2, 3, 0, 1)  # -> [16, 64, rb, t]
+    return out.view(Mp, N)[:M]

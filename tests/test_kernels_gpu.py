@@ -389,3 +389,51 @@ def test_linear_split_k_grads(rows):
     torch.testing.assert_close(W.grad.double(), W2.grad, atol=1e-2 * rows ** 0.5 / 10, rtol=1e-3)
     torch.testing.assert_close(b.grad.double(), b2.grad, atol=1e-3 * rows ** 0.5, rtol=1e-3)
     torch.testing.assert_close(x.grad.double(), x2.grad, atol=1e-3, rtol=1e-3)
+
+
+@pytest.mark.parametrize("M", [1, 300, 256 * 3, 70001])
+@pytest.mark.parametrize("N,K1,K2", [(256, 128, 128), (256, 256, 256), (256, 192, 192),
+                                      (192, 256, 0), (128, 192, 256)])
+@pytest.mark.parametrize("mode", ["relu", "plain", "cin_maskin"])
+def test_dual_gemm(M, N, K1, K2, mode):
+    from dgraph_amd.ops.dense import dual_gemm, tile32_mask_words
+
+    g = torch.Generator().manual_seed(M + N + K1)
+    A1 = torch.randn(M, K1, generator=g).to(torch.bfloat16)
+    B1 = (torch.randn(K1, N, generator=g) / K1 ** 0.5).to(torch.bfloat16)
+    A2 = torch.randn(M, K2, generator=g).to(torch.bfloat16) if K2 else None
+    B2 = (torch.randn(K2, N, generator=g) / K2 ** 0.5).to(torch.bfloat16) if K2 else None
+    bias = torch.randn(N, generator=g)
+    ref = A1.float() @ B1.float() + bias
+    if K2:
+        ref += A2.float() @ B2.float()
+    d = lambda t: None if t is None else t.to(DEV)  # noqa: E731
+    kw = dict(A2=d(A2), B2t=None if B2 is None else d(B2.t().contiguous()), bias=d(bias))
+    words = tile32_mask_words(M, N)
+    if mode == "relu":
+        mo = torch.zeros(words, dtype=torch.int64, device=DEV)
+        out = dual_gemm(d(A1), d(B1.t().contiguous()), relu=True, mask_out=mo, **kw)
+        keep = ref > 0
+        torch.testing.assert_close(out.float().cpu(), torch.where(keep, ref, 0.0),
+                                   atol=3e-2, rtol=2e-2)
+        dec = R.tile32_decode(mo, M, N)
+        # rows close to 0 may flip in bf16: compare where |ref| is not tiny
+        sure = ref.abs() > 1e-2
+        assert torch.equal(dec[sure], keep[sure])
+        assert torch.equal(R.tile32_encode(dec), mo.cpu()[:R.tile32_encode(dec).numel()])
+    elif mode == "plain":
+        out = dual_gemm(d(A1), d(B1.t().contiguous()), **kw)
+        torch.testing.assert_close(out.float().cpu(), ref, atol=3e-2, rtol=2e-2)
+    else:
+        cin = torch.randn(M, N, generator=g).to(torch.bfloat16)
+        keep = torch.rand(M, N, generator=g) > 0.4
+        mi = R.tile32_encode(keep).to(DEV)
+        out = dual_gemm(d(A1), d(B1.t().contiguous()), cin=d(cin), mask_in=mi, **kw)
+        exp = torch.where(keep, ref + cin.float(), 0.0)
+        torch.testing.assert_close(out.float().cpu(), exp, atol=3e-2, rtol=2e-2)
+
+
+def test_tile32_roundtrip_cpu():
+    g = torch.Generator().manual_seed(0)
+    keep = torch.rand(333, 192, generator=g) > 0.5
+    assert torch.equal(R.tile32_decode(R.tile32_encode(keep), 333, 192), keep)
