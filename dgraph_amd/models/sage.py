@@ -26,11 +26,11 @@ import torch.nn as nn
 import torch.nn.functional as Fn
 from torch.autograd import Function
 
+from .. import _native
 from ..ops import kernels as K
+from ..ops.dense import (col_sum_f32, dual_gemm, dual_gemm_shape_ok, mm_f32,  # noqa: F401
+                         tile32_mask_words, wgrad)
 from ..parallel.dist_graph import DistGraph
-
-
-from ..ops.dense import col_sum_f32, mm_f32, wgrad  # noqa: F401  (re-exported)
 
 
 class SAGELayerFn(Function):
@@ -227,6 +227,24 @@ class SageWorkspace:
         return self.slots[name][: L * F].view(L, F)
 
 
+def _fusable(t: torch.Tensor, N: int, K1: int, K2: int = 0) -> bool:
+    """Can the native MFMA dual GEMM (csrc/kernels/dual_gemm.hip) run this combine?"""
+    return (t.is_cuda and t.dtype == torch.bfloat16 and _native.available()
+            and dual_gemm_shape_ok(N, K1, K2))
+
+
+def _bwd_fused(specs, dims_p, i: int, need_dx: bool, t: torch.Tensor) -> bool:
+    """Layer i's input gradient is produced by one dual GEMM (pf: g Ws^T + dz Wn^T;
+    aggregate-first with the u-trick: g Ws^T + u Wn^T) — so it can also apply the
+    previous layer's ReLU mask in its epilogue."""
+    _, pf = specs[i]
+    if not need_dx:
+        return False
+    if not pf and dims_p[i + 1] > 2 * dims_p[i]:
+        return False
+    return _fusable(t, dims_p[i], dims_p[i + 1], dims_p[i + 1])
+
+
 class SAGEStackFn(Function):
     """The whole layer stack as ONE autograd node (memory-lean training path).
 
@@ -264,20 +282,39 @@ class SAGEStackFn(Function):
             ws, wn, b = _padded(params, i, dims_p, dt)
             ws_, wn_ = ws, wn
             last = i == n - 1
-            Fo = dims_p[i + 1]
+            Fi, Fo = dims_p[i], dims_p[i + 1]
             y = V("tmp_b" if last else f"act{i + 1}", Fo)
+            # one MFMA dual GEMM for the whole combine (+ bias, ReLU, 1-bit mask) when the
+            # shape is supported and, for a ReLU layer, the backward consumer of its mask
+            # (layer i + 1's input-gradient GEMM) is fused too (same "tile32" mask layout)
+            fused = _fusable(h, Fo, Fi, 0 if pf else Fi) and (
+                not relu or (i + 1 < n and _bwd_fused(specs, dims_p, i + 1, True, h)))
+            mask = None
+            if fused and relu:
+                mask = torch.empty(tile32_mask_words(L, Fo), dtype=torch.int64,
+                                   device=h.device)
             if pf:
                 z = torch.mm(h, wn_, out=V("tmp_a", Fo))
                 graph.aggregate(z, mean=True, out=y)
                 del z
-                y.addmm_(h, ws_)
+                if fused:
+                    dual_gemm(h, ws_.t().contiguous(), bias=b, cin=y, out=y, relu=relu,
+                              mask_out=mask)
+                else:
+                    y.addmm_(h, ws_)
             else:
                 slot = "agg0" if (i == 0 and keep0) else "tmp_a"
-                a = graph.aggregate(h, mean=True, out=V(slot, dims_p[i]))
-                torch.mm(h, ws_, out=y)
-                y.addmm_(a, wn_)
+                a = graph.aggregate(h, mean=True, out=V(slot, Fi))
+                if fused:
+                    dual_gemm(h, ws_.t().contiguous(), a, wn_.t().contiguous(), bias=b, out=y,
+                              relu=relu, mask_out=mask)
+                else:
+                    torch.mm(h, ws_, out=y)
+                    y.addmm_(a, wn_)
                 del a
-            if relu and Fo % 8 == 0 and y.is_contiguous():
+            if fused:
+                masks.append(("t32", mask) if relu else None)
+            elif relu and Fo % 8 == 0 and y.is_contiguous():
                 bits = torch.empty(K.mask_words(y.numel()), dtype=torch.int32, device=y.device)
                 K.bias_relu_pack(y, b, bits, relu=True)
                 masks.append(bits)
@@ -334,6 +371,7 @@ class SAGEStackFn(Function):
                 g = g.clone()  # never modify the caller's gradient in place
         grads = [None] * len(params)
         dx0 = None
+        g_masked = False  # g already carries this layer's ReLU derivative (fused epilogue)
         for i in reversed(range(n)):
             relu, pf = specs[i]
             ws, wn, b = params[3 * i], params[3 * i + 1], params[3 * i + 2]
@@ -342,7 +380,11 @@ class SAGEStackFn(Function):
             m = masks[i]
             masks[i] = None
             if relu:
-                if m.dtype == torch.int32:
+                if isinstance(m, tuple):
+                    if not g_masked:
+                        raise RuntimeError("SAGEStackFn: tile32 ReLU mask was not consumed by "
+                                           "the fused input-gradient GEMM")
+                elif m.dtype == torch.int32:
                     K.relu_mask_bwd(g, m)
                 else:
                     g = torch.where(m > 0, g, torch.zeros((), dtype=g.dtype, device=g.device))
@@ -351,6 +393,11 @@ class SAGEStackFn(Function):
             acts[i] = None
             recyclable = i > 0  # hidden activations are private to this node
             need_dx = i > 0 or ctx.x0_requires_grad
+            # the previous layer's mask, applied inside the fused dx GEMM when it is tile32
+            prev = masks[i - 1] if i > 0 else None
+            fuse_dx = _bwd_fused(specs, dims, i, need_dx, g)
+            mask_in = prev[1] if (fuse_dx and isinstance(prev, tuple)) else None
+            g_masked = mask_in is not None
             grads[3 * i] = wgrad(x, g)[:r_in, :r_out].to(ws.dtype)
             if b is not None:
                 grads[3 * i + 2] = col_sum_f32(g)[:r_out].to(b.dtype)
@@ -359,8 +406,12 @@ class SAGEStackFn(Function):
                 dz = graph.aggregate_T(g, mean=True, out=V("tmp_b", dims[i + 1]))
                 grads[3 * i + 1] = wgrad(x, dz)[:r_in, :r_out].to(wn.dtype)
                 if need_dx:
-                    dx = torch.mm(g, ws_.t(), out=x) if recyclable else g @ ws_.t()
-                    dx.addmm_(dz, wn_.t())
+                    if fuse_dx:
+                        dx = dual_gemm(g, ws_, dz, wn_, out=x if recyclable else None,
+                                       mask_in=mask_in)
+                    else:
+                        dx = torch.mm(g, ws_.t(), out=x) if recyclable else g @ ws_.t()
+                        dx.addmm_(dz, wn_.t())
                 del dz
             elif need_dx and dims[i + 1] <= 2 * dims[i]:
                 # u = A^T g gives both gradients with ONE SpMM at F_out:
@@ -369,8 +420,14 @@ class SAGEStackFn(Function):
                 u_name = "tmp_b" if (i == n - 1 and ctx.out_rows is not None) else "tmp_a"
                 u = graph.aggregate_T(g, mean=True, out=V(u_name, dims[i + 1]))
                 grads[3 * i + 1] = wgrad(x, u)[:r_in, :r_out].to(wn.dtype)
-                dx = torch.mm(g, ws_.t(), out=x) if recyclable else g @ ws_.t()
-                dx.addmm_(u, wn_.t())
+                if fuse_dx:
+                    # W_self / W_neigh as stored ([F_in, F_out]) are the transposed right
+                    # operands of g W^T: no weight copy
+                    dx = dual_gemm(g, ws_, u, wn_, out=x if recyclable else None,
+                                   mask_in=mask_in)
+                else:
+                    dx = torch.mm(g, ws_.t(), out=x) if recyclable else g @ ws_.t()
+                    dx.addmm_(u, wn_.t())
                 del u
             else:
                 # tmp_a may still hold g for the last layer: recompute into tmp_b then

@@ -129,3 +129,8 @@ def dual_gemm(A1: torch.Tensor, B1t: torch.Tensor, A2=None, B2t=None, bias=None,
                             None if B2t is None else B2t.contiguous(), b, cin, out, mask_out,
                             mask_in, bool(relu))
     return out
+
+
+def dual_gemm_shape_ok(N: int, K1: int, K2: int = 0) -> bool:
+    ks = (128, 192, 256)
+    return N in ks and K1 in ks and (K2 == 0 or K2 in ks)
