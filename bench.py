@@ -183,7 +183,7 @@ def main():
         }
         print(json.dumps(rec), flush=True)
     comm.destroy()
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -47,12 +47,17 @@ def main():
         B1t = B1.t().contiguous()
         B2t = B2.t().contiguous() if K2 else None
         relu = K2 > 0
-        fused = timeit(lambda: dual_gemm(A1, B1t, A2, B2t, bias=bias, out=out, relu=relu,
-                                         mask_out=mo if relu else None))
+        # K2 == 0 is the SAGE last-layer combine: out = A1 B1 + bias + out (cin in place)
+        cin = out if not K2 else None
+        fused = timeit(lambda: dual_gemm(A1, B1t, A2, B2t, bias=bias, cin=cin, out=out,
+                                         relu=relu, mask_out=mo if relu else None))
         bits = torch.empty(K.mask_words(M * N), dtype=torch.int32, device=dev)
 
         def lib():
-            torch.mm(A1, B1, out=out)
+            if K2:
+                torch.mm(A1, B1, out=out)
+            else:
+                out.addmm_(A1, B1)
             if K2:
                 out.addmm_(A2, B2)
             if relu:
@@ -61,7 +66,7 @@ def main():
                 out.add_(bias.to(out.dtype))
 
         ref_ms = timeit(lib)
-        nbytes = (M * (K1 + K2) + M * N) * 2
+        nbytes = (M * (K1 + K2) + M * N * (1 if K2 else 2)) * 2
         res[spec] = {"fused_ms": fused, "library_ms": ref_ms, "speedup": ref_ms / fused,
                      "fused_TBps": nbytes / fused / 1e9}
         print(f"N={N} K1={K1} K2={K2}: fused {fused:.2f} ms ({nbytes / fused / 1e9:.2f} TB/s) "

@@ -390,7 +390,11 @@ void dual_gemm_op(const at::Tensor& A1, const at::Tensor& B1t, const c10::option
   const int64_t M = A1.size(0), K1 = A1.size(1), N = B1t.size(0);
   TORCH_CHECK(B1t.size(1) == K1 && B1t.is_contiguous(), "B1t must be contiguous [N, K1]");
   TORCH_CHECK(out.size(0) == M && out.size(1) == N, "out must be [M, N]");
-  TORCH_CHECK(A1.stride(0) % 8 == 0 && out.stride(0) % 1 == 0, "A1 row stride % 8");
+  // the kernel moves A, cin and out rows in 16-B vectors
+  auto al16 = [](const at::Tensor& t) {
+    return t.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0;
+  };
+  TORCH_CHECK(al16(A1) && al16(out), "dual_gemm: A1/out rows must be 16-B aligned");
   const void* a2 = nullptr;
   const void* b2 = nullptr;
   int64_t K2 = 0, lda2 = 0;
@@ -400,7 +404,7 @@ void dual_gemm_op(const at::Tensor& A1, const at::Tensor& B1t, const c10::option
     chk_bf16(*B2t, "B2t");
     K2 = A2->size(1);
     TORCH_CHECK(A2->size(0) == M && B2t->size(0) == N && B2t->size(1) == K2 &&
-                    B2t->is_contiguous() && A2->stride(0) % 8 == 0,
+                    B2t->is_contiguous() && al16(*A2),
                 "A2/B2t shape mismatch");
     a2 = A2->data_ptr();
     b2 = B2t->data_ptr();
@@ -414,7 +418,8 @@ void dual_gemm_op(const at::Tensor& A1, const at::Tensor& B1t, const c10::option
   int64_t ldc = 0;
   if (cin.has_value() && cin->defined()) {
     chk_bf16(*cin, "cin");
-    TORCH_CHECK(cin->size(0) == M && cin->size(1) == N, "cin must be [M, N]");
+    TORCH_CHECK(cin->size(0) == M && cin->size(1) == N && al16(*cin),
+                "cin must be [M, N] with 16-B aligned rows");
     cp = cin->data_ptr();
     ldc = cin->stride(0);
   }

@@ -179,12 +179,26 @@ __global__ __launch_bounds__(kThreads, 1) void dual_gemm_kernel(
       uint64_t keep_in = 0;
       if (mask_in && lane < 16) keep_in = mask_in[(rb * NT + t) * 16 + lane];
       uint64_t my_word = 0;
+      if (cin) {
+        // stage the tile's cin rows through the LDS tile with coalesced 16-B loads (per-
+        // element 2-byte loads in the C layout ran this kernel 3x slower)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int rr = (lane >> 2) + 16 * q;
+          const int64_t row = row0 + rr;
+          uint4 v = make_uint4(0, 0, 0, 0);
+          if (row < M) v = *reinterpret_cast<const uint4*>(cin + row * ldc + t * 32 + (lane & 3) * 8);
+          *reinterpret_cast<uint4*>(&sE[rr * kEW + (lane & 3) * 8]) = v;
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int rr = (r & 3) + 8 * (r >> 2) + rsub;
         const int64_t row = row0 + rr;
         float v = acc[u][r] + bv;
-        if (cin && row < M) v += bf16_to_f32(cin[row * ldc + col]);
+        if (cin) v += bf16_to_f32(sE[rr * kEW + col_l]);
         if (mask_in) {
           const uint64_t w =
               (static_cast<uint64_t>(__shfl(static_cast<int>(keep_in), r, 64)) & 0xffffffffull) |
