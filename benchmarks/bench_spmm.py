@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--global-frac", type=float, default=0.05)
     ap.add_argument("--variants", default="1:0,2:0,2:1")
     ap.add_argument("--slices", default="1")
+    ap.add_argument("--mean", default="row", choices=["row", "col"],
+                    help="mean as a row scale (forward) or a column scale (transposed)")
     a = ap.parse_args()
     from dgraph_amd import _native
     from dgraph_amd.data.synthetic import SHAPES, build_partition
@@ -36,6 +38,7 @@ def main():
     p = build_partition(shape, 0, 1, dev, global_frac=a.global_frac)
     csr = p["csr"]
     inv = csr.inv_degree()
+    sc = {"row_scale": inv} if a.mean == "row" else {"col_scale": inv}
     variants = [tuple(int(v) for v in s.split(":")) for s in a.variants.split(",")]
     res = {}
     for F in [int(f) for f in a.feats.split(",")]:
@@ -49,7 +52,7 @@ def main():
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 torch.cuda.synchronize()
                 s.record()
-                K.spmm(csr.rowptr, csr.col, x, out, row_scale=inv)
+                K.spmm(csr.rowptr, csr.col, x, out, **sc)
                 e.record()
                 torch.cuda.synchronize()
                 if r > 0:
@@ -62,7 +65,9 @@ def main():
                     assert err < 5e-2, f"variant {v} differs by {err}"
         nbytes = csr.nnz * (F * 2 + csr.col.element_size()) + p["L"] * F * 2
         # feature-sliced execution (narrower gathered rows -> smaller per-XCD working set)
-        for s in [int(v) for v in a.slices.split(",") if int(v) > 1 and F % int(v) == 0]:
+        for s, v in [(int(sv), v) for sv in a.slices.split(",") for v in variants
+                     if int(sv) > 1 and F % int(sv) == 0]:
+            ops.set_spmm_config(*v)
             ts = []
             w = F // s
             for r in range(a.rounds + 1):
@@ -71,14 +76,15 @@ def main():
                 st.record()
                 for j in range(s):
                     K.spmm(csr.rowptr, csr.col, x[:, j * w:(j + 1) * w],
-                           out[:, j * w:(j + 1) * w], row_scale=inv)
+                           out[:, j * w:(j + 1) * w], **sc)
                 en.record()
                 torch.cuda.synchronize()
                 if r > 0:
                     ts.append(st.elapsed_time(en))
             ms = statistics.median(ts)
-            res[f"F{F}_slices{s}"] = {"ms": round(ms, 3), "TBps": round(nbytes / ms / 1e9, 3)}
-            print(f"F={F:4d} slices={s}: {ms:8.2f} ms  {nbytes / ms / 1e9:6.2f} TB/s effective",
+            res[f"F{F}_slices{s}_v{v[0]}_xcd{v[1]}"] = {"ms": round(ms, 3),
+                                                         "TBps": round(nbytes / ms / 1e9, 3)}
+            print(f"F={F:4d} slices={s} variant={v[0]} xcd={v[1]}: {ms:8.2f} ms  {nbytes / ms / 1e9:6.2f} TB/s effective",
                   flush=True)
         for v in variants:
             ms = statistics.median(times[v])
@@ -87,7 +93,7 @@ def main():
             print(f"F={F:4d} variant={v[0]} xcd={v[1]}: {ms:8.2f} ms  "
                   f"{nbytes / ms / 1e9:6.2f} TB/s effective", flush=True)
         del x, out, ref
-    ops.set_spmm_config(2, 1)
+    ops.set_spmm_config(2, 2, 128)
     print(json.dumps({"shape": shape.name, "nnz": csr.nnz, "rows": p["L"], "results": res}))
 
 

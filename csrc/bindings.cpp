@@ -444,12 +444,13 @@ void dual_gemm_op(const at::Tensor& A1, const at::Tensor& B1t, const c10::option
 
 int64_t tile32_mask_words_op(int64_t M, int64_t N) { return dgraph::tile32_mask_words(M, N); }
 
-void set_spmm_config_op(int64_t variant, int64_t xcd) {
-  dgraph::set_spmm_config(static_cast<int>(variant), static_cast<int>(xcd));
+void set_spmm_config_op(int64_t variant, int64_t xcd, int64_t pass_cols) {
+  dgraph::set_spmm_config(static_cast<int>(variant), static_cast<int>(xcd),
+                          static_cast<int>(pass_cols));
 }
 
 TORCH_LIBRARY(dgraph_amd, m) {
-  m.def("set_spmm_config(int variant, int xcd) -> ()", &set_spmm_config_op);
+  m.def("set_spmm_config(int variant, int xcd, int pass_cols=-1) -> ()", &set_spmm_config_op);
   m.def("bias_relu_pack(Tensor(a!) y, Tensor? bias, Tensor(b!)? bits, bool relu) -> ()");
   m.def("relu_mask_bwd(Tensor(a!) g, Tensor bits) -> ()");
   m.def("col_sum(Tensor g) -> Tensor");

@@ -22,8 +22,11 @@ enum class IType : int { I32 = 0, I64 = 1 };
 // Deterministic: one wavefront owns an output row, fixed summation order.
 // ---------------------------------------------------------------------------
 // Kernel selection (tuning / A-B measurement): variant 1 = per-group index loads,
-// 2 = cooperative index load + shuffles (default); xcd = XCD-aware row chunking.
-void set_spmm_config(int variant, int xcd);
+// 2 = cooperative index load + shuffles (default); xcd: row mapping (0 grid-stride,
+// 1 XCD-chunked grid-stride, 2 XCD-chunked in-order (default), 3 in-order); pass_cols:
+// bf16 rows wider than this (and a multiple of it) run as column passes (0 = never).
+// Negative arguments leave a setting unchanged.
+void set_spmm_config(int variant, int xcd, int pass_cols);
 
 hipError_t spmm_csr(DType dt, IType it, const int64_t* rowptr, const void* col,
                     const float* ew, int heads, int head_dim, const float* col_scale,

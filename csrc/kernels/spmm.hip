@@ -165,13 +165,20 @@ __global__ __launch_bounds__(256) void spmm_csr_v2_kernel(
             const int kk = k0 + g + u * G;
             const int src = kk < n ? kk : 0;
             const int64_t c = static_cast<int64_t>(__shfl(my_c, src, kWave));
-            float wu = __shfl(my_w, src, kWave);
-            if (ew) wu *= ew[(base + src) * heads + h];
-            w[u] = kk < n ? wu : 0.f;
             // unconditional load (padding slots re-read slot 0 with weight 0; lanes past
             // F read column 0): a per-slot "load or zero" select makes hipcc branch
             // around each load and drain vmcnt per slot (guide §5 trap (c))
             v[u] = *reinterpret_cast<const R*>(x + c * ldx + (active ? f : 0));
+          }
+          // weights after the row loads are issued: the col_scale gather (a dependent
+          // load of my_c) then overlaps the row gathers instead of gating them
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const int kk = k0 + g + u * G;
+            const int src = kk < n ? kk : 0;
+            float wu = __shfl(my_w, src, kWave);
+            if (ew) wu *= ew[(base + src) * heads + h];
+            w[u] = kk < n ? wu : 0.f;
           }
 #pragma unroll
           for (int u = 0; u < U; ++u) {
@@ -208,7 +215,13 @@ __global__ __launch_bounds__(256) void spmm_csr_v2_kernel(
 }
 
 int g_spmm_variant = 2;  // 1 = per-group index loads, 2 = cooperative + shuffles
-int g_spmm_xcd = 1;
+// 0 = grid-stride, 1 = XCD-chunked grid-stride, 2 = XCD-chunked in-order (default),
+// 3 = in-order without chunking. The in-order mappings keep the resident waves on a
+// narrow advancing row window, so the neighbour rows they gather (which cluster near the
+// row ids on locality-ordered graphs) are reused from the Infinity Cache: papers100M-
+// shaped graph, F=256: 313 ms (1) -> 211 ms (2) (benchmarks/bench_spmm.py).
+int g_spmm_xcd = 2;
+int g_spmm_pass_cols = 128;  // bf16 rows wider than this run as column passes
 
 template <typename T, typename IdxT, int VEC>
 hipError_t launch_lpr(const int64_t* rowptr, const IdxT* col, const float* ew, int heads,
@@ -216,8 +229,16 @@ hipError_t launch_lpr(const int64_t* rowptr, const IdxT* col, const float* ew, i
                       T* out, int64_t ldo, int64_t nrows, int F, float beta, hipStream_t st) {
   const int lanes_needed = (F + VEC - 1) / VEC;
   int64_t blocks = cap_blocks((nrows + 3) / 4, 256 * 32);
-  const bool xcd = g_spmm_xcd && blocks >= 64;
+  if (g_spmm_xcd == 3) blocks = (nrows + 3) / 4;  // in-order, one row per wave, no chunking
+  const bool xcd = (g_spmm_xcd == 1 || g_spmm_xcd == 2) && blocks >= 64;
   if (xcd) blocks = (blocks / 8) * 8;
+  if (xcd && g_spmm_xcd == 2) {
+    // in-order mapping: enough blocks that every wave owns ONE row of its XCD's chunk,
+    // so each XCD's resident waves sweep a narrow, advancing row window (in dispatch
+    // order) instead of a grid-stride spread over the whole chunk
+    const int64_t chunk = (nrows + 7) / 8;
+    blocks = 8 * ((chunk + 3) / 4);
+  }
   dim3 grid(static_cast<unsigned>(blocks)), block(256);
   if (g_spmm_variant == 2) {
     // U rows in flight per lane group: ~16 neighbour rows per wave
@@ -277,9 +298,10 @@ hipError_t launch_vec(const int64_t* rowptr, const IdxT* col, const float* ew, i
 
 }  // namespace
 
-void set_spmm_config(int variant, int xcd) {
+void set_spmm_config(int variant, int xcd, int pass_cols) {
   if (variant == 1 || variant == 2) g_spmm_variant = variant;
-  if (xcd == 0 || xcd == 1) g_spmm_xcd = xcd;
+  if (xcd >= 0 && xcd <= 3) g_spmm_xcd = xcd;
+  if (pass_cols >= 0) g_spmm_pass_cols = pass_cols;
 }
 
 hipError_t spmm_csr(DType dt, IType it, const int64_t* rowptr, const void* col,
@@ -295,6 +317,24 @@ hipError_t spmm_csr(DType dt, IType it, const int64_t* rowptr, const void* col,
   if (dt == DType::F32) {
     if (it == IType::I32) return launch_vec<float, int32_t>(DG_ARGS(float, int32_t));
     return launch_vec<float, int64_t>(DG_ARGS(float, int64_t));
+  }
+  const int pc = g_spmm_pass_cols;
+  if (heads == 1 && pc > 0 && F > pc && F % pc == 0) {
+    // column passes of 256-B rows: a pass's gathered window (rows near the front times
+    // 256 B) stays cache-resident where a full 512-B row window does not (-11% at F=256)
+    for (int c0 = 0; c0 < F; c0 += pc) {
+      const auto* xp = static_cast<const uint16_t*>(x) + c0;
+      auto* op = static_cast<uint16_t*>(out) + c0;
+      hipError_t err = it == IType::I32
+          ? launch_vec<uint16_t, int32_t>(rowptr, static_cast<const int32_t*>(col), ew, 1, pc,
+                                          col_scale, row_scale, xp, ldx, op, ldo, nrows, pc,
+                                          beta, stream)
+          : launch_vec<uint16_t, int64_t>(rowptr, static_cast<const int64_t*>(col), ew, 1, pc,
+                                          col_scale, row_scale, xp, ldx, op, ldo, nrows, pc,
+                                          beta, stream);
+      if (err != hipSuccess) return err;
+    }
+    return hipSuccess;
   }
   if (it == IType::I32) return launch_vec<uint16_t, int32_t>(DG_ARGS(uint16_t, int32_t));
   return launch_vec<uint16_t, int64_t>(DG_ARGS(uint16_t, int64_t));

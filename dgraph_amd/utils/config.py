@@ -27,7 +27,8 @@ class CommConfig:
 @dataclass
 class KernelConfig:
     spmm_variant: int = 2
-    spmm_xcd_remap: bool = True
+    spmm_row_map: int = 2  # 0 grid-stride, 1 XCD grid-stride, 2 XCD in-order, 3 in-order
+    spmm_pass_cols: int = 128
     deterministic: bool = True      # segment sums only, no float atomics
 
 
@@ -88,7 +89,8 @@ class RunConfig:
 
         if _native.available():
             _native.ops().set_spmm_config(self.kernels.spmm_variant,
-                                          int(self.kernels.spmm_xcd_remap))
+                                          self.kernels.spmm_row_map,
+                                          self.kernels.spmm_pass_cols)
         os.environ["DGRAPH_SHMEM_TRANSPORT"] = self.comm.shmem_transport
         return self
 

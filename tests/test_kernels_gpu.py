@@ -72,7 +72,7 @@ def test_spmm_strided_and_empty():
     torch.testing.assert_close(out.cpu(), ref, atol=1e-4, rtol=1e-4)
 
 
-@pytest.mark.parametrize("variant,xcd", [(1, 0), (2, 0), (2, 1)])
+@pytest.mark.parametrize("variant,xcd", [(1, 0), (2, 0), (2, 1), (2, 2), (2, 3)])
 @pytest.mark.parametrize("F", [16, 40, 64, 128, 256])
 def test_spmm_variants_agree_ragged_rows(variant, xcd, F):
     """Rows whose degrees are not multiples of the lane-group count and exceed one
@@ -91,8 +91,30 @@ def test_spmm_variants_agree_ragged_rows(variant, xcd, F):
         ops.set_spmm_config(variant, xcd)
         out = K.spmm(rowptr.to(DEV), col.to(DEV), x)
     finally:
-        ops.set_spmm_config(2, 1)
+        ops.set_spmm_config(2, 2)
     torch.testing.assert_close(out.cpu(), ref, atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize("pass_cols", [0, 64, 128])
+@pytest.mark.parametrize("F", [192, 256])
+def test_spmm_column_passes_bf16(pass_cols, F):
+    """bf16 rows wider than ``pass_cols`` run as column passes (col_scale + beta too)."""
+    from dgraph_amd import _native
+
+    csr = _rand_csr(900, 800, 37, torch.int32, DEV, skew=True)
+    x = torch.randn(800, F, device=DEV).to(torch.bfloat16)
+    cs = torch.rand(800, device=DEV)
+    out0 = torch.randn(900, F, device=DEV).to(torch.bfloat16)
+    ref = R.spmm(csr.rowptr.cpu(), csr.col.cpu(), x.float().cpu(), out0.float().cpu(),
+                 col_scale=cs.cpu(), beta=0.5)
+    ops = _native.ops()
+    try:
+        ops.set_spmm_config(2, 2, pass_cols)
+        out = out0.clone()
+        K.spmm(csr.rowptr, csr.col, x, out, col_scale=cs, beta=0.5)
+    finally:
+        ops.set_spmm_config(2, 2, 128)
+    torch.testing.assert_close(out.float().cpu(), ref, atol=0.1, rtol=2e-2)
 
 
 def test_spmm_deterministic():
