@@ -23,7 +23,9 @@ def main():
     ap.add_argument("--feats", default="128,172,256")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--global-frac", type=float, default=0.05)
-    ap.add_argument("--variants", default="1:0,2:0,2:1")
+    ap.add_argument("--window", type=int, default=1 << 14)
+    ap.add_argument("--variants", default="2:2:128,4:0:128,4:2:64",
+                    help="comma list of variant:row_map:pass_cols")
     ap.add_argument("--slices", default="1")
     ap.add_argument("--mean", default="row", choices=["row", "col"],
                     help="mean as a row scale (forward) or a column scale (transposed)")
@@ -35,7 +37,7 @@ def main():
     ops = _native.ops()
     dev = torch.device("cuda", 0)
     shape = SHAPES[a.shape] if a.scale == 1.0 else SHAPES[a.shape].scaled(a.scale)
-    p = build_partition(shape, 0, 1, dev, global_frac=a.global_frac)
+    p = build_partition(shape, 0, 1, dev, global_frac=a.global_frac, window=a.window)
     csr = p["csr"]
     inv = csr.inv_degree()
     sc = {"row_scale": inv} if a.mean == "row" else {"col_scale": inv}
@@ -90,10 +92,10 @@ def main():
             ms = statistics.median(times[v])
             res[f"F{F}_v{v[0]}_xcd{v[1]}"] = {"ms": round(ms, 3),
                                               "TBps": round(nbytes / ms / 1e9, 3)}
-            print(f"F={F:4d} variant={v[0]} xcd={v[1]}: {ms:8.2f} ms  "
+            print(f"F={F:4d} variant={v} window={a.window}: {ms:8.2f} ms  "
                   f"{nbytes / ms / 1e9:6.2f} TB/s effective", flush=True)
         del x, out, ref
-    ops.set_spmm_config(2, 2, 128)
+    ops.set_spmm_config(-1, -1)
     print(json.dumps({"shape": shape.name, "nnz": csr.nnz, "rows": p["L"], "results": res}))
 
 

@@ -214,14 +214,204 @@ __global__ __launch_bounds__(256) void spmm_csr_v2_kernel(
   }
 }
 
-int g_spmm_variant = 2;  // 1 = per-group index loads, 2 = cooperative + shuffles
+// v3 (tried, removed): the v2 data flow with packed-fp32 accumulate and no per-element
+// padding select. Same time as v2 (76.7 vs 76.9 ms at F=128): v2 is not VALU bound, it
+// pays a fixed ~40 ms per pass for its one-row-per-wave structure (see v4).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// v4 (bf16 rows, one head): ROW-GROUP kernel. v2/v3 give a whole wave to one row and
+// split its ~30 neighbours over the lane groups, so every row pays a cross-group
+// butterfly, a dependent rowptr -> col -> row chain and its own wave launch: ~40 ms of
+// fixed cost per pass over the papers100M CSR, whatever the width. That fixed cost is
+// what makes narrow passes (whose neighbour windows fit the 4 MiB per-XCD L2) lose.
+// v4 gives each LPR-lane group its OWN row (G = 64/LPR consecutive rows per wave):
+//   * no cross-lane reduction at all; one 16-B store per lane writes G rows at once;
+//   * each lane loads one column id of its group's row per chunk of LPR neighbours, and
+//     the next chunk's ids are prefetched while the current chunk's rows are in flight;
+//   * neighbour c of row g is broadcast in-group with one ds_bpermute, its 16-B slice is
+//     unpacked and added with packed fp32 math (v_pk_fma_f32, 1.5 VALU per element);
+//   * trip count = the largest degree of the G rows (wave-uniform); slots past a row's
+//     degree read row 0 with weight 0 (no branches around loads).
+template <typename IdxT, int LPR, bool WEIGHTED, bool XCD>
+__global__ __launch_bounds__(256) void spmm_bf16_rowgroup_kernel(
+    const int64_t* __restrict__ rowptr, const IdxT* __restrict__ col,
+    const float* __restrict__ ew, const float* __restrict__ col_scale,
+    const float* __restrict__ row_scale, const uint16_t* __restrict__ x, int64_t ldx,
+    uint16_t* __restrict__ out, int64_t ldo, int64_t nrows, int F, float beta) {
+  constexpr int VEC = 8;
+  constexpr int G = kWave / LPR;
+  constexpr int U = LPR < 8 ? LPR : 8;  // neighbour rows in flight per lane per batch
+  const int lane = threadIdx.x & (kWave - 1);
+  const int g = lane / LPR;
+  const int l = lane % LPR;
+  const int wpb = blockDim.x >> 6;
+  const int64_t ngroups = (nrows + G - 1) / G;
+  int64_t q0, qstep, qend;
+  if constexpr (XCD) {
+    const int nx = 8;
+    const int64_t bx = blockIdx.x % nx;
+    const int64_t chunk = (ngroups + nx - 1) / nx;
+    const int64_t lo = bx * chunk;
+    qend = lo + chunk < ngroups ? lo + chunk : ngroups;
+    q0 = lo + (blockIdx.x / nx) * wpb + (threadIdx.x >> 6);
+    qstep = (gridDim.x / nx) * wpb;
+  } else {
+    q0 = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+    qstep = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
+    qend = ngroups;
+  }
+  const uint32_t ldx32 = static_cast<uint32_t>(ldx);
+  const int f = l * VEC;  // launcher guarantees F <= LPR * VEC
+  const bool active = f < F;
+  const uint16_t* xf = x + (active ? f : 0);
+  for (int64_t q = q0; q < qend; q += qstep) {
+    const int64_t r = q * G + g;
+    const bool has_row = r < nrows;
+    const int64_t s = has_row ? rowptr[r] : 0;
+    const int deg = has_row ? static_cast<int>(rowptr[r + 1] - s) : 0;
+    int maxdeg = deg;
+#pragma unroll
+    for (int off = LPR; off < kWave; off <<= 1) {
+      const int o = __shfl_xor(maxdeg, off, kWave);
+      maxdeg = o > maxdeg ? o : maxdeg;
+    }
+    f32x2 acc[VEC / 2];
+#pragma unroll
+    for (int i = 0; i < VEC / 2; ++i) acc[i] = f32x2{0.f, 0.f};
+    IdxT my_c = l < deg ? col[s + l] : IdxT(0);
+    for (int k0 = 0; k0 < maxdeg; k0 += LPR) {
+      // prefetch the next chunk's ids (and weights) before this chunk's row loads
+      const int kn = k0 + LPR + l;
+      IdxT nx_c = IdxT(0);
+      if (k0 + LPR < maxdeg && kn < deg) nx_c = col[s + kn];
+      float my_w = 0.f;
+      if constexpr (WEIGHTED) {
+        if (k0 + l < deg) {
+          my_w = ew ? ew[s + k0 + l] : 1.f;
+          if (col_scale) my_w *= col_scale[my_c];
+        }
+      }
+#pragma unroll
+      for (int j0 = 0; j0 < LPR; j0 += U) {
+        if (j0 > 0 && k0 + j0 >= maxdeg) break;  // wave-uniform: no all-padding batch
+        uint4 v[U];
+        uint32_t c[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          c[u] = static_cast<uint32_t>(__shfl(static_cast<int>(my_c), g * LPR + j0 + u, kWave));
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          v[u] = *reinterpret_cast<const uint4*>(xf + static_cast<uint64_t>(c[u]) * ldx32);
+        float w[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if constexpr (WEIGHTED) {
+            w[u] = __shfl(my_w, g * LPR + j0 + u, kWave);  // 0 past the degree
+          } else {
+            w[u] = (k0 + j0 + u < deg) ? 1.f : 0.f;
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const uint32_t d[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+          const f32x2 ww{w[u], w[u]};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const f32x2 t{__uint_as_float(d[i] << 16), __uint_as_float(d[i] & 0xffff0000u)};
+            acc[i] = __builtin_elementwise_fma(t, ww, acc[i]);
+          }
+        }
+      }
+      my_c = nx_c;
+    }
+    if (has_row && active) {
+      const float rs = row_scale ? row_scale[r] : 1.f;
+      uint16_t* o = out + r * ldo + f;
+      float res[VEC];
+      if (beta != 0.f) {
+        float old[VEC];
+        load_vec_f32<uint16_t, VEC>(o, old);
+#pragma unroll
+        for (int i = 0; i < VEC / 2; ++i) {
+          res[2 * i] = fmaf(acc[i].x, rs, beta * old[2 * i]);
+          res[2 * i + 1] = fmaf(acc[i].y, rs, beta * old[2 * i + 1]);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < VEC / 2; ++i) {
+          res[2 * i] = acc[i].x * rs;
+          res[2 * i + 1] = acc[i].y * rs;
+        }
+      }
+      store_vec_f32<uint16_t, VEC>(o, res);
+    }
+  }
+}
+
+template <typename IdxT>
+hipError_t launch_rowgroup(const int64_t* rowptr, const IdxT* col, const float* ew,
+                           const float* cs, const float* rs, const uint16_t* x, int64_t ldx,
+                           uint16_t* out, int64_t ldo, int64_t nrows, int F, float beta,
+                           bool xcd_mode, hipStream_t st) {
+  // one pass covers LPR * 8 columns; the caller splits wider rows into passes
+  const int lanes = (F + 7) / 8;
+  const int LPR = lanes <= 4 ? 4 : lanes <= 8 ? 8 : lanes <= 16 ? 16 : lanes <= 32 ? 32 : 64;
+  const int64_t G = kWave / LPR;
+  const int64_t ngroups = (nrows + G - 1) / G;
+  int64_t blocks = (ngroups + 3) / 4;
+  bool xcd = xcd_mode && blocks >= 64;
+  if (xcd) blocks = 8 * (((ngroups + 7) / 8 + 3) / 4);  // in-order: one group per wave
+  if (blocks > 0x7fffffff) return hipErrorInvalidValue;
+  const bool weighted = ew != nullptr || cs != nullptr;
+  dim3 grid(static_cast<unsigned>(blocks)), block(256);
+#define DG_RG(LPR_)                                                                          \
+  if (LPR == LPR_) {                                                                         \
+    if (weighted) {                                                                          \
+      if (xcd)                                                                               \
+        hipLaunchKernelGGL((spmm_bf16_rowgroup_kernel<IdxT, LPR_, true, true>), grid, block, \
+                           0, st, rowptr, col, ew, cs, rs, x, ldx, out, ldo, nrows, F, beta); \
+      else                                                                                   \
+        hipLaunchKernelGGL((spmm_bf16_rowgroup_kernel<IdxT, LPR_, true, false>), grid,       \
+                           block, 0, st, rowptr, col, ew, cs, rs, x, ldx, out, ldo, nrows,   \
+                           F, beta);                                                         \
+    } else {                                                                                 \
+      if (xcd)                                                                               \
+        hipLaunchKernelGGL((spmm_bf16_rowgroup_kernel<IdxT, LPR_, false, true>), grid,       \
+                           block, 0, st, rowptr, col, ew, cs, rs, x, ldx, out, ldo, nrows,   \
+                           F, beta);                                                         \
+      else                                                                                   \
+        hipLaunchKernelGGL((spmm_bf16_rowgroup_kernel<IdxT, LPR_, false, false>), grid,      \
+                           block, 0, st, rowptr, col, ew, cs, rs, x, ldx, out, ldo, nrows,   \
+                           F, beta);                                                         \
+    }                                                                                        \
+    return hipGetLastError();                                                                \
+  }
+  DG_RG(4)
+  DG_RG(8)
+  DG_RG(16)
+  DG_RG(32)
+  DG_RG(64)
+#undef DG_RG
+  return hipErrorInvalidValue;
+}
+
+// 1 = per-group index loads, 2 = cooperative + shuffles (fp32 and unaligned bf16 rows),
+// 4 = row groups (bf16, 16-B aligned rows: the default). papers100M-shaped CSR, window
+// 16384, bf16: F=128 95.3 ms (v2, xcd 2, 128-col passes) -> 64.2 ms (v4, xcd 0, 64-col
+// passes); F=256 190.8 -> 129.1 ms (benchmarks/bench_spmm.py). With row groups the plain
+// in-order grid (all XCDs on one advancing row band) beats XCD-chunking by 2-7 %, and
+// 64-column passes cost the same per column as 128 (192 = 3 x 64 beats 128 + 64).
+constexpr int kSpmmDefaultVariant = 4;
+constexpr int kSpmmDefaultXcd = 0;
+constexpr int kSpmmDefaultPassCols = 64;
+int g_spmm_variant = kSpmmDefaultVariant;
 // 0 = grid-stride, 1 = XCD-chunked grid-stride, 2 = XCD-chunked in-order (default),
 // 3 = in-order without chunking. The in-order mappings keep the resident waves on a
 // narrow advancing row window, so the neighbour rows they gather (which cluster near the
 // row ids on locality-ordered graphs) are reused from the Infinity Cache: papers100M-
 // shaped graph, F=256: 313 ms (1) -> 211 ms (2) (benchmarks/bench_spmm.py).
-int g_spmm_xcd = 2;
-int g_spmm_pass_cols = 128;  // bf16 rows wider than this run as column passes
+int g_spmm_xcd = kSpmmDefaultXcd;
+int g_spmm_pass_cols = kSpmmDefaultPassCols;  // bf16 rows wider than this run as passes
 
 template <typename T, typename IdxT, int VEC>
 hipError_t launch_lpr(const int64_t* rowptr, const IdxT* col, const float* ew, int heads,
@@ -240,7 +430,7 @@ hipError_t launch_lpr(const int64_t* rowptr, const IdxT* col, const float* ew, i
     blocks = 8 * ((chunk + 3) / 4);
   }
   dim3 grid(static_cast<unsigned>(blocks)), block(256);
-  if (g_spmm_variant == 2) {
+  if (g_spmm_variant >= 2) {
     // U rows in flight per lane group: ~16 neighbour rows per wave
 #define DG_V2(LPR_, U_)                                                                    \
   if (xcd)                                                                                 \
@@ -299,7 +489,13 @@ hipError_t launch_vec(const int64_t* rowptr, const IdxT* col, const float* ew, i
 }  // namespace
 
 void set_spmm_config(int variant, int xcd, int pass_cols) {
-  if (variant == 1 || variant == 2) g_spmm_variant = variant;
+  if (variant < 0) {  // restore the defaults
+    g_spmm_variant = kSpmmDefaultVariant;
+    g_spmm_xcd = kSpmmDefaultXcd;
+    g_spmm_pass_cols = kSpmmDefaultPassCols;
+    return;
+  }
+  if (variant == 1 || variant == 2 || variant == 4) g_spmm_variant = variant;
   if (xcd >= 0 && xcd <= 3) g_spmm_xcd = xcd;
   if (pass_cols >= 0) g_spmm_pass_cols = pass_cols;
 }
@@ -317,6 +513,24 @@ hipError_t spmm_csr(DType dt, IType it, const int64_t* rowptr, const void* col,
   if (dt == DType::F32) {
     if (it == IType::I32) return launch_vec<float, int32_t>(DG_ARGS(float, int32_t));
     return launch_vec<float, int64_t>(DG_ARGS(float, int64_t));
+  }
+  if (g_spmm_variant == 4 && heads <= 1 && F % 8 == 0 && ldx % 8 == 0 && ldo % 8 == 0 &&
+      aligned(x, 16) && aligned(out, 16) && ldx < (int64_t(1) << 31)) {
+    int pc = g_spmm_pass_cols > 0 ? g_spmm_pass_cols : 512;
+    pc = pc > 512 ? 512 : (pc < 8 ? 8 : pc - pc % 8);
+    const bool xcd = g_spmm_xcd == 1 || g_spmm_xcd == 2;
+    for (int c0 = 0; c0 < F; c0 += pc) {
+      const int w = F - c0 < pc ? F - c0 : pc;
+      const auto* xp = static_cast<const uint16_t*>(x) + c0;
+      auto* op = static_cast<uint16_t*>(out) + c0;
+      hipError_t err = it == IType::I32
+          ? launch_rowgroup<int32_t>(rowptr, static_cast<const int32_t*>(col), ew, col_scale,
+                                     row_scale, xp, ldx, op, ldo, nrows, w, beta, xcd, stream)
+          : launch_rowgroup<int64_t>(rowptr, static_cast<const int64_t*>(col), ew, col_scale,
+                                     row_scale, xp, ldx, op, ldo, nrows, w, beta, xcd, stream);
+      if (err != hipSuccess) return err;
+    }
+    return hipSuccess;
   }
   const int pc = g_spmm_pass_cols;
   if (heads == 1 && pc > 0 && F > pc && F % pc == 0) {

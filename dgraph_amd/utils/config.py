@@ -26,9 +26,9 @@ class CommConfig:
 
 @dataclass
 class KernelConfig:
-    spmm_variant: int = 2
-    spmm_row_map: int = 2  # 0 grid-stride, 1 XCD grid-stride, 2 XCD in-order, 3 in-order
-    spmm_pass_cols: int = 128
+    spmm_variant: int = 4
+    spmm_row_map: int = 0  # 0 grid-stride / in-order, 1-2 XCD-chunked, 3 in-order (v2)
+    spmm_pass_cols: int = 64
     deterministic: bool = True      # segment sums only, no float atomics
 
 

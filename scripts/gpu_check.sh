@@ -20,7 +20,7 @@ run() {  # run <name> <timeout> <cmd...>
 
 STEPS=${STEPS:-smoke,tests,bench_small,bench}
 [[ $STEPS == *smoke* ]] && run smoke 400 python __graft_entry__.py smoke
-[[ $STEPS == *tests* ]] && run pytest_gpu 900 python -m pytest tests -x -q -m gpu
+[[ $STEPS == *tests* ]] && run pytest_gpu 900 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread
 [[ $STEPS == *bench_small* ]] && run bench_products 600 python bench.py --shape ogbn-products --steps 5 --warmup 2 --verbose
 [[ $STEPS == *bench,* || $STEPS == *bench ]] && run bench_papers 1000 python bench.py --steps 5 --warmup 2 --verbose
 echo done

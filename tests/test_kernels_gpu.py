@@ -91,13 +91,53 @@ def test_spmm_variants_agree_ragged_rows(variant, xcd, F):
         ops.set_spmm_config(variant, xcd)
         out = K.spmm(rowptr.to(DEV), col.to(DEV), x)
     finally:
-        ops.set_spmm_config(2, 2)
+        ops.set_spmm_config(-1, -1)
     torch.testing.assert_close(out.cpu(), ref, atol=1e-4, rtol=1e-4)
 
 
+@pytest.mark.parametrize("variant,xcd", [(2, 2), (2, 0), (4, 2), (4, 0)])
+@pytest.mark.parametrize("F", [8, 40, 64, 128, 192, 256, 520])
+@pytest.mark.parametrize("mode", ["row", "col", "ew_beta"])
+def test_spmm_bf16_variants_ragged(variant, xcd, F, mode):
+    """bf16 kernels (v3 packed math, v4 row groups) on ragged degrees 0..199, every
+    weighting mode, against the fp32 reference."""
+    from dgraph_amd import _native
+
+    g = torch.Generator().manual_seed(F + variant)
+    deg = torch.randint(0, 200, (301,), generator=g)
+    deg[::17] = 0
+    rowptr = torch.zeros(302, dtype=torch.long)
+    rowptr[1:] = torch.cumsum(deg, 0)
+    col = torch.randint(0, 500, (int(rowptr[-1]),), generator=g, dtype=torch.int32)
+    x = torch.randn(500, F, generator=g).to(torch.bfloat16)
+    kw, rkw = {}, {}
+    out0 = None
+    if mode == "row":
+        rs = torch.rand(301, generator=g)
+        kw, rkw = {"row_scale": rs.to(DEV)}, {"row_scale": rs}
+    elif mode == "col":
+        cs = torch.rand(500, generator=g)
+        kw, rkw = {"col_scale": cs.to(DEV)}, {"col_scale": cs}
+    else:
+        ew = torch.rand(col.numel(), generator=g)
+        out0 = torch.randn(301, F, generator=g).to(torch.bfloat16)
+        kw, rkw = {"edge_weight": ew.to(DEV), "beta": 0.5}, {"edge_weight": ew, "beta": 0.5}
+    base = out0.float() if out0 is not None else torch.empty(301, F)
+    ref = R.spmm(rowptr, col, x.float(), base, **rkw)
+    ops = _native.ops()
+    try:
+        ops.set_spmm_config(variant, xcd, 128)
+        out = out0.to(DEV) if out0 is not None else None
+        out = K.spmm(rowptr.to(DEV), col.to(DEV), x.to(DEV), out, **kw)
+    finally:
+        ops.set_spmm_config(-1, -1)
+    torch.testing.assert_close(out.float().cpu(), ref, atol=0.05, rtol=1e-2)
+
+
+@pytest.mark.parametrize("K_VARIANT", [2, 4])
 @pytest.mark.parametrize("pass_cols", [0, 64, 128])
 @pytest.mark.parametrize("F", [192, 256])
-def test_spmm_column_passes_bf16(pass_cols, F):
+def test_spmm_column_passes_bf16(pass_cols, F, K_VARIANT):
     """bf16 rows wider than ``pass_cols`` run as column passes (col_scale + beta too)."""
     from dgraph_amd import _native
 
@@ -109,11 +149,12 @@ def test_spmm_column_passes_bf16(pass_cols, F):
                  col_scale=cs.cpu(), beta=0.5)
     ops = _native.ops()
     try:
-        ops.set_spmm_config(2, 2, pass_cols)
+        ops.set_spmm_config(-1, -1)
+        ops.set_spmm_config(K_VARIANT, 2, pass_cols)
         out = out0.clone()
         K.spmm(csr.rowptr, csr.col, x, out, col_scale=cs, beta=0.5)
     finally:
-        ops.set_spmm_config(2, 2, 128)
+        ops.set_spmm_config(-1, -1)
     torch.testing.assert_close(out.float().cpu(), ref, atol=0.1, rtol=2e-2)
 
 
