@@ -232,8 +232,29 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 //     unpacked and added with packed fp32 math (v_pk_fma_f32, 1.5 VALU per element);
 //   * trip count = the largest degree of the G rows (wave-uniform); slots past a row's
 //     degree read row 0 with weight 0 (no branches around loads).
-template <typename IdxT, int LPR, bool WEIGHTED, bool XCD>
-__global__ __launch_bounds__(256) void spmm_bf16_rowgroup_kernel(
+//   * weights (edge weights and/or a column scale, compile-time WMODE bits) are loaded
+//     branch-free one chunk ahead, after the current chunk's row loads are issued: a
+//     runtime "if (col_scale)" made hipcc drain vmcnt at the chunk top (weighted passes
+//     ran 54 % slower than unweighted ones).
+// A global load hipcc cannot move (it sinks a plain prefetch load down to its first use)
+// and does not track: the caller waits with an explicit s_waitcnt before the use.
+// Extra untracked loads only make hipcc's own vmcnt waits conservative (in-order count).
+__device__ __forceinline__ int32_t load_nosink(const int32_t* p) {
+  int32_t v;
+  asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(p));
+  return v;
+}
+__device__ __forceinline__ int64_t load_nosink(const int64_t* p) {
+  int64_t v;
+  asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p));
+  return v;
+}
+
+// (second bound: at least 6 waves per SIMD for <= 64-column passes; unbounded, the
+// weighted LPR-8 variant took 118 VGPRs = 4 waves and ran 55 % slower than unweighted;
+// wider weighted variants would spill under the bound)
+template <typename IdxT, int LPR, int WMODE, bool XCD>
+__global__ __launch_bounds__(256, (LPR <= 8 ? 6 : 1)) void spmm_bf16_rowgroup_kernel(
     const int64_t* __restrict__ rowptr, const IdxT* __restrict__ col,
     const float* __restrict__ ew, const float* __restrict__ col_scale,
     const float* __restrict__ row_scale, const uint16_t* __restrict__ x, int64_t ldx,
@@ -241,6 +262,9 @@ __global__ __launch_bounds__(256) void spmm_bf16_rowgroup_kernel(
   constexpr int VEC = 8;
   constexpr int G = kWave / LPR;
   constexpr int U = LPR < 8 ? LPR : 8;  // neighbour rows in flight per lane per batch
+  constexpr bool HAS_EW = (WMODE & 1) != 0;
+  constexpr bool HAS_CS = (WMODE & 2) != 0;
+  constexpr bool WEIGHTED = WMODE != 0;
   const int lane = threadIdx.x & (kWave - 1);
   const int g = lane / LPR;
   const int l = lane % LPR;
@@ -278,19 +302,30 @@ __global__ __launch_bounds__(256) void spmm_bf16_rowgroup_kernel(
     f32x2 acc[VEC / 2];
 #pragma unroll
     for (int i = 0; i < VEC / 2; ++i) acc[i] = f32x2{0.f, 0.f};
-    IdxT my_c = l < deg ? col[s + l] : IdxT(0);
+    // slot k of this group's row: its column id and weight (0 for padding slots, whose
+    // id is col[0], a valid row). Branch-free loads at clamped addresses (the CSR has
+    // >= 1 entry whenever maxdeg > 0); no select on the loaded id, so nothing waits for
+    // a prefetch before its first use.
+    auto load_c = [&](int k) -> IdxT { return col[k < deg ? s + k : 0]; };
+    auto load_w = [&](IdxT c, int k) -> float {
+      float w = k < deg ? 1.f : 0.f;
+      if constexpr (HAS_EW) w *= ew[k < deg ? s + k : 0];
+      if constexpr (HAS_CS) w *= col_scale[c];
+      return w;
+    };
+    IdxT my_c = IdxT(0);
+    float my_w = 0.f;
+    if (maxdeg > 0) {
+      my_c = load_c(l);
+      if constexpr (WEIGHTED) my_w = load_w(my_c, l);
+    }
     for (int k0 = 0; k0 < maxdeg; k0 += LPR) {
-      // prefetch the next chunk's ids (and weights) before this chunk's row loads
       const int kn = k0 + LPR + l;
-      IdxT nx_c = IdxT(0);
-      if (k0 + LPR < maxdeg && kn < deg) nx_c = col[s + kn];
-      float my_w = 0.f;
-      if constexpr (WEIGHTED) {
-        if (k0 + l < deg) {
-          my_w = ew ? ew[s + k0 + l] : 1.f;
-          if (col_scale) my_w *= col_scale[my_c];
-        }
-      }
+      IdxT nx_c;
+      // the previous chunk's asm prefetch of my_c is invisible to hipcc's waitcnt pass:
+      // wait for it here (tied to my_c so no use moves above). By now that chunk's row
+      // loads have been consumed, so this waits on nothing else.
+      if constexpr (!WEIGHTED) asm volatile("s_waitcnt vmcnt(0)" : "+v"(my_c));
 #pragma unroll
       for (int j0 = 0; j0 < LPR; j0 += U) {
         if (j0 > 0 && k0 + j0 >= maxdeg) break;  // wave-uniform: no all-padding batch
@@ -299,6 +334,18 @@ __global__ __launch_bounds__(256) void spmm_bf16_rowgroup_kernel(
 #pragma unroll
         for (int u = 0; u < U; ++u)
           c[u] = static_cast<uint32_t>(__shfl(static_cast<int>(my_c), g * LPR + j0 + u, kWave));
+        // next chunk's ids in flight during this chunk, issued after this batch's id
+        // shuffles (issued first, hipcc waited for it before the shuffles) and
+        // unconditionally (past the last chunk it re-reads col[0]; under a branch hipcc
+        // waited for it at the join)
+        // (an asm load: a plain load is sunk by LLVM to its use at the next chunk top,
+        // where the wave then waits for it; a volatile one waits at once)
+        // Weighted passes read the ids again in this chunk (the next weights), so there
+        // a plain load stays put.
+        if (j0 == 0) {
+          if constexpr (WEIGHTED) nx_c = load_c(kn);
+          else nx_c = load_nosink(col + (kn < deg ? s + kn : 0));
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u)
           v[u] = *reinterpret_cast<const uint4*>(xf + static_cast<uint64_t>(c[u]) * ldx32);
@@ -322,6 +369,7 @@ __global__ __launch_bounds__(256) void spmm_bf16_rowgroup_kernel(
           }
         }
       }
+      if constexpr (WEIGHTED) my_w = load_w(nx_c, kn);
       my_c = nx_c;
     }
     if (has_row && active) {
@@ -362,35 +410,25 @@ hipError_t launch_rowgroup(const int64_t* rowptr, const IdxT* col, const float* 
   bool xcd = xcd_mode && blocks >= 64;
   if (xcd) blocks = 8 * (((ngroups + 7) / 8 + 3) / 4);  // in-order: one group per wave
   if (blocks > 0x7fffffff) return hipErrorInvalidValue;
-  const bool weighted = ew != nullptr || cs != nullptr;
+  const int wmode = (ew != nullptr ? 1 : 0) | (cs != nullptr ? 2 : 0);
   dim3 grid(static_cast<unsigned>(blocks)), block(256);
-#define DG_RG(LPR_)                                                                          \
-  if (LPR == LPR_) {                                                                         \
-    if (weighted) {                                                                          \
-      if (xcd)                                                                               \
-        hipLaunchKernelGGL((spmm_bf16_rowgroup_kernel<IdxT, LPR_, true, true>), grid, block, \
-                           0, st, rowptr, col, ew, cs, rs, x, ldx, out, ldo, nrows, F, beta); \
-      else                                                                                   \
-        hipLaunchKernelGGL((spmm_bf16_rowgroup_kernel<IdxT, LPR_, true, false>), grid,       \
-                           block, 0, st, rowptr, col, ew, cs, rs, x, ldx, out, ldo, nrows,   \
-                           F, beta);                                                         \
-    } else {                                                                                 \
-      if (xcd)                                                                               \
-        hipLaunchKernelGGL((spmm_bf16_rowgroup_kernel<IdxT, LPR_, false, true>), grid,       \
-                           block, 0, st, rowptr, col, ew, cs, rs, x, ldx, out, ldo, nrows,   \
-                           F, beta);                                                         \
-      else                                                                                   \
-        hipLaunchKernelGGL((spmm_bf16_rowgroup_kernel<IdxT, LPR_, false, false>), grid,      \
-                           block, 0, st, rowptr, col, ew, cs, rs, x, ldx, out, ldo, nrows,   \
-                           F, beta);                                                         \
-    }                                                                                        \
+#define DG_RG_W(LPR_, W_)                                                                    \
+  if (LPR == LPR_ && wmode == W_) {                                                          \
+    if (xcd)                                                                                 \
+      hipLaunchKernelGGL((spmm_bf16_rowgroup_kernel<IdxT, LPR_, W_, true>), grid, block, 0,  \
+                         st, rowptr, col, ew, cs, rs, x, ldx, out, ldo, nrows, F, beta);     \
+    else                                                                                     \
+      hipLaunchKernelGGL((spmm_bf16_rowgroup_kernel<IdxT, LPR_, W_, false>), grid, block, 0, \
+                         st, rowptr, col, ew, cs, rs, x, ldx, out, ldo, nrows, F, beta);     \
     return hipGetLastError();                                                                \
   }
+#define DG_RG(LPR_) DG_RG_W(LPR_, 0) DG_RG_W(LPR_, 1) DG_RG_W(LPR_, 2) DG_RG_W(LPR_, 3)
   DG_RG(4)
   DG_RG(8)
   DG_RG(16)
   DG_RG(32)
   DG_RG(64)
+#undef DG_RG_W
 #undef DG_RG
   return hipErrorInvalidValue;
 }

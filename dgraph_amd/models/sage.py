@@ -361,7 +361,15 @@ class SAGEStackFn(Function):
         gyp = gy.to(dt)
         if Cp != C:
             gyp = Fn.pad(gyp, (0, Cp - C))
-        if ctx.out_rows is not None:
+        # Output-layer gradient sparsity: dL/dy is zero off the loss rows, so a
+        # project-first last layer (y = A z + h Ws, z = h Wn) back-propagates through
+        # A[rows, :]^T only, and its g-side GEMMs run on |rows| rows (exact, not an
+        # approximation: the dense path would multiply by zero rows).
+        lr, lpf = specs[n - 1]
+        sparse_last = ctx.out_rows is not None and lpf and not lr
+        if sparse_last:
+            g = gyp.contiguous()
+        elif ctx.out_rows is not None:
             g = V("tmp_a", Cp)
             g.zero_()
             g.index_copy_(0, ctx.out_rows, gyp)
@@ -377,6 +385,41 @@ class SAGEStackFn(Function):
             ws, wn, b = params[3 * i], params[3 * i + 1], params[3 * i + 2]
             ws_, wn_, _ = _padded(params, i, dims, dt)
             r_in, r_out = dims_true[i], dims_true[i + 1]
+            if i == n - 1 and sparse_last:
+                masks[i] = None
+                rows = ctx.out_rows
+                x = acts[i]
+                acts[i] = None
+                x_rows = x.index_select(0, rows)
+                grads[3 * i] = wgrad(x_rows, g)[:r_in, :r_out].to(ws.dtype)
+                if b is not None:
+                    grads[3 * i + 2] = col_sum_f32(g)[:r_out].to(b.dtype)
+                dz = graph.aggregate_T_rows(g, rows, mean=True, out=V("tmp_b", dims[i + 1]))
+                grads[3 * i + 1] = wgrad(x, dz)[:r_in, :r_out].to(wn.dtype)
+                dx = None
+                if i > 0 or ctx.x0_requires_grad:
+                    prev = masks[i - 1] if i > 0 else None
+                    mask_in = prev[1] if isinstance(prev, tuple) else None
+                    # dh = mask * (dz Wn^T) + scatter_rows(mask_rows * (g Ws^T)); a
+                    # non-fused mask is applied to all of dh at the next layer instead
+                    if _fusable(dz, dims[i], dims[i + 1]):
+                        dx = dual_gemm(dz, wn_, out=x if i > 0 else None, mask_in=mask_in)
+                    elif mask_in is not None:
+                        raise RuntimeError("SAGEStackFn: tile32 ReLU mask needs the fused "
+                                           "input-gradient GEMM")
+                    else:
+                        dx = torch.mm(dz, wn_.t(), out=x) if i > 0 else dz @ wn_.t()
+                    p = g @ ws_.t()
+                    if mask_in is not None:
+                        p = p * (x_rows > 0)
+                    dx.index_add_(0, rows, p)
+                    g_masked = mask_in is not None
+                    del p
+                del dz, x, x_rows
+                g = dx
+                if i == 0:
+                    dx0 = dx
+                continue
             m = masks[i]
             masks[i] = None
             if relu:

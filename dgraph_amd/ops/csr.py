@@ -150,6 +150,23 @@ class CSR:
                 self._transpose = t
         return self._transpose
 
+    def select_rows(self, rows: torch.Tensor) -> "CSR":
+        """CSR of the row subset ``rows`` (in that order; columns unchanged). Used for the
+        output layer's gradient, which is nonzero only on the loss rows: A[rows, :]^T
+        touches ~|rows| x avg-degree entries instead of every edge."""
+        rows = rows.long()
+        deg = self.degree()[rows]
+        rowptr = torch.zeros(rows.numel() + 1, dtype=torch.long, device=self.device)
+        torch.cumsum(deg, 0, out=rowptr[1:])
+        nnz = int(rowptr[-1].item())
+        if nnz == 0:
+            return CSR(rowptr, self.col[:0].clone(), self.num_cols)
+        # slot k of new row j reads old slot rowptr[rows[j]] + (k - rowptr_new[j])
+        shift = torch.repeat_interleave(self.rowptr[rows] - rowptr[:-1], deg,
+                                        output_size=nnz)
+        src = torch.arange(nnz, device=self.device, dtype=torch.long).add_(shift)
+        return CSR(rowptr, self.col[src].contiguous(), self.num_cols)
+
     def split_columns(self, boundary: int) -> tuple["CSR", "CSR"]:
         """Split into (cols < boundary) and (cols >= boundary, shifted by -boundary).
 

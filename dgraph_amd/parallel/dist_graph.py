@@ -46,6 +46,7 @@ class DistGraph:
         self.inv_deg = csr.inv_degree()
         self.symmetric = symmetric
         self.overlap = overlap
+        self._restrict_cache = {}
         if self.H > 0 or (send_local_idx is not None and send_local_idx.numel() > 0):
             self.interior, self.halo = csr.split_columns(self.L)
             self.interior.symmetric = symmetric
@@ -108,6 +109,40 @@ class DistGraph:
         if not self.overlap:
             work.wait()
         out = K.spmm(it.rowptr, it.col, g, out, col_scale=cs)
+        work.wait()
+        st = self.send_map.transpose_csr()
+        K.spmm(st.rowptr, st.col, sg, out, beta=1.0)
+        return out
+
+    def _restricted(self, rows: torch.Tensor):
+        """Cached transposes of the row-restricted blocks A[rows, :] (interior and halo)
+        and the mean weights of those rows, for :meth:`aggregate_T_rows`."""
+        key = (rows.data_ptr(), rows.numel(), str(rows.device))
+        hit = self._restrict_cache.get(key)
+        if hit is None:
+            it = self.interior.select_rows(rows).transpose()
+            ht = self.halo.select_rows(rows).transpose() if self.halo is not None else None
+            hit = (it, ht, self.inv_deg[rows.long()].contiguous())
+            self._restrict_cache = {key: hit}  # one loss-row set at a time
+        return hit
+
+    def aggregate_T_rows(self, g_rows: torch.Tensor, rows: torch.Tensor, mean: bool = True,
+                         out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """``aggregate_T(g)`` for a ``g`` that is zero outside ``rows`` (given as the
+        ``[len(rows), F]`` nonzero block): the transposed SpMM over A[rows, :] only. For an
+        output layer trained on 1 % of the vertices this reads ~1 % of the edges, with
+        exactly the result of the dense call. Halo contributions take the same
+        reverse all-to-all as :meth:`aggregate_T`."""
+        it, ht, cs_rows = self._restricted(rows)
+        cs = cs_rows if mean else None
+        g_rows = g_rows.contiguous()
+        if self.halo is None:
+            return K.spmm(it.rowptr, it.col, g_rows, out, col_scale=cs)
+        hg = K.spmm(ht.rowptr, ht.col, g_rows, col_scale=cs)
+        sg, work = self.a2a_rev(hg, async_op=True)
+        if not self.overlap:
+            work.wait()
+        out = K.spmm(it.rowptr, it.col, g_rows, out, col_scale=cs)
         work.wait()
         st = self.send_map.transpose_csr()
         K.spmm(st.rowptr, st.col, sg, out, beta=1.0)
