@@ -437,11 +437,12 @@ hipError_t launch_rowgroup(const int64_t* rowptr, const IdxT* col, const float* 
 // 4 = row groups (bf16, 16-B aligned rows: the default). papers100M-shaped CSR, window
 // 16384, bf16: F=128 95.3 ms (v2, xcd 2, 128-col passes) -> 64.2 ms (v4, xcd 0, 64-col
 // passes); F=256 190.8 -> 129.1 ms (benchmarks/bench_spmm.py). With row groups the plain
-// in-order grid (all XCDs on one advancing row band) beats XCD-chunking by 2-7 %, and
-// 64-column passes cost the same per column as 128 (192 = 3 x 64 beats 128 + 64).
+// in-order grid (all XCDs on one advancing row band) beats XCD-chunking by 2-7 %.
+// Unweighted passes cost the same per column at 64 and 128 columns; weighted (column
+// scale) ones are cheaper at 128 (80 vs 2 x 50 ms per 128 columns), hence 128.
 constexpr int kSpmmDefaultVariant = 4;
 constexpr int kSpmmDefaultXcd = 0;
-constexpr int kSpmmDefaultPassCols = 64;
+constexpr int kSpmmDefaultPassCols = 128;
 int g_spmm_variant = kSpmmDefaultVariant;
 // 0 = grid-stride, 1 = XCD-chunked grid-stride, 2 = XCD-chunked in-order (default),
 // 3 = in-order without chunking. The in-order mappings keep the resident waves on a

@@ -461,7 +461,12 @@ class SAGEStackFn(Function):
                 #   dW_neigh = (A h)^T g = h^T u,   dh = g W_self^T + u W_neigh^T
                 # (instead of recomputing A h AND aggregating A^T (g W_neigh^T))
                 u_name = "tmp_b" if (i == n - 1 and ctx.out_rows is not None) else "tmp_a"
-                u = graph.aggregate_T(g, mean=True, out=V(u_name, dims[i + 1]))
+                # the other temp slot is free here: pre-scaled (unweighted) SpMM passes
+                scratch = ws_obj.slots["tmp_b" if u_name == "tmp_a" else "tmp_a"] \
+                    if use_ws and i < n - 1 else None
+                u = graph.aggregate_T(g, mean=True, out=V(u_name, dims[i + 1]),
+                                      scratch=scratch)
+                del scratch
                 grads[3 * i + 1] = wgrad(x, u)[:r_in, :r_out].to(wn.dtype)
                 if fuse_dx:
                     # W_self / W_neigh as stored ([F_in, F_out]) are the transposed right

@@ -96,19 +96,48 @@ class DistGraph:
         K.spmm(self.halo.rowptr, self.halo.col, recv, out, row_scale=rs, beta=1.0)
         return out
 
+    @staticmethod
+    def _spmm_col_scaled(csr: CSR, g: torch.Tensor, cs: torch.Tensor, out, scratch):
+        """``A g`` with a column scale. With a ``scratch`` buffer (a free workspace slot)
+        the scale is applied to column slices of ``g`` first (one streaming pass) and the
+        SpMM runs unweighted: a per-edge scale gather costs the gather-bound kernel a
+        second scattered load per neighbour (+25-55 % per pass, benchmarks/bench_spmm.py
+        --mean col)."""
+        rows, F = g.shape
+        S = 0 if scratch is None else min(F, (scratch.numel() // max(rows, 1)) // 64 * 64)
+        if S < 64 or g.dtype != torch.bfloat16 or not g.is_cuda:
+            return K.spmm(csr.rowptr, csr.col, g, out, col_scale=cs)
+        if out is None:
+            out = torch.empty(csr.num_rows, F, dtype=g.dtype, device=g.device)
+        csb = cs.unsqueeze(1)
+        for c0 in range(0, F, S):
+            w = min(S, F - c0)
+            buf = scratch[: rows * w].view(rows, w)
+            torch.mul(g[:, c0:c0 + w], csb, out=buf)
+            K.spmm(csr.rowptr, csr.col, buf, out[:, c0:c0 + w])
+        return out
+
     def aggregate_T(self, g: torch.Tensor, mean: bool = True,
-                    out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                    out: Optional[torch.Tensor] = None,
+                    scratch: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Transposed aggregation (the backward of :meth:`aggregate`). ``scratch``: an
+        optional free buffer (any shape, same dtype as ``g``) for the pre-scaled path."""
         cs = self.inv_deg if mean else None
         g = g.contiguous()
         it = self.interior if self.interior.symmetric else self.interior.transpose()
         if self.halo is None:
+            if cs is not None and scratch is not None:
+                return self._spmm_col_scaled(it, g, cs, out, scratch.reshape(-1))
             return K.spmm(it.rowptr, it.col, g, out, col_scale=cs)
         ht = self.halo.transpose()
         hg = K.spmm(ht.rowptr, ht.col, g, col_scale=cs)
         sg, work = self.a2a_rev(hg, async_op=True)
         if not self.overlap:
             work.wait()
-        out = K.spmm(it.rowptr, it.col, g, out, col_scale=cs)
+        if cs is not None and scratch is not None:
+            out = self._spmm_col_scaled(it, g, cs, out, scratch.reshape(-1))
+        else:
+            out = K.spmm(it.rowptr, it.col, g, out, col_scale=cs)
         work.wait()
         st = self.send_map.transpose_csr()
         K.spmm(st.rowptr, st.col, sg, out, beta=1.0)

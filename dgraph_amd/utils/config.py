@@ -28,7 +28,7 @@ class CommConfig:
 class KernelConfig:
     spmm_variant: int = 4
     spmm_row_map: int = 0  # 0 grid-stride / in-order, 1-2 XCD-chunked, 3 in-order (v2)
-    spmm_pass_cols: int = 64
+    spmm_pass_cols: int = 128
     deterministic: bool = True      # segment sums only, no float atomics
 
 

@@ -538,3 +538,33 @@ def test_sage_stack_fused_dual_gemm_matches_unfused(monkeypatch):
     for a, b in zip(res[True][1], res[False][1]):
         rel = (a - b).norm() / b.norm().clamp_min(1e-12)
         assert rel < 3e-2, float(rel)
+
+
+@pytest.mark.parametrize("F,scratch_cols", [(256, 128), (192, 70), (128, 500)])
+def test_aggregate_T_prescaled_matches_weighted(F, scratch_cols):
+    """DistGraph.aggregate_T with a scratch slot (column slices pre-scaled, unweighted
+    SpMM) equals the weighted-kernel path."""
+    from dgraph_amd.parallel.dist_graph import DistGraph
+
+    csr = _rand_csr(3000, 3000, 20, torch.int32, DEV, skew=True, seed=F)
+    g = DistGraph(csr, 3000, 0)
+    x = torch.randn(3000, F, device=DEV).to(torch.bfloat16)
+    ref = g.aggregate_T(x)
+    scratch = torch.empty(3000 * scratch_cols, dtype=torch.bfloat16, device=DEV)
+    out = g.aggregate_T(x, scratch=scratch)
+    torch.testing.assert_close(out.float(), ref.float(), atol=2e-2, rtol=2e-2)
+
+
+def test_aggregate_T_rows_matches_dense():
+    """The output-layer path: aggregate_T of a gradient that is zero off ``rows``."""
+    from dgraph_amd.parallel.dist_graph import DistGraph
+
+    csr = _rand_csr(2000, 2000, 15, torch.int32, DEV, seed=3)
+    g = DistGraph(csr, 2000, 0)
+    rows = torch.randperm(2000, device=DEV)[:150].sort().values
+    gr = torch.randn(150, 192, device=DEV).to(torch.bfloat16)
+    dense = torch.zeros(2000, 192, device=DEV, dtype=torch.bfloat16)
+    dense[rows] = gr
+    ref = g.aggregate_T(dense)
+    out = g.aggregate_T_rows(gr, rows)
+    torch.testing.assert_close(out.float(), ref.float(), atol=2e-2, rtol=2e-2)
