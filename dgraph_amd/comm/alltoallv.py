@@ -76,6 +76,11 @@ class AllToAllV:
         CommStats.calls += 1
         CommStats.bytes_sent += self.total_send * row_bytes
         CommStats.bytes_recv += self.total_recv * row_bytes
+        from .faults import FaultInjector
+
+        if FaultInjector.active():
+            send = FaultInjector.before_exchange(
+                send, dist.get_rank() if dist.is_initialized() else 0)
         if self._world <= 1 or not dist.is_initialized() or dist.get_world_size(self.group) == 1:
             if self.total_send:
                 out.copy_(send)

@@ -63,6 +63,9 @@ class DistGraph:
         # drop the un-split copy's column array when split (memory: 288 GB budget)
         if self.halo is not None:
             self.csr = None
+        from ..utils.diagnostics import maybe_validate
+
+        maybe_validate(self)  # DGRAPH_CHECK_PLANS=1: once per plan, not per call
 
     @property
     def device(self):

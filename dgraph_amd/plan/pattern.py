@@ -280,3 +280,118 @@ def build_communication_pattern(
         local_vertices=local_c,
         num_local_neighbor_vertices=L_n,
     )
+
+
+# --------------------------------------------------------------------------------------
+# Offline builder: every rank's pattern in one process (no process group)
+# --------------------------------------------------------------------------------------
+def build_all_patterns_offline(
+    global_edge_list: torch.Tensor,
+    partitioning: torch.Tensor,
+    world_size: int,
+    neighbor_partitioning: Optional[torch.Tensor] = None,
+) -> List[CommunicationPattern]:
+    """The patterns :func:`build_communication_pattern` would produce on each of
+    ``world_size`` ranks, computed in ONE process with the two collectives (request-count
+    all-to-all, id all-to-all-v) and the comm-map all-gather carried out in memory.
+
+    This is the plan-cache generator of the reference (experiments/OGB/GenerateCache.py,
+    OGB-LSC/CacheGenerator.py:119-170 with its dummy communicator) as a library call:
+    plans for a W-rank job can be built and saved on one host and loaded by each rank
+    (:func:`save_patterns` / :func:`load_pattern`)."""
+    dev = global_edge_list.device
+    W = int(world_size)
+    nbr_part = partitioning if neighbor_partitioning is None else neighbor_partitioning
+    V_c, V_n = partitioning.numel(), nbr_part.numel()
+    per = []
+    for r in range(W):
+        local_c = compute_local_vertices(partitioning, r)
+        local_n = local_c if neighbor_partitioning is None else compute_local_vertices(nbr_part, r)
+        mine = global_edge_list[partitioning[global_edge_list[:, 0]] == r]
+        nbr = mine[:, 1]
+        owner = nbr_part[nbr]
+        remote = owner != r
+        key = torch.unique(owner[remote] * V_n + nbr[remote])
+        h_owner = torch.div(key, V_n, rounding_mode="floor")
+        halo = key - h_owner * V_n
+        req = torch.bincount(h_owner, minlength=W) if halo.numel() else \
+            torch.zeros(W, dtype=torch.long, device=dev)
+        g2l_c = _inverse_map(local_c, V_c)
+        g2l_n = _inverse_map(local_n, V_n)
+        g2l_n[halo] = torch.arange(local_n.numel(), local_n.numel() + halo.numel(), device=dev)
+        per.append(dict(local_c=local_c, local_n=local_n, mine=mine, halo=halo,
+                        h_owner=h_owner, req=req, g2l_c=g2l_c, g2l_n=g2l_n))
+    # comm_map[q, p] = rows q sends to p = ids p requests from q
+    comm_map = torch.stack([per[p]["req"] for p in range(W)], dim=1).long()
+    out = []
+    for q in range(W):
+        P = per[q]
+        # what q sends, peer order: the ids each peer p requested from q (p's receive order)
+        wanted = [per[p]["halo"][per[p]["h_owner"] == q] for p in range(W)]
+        wanted = torch.cat(wanted) if wanted else P["halo"][:0]
+        send_local_idx = P["g2l_n"][wanted] if wanted.numel() else \
+            torch.zeros(0, dtype=torch.long, device=dev)
+        if send_local_idx.numel() and bool(((send_local_idx < 0) |
+                                            (send_local_idx >= P["local_n"].numel())).any()):
+            raise RuntimeError("halo request for a vertex the sender does not own")
+        send_offset = torch.zeros(W + 1, dtype=torch.long, device=dev)
+        send_offset[1:] = torch.cumsum(comm_map[q].to(dev), 0)
+        recv_offset, _ = compute_recv_offsets(comm_map, q)
+        mine = P["mine"]
+        out.append(CommunicationPattern(
+            rank=q, world_size=W,
+            num_local_vertices=P["local_c"].numel(),
+            num_halo_vertices=P["halo"].numel(),
+            local_edge_list=torch.stack([P["g2l_c"][mine[:, 0]], P["g2l_n"][mine[:, 1]]], 1),
+            send_local_idx=send_local_idx,
+            send_offset=send_offset,
+            recv_offset=recv_offset,
+            comm_map=comm_map.clone(),
+            put_forward_remote_offset=comm_map[:q, :].sum(0),
+            put_backward_remote_offset=comm_map[:, :q].sum(1),
+            halo_vertices=P["halo"],
+            local_vertices=P["local_c"],
+            num_local_neighbor_vertices=P["local_n"].numel(),
+        ))
+    return out
+
+
+_PATTERN_TENSORS = ("local_edge_list", "send_local_idx", "send_offset", "recv_offset",
+                    "comm_map", "put_forward_remote_offset", "put_backward_remote_offset",
+                    "halo_vertices", "local_vertices")
+_PATTERN_INTS = ("rank", "world_size", "num_local_vertices", "num_halo_vertices",
+                 "num_local_neighbor_vertices")
+
+
+def pattern_to_dict(cp: CommunicationPattern) -> dict:
+    """Plain tensors + ints (loadable with ``torch.load(weights_only=True)``, no pickled
+    classes: SURVEY.md §5.4)."""
+    d = {k: getattr(cp, k) for k in _PATTERN_TENSORS if getattr(cp, k) is not None}
+    d.update({k: int(getattr(cp, k)) for k in _PATTERN_INTS if getattr(cp, k) is not None})
+    return d
+
+
+def pattern_from_dict(d: dict) -> CommunicationPattern:
+    return CommunicationPattern(**{k: d[k] for k in _PATTERN_TENSORS + _PATTERN_INTS if k in d})
+
+
+def save_patterns(patterns: List[CommunicationPattern], directory: str, name: str) -> List[str]:
+    """``{directory}/{name}_rank_{r}_of_{W}_comm_pattern.pt`` per rank (the reference's
+    per-rank plan file naming, distributed_graph_dataset.py:399-410)."""
+    import os
+
+    os.makedirs(directory, exist_ok=True)
+    paths = []
+    for cp in patterns:
+        p = os.path.join(directory, f"{name}_rank_{cp.rank}_of_{cp.world_size}_comm_pattern.pt")
+        torch.save(pattern_to_dict(cp), p)
+        paths.append(p)
+    return paths
+
+
+def load_pattern(directory: str, name: str, rank: int, world_size: int,
+                 map_location="cpu") -> CommunicationPattern:
+    import os
+
+    p = os.path.join(directory, f"{name}_rank_{rank}_of_{world_size}_comm_pattern.pt")
+    return pattern_from_dict(torch.load(p, map_location=map_location, weights_only=True))
