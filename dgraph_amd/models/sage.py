@@ -304,7 +304,10 @@ class SAGEStackFn(Function):
                     y.addmm_(h, ws_)
             else:
                 slot = "agg0" if (i == 0 and keep0) else "tmp_a"
-                a = graph.aggregate(h, mean=True, out=V(slot, Fi))
+                # layer 0 aggregates the input features: read-only without grad, so
+                # their halo rows are exchanged once and kept (DistGraph._static_halo)
+                a = graph.aggregate(h, mean=True, out=V(slot, Fi),
+                                    static=i == 0 and not x0.requires_grad)
                 if fused:
                     dual_gemm(h, ws_.t().contiguous(), a, wn_.t().contiguous(), bias=b, out=y,
                               relu=relu, mask_out=mask)
@@ -487,7 +490,8 @@ class SAGEStackFn(Function):
                 else:
                     a_buf = V(a_name, dims[i])
                 if not (i == 0 and ctx.keep0):
-                    a = graph.aggregate(x, mean=True, out=a_buf)
+                    a = graph.aggregate(x, mean=True, out=a_buf,
+                                        static=i == 0 and not ctx.x0_requires_grad)
                 grads[3 * i + 1] = wgrad(a, g)[:r_in, :r_out].to(wn.dtype)
                 if need_dx:
                     t = torch.mm(g, wn_.t(), out=a)

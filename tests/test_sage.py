@@ -76,7 +76,7 @@ def test_workspace_guard():
         o1.sum().backward()
 
 
-def _train_losses(rank, world, steps, out):
+def _train_losses(rank, world, steps, out, hidden=32):
     import torch.distributed as dist
 
     from dgraph_amd.parallel.grad_sync import GradSync
@@ -90,7 +90,7 @@ def _train_losses(rank, world, steps, out):
     if world > 1:
         dist.all_reduce(n)
     torch.manual_seed(0)
-    m = GraphSAGE(SHAPE.num_features, 32, SHAPE.num_classes, 3)
+    m = GraphSAGE(SHAPE.num_features, hidden, SHAPE.num_classes, 3)
     opt = torch.optim.Adam(m.parameters(), lr=1e-2)
     sync = GradSync(m.parameters())
     losses = []
@@ -110,10 +110,13 @@ def _train_losses(rank, world, steps, out):
 
 
 @pytest.mark.parametrize("world", [2, 3])
-def test_distributed_training_matches_single_rank(ranks, tmp_path, world):
-    """Halo-overlapped DistGraph training on W ranks follows the same loss curve as W=1."""
-    _train_losses(0, 1, 4, tmp_path / "w1.pt")
-    ranks(_train_losses, world, 4, str(tmp_path / "wn.pt"))
+@pytest.mark.parametrize("hidden", [32, 64])
+def test_distributed_training_matches_single_rank(ranks, tmp_path, world, hidden):
+    """Halo-overlapped DistGraph training on W ranks follows the same loss curve as W=1.
+    hidden=64 > 40 classes makes the output layer project-first: its backward takes the
+    row-restricted path with the contributing-rows reverse exchange."""
+    _train_losses(0, 1, 4, tmp_path / "w1.pt", hidden)
+    ranks(_train_losses, world, 4, str(tmp_path / "wn.pt"), hidden)
     a = torch.load(tmp_path / "w1.pt", weights_only=True)
     b = torch.load(tmp_path / "wn.pt", weights_only=True)
     torch.testing.assert_close(a, b, atol=1e-5, rtol=1e-5)
@@ -137,3 +140,29 @@ def test_layer0_aggregate_kept_or_recomputed(monkeypatch, keep_agg0):
     _dense_forward(m, x, A)[rows].square().mean().backward()
     for a, q in zip(grads, m.parameters()):
         torch.testing.assert_close(a, q.grad, atol=1e-6, rtol=1e-4)
+
+
+def _static_halo(rank, world):
+    from dgraph_amd.comm.alltoallv import CommStats
+
+    p = build_partition(SHAPE, rank, world, "cpu")
+    g = DistGraph(p["csr"], p["L"], p["H"], p["send_local_idx"], p["send_splits"],
+                  p["recv_splits"])
+    x, _, _ = node_data(SHAPE, rank, p["offsets"], "cpu", dtype=torch.float32)
+    ref = g.aggregate(x)
+    c0 = CommStats.calls
+    a = g.aggregate(x, static=True)
+    b = g.aggregate(x, static=True)
+    assert CommStats.calls == c0 + 1  # exchanged once, then reused
+    torch.testing.assert_close(a, ref)
+    torch.testing.assert_close(b, ref)
+    x.mul_(2.0)  # in-place update: version bump -> re-exchange
+    torch.testing.assert_close(g.aggregate(x, static=True), 2.0 * ref)
+    assert CommStats.calls == c0 + 2
+    y = x.clone()  # a different tensor with equal contents
+    torch.testing.assert_close(g.aggregate(y, static=True), 2.0 * ref)
+    assert CommStats.calls == c0 + 3
+
+
+def test_static_feature_halo_cached(ranks):
+    ranks(_static_halo, 2)
