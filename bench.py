@@ -49,6 +49,10 @@ def parse():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--rehearse-world", type=int, default=0,
+                    help="single process: run rank --rehearse-rank of a W-way partition with "
+                         "a loopback halo exchange (per-rank compute + memory; no peers)")
+    ap.add_argument("--rehearse-rank", type=int, default=0)
     return ap.parse_args()
 
 
@@ -77,10 +81,12 @@ def main():
         shape = shape.scaled(args.scale)
 
     t0 = time.time()
-    part = build_partition(shape, rank, world, dev, seed=args.seed,
-                           global_frac=args.global_frac, window=args.window)
+    rehearse = args.rehearse_world > 1 and world == 1
+    p_rank, p_world = (args.rehearse_rank, args.rehearse_world) if rehearse else (rank, world)
+    part = build_partition(shape, p_rank, p_world, dev, seed=args.seed,
+                           global_frac=args.global_frac, window=args.window, rehearse=rehearse)
     csr = part["csr"]
-    if world == 1:
+    if p_world == 1:
         csr.num_cols = part["L"]
     graph = DistGraph(csr, part["L"], part["H"], part["send_local_idx"], part["send_splits"],
                       # the synthetic graph is symmetrised, so the interior (local x local)
@@ -89,7 +95,7 @@ def main():
                       overlap=not args.no_overlap)
     graph.prepare_backward()
     dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
-    x, y, train = node_data(shape, rank, part["offsets"], dev, seed=args.seed, dtype=dtype)
+    x, y, train = node_data(shape, p_rank, part["offsets"], dev, seed=args.seed, dtype=dtype)
     train_idx = torch.nonzero(train, as_tuple=True)[0]
     y_train = y[train_idx]
     del y, train
@@ -148,7 +154,13 @@ def main():
     final_loss = float(lt.item())
     peak_gb = torch.cuda.max_memory_allocated() / 1e9 if dev.type == "cuda" else 0.0
     edges_per_s = args.layers * E_msg / (ms_per_step / 1000.0)
-    if rank == 0:
+    if rehearse:
+        # not a whole-job number: one rank's compute with a loopback exchange
+        print(json.dumps({"rehearsal": True, "rank": p_rank, "world": p_world,
+                          "ms_per_step_compute_loopback": ms_per_step, "L": part["L"],
+                          "H": part["H"], "E_local": E_msg, "peak_mem_gb": round(peak_gb, 2),
+                          "final_loss_local": final_loss}), flush=True)
+    elif rank == 0:
         rec = {
             "metric": "edges_per_s",
             "value": edges_per_s,

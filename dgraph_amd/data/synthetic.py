@@ -196,11 +196,14 @@ def localize_columns(csr: CSR, rank: int, offsets: List[int]):
 
 
 def build_partition(shape: GraphShape, rank: int, world_size: int, device, seed: int = 0,
-                    global_frac: float = 0.05, window: int = 1 << 14, group=None):
+                    global_frac: float = 0.05, window: int = 1 << 14, group=None,
+                    rehearse: bool = False):
     """Full per-rank partition: local CSR (local+halo columns) and the halo send plan.
 
     Returns a dict with keys csr, L, H, halo_gids, send_local_idx, send_splits,
-    recv_splits, offsets. Collective over ``group`` when world_size > 1.
+    recv_splits, offsets. Collective over ``group`` when world_size > 1, unless
+    ``rehearse``: then rank ``rank`` of a ``world_size``-way partition is built alone, with
+    a loopback send plan of the right size (bench.py --rehearse-world).
     """
     from ..plan.pattern import _alltoall_counts, _alltoallv_ids
 
@@ -213,6 +216,19 @@ def build_partition(shape: GraphShape, rank: int, world_size: int, device, seed:
                     send_splits=[0], recv_splits=[0], offsets=offsets)
     csr, halo, recv_splits = localize_columns(csr_g, rank, offsets)
     del csr_g
+    if world_size > 1 and rehearse:
+        # one rank of a W-way job in a single process (no peers): the graph is symmetric,
+        # so the rows this rank must send mirror the rows it receives; send the matching
+        # number of local rows (spread over the partition) so every buffer, plan and
+        # kernel has its real shape while the exchange is a local loopback.
+        send_splits = list(recv_splits)
+        n_send = sum(send_splits)
+        idt = index_dtype_for(L)
+        send_local_idx = (torch.arange(n_send, device=device, dtype=torch.long) * 7919 % max(L, 1)
+                          ).to(idt)
+        return dict(csr=csr, L=L, H=int(halo.numel()), halo_gids=halo,
+                    send_local_idx=send_local_idx, send_splits=send_splits,
+                    recv_splits=recv_splits, offsets=offsets)
     if world_size > 1:
         req = torch.tensor(recv_splits, dtype=torch.long, device=device)
         send_counts = _alltoall_counts(req, group)

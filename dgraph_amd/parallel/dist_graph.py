@@ -169,6 +169,12 @@ class DistGraph:
         K.spmm(st.rowptr, st.col, sg, out, beta=1.0)
         return out
 
+    def _peers(self) -> bool:
+        """True when the plan's peers exist (a process group of the plan's size)."""
+        import torch.distributed as dist
+
+        return dist.is_initialized() and dist.get_world_size(self.a2a.group) > 1
+
     def _restricted(self, rows: torch.Tensor):
         """Cached pieces of :meth:`aggregate_T_rows` for one loss-row set: the transposed
         interior block A[rows, :L]^T, and for the halo block only the halo rows that
@@ -195,9 +201,13 @@ class DistGraph:
             W = recv_off.numel() - 1
             cnt = torch.bincount(owner, minlength=W)
             slot = nz - recv_off[owner]
-            peer_cnt = _alltoall_counts(cnt, self.a2a.group)
+            if self._peers():
+                peer_cnt = _alltoall_counts(cnt, self.a2a.group)
+            else:  # single-process rehearsal of a W-way rank: mirrored loopback plan
+                peer_cnt = cnt.clone()
             cnt_l, peer_l = [int(v) for v in cnt.tolist()], [int(v) for v in peer_cnt.tolist()]
-            peer_slot = _alltoallv_ids(slot, cnt_l, peer_l, self.a2a.group)
+            peer_slot = _alltoallv_ids(slot, cnt_l, peer_l, self.a2a.group) if self._peers() \
+                else slot
             send_off = torch.zeros(W + 1, dtype=torch.long, device=dev)
             send_off[1:] = torch.cumsum(torch.tensor(self.a2a.send_splits, device=dev), 0)
             base = torch.repeat_interleave(send_off[:-1], peer_cnt.to(dev))
