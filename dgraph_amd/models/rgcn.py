@@ -1,0 +1,169 @@
+"""Relational GCN for heterogeneous graphs (BASELINE config 4: MAG240M-shaped R-GCN).
+
+The reference ships only an RGAT for OGB-LSC (experiments/OGB-LSC/RGAT.py:271-382); this
+is the R-GCN (mean-aggregating relational graph conv, the OGB-LSC "R-GraphSAGE" baseline)
+with the same layer skeleton — per-layer skip ``Linear`` shared by all node types, one
+convolution per relation, synchronised BatchNorm, ReLU, dropout, MLP head on the target
+type — so it plugs into the same trainer:
+
+    h_d^{l+1} = dropout(relu(BN( skip_l(h_d^l) + sum_{r: s->d} mean_{j in N_r(i)} h_s^l[j] W_r^l )))
+
+Two execution paths:
+
+* :class:`HeteroGraph` (``dgraph_amd.parallel.hetero_graph``; built by
+  ``dgraph_amd.data.mag.build_hetero_partition``) — the MI355X hot path. Layer 0 is
+  transform-first: ONE GEMM per source type ``X_s [W_r1 | W_r2 ...]`` on the local rows
+  and on the halo feature rows fetched once (one-sided heap get, or one all-to-all-v), then
+  per-relation SpMMs over column slices — no communication at all in layer 0, forward or
+  backward. Later layers aggregate first with one overlapped halo exchange per source
+  type. Only the (layer, type) pairs that reach the loss are computed (a 2-layer model
+  never touches the author->institution relation, and its last layer updates papers only).
+* :class:`dgraph_amd.data.hetero.RelationGraph` lists (the RGAT dataset objects) — the
+  per-relation halo-exchange path, for API parity with ``CommAwareRGAT``.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..ops.aggregate import aggregate
+from ..parallel.hetero_graph import SourceGraph, source_aggregate
+from .norm import DistributedBatchNorm1D
+
+
+@dataclass
+class HeteroGraph:
+    """One rank's view: ``sources[s]`` = :class:`SourceGraph` of source type ``s``;
+    ``num_local[t]`` = owned vertices of type ``t``."""
+
+    sources: Dict[int, SourceGraph]
+    num_local: Dict[int, int]
+    edge_types: List[Tuple[int, int]]
+    extra: dict = field(default_factory=dict)
+
+    @staticmethod
+    def from_partition(part: dict, edge_types, group=None, overlap: bool = True,
+                       rank: int = 0) -> "HeteroGraph":
+        offs = part["offsets"]
+        srcs = {s: SourceGraph.from_partition(d, group, overlap, src_offsets=offs[s])
+                for s, d in part["sources"].items()}
+        nl = {t: offs[t][rank + 1] - offs[t][rank] for t in offs}
+        return HeteroGraph(srcs, nl, list(edge_types))
+
+
+def layer_plan(edge_types: Sequence[Tuple[int, int]], num_layers: int, target: int = 0,
+               available: Optional[Sequence[int]] = None):
+    """(types computed, relations used) per layer, pruned backwards from the target type."""
+    need = [set() for _ in range(num_layers)]
+    rels = [[] for _ in range(num_layers)]
+    want = {target}
+    for l in range(num_layers - 1, -1, -1):
+        need[l] = set(want)
+        rels[l] = [r for r, (s, d) in enumerate(edge_types)
+                   if d in want and (available is None or r in available)]
+        want = set(want) | {edge_types[r][0] for r in rels[l]}
+    return need, rels
+
+
+class CommAwareRGCN(nn.Module):
+    def __init__(self, in_channels: int, hidden_channels: int, out_channels: int,
+                 num_relations: int, num_layers: int = 2, dropout: float = 0.5,
+                 edge_types: Optional[Sequence[Tuple[int, int]]] = None, comm=None,
+                 target_type: int = 0, bn_group=None, num_node_types: int = 3):
+        super().__init__()
+        self.num_layers, self.dropout, self.comm = num_layers, dropout, comm
+        self.hidden = hidden_channels
+        self.edge_types = list(edge_types) if edge_types is not None else None
+        self.target = target_type
+        self.num_node_types = num_node_types
+        self.convs = nn.ModuleList()
+        self.skips = nn.ModuleList()
+        for i in range(num_layers):
+            cin = in_channels if i == 0 else hidden_channels
+            self.convs.append(nn.ModuleList([nn.Linear(cin, hidden_channels, bias=False)
+                                             for _ in range(num_relations)]))
+            self.skips.append(nn.Linear(cin, hidden_channels))
+        self.bns = nn.ModuleList([DistributedBatchNorm1D(hidden_channels, recompute=True,
+                                                         group=bn_group)
+                                  for _ in range(num_layers)])
+        self.mlp = nn.Sequential(
+            nn.Linear(hidden_channels, hidden_channels),
+            DistributedBatchNorm1D(hidden_channels, recompute=True, group=bn_group),
+            nn.ReLU(inplace=True),
+            nn.Dropout(dropout),
+            nn.Linear(hidden_channels, out_channels),
+        )
+
+    # ------------------------------------------------------------------ helpers
+    def _finish(self, l: int, t: torch.Tensor) -> torch.Tensor:
+        t = torch.relu(self.bns[l](t))
+        return F.dropout(t, self.dropout, self.training)
+
+    def forward(self, xs, graph, edge_types=None) -> torch.Tensor:
+        if isinstance(graph, HeteroGraph):
+            return self._forward_hetero(xs, graph)
+        return self._forward_relations(xs, edge_types, graph)
+
+    # ------------------------------------------------------------------ hot path
+    def _forward_hetero(self, xs: Dict[int, torch.Tensor], g: HeteroGraph) -> torch.Tensor:
+        ets = g.edge_types
+        avail = [r for s in g.sources.values() for r in s.ranges]
+        need, rels = layer_plan(ets, self.num_layers, self.target, avail)
+        h = dict(xs)
+        for l in range(self.num_layers):
+            tmp = {t: self.skips[l](h[t]) for t in sorted(need[l])}
+            by_src: Dict[int, List[int]] = {}
+            for r in rels[l]:
+                by_src.setdefault(ets[r][0], []).append(r)
+            for s, rs in sorted(by_src.items()):
+                sg = g.sources[s]
+                if l == 0:
+                    # transform-first: one GEMM over [W_r1 | W_r2 ...], static halo rows
+                    W = torch.cat([self.convs[0][r].weight for r in rs], 0)
+                    z = F.linear(h[s], W)
+                    xh = sg.static_halo(xs[s])
+                    zh = F.linear(xh, W) if xh is not None else None
+                    C = self.hidden
+                    spec = [(r, i * C, (i + 1) * C) for i, r in enumerate(rs)]
+                    outs = source_aggregate(z, sg, spec, static_halo=zh) if zh is not None \
+                        else source_aggregate(z, sg, spec)
+                    for r, o in zip(rs, outs):
+                        d = ets[r][1]
+                        tmp[d] = tmp[d] + o.to(tmp[d].dtype)
+                else:
+                    spec = [(r, 0, h[s].shape[1]) for r in rs]
+                    outs = source_aggregate(h[s], sg, spec)
+                    for r, o in zip(rs, outs):
+                        d = ets[r][1]
+                        tmp[d] = tmp[d] + self.convs[l][r](o)
+            h = {t: self._finish(l, v) for t, v in tmp.items()}
+        return self.mlp(h[self.target])
+
+    # ------------------------------------------------------------------ RelationGraph path
+    def _forward_relations(self, xs: List[torch.Tensor], edge_types, graphs) -> torch.Tensor:
+        from ..parallel.halo import HaloExchange
+        import torch.distributed as dist
+
+        ets = list(edge_types)
+        W = self.comm.get_world_size() if self.comm is not None else (
+            dist.get_world_size() if dist.is_initialized() else 1)
+        need, rels = layer_plan(ets, self.num_layers, self.target)
+        h = list(xs)
+        halo = HaloExchange(self.comm) if W > 1 else None
+        for l in range(self.num_layers):
+            tmp = {t: self.skips[l](h[t]) for t in sorted(need[l])}
+            for r in rels[l]:
+                s, d = ets[r]
+                g = graphs[r]
+                xs_all = h[s]
+                if halo is not None:
+                    xs_all = torch.cat([xs_all, halo(h[s], g.pattern)], 0)
+                agg = aggregate(xs_all, g.csr, reduce="mean")
+                tmp[d] = tmp[d] + self.convs[l][r](agg)
+            h = dict(h) if isinstance(h, dict) else {i: v for i, v in enumerate(h)}
+            h.update({t: self._finish(l, v) for t, v in tmp.items()})
+        return self.mlp(h[self.target])
