@@ -371,6 +371,75 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> layer_norm_bwd_op(
   return {dx, sums[0], sums[1]};
 }
 
+// -------------------------------------------------------------------------------- BN
+void bn_check(const at::Tensor& t, const at::Tensor& ref, const char* name) {
+  check_dev(t, ref, name);
+  check_rows(t, name);
+  TORCH_CHECK(t.sizes() == ref.sizes() && t.scalar_type() == ref.scalar_type(), "bn: ", name,
+              " must match x");
+}
+
+const float* bn_vec(const c10::optional<at::Tensor>& t, const at::Tensor& x, const char* name) {
+  const float* p = opt_f32(t, x, name);
+  if (p) TORCH_CHECK(t->numel() == x.size(1), "bn: ", name, " must have F elements");
+  return p;
+}
+
+at::Tensor bn_reduce_op(const at::Tensor& x, const c10::optional<at::Tensor>& dy,
+                        const at::Tensor& center, const c10::optional<at::Tensor>& rstd,
+                        const c10::optional<at::Tensor>& gamma,
+                        const c10::optional<at::Tensor>& beta, bool relu, int64_t mode) {
+  check_dev(x, x, "x");
+  check_rows(x, "x");
+  TORCH_CHECK(mode == 0 || mode == 1, "bn_reduce: mode 0 (stats) or 1 (backward)");
+  const void* dyp = nullptr;
+  int64_t ldy = 0;
+  if (mode == 1) {
+    TORCH_CHECK(dy.has_value() && dy->defined(), "bn_reduce: backward needs dy");
+    bn_check(*dy, x, "dy");
+    dyp = dy->data_ptr();
+    ldy = dy->stride(0);
+    TORCH_CHECK(rstd.has_value() && rstd->defined(), "bn_reduce: backward needs rstd");
+  }
+  const int64_t N = x.size(0), F = x.size(1);
+  const int nb = bn_reduce_blocks(N);
+  auto partial = at::empty({nb, 2, F}, x.options().dtype(at::kFloat));
+  auto out = at::empty({2, F}, x.options().dtype(at::kDouble));
+  c10::DeviceGuard g(x.device());
+  DG_HIP_CHECK(bn_reduce(dtype_of(x), static_cast<int>(mode), x.data_ptr(), x.stride(0), dyp, ldy,
+                         N, static_cast<int>(F), bn_vec(center, x, "center"),
+                         bn_vec(rstd, x, "rstd"), bn_vec(gamma, x, "gamma"),
+                         bn_vec(beta, x, "beta"), relu, partial.data_ptr<float>(), nb,
+                         out.data_ptr<double>(), cur_stream(x)));
+  return out;
+}
+
+at::Tensor bn_apply_op(const at::Tensor& x, const c10::optional<at::Tensor>& dy,
+                       const at::Tensor& mean, const at::Tensor& rstd,
+                       const c10::optional<at::Tensor>& gamma,
+                       const c10::optional<at::Tensor>& beta, const c10::optional<at::Tensor>& c1,
+                       const c10::optional<at::Tensor>& c2, bool relu, int64_t mode) {
+  check_dev(x, x, "x");
+  check_rows(x, "x");
+  TORCH_CHECK(mode == 0 || mode == 1, "bn_apply: mode 0 (forward) or 1 (backward)");
+  const void* dyp = nullptr;
+  int64_t ldy = 0;
+  if (mode == 1) {
+    TORCH_CHECK(dy.has_value() && dy->defined(), "bn_apply: backward needs dy");
+    bn_check(*dy, x, "dy");
+    dyp = dy->data_ptr();
+    ldy = dy->stride(0);
+  }
+  auto out = at::empty(x.sizes(), x.options());
+  c10::DeviceGuard g(x.device());
+  DG_HIP_CHECK(bn_apply(dtype_of(x), static_cast<int>(mode), x.data_ptr(), x.stride(0), dyp, ldy,
+                        out.data_ptr(), out.stride(0), x.size(0), static_cast<int>(x.size(1)),
+                        bn_vec(mean, x, "mean"), bn_vec(rstd, x, "rstd"),
+                        bn_vec(gamma, x, "gamma"), bn_vec(beta, x, "beta"), bn_vec(c1, x, "c1"),
+                        bn_vec(c2, x, "c2"), relu, cur_stream(x)));
+  return out;
+}
+
 int64_t tile32_mask_words(int64_t M, int64_t N) { return (M + 255) / 256 * 8 * (N / 32) * 16; }
 
 void dual_gemm_op(const at::Tensor& A1, const at::Tensor& B1t, const c10::optional<at::Tensor>& A2,
@@ -460,6 +529,10 @@ TORCH_LIBRARY(dgraph_amd, m) {
         "(Tensor, Tensor, Tensor)");
   m.def("layer_norm_bwd(Tensor dy, Tensor x, Tensor mean, Tensor rstd, Tensor? gamma) -> "
         "(Tensor, Tensor, Tensor)");
+  m.def("bn_reduce(Tensor x, Tensor? dy, Tensor center, Tensor? rstd, Tensor? gamma, "
+        "Tensor? beta, bool relu, int mode) -> Tensor");
+  m.def("bn_apply(Tensor x, Tensor? dy, Tensor mean, Tensor rstd, Tensor? gamma, Tensor? beta, "
+        "Tensor? c1, Tensor? c2, bool relu, int mode) -> Tensor");
   m.def("dual_gemm(Tensor A1, Tensor B1t, Tensor? A2, Tensor? B2t, Tensor? bias, Tensor? cin, "
         "Tensor(a!) out, Tensor(b!)? mask_out, Tensor? mask_in, bool relu) -> ()");
   m.def("tile32_mask_words(int M, int N) -> int", &tile32_mask_words_op);
@@ -489,4 +562,6 @@ TORCH_LIBRARY_IMPL(dgraph_amd, CUDA, m) {
   m.impl("layer_norm_fwd", &dgraph::layer_norm_fwd_op);
   m.impl("dual_gemm", &dgraph::dual_gemm_op);
   m.impl("layer_norm_bwd", &dgraph::layer_norm_bwd_op);
+  m.impl("bn_reduce", &dgraph::bn_reduce_op);
+  m.impl("bn_apply", &dgraph::bn_apply_op);
 }

@@ -102,6 +102,24 @@ hipError_t layer_norm_bwd(DType dt, const void* dy, const void* x, const float* 
                           int nblocks, int64_t N, int F, hipStream_t st);
 
 // ---------------------------------------------------------------------------
+// Synchronised BatchNorm pieces (batchnorm.hip, K-new-7), fp32 statistics, no fp32 copy
+// of x. bn_reduce mode 0: out = (sum (x - center), sum (x - center)^2); mode 1: out =
+// (sum dy', sum dy' * xhat), dy' = dy * [xhat*g+b > 0] when relu. out is fp64 [2][F];
+// partial is fp32 [nblocks][2][F] scratch with nblocks = bn_reduce_blocks(N).
+// bn_apply mode 0: y = act((x - mean) * rstd * g + b); mode 1: dx = (dy' - c1 - xhat * c2)
+// * rstd * g. gamma/beta/c1/c2 may be null (g = 1, b = 0).
+// ---------------------------------------------------------------------------
+int bn_reduce_blocks(int64_t N);
+hipError_t bn_reduce(DType dt, int mode, const void* x, int64_t ldx, const void* dy,
+                     int64_t ldy, int64_t N, int F, const float* center, const float* rstd,
+                     const float* gamma, const float* beta, bool relu, float* partial,
+                     int nblocks, double* out, hipStream_t st);
+hipError_t bn_apply(DType dt, int mode, const void* x, int64_t ldx, const void* dy,
+                    int64_t ldy, void* out, int64_t ldo, int64_t N, int F, const float* mean,
+                    const float* rstd, const float* gamma, const float* beta, const float* c1,
+                    const float* c2, bool relu, hipStream_t st);
+
+// ---------------------------------------------------------------------------
 // Fused tall-skinny MFMA dual GEMM (dual_gemm.hip), bf16 in / fp32 accumulate:
 //   out = epi(A1 @ B1 (+ A2 @ B2) (+ bias) (+ cin)); B given transposed (Bt[N][K]).
 // N in {128,192,256}; K1, K2 in {128,192,256} (K2 = 0: single GEMM); lda % 8 == 0.

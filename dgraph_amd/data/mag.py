@@ -210,13 +210,13 @@ def build_hetero_partition(shape: HeteroShape, rank: int, world_size: int, devic
 def hetero_node_data(shape: HeteroShape, rank: int, offsets, device, seed: int = 0,
                      dtype=torch.bfloat16, feature_types=(0, 1, 2), alloc=None):
     """Random features per node type ([L_t, F], seeded per global vertex chunk so values do
-    not depend on W), paper labels and the paper train mask. ``alloc(shape, dtype)`` places
+    not depend on W), paper labels and the paper train mask. ``alloc(type, shape, dtype)`` places
     the feature tensors (e.g. on the symmetric heap for one-sided remote gets)."""
     C = 1 << 20
     feats = {}
     for t in feature_types:
         lo, hi = offsets[t][rank], offsets[t][rank + 1]
-        x = alloc((hi - lo, shape.num_features), dtype) if alloc is not None else \
+        x = alloc(t, (hi - lo, shape.num_features), dtype) if alloc is not None else \
             torch.empty(hi - lo, shape.num_features, device=device, dtype=dtype)
         g = torch.Generator(device=device)
         for c in range(lo // C, (hi + C - 1) // C):

@@ -3,8 +3,9 @@
 Counterpart of ``DistributedBatchNorm1D`` (experiments/OGB-LSC/distributed_layers.py:77-214)
 with its defects fixed:
 
-* statistics are exact: every rank contributes ``(n_r, mean_r, M2_r)`` (one fused
-  ``torch.var_mean`` pass, fp32) and the ranks' moments are combined with Chan's parallel
+* statistics are exact: every rank contributes ``(n_r, mean_r, M2_r)`` (one pass of the
+  native ``bn_reduce`` kernel on GPU tensors — bf16 read as is, shifted fp32 partial sums,
+  fp64 totals; ``torch.var_mean`` elsewhere) and the ranks' moments are combined with Chan's parallel
   formula after ONE all-gather of a ``[W, 2F+1]`` buffer — the reference divided the local
   *mean* by the global row count and all-reduced its numerator after using it;
 * backward uses the textbook closed form
@@ -17,7 +18,10 @@ with its defects fixed:
 * the running variance uses the unbiased estimate (as ``torch.nn.BatchNorm1d``).
 
 ``recompute=True`` keeps only the input and recomputes ``x_hat`` in backward (the
-reference's ``DistributedBN_with_Recompute``); otherwise ``x_hat`` is saved.
+reference's ``DistributedBN_with_Recompute``); otherwise ``x_hat`` is saved. The native
+GPU path always recomputes (saving the bf16 input is cheaper than an fp32 ``x_hat``) and
+can fuse the following ReLU (``forward(x, relu=True)``: the mask is recomputed from ``x``
+in backward, nothing extra is stored).
 """
 from __future__ import annotations
 
@@ -37,18 +41,42 @@ def _cdt(x: torch.Tensor) -> torch.dtype:
     return torch.float64 if x.dtype == torch.float64 else torch.float32
 
 
+def _native_ok(x: torch.Tensor) -> bool:
+    return (x.is_cuda and x.dim() == 2 and x.dtype in (torch.float32, torch.bfloat16)
+            and (x.stride(1) == 1 or x.shape[1] <= 1))
+
+
+def _ops():
+    from .. import _native
+
+    return _native.ops()
+
+
+def _local_moments(x: torch.Tensor):
+    """(n, mean, biased var) of this rank's rows, fp32 (fp64 for fp64 inputs)."""
+    n, F = x.shape[0], x.shape[1]
+    if n == 0:
+        z = x.new_zeros(F, dtype=_cdt(x))
+        return 0, z, z.clone()
+    if _native_ok(x):
+        # one pass over x (bf16 stays bf16): sums shifted by the first row, fp64 totals
+        center = x[0].float().contiguous()
+        s = _ops().bn_reduce(x, None, center, None, None, None, False, 0)
+        m1 = s[0] / n
+        mean = (center.double() + m1).float()
+        var = (s[1] / n - m1 * m1).clamp_min(0).float()
+        return n, mean, var
+    var, mean = torch.var_mean(x.to(_cdt(x)), dim=0, unbiased=False)
+    return n, mean, var
+
+
 def global_moments(x: torch.Tensor, group=None):
     """(N, mean, biased var) of the rows of ``x`` over every rank of ``group`` (fp32)."""
-    xf = x.to(_cdt(x))
-    n = x.shape[0]
+    n, mean, var = _local_moments(x)
     F = x.shape[1]
-    if n > 0:
-        var, mean = torch.var_mean(xf, dim=0, unbiased=False)
-    else:
-        var = mean = xf.new_zeros(F)
     if _world(group) == 1:
         return float(n), mean, var
-    packed = torch.cat([xf.new_tensor([float(n)]), mean, var * n])
+    packed = torch.cat([mean.new_tensor([float(n)]), mean, var * n])
     out = [torch.empty_like(packed) for _ in range(_world(group))]
     dist.all_gather(out, packed, group=group)
     allp = torch.stack(out)
@@ -59,45 +87,81 @@ def global_moments(x: torch.Tensor, group=None):
     return N, gmean, m2 / max(N, 1.0)
 
 
+def _vec(p: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+    return None if p is None else p.reshape(-1).float().contiguous()
+
+
 class _SyncBNFn(Function):
+    """``y = act(BN(x))`` with global statistics; ``act`` is ReLU when ``relu``.
+
+    GPU (fp32/bf16 [N, F]): native kernels (csrc/kernels/batchnorm.hip) — one pass for the
+    statistics, one fused normalise/affine/ReLU pass, and in backward one fused reduction
+    and one fused apply; only ``x`` is saved and nothing is materialised in fp32.
+    Elsewhere: PyTorch reference math (``recompute`` saves ``x`` instead of ``x_hat``)."""
+
     @staticmethod
-    def forward(ctx, x, gamma, beta, eps: float, group, recompute: bool, box: list):
+    def forward(ctx, x, gamma, beta, eps: float, group, recompute: bool, box: list,
+                relu: bool = False):
         N, mean, var = global_moments(x, group)
         box.append(N)
         rstd = torch.rsqrt(var + eps)
+        ctx.group, ctx.N, ctx.relu = group, N, relu
+        ctx.has_affine = gamma is not None
+        ctx.gshape = None if gamma is None else gamma.shape
+        ctx.gdtype = None if gamma is None else gamma.dtype
+        ctx.native = _native_ok(x)
+        g, b = _vec(gamma), _vec(beta)
+        if ctx.native:
+            y = _ops().bn_apply(x, None, mean, rstd, g, b, None, None, relu, 0)
+            ctx.save_for_backward(x, mean, rstd, g, b)
+            return y, mean, var
+        ctx.recompute = recompute
         xhat = (x.to(mean.dtype) - mean) * rstd
         y = xhat
         if gamma is not None:
-            y = y * gamma.reshape(-1).to(mean.dtype) + beta.reshape(-1).to(mean.dtype)
-        ctx.group, ctx.N, ctx.recompute = group, N, recompute
-        ctx.has_affine = gamma is not None
-        ctx.gshape = None if gamma is None else gamma.shape
-        ctx.save_for_backward(x if recompute else xhat, mean, rstd,
-                              gamma if gamma is not None else rstd)
+            y = y * g.to(mean.dtype) + b.to(mean.dtype)
+        if relu:
+            y = torch.relu(y)
+        ctx.save_for_backward(x if recompute else xhat, mean, rstd, g, b)
         return y.to(x.dtype), mean, var
 
     @staticmethod
     def backward(ctx, dy, _dm, _dv):
-        saved, mean, rstd, gamma = ctx.saved_tensors
-        xhat = (saved.to(mean.dtype) - mean) * rstd if ctx.recompute else saved
-        dyf = dy.to(mean.dtype)
-        g = gamma.reshape(-1).to(mean.dtype) if ctx.has_affine else None
-        sum_dy = dyf.sum(0)
-        sum_dy_xhat = (dyf * xhat).sum(0)
+        saved, mean, rstd, g, b = ctx.saved_tensors
+        F = mean.numel()
+        Nf = max(ctx.N, 1.0)
+        if ctx.native:
+            x = saved
+            dy = dy.to(x.dtype)
+            if dy.stride(1) != 1 or dy.shape != x.shape:
+                dy = dy.contiguous()
+            s = _ops().bn_reduce(x, dy, mean, rstd, g, b, ctx.relu, 1).float()
+            sum_dy, sum_dy_xhat = s[0], s[1]
+        else:
+            xhat = (saved.to(mean.dtype) - mean) * rstd if ctx.recompute else saved
+            dyf = dy.to(mean.dtype)
+            if ctx.relu:
+                pre = xhat * g.to(mean.dtype) + b.to(mean.dtype) if g is not None else xhat
+                dyf = dyf * (pre > 0)
+            sum_dy = dyf.sum(0)
+            sum_dy_xhat = (dyf * xhat).sum(0)
         dgamma = dbeta = None
         if ctx.has_affine:
-            dgamma = sum_dy_xhat.reshape(ctx.gshape).to(gamma.dtype)
-            dbeta = sum_dy.reshape(ctx.gshape).to(gamma.dtype)
+            dgamma = sum_dy_xhat.reshape(ctx.gshape).to(ctx.gdtype)
+            dbeta = sum_dy.reshape(ctx.gshape).to(ctx.gdtype)
         glob = torch.cat([sum_dy, sum_dy_xhat])
         if _world(ctx.group) > 1:
             dist.all_reduce(glob, group=ctx.group)
-        F = sum_dy.numel()
-        N = max(ctx.N, 1.0)
-        m_dy, m_dyx = glob[:F] / N, glob[F:] / N
-        dx = (dyf - m_dy - xhat * m_dyx) * rstd
-        if g is not None:
-            dx = dx * g
-        return dx.to(dy.dtype), dgamma, dbeta, None, None, None, None
+        m_dy, m_dyx = glob[:F] / Nf, glob[F:] / Nf
+        if ctx.native:
+            dx = _ops().bn_apply(saved, dy, mean, rstd, g, b, m_dy.contiguous(),
+                                 m_dyx.contiguous(), ctx.relu, 1)
+        else:
+            dx = (dyf - m_dy - xhat * m_dyx) * rstd
+            if g is not None:
+                dx = dx * g.to(mean.dtype)
+            dx = dx.to(dy.dtype)
+        return dx, dgamma, dbeta, None, None, None, None, None
 
 
 class DistributedBatchNorm1D(nn.Module):
@@ -126,7 +190,8 @@ class DistributedBatchNorm1D(nn.Module):
         self.recompute = recompute
         self.group = group
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, relu: bool = False) -> torch.Tensor:
+        """``BN(x)``, or ``relu(BN(x))`` fused into the same kernels when ``relu``."""
         squeeze = False
         if x.dim() == 3:
             if x.size(0) != 1:
@@ -137,7 +202,7 @@ class DistributedBatchNorm1D(nn.Module):
         if self.training or not self.track_running_stats:
             box: list = []
             y, mean, var = _SyncBNFn.apply(x, self.gamma, self.beta, self.eps, self.group,
-                                           self.recompute, box)
+                                           self.recompute, box, relu)
             if self.training and self.track_running_stats:
                 with torch.no_grad():
                     self.num_batches_tracked += 1
@@ -149,6 +214,8 @@ class DistributedBatchNorm1D(nn.Module):
             y = (x.to(_cdt(x)) - self.running_mean) * torch.rsqrt(self.running_var + self.eps)
             if self.gamma is not None:
                 y = y * self.gamma + self.beta
+            if relu:
+                y = torch.relu(y)
             y = y.to(x.dtype)
         return y.unsqueeze(0) if squeeze else y
 

@@ -31,6 +31,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.aggregate import aggregate
+from ..ops.dense import linear as _dense_linear
 from ..parallel.hetero_graph import SourceGraph, source_aggregate
 from .norm import DistributedBatchNorm1D
 
@@ -99,8 +100,18 @@ class CommAwareRGCN(nn.Module):
         )
 
     # ------------------------------------------------------------------ helpers
+    @staticmethod
+    def _lin(mod: nn.Linear, x: torch.Tensor) -> torch.Tensor:
+        # tall-skinny-aware backward: split-K weight gradient, native bias column sum
+        return _dense_linear(x, mod.weight, mod.bias)
+
+    def _head(self, h: torch.Tensor) -> torch.Tensor:
+        lin1, bn, _, drop, lin2 = self.mlp
+        t = bn(self._lin(lin1, h), relu=True)
+        return self._lin(lin2, drop(t))
+
     def _finish(self, l: int, t: torch.Tensor) -> torch.Tensor:
-        t = torch.relu(self.bns[l](t))
+        t = self.bns[l](t, relu=True)  # BN + ReLU fused (native kernels on GPU)
         return F.dropout(t, self.dropout, self.training)
 
     def forward(self, xs, graph, edge_types=None) -> torch.Tensor:
@@ -115,7 +126,7 @@ class CommAwareRGCN(nn.Module):
         need, rels = layer_plan(ets, self.num_layers, self.target, avail)
         h = dict(xs)
         for l in range(self.num_layers):
-            tmp = {t: self.skips[l](h[t]) for t in sorted(need[l])}
+            tmp = {t: self._lin(self.skips[l], h[t]) for t in sorted(need[l])}
             by_src: Dict[int, List[int]] = {}
             for r in rels[l]:
                 by_src.setdefault(ets[r][0], []).append(r)
@@ -124,24 +135,24 @@ class CommAwareRGCN(nn.Module):
                 if l == 0:
                     # transform-first: one GEMM over [W_r1 | W_r2 ...], static halo rows
                     W = torch.cat([self.convs[0][r].weight for r in rs], 0)
-                    z = F.linear(h[s], W)
+                    z = _dense_linear(h[s], W)
                     xh = sg.static_halo(xs[s])
-                    zh = F.linear(xh, W) if xh is not None else None
+                    zh = _dense_linear(xh, W) if xh is not None else None
                     C = self.hidden
                     spec = [(r, i * C, (i + 1) * C) for i, r in enumerate(rs)]
                     outs = source_aggregate(z, sg, spec, static_halo=zh) if zh is not None \
                         else source_aggregate(z, sg, spec)
                     for r, o in zip(rs, outs):
                         d = ets[r][1]
-                        tmp[d] = tmp[d] + o.to(tmp[d].dtype)
+                        tmp[d] = tmp[d].add_(o.to(tmp[d].dtype))  # linear outputs are not saved
                 else:
                     spec = [(r, 0, h[s].shape[1]) for r in rs]
                     outs = source_aggregate(h[s], sg, spec)
                     for r, o in zip(rs, outs):
                         d = ets[r][1]
-                        tmp[d] = tmp[d] + self.convs[l][r](o)
+                        tmp[d] = tmp[d].add_(self._lin(self.convs[l][r], o))
             h = {t: self._finish(l, v) for t, v in tmp.items()}
-        return self.mlp(h[self.target])
+        return self._head(h[self.target])
 
     # ------------------------------------------------------------------ RelationGraph path
     def _forward_relations(self, xs: List[torch.Tensor], edge_types, graphs) -> torch.Tensor:
@@ -166,4 +177,4 @@ class CommAwareRGCN(nn.Module):
                 tmp[d] = tmp[d] + self.convs[l][r](agg)
             h = dict(h) if isinstance(h, dict) else {i: v for i, v in enumerate(h)}
             h.update({t: self._finish(l, v) for t, v in tmp.items()})
-        return self.mlp(h[self.target])
+        return self._head(h[self.target])
