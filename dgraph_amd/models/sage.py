@@ -293,6 +293,19 @@ class SAGEStackFn(Function):
             if fused and relu:
                 mask = torch.empty(tile32_mask_words(L, Fo), dtype=torch.int64,
                                    device=h.device)
+            if last and pf and not relu and out_rows is not None:
+                # only the loss rows leave the node: y[rows] = A[rows, :] (h Wn) +
+                # h[rows] Ws + b — the row-restricted SpMM reads ~|rows|/L of the edges
+                # and receives only the halo rows those rows touch
+                z = torch.mm(h, wn_, out=V("tmp_a", Fo))
+                y_rows = graph.aggregate_rows(z, out_rows, mean=True)
+                del z
+                if b is not None:
+                    y_rows.add_(b.to(dt))
+                y_rows.addmm_(h.index_select(0, out_rows), ws_)
+                masks.append(None)
+                h = y_rows
+                break
             if pf:
                 z = torch.mm(h, wn_, out=V("tmp_a", Fo))
                 graph.aggregate(z, mean=True, out=y)
@@ -339,8 +352,10 @@ class SAGEStackFn(Function):
         ctx.out_rows = out_rows
         C = dims[-1]
         if out_rows is not None:
-            # the last layer is computed for every vertex; only the requested rows leave
-            # the node, so autograd never holds a dense [V, C] output gradient
+            # only the requested rows leave the node, so autograd never holds a dense
+            # [V, C] output gradient (a project-first last layer computed just those rows)
+            if h.shape[0] == out_rows.numel() and specs[-1][1] and not specs[-1][0]:
+                return h[:, :C].contiguous() if C != h.shape[1] else h
             return h.index_select(0, out_rows)[:, :C].contiguous()
         return h[:, :C] if C != h.shape[1] else h
 

@@ -48,6 +48,7 @@ class DistGraph:
         self.symmetric = symmetric
         self.overlap = overlap
         self._restrict_cache = {}
+        self._restrict_fwd_cache = {}
         self._static_cache = {}
         if self.H > 0 or (send_local_idx is not None and send_local_idx.numel() > 0):
             self.interior, self.halo = csr.split_columns(self.L)
@@ -213,7 +214,7 @@ class DistGraph:
             base = torch.repeat_interleave(send_off[:-1], peer_cnt.to(dev))
             recv_local = self.send_map.idx.long()[base + peer_slot.to(dev)]
             sub = (ht_nz, AllToAllV(cnt_l, peer_l, self.a2a.group),
-                   IndexMap(recv_local, self.L).transpose_csr())
+                   IndexMap(recv_local, self.L).transpose_csr(), nz, recv_local)
         hit = (it, cs, sub)
         self._restrict_cache = {key: hit}  # one loss-row set at a time
         return hit
@@ -230,7 +231,7 @@ class DistGraph:
         g_rows = g_rows.contiguous()
         if sub is None:
             return K.spmm(it.rowptr, it.col, g_rows, out, col_scale=cs)
-        ht_nz, a2a_sub, st = sub
+        ht_nz, a2a_sub, st = sub[:3]
         hg = K.spmm(ht_nz.rowptr, ht_nz.col, g_rows, col_scale=cs)
         sg, work = a2a_sub(hg, async_op=True)
         if not self.overlap:
@@ -238,6 +239,50 @@ class DistGraph:
         out = K.spmm(it.rowptr, it.col, g_rows, out, col_scale=cs)
         work.wait()
         K.spmm(st.rowptr, st.col, sg, out, beta=1.0)
+        return out
+
+    def _restricted_fwd(self, rows: torch.Tensor):
+        """Forward counterpart of :meth:`_restricted`: A[rows, :L] and A[rows, halo] with
+        the halo columns renumbered onto the contributing halo rows only, plus the
+        forward sub-plan (owners send just those rows: the reverse of the backward
+        sub-plan)."""
+        key = (rows.data_ptr(), rows.numel(), str(rows.device))
+        hit = self._restrict_fwd_cache.get(key)
+        if hit is not None:
+            return hit
+        ir = self.interior.select_rows(rows)
+        rs = self.inv_deg[rows.long()].contiguous()
+        hsub = None
+        if self.halo is not None:
+            _, _, sub = self._restricted(rows)
+            _, a2a_sub, _, nz, recv_local = sub
+            hr = self.halo.select_rows(rows)
+            pos = torch.full((self.H,), -1, dtype=torch.long, device=nz.device)
+            pos[nz] = torch.arange(nz.numel(), device=nz.device)
+            hr = CSR(hr.rowptr, pos[hr.col.long()].to(torch.int32).contiguous(),
+                     max(int(nz.numel()), 1))
+            hsub = (hr, a2a_sub.reversed(), recv_local.to(self.send_map.idx.dtype))
+        hit = (ir, rs, hsub)
+        self._restrict_fwd_cache = {key: hit}
+        return hit
+
+    def aggregate_rows(self, x: torch.Tensor, rows: torch.Tensor, mean: bool = True,
+                       out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """``aggregate(x)[rows]`` without aggregating the other rows: A[rows, :] x over the
+        interior block, and over only the halo rows that neighbour ``rows`` (the owners
+        send just those, overlapped with the interior SpMM). The first call for a row set
+        is collective (sub-plan exchange, shared with :meth:`aggregate_T_rows`)."""
+        ir, rs, hsub = self._restricted_fwd(rows)
+        rsc = rs if mean else None
+        if hsub is None:
+            return K.spmm(ir.rowptr, ir.col, x, out, row_scale=rsc)
+        hr, a2a_f, recv_local = hsub
+        recv, work = a2a_f(K.gather_rows(x, recv_local), async_op=True)
+        if not self.overlap:
+            work.wait()
+        out = K.spmm(ir.rowptr, ir.col, x, out, row_scale=rsc)
+        work.wait()
+        K.spmm(hr.rowptr, hr.col, recv, out, row_scale=rsc, beta=1.0)
         return out
 
     def prepare_backward(self):
