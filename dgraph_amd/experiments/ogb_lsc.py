@@ -1,4 +1,4 @@
-"""OGB-LSC (MAG240M-like) RGAT experiment (experiments/OGB-LSC/{main,Trainer,config}.py).
+"""OGB-LSC (MAG240M-like) RGAT / R-GCN experiment (experiments/OGB-LSC/{main,Trainer,config}.py).
 
 Full-graph training of :class:`~dgraph_amd.models.rgat.CommAwareRGAT` on a heterogeneous
 paper/author/institution graph: Adam (lr 1e-4, weight decay 5e-4) with a StepLR schedule,
@@ -26,6 +26,7 @@ from ..data.hetero import (DGraph_MAG240M_Dataset, SyntheticHeteroConfig,
                            SyntheticHeterogeneousDataset)
 from ..models.norm import GetGlobalVal
 from ..models.rgat import CommAwareRGAT
+from ..models.rgcn import CommAwareRGCN
 from ..parallel.grad_sync import GradSync
 from ..utils.metrics import print_on_rank_zero
 
@@ -38,6 +39,7 @@ class ModelConfig:
     heads: int = 1          # reference default 4 was unused; must divide hidden_channels
     use_cache: bool = True
     relations: str = "all"
+    model: str = "rgat"     # "rgat" (reference model) or "rgcn" (BASELINE config 4)
 
 
 @dataclass
@@ -74,11 +76,19 @@ class Trainer:
         self.device = device or _device()
         mc, tc = self.model_config, self.training_config
         torch.manual_seed(seed)
-        self.model = CommAwareRGAT(
-            in_channels=dataset.num_features, out_channels=dataset.num_classes,
-            hidden_channels=mc.hidden_channels, num_relations=dataset.num_relations,
-            num_layers=mc.num_layers, heads=mc.heads, comm=comm, dropout=mc.dropout,
-            relations=mc.relations, bn_group=comm.group).to(self.device)
+        if mc.model == "rgcn":
+            self.model = CommAwareRGCN(
+                dataset.num_features, mc.hidden_channels, dataset.num_classes,
+                dataset.num_relations, mc.num_layers, dropout=mc.dropout,
+                edge_types=dataset.edge_types, comm=comm, bn_group=comm.group).to(self.device)
+        elif mc.model == "rgat":
+            self.model = CommAwareRGAT(
+                in_channels=dataset.num_features, out_channels=dataset.num_classes,
+                hidden_channels=mc.hidden_channels, num_relations=dataset.num_relations,
+                num_layers=mc.num_layers, heads=mc.heads, comm=comm, dropout=mc.dropout,
+                relations=mc.relations, bn_group=comm.group).to(self.device)
+        else:
+            raise ValueError(f"unknown model {mc.model!r} (rgat | rgcn)")
         self.sync = GradSync(self.model.parameters(), group=comm.group)
         self.optimizer = torch.optim.Adam(self.model.parameters(), lr=tc.lr,
                                           weight_decay=tc.weight_decay)
@@ -134,7 +144,7 @@ def main(comm_type: str = "nccl", dataset: str = "synthetic", num_papers: int = 
          num_authors: int = 512, num_institutions: int = 16, num_features: int = 16,
          num_classes: int = 153, epochs: int = 100, hidden_channels: int = 2,
          num_layers: int = 2, heads: int = 1, dropout: float = 0.5, lr: float = 1e-4,
-         data_dir: str = "data/MAG240M", cache_dir: str = None):
+         data_dir: str = "data/MAG240M", cache_dir: str = None, model: str = "rgat"):
     if dataset not in ("synthetic", "mag240m"):
         raise ValueError(f"Invalid dataset: {dataset}")
     if comm_type not in ("nccl", "nvshmem", "rocshmem", "gloo", "mpi"):
@@ -149,7 +159,7 @@ def main(comm_type: str = "nccl", dataset: str = "synthetic", num_papers: int = 
         ds = DGraph_MAG240M_Dataset(comm, data_dir=data_dir)
     trainer = Trainer(ds, comm, ModelConfig(hidden_channels=hidden_channels,
                                             num_layers=num_layers, heads=heads,
-                                            dropout=dropout),
+                                            dropout=dropout, model=model),
                       TrainingConfig(epochs=epochs, lr=lr))
     trainer.prepare_data()
     final = trainer.train()
@@ -168,7 +178,7 @@ def cli(argv=None):
                                ("hidden_channels", int, 2), ("num_layers", int, 2),
                                ("heads", int, 1), ("dropout", float, 0.5),
                                ("lr", float, 1e-4), ("data_dir", str, "data/MAG240M"),
-                               ("cache_dir", str, None)]:
+                               ("cache_dir", str, None), ("model", str, "rgat")]:
         p.add_argument(f"--{name}", type=typ, default=default)
     main(**vars(p.parse_args(argv)))
     Communicator.instance().destroy()

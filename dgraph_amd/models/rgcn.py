@@ -115,8 +115,12 @@ class CommAwareRGCN(nn.Module):
         return F.dropout(t, self.dropout, self.training)
 
     def forward(self, xs, graph, edge_types=None) -> torch.Tensor:
+        """``forward(xs, HeteroGraph)`` (hot path), or the RelationGraph path with either
+        argument order: ``(xs, graphs, edge_types)`` or RGAT's ``(xs, edge_types, graphs)``."""
         if isinstance(graph, HeteroGraph):
             return self._forward_hetero(xs, graph)
+        if edge_types is not None and len(graph) and isinstance(graph[0], tuple):
+            graph, edge_types = edge_types, graph
         return self._forward_relations(xs, edge_types, graph)
 
     # ------------------------------------------------------------------ hot path

@@ -38,7 +38,7 @@ def test_ogb_gcn_trainer(ranks, tmp_path, world):
         np.testing.assert_allclose(tr, np.load(other), rtol=1e-4, atol=1e-5)
 
 
-def _lsc(rank, world, out_path):
+def _lsc(rank, world, out_path, model="rgat"):
     import torch
 
     from dgraph_amd import Communicator
@@ -48,14 +48,15 @@ def _lsc(rank, world, out_path):
     trainer, final, accs = ogb_lsc.main(comm_type="nccl", num_papers=200, num_authors=300,
                                         num_institutions=12, num_features=8, num_classes=4,
                                         epochs=6, hidden_channels=16, heads=2, dropout=0.0,
-                                        lr=1e-2)
+                                        lr=1e-2, model=model)
     if rank == 0:
         np.save(out_path, np.array([h["loss"] for h in trainer.history] + list(accs)))
     Communicator.instance().destroy()
 
 
-def test_ogb_lsc_trainer_two_ranks(ranks, tmp_path):
-    ranks(_lsc, 2, str(tmp_path / "lsc.npy"))
+@pytest.mark.parametrize("model", ["rgat", "rgcn"])
+def test_ogb_lsc_trainer_two_ranks(ranks, tmp_path, model):
+    ranks(_lsc, 2, str(tmp_path / "lsc.npy"), model)
     r = np.load(tmp_path / "lsc.npy")
     losses, accs = r[:6], r[6:]
     assert np.isfinite(losses).all() and losses[-1] < losses[0]
