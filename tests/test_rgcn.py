@@ -162,27 +162,40 @@ def test_relation_graph_path_trains():
 
 
 @pytest.mark.gpu
-def test_hot_path_gpu_matches_cpu():
-    """bf16 R-GCN on the MI355X (native SpMM over strided relation column slices, native
-    BN+ReLU, tall-skinny linears) vs the fp32 CPU run of the same model and graph."""
+@pytest.mark.parametrize("gpu_dtype", ["fp32", "bf16"])
+def test_hot_path_gpu_matches_cpu(gpu_dtype):
+    """R-GCN on the MI355X (native SpMM over strided relation column slices, native
+    BN+ReLU, tall-skinny linears) vs the fp32 CPU run of the same model and graph: tight
+    in fp32 (same math), loose in bf16 autocast (two BN backwards amplify bf16 rounding)."""
     shape = HETERO_SHAPES["mag240m"].scaled(1e-4)
+    # graph and data generated once on the CPU (device RNG streams differ), then moved
+    part_cpu = build_hetero_partition(shape, 0, 1, "cpu", global_frac=0.2, window=256)
+    feats_cpu, y_cpu, tr_cpu = hetero_node_data(shape, 0, part_cpu["offsets"], "cpu",
+                                                dtype=torch.float32)
+    bf16 = gpu_dtype == "bf16"
     res = {}
-    for dev, dt in (("cpu", torch.float32), ("cuda", torch.bfloat16)):
-        part = build_hetero_partition(shape, 0, 1, dev, global_frac=0.2, window=256)
+    for dev in ("cpu", "cuda"):
+        part = {"offsets": part_cpu["offsets"], "sources": {
+            s: {k: (v.to(dev) if hasattr(v, "to") else v) for k, v in d.items()}
+            for s, d in part_cpu["sources"].items()}}
         g = HeteroGraph.from_partition(part, EDGE_TYPES)
-        feats, y, tr = hetero_node_data(shape, 0, part["offsets"], dev, dtype=dt)
-        feats = {t: v[:, :64].contiguous() for t, v in feats.items()}
+        dt = torch.bfloat16 if (bf16 and dev == "cuda") else torch.float32
+        feats = {t: v[:, :64].to(dt).to(dev).contiguous() for t, v in feats_cpu.items()}
+        y, tr = y_cpu.to(dev), tr_cpu.to(dev)
         torch.manual_seed(0)
         m = CommAwareRGCN(64, 64, shape.num_classes, 5, 2, dropout=0.0).to(dev)
-        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=dev == "cuda"):
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=bf16 and dev == "cuda"):
             out = m(feats, g)
         loss = F.cross_entropy(out[tr].float(), y[tr])
         loss.backward()
         res[dev] = (out.float().cpu(), {n: p.grad.float().cpu() for n, p in m.named_parameters()
                                         if p.grad is not None})
-    torch.testing.assert_close(res["cuda"][0], res["cpu"][0], atol=6e-2, rtol=6e-2)
+    fwd_tol, grad_tol = (6e-2, 1.5e-1) if bf16 else (1e-3, 1e-3)
+    torch.testing.assert_close(res["cuda"][0], res["cpu"][0], atol=fwd_tol, rtol=fwd_tol)
     assert res["cuda"][1].keys() == res["cpu"][1].keys()
     for n, b in res["cpu"][1].items():
         a = res["cuda"][1][n]
-        rel = (a - b).norm() / b.norm().clamp_min(1e-12)
-        assert rel < 5e-2, (n, float(rel))
+        # biases feeding a BatchNorm have a zero true gradient (BN removes the column
+        # mean): compare those on an absolute scale
+        rel = (a - b).norm() / b.norm().clamp_min(1e-2 if bf16 else 1e-4)
+        assert rel < grad_tol, (n, float(rel))
