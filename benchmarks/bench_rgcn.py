@@ -27,7 +27,9 @@ import os
 import sys
 import time
 
-os.environ.setdefault("PYTORCH_ALLOC_CONF", "max_split_size_mb:512")
+# (no max_split_size here, unlike bench.py: the relation tensors come in many different
+#  large sizes, and unsplittable cached blocks then miss on almost every request —
+#  hipMalloc/hipFree churn took a W=8 rank's step from 476 ms to 3.1 s)
 
 import torch
 import torch.distributed as dist
