@@ -48,6 +48,13 @@ def icosahedron() -> Tuple[np.ndarray, np.ndarray]:
             v += [(0.0, a, b), (a, b, 0.0), (b, 0.0, a)]
     v = np.asarray(v, dtype=np.float64)
     v /= np.linalg.norm(v, axis=1, keepdims=True)
+    # GraphCast orientation (data_utils/icosahedral_mesh.py:100-175): rotate about y by
+    # (pi - dihedral angle) / 2 so two faces sit symmetric about each pole. The grid2mesh
+    # kNN counts depend on it: 1 618 824 edges at level 6 on the 721x1440 grid, as pinned
+    # by experiments/GraphCast/tests/test_single_graph_data.py:27.
+    ang = (math.pi - 2.0 * math.asin(phi / math.sqrt(3.0))) / 2.0
+    c, s = math.cos(ang), math.sin(ang)
+    v = v @ np.array([[c, 0.0, -s], [0.0, 1.0, 0.0], [s, 0.0, c]])
     faces = ConvexHull(v).simplices.astype(np.int64)
     # orient counter-clockwise seen from outside
     a, b, c = v[faces[:, 0]], v[faces[:, 1]], v[faces[:, 2]]
@@ -149,11 +156,18 @@ class GlobalGraphCastGraph:
     m2g: Tuple[np.ndarray, np.ndarray]   # (mesh src, grid dst)
 
 
-def build_global_graph(mesh_level: int = 6, grid_shape=(721, 1440)) -> GlobalGraphCastGraph:
+def build_global_graph(mesh_level: int = 6, grid_shape=(721, 1440),
+                       duplicate_mesh_edges: bool = False) -> GlobalGraphCastGraph:
+    """``duplicate_mesh_edges=True`` reproduces the reference's mesh edge list, which
+    bidirects the already bidirectional multimesh (``create_graph(to_bidirected=True)``,
+    data_utils/graphcast_graph.py:228-233) and so carries every edge twice (655 320 at
+    level 6); the default keeps each directed edge once, as in the GraphCast paper."""
     from scipy.spatial import cKDTree
 
     verts, faces = mesh_hierarchy(mesh_level)
     m_src, m_dst = multimesh_edges(faces)
+    if duplicate_mesh_edges:
+        m_src, m_dst = np.concatenate([m_src, m_dst]), np.concatenate([m_dst, m_src])
     fs, fd = faces_to_edges(faces[-1])
     max_len = float(np.linalg.norm(verts[fs] - verts[fd], axis=1).max())
     lat, lon = lat_lon_grid(grid_shape)

@@ -51,6 +51,20 @@ def test_graph_sizes_small():
     assert pg.m2m.num_edges == g.m2m[0].size
 
 
+def test_static_graph_sizes_match_reference():
+    """Level-6 multimesh on the 721x1440 grid: the sizes the reference pins
+    (experiments/GraphCast/tests/test_single_graph_data.py:21-33)."""
+    g = build_global_graph(6, (721, 1440), duplicate_mesh_edges=True)
+    assert g.mesh_xyz.shape == (40962, 3)
+    assert g.m2m[0].size == g.m2m[1].size == 655320
+    assert g.g2m[0].size == g.g2m[1].size == 1618824
+    assert g.m2g[0].size == g.m2g[1].size == 3114720
+    assert edge_features(g.mesh_xyz[g.m2m[0]], g.mesh_xyz[g.m2m[1]]).shape == (655320, 4)
+    # default layout: each directed multimesh edge once (the paper's 327 660)
+    s, d = multimesh_edges(mesh_hierarchy(6)[1])
+    assert s.size == 327660 and len(set(zip(s.tolist(), d.tolist()))) == 327660
+
+
 def _ref_edge(block, xs, xd, e, s, d):
     return block.mesh_mlp(torch.cat([xs[s], xd[d], e], 1)) + e
 
