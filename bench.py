@@ -53,12 +53,29 @@ def parse():
                     help="single process: run rank --rehearse-rank of a W-way partition with "
                          "a loopback halo exchange (per-rank compute + memory; no peers)")
     ap.add_argument("--rehearse-rank", type=int, default=0)
+    ap.add_argument("--profile-ops", default="",
+                    help="after the timed steps, profile one extra step with "
+                         "torch.profiler and write the per-op device-time table here")
     return ap.parse_args()
 
 
 def log(rank, *a):
     if rank == 0:
         print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def _profile_one_step(step, path):
+    """Per-aten-op device time of one (untimed) step, grouped by input shape."""
+    from torch.profiler import ProfilerActivity, profile
+
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA],
+                 record_shapes=True) as prof:
+        step()
+        torch.cuda.synchronize()
+    ka = prof.key_averages(group_by_input_shape=True)
+    with open(path, "w") as f:
+        f.write(ka.table(sort_by="self_cuda_time_total", row_limit=60, max_name_column_width=60,
+                         max_shapes_column_width=90))
 
 
 def main():
@@ -143,6 +160,8 @@ def main():
         l = step()
     barrier_sync()
     elapsed = time.perf_counter() - t_start
+    if args.profile_ops and rank == 0:
+        _profile_one_step(step, args.profile_ops)
     ms = torch.tensor([elapsed * 1000.0 / max(args.steps, 1)], dtype=torch.float64,
                       device=dev)
     if world > 1:

@@ -218,6 +218,28 @@ at::Tensor col_sum_op(const at::Tensor& g) {
   return partial.sum(0);
 }
 
+// out[r, :] = x[r, :] * s[r] for a row-strided 2-D x (a column slice of a wider tensor)
+void row_scale_cols_op(const at::Tensor& x, const at::Tensor& s, const at::Tensor& out) {
+  check_dev(x, x, "x");
+  check_dev(x, out, "out");
+  check_dev(x, s, "s");
+  TORCH_CHECK(x.dim() == 2 && out.dim() == 2 && x.sizes() == out.sizes(), "shape mismatch");
+  TORCH_CHECK(x.scalar_type() == out.scalar_type(), "dtype mismatch");
+  TORCH_CHECK(s.scalar_type() == at::kFloat && s.is_contiguous() && s.numel() == x.size(0),
+              "s must be contiguous fp32 [rows]");
+  TORCH_CHECK(x.stride(1) == 1 && out.stride(1) == 1, "rows must be unit-stride");
+  const int64_t vec = x.scalar_type() == at::kBFloat16 ? 8 : 4;
+  TORCH_CHECK(x.size(1) % vec == 0 && x.stride(0) % vec == 0 && out.stride(0) % vec == 0,
+              "row_scale_cols needs 16-B vectors (width and row strides)");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0,
+              "row_scale_cols needs 16-B aligned x/out");
+  c10::DeviceGuard gd(x.device());
+  DG_HIP_CHECK(row_scale_cols(dtype_of(x), x.data_ptr(), x.stride(0), s.data_ptr<float>(),
+                              out.data_ptr(), out.stride(0), x.size(0),
+                              static_cast<int>(x.size(1)), cur_stream(x)));
+}
+
 // mode 0 (agg): out[r] = sum_c relu(rowterm[r] + gat[c]); mode 1 (cnt): out[r] = rowmul[r] *
 // #{c : rowterm[r] + gat[c] > 0}; mode 2 (tgrad): out[r] = sum_c gat2[c] * [rowterm[r]+gat[c]>0]
 void pair_relu_op(const at::Tensor& rowptr, const at::Tensor& col, int64_t mode,
@@ -523,6 +545,7 @@ TORCH_LIBRARY(dgraph_amd, m) {
   m.def("bias_relu_pack(Tensor(a!) y, Tensor? bias, Tensor(b!)? bits, bool relu) -> ()");
   m.def("relu_mask_bwd(Tensor(a!) g, Tensor bits) -> ()");
   m.def("col_sum(Tensor g) -> Tensor");
+  m.def("row_scale_cols(Tensor x, Tensor s, Tensor(a!) out) -> ()");
   m.def("pair_relu(Tensor rowptr, Tensor col, int mode, Tensor rowterm, Tensor gat, Tensor? gat2, "
         "Tensor? rowmul, Tensor(a!) out) -> ()");
   m.def("layer_norm_fwd(Tensor x, Tensor? gamma, Tensor? beta, Tensor? res, float eps) -> "
@@ -557,6 +580,7 @@ TORCH_LIBRARY_IMPL(dgraph_amd, CUDA, m) {
   m.impl("bias_relu_pack", &dgraph::bias_relu_pack_op);
   m.impl("relu_mask_bwd", &dgraph::relu_mask_bwd_op);
   m.impl("col_sum", &dgraph::col_sum_op);
+  m.impl("row_scale_cols", &dgraph::row_scale_cols_op);
   m.impl("pair_relu", &dgraph::pair_relu_op);
   m.impl("gather_add_act", &dgraph::gather_add_act_op);
   m.impl("layer_norm_fwd", &dgraph::layer_norm_fwd_op);

@@ -73,6 +73,10 @@ hipError_t relu_mask_bwd(DType dt, void* g, const uint32_t* bits, int64_t numel,
                          hipStream_t stream);
 hipError_t col_sum_partial(DType dt, const void* g, int64_t ld, int64_t L, int F,
                            float* partial, int nblocks, hipStream_t stream);
+//   row_scale_cols: out[r, 0:w] = x[r, c0:c0+w] * s[r] (x already offset by c0; w % 8 == 0,
+//                   16-B aligned rows).
+hipError_t row_scale_cols(DType dt, const void* x, int64_t ldx, const float* s, void* out,
+                          int64_t ldo, int64_t L, int w, hipStream_t stream);
 
 // ---------------------------------------------------------------------------
 // Fused edge-MLP kernels (edge_fused.hip, K-new-6). mode 0: out[r] = sum relu(R[r]+X[c]);

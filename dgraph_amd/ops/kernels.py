@@ -132,6 +132,15 @@ def col_sum(g: torch.Tensor) -> torch.Tensor:
     return _ref.col_sum(g)
 
 
+def row_scale_cols(x: torch.Tensor, s: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    """``out[r, :] = x[r, :] * s[r]`` for a row-strided ``x`` (e.g. a column slice);
+    fp32 ``s``. Native: one streaming pass with 16-B lanes (elementwise.hip)."""
+    if _native_ok(x):
+        _native.ops().row_scale_cols(x, _f32(s), out)
+        return out
+    return _ref.row_scale_cols(x, s, out)
+
+
 def bias_relu_pack(y: torch.Tensor, bias: Optional[torch.Tensor] = None,
                    bits: Optional[torch.Tensor] = None, relu: bool = True) -> None:
     """In place ``y = act(y + bias)``; optional 1-bit keep mask (int32 words)."""

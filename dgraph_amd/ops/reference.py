@@ -153,6 +153,11 @@ def relu_mask_bwd(g: torch.Tensor, bits: torch.Tensor) -> None:
     g.masked_fill_(~keep, 0)
 
 
+def row_scale_cols(x: torch.Tensor, s: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    out.copy_((x.float() * s.float().unsqueeze(1)).to(out.dtype))
+    return out
+
+
 def col_sum(g: torch.Tensor) -> torch.Tensor:
     return g.float().sum(0)
 

@@ -136,11 +136,14 @@ class DistGraph:
             return K.spmm(csr.rowptr, csr.col, g, out, col_scale=cs)
         if out is None:
             out = torch.empty(csr.num_rows, F, dtype=g.dtype, device=g.device)
-        csb = cs.unsqueeze(1)
+        aligned = g.data_ptr() % 16 == 0 and scratch.data_ptr() % 16 == 0 and F % 8 == 0
         for c0 in range(0, F, S):
             w = min(S, F - c0)
             buf = scratch[: rows * w].view(rows, w)
-            torch.mul(g[:, c0:c0 + w], csb, out=buf)
+            if aligned and w % 8 == 0:
+                K.row_scale_cols(g[:, c0:c0 + w], cs, buf)
+            else:
+                torch.mul(g[:, c0:c0 + w], cs.unsqueeze(1), out=buf)
             K.spmm(csr.rowptr, csr.col, buf, out[:, c0:c0 + w])
         return out
 

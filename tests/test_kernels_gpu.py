@@ -570,3 +570,15 @@ def test_aggregate_T_rows_matches_dense():
     ref = g.aggregate_T(dense)
     out = g.aggregate_T_rows(gr, rows)
     torch.testing.assert_close(out.float(), ref.float(), atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("F,c0,w", [(256, 128, 128), (192, 64, 128), (64, 0, 64), (40, 8, 24)])
+def test_row_scale_cols(dtype, F, c0, w):
+    """Native column-slice row scale vs the fp32 PyTorch reference."""
+    g = torch.randn(50_003, F, device=DEV).to(dtype)
+    s = torch.rand(50_003, device=DEV) + 0.1
+    out = torch.empty(50_003, w, device=DEV, dtype=dtype)
+    K.row_scale_cols(g[:, c0:c0 + w], s, out)
+    ref = (g[:, c0:c0 + w].float() * s.unsqueeze(1)).to(dtype)
+    torch.testing.assert_close(out.float(), ref.float(), atol=0, rtol=0)
