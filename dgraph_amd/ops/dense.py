@@ -24,8 +24,29 @@ def mm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     return torch.mm(a, b).float()
 
 
+_PARTIALS: dict = {}
+
+
+def _partials(dev: torch.device, n: int) -> torch.Tensor:
+    """Resident fp32 workspace for the split-K partial products, grown on demand and kept:
+    allocating ~2 GB per call next to a 269 GB working set made the caching allocator
+    free and re-map blocks (184 ms of host time per wgrad, profiles/)."""
+    buf = _PARTIALS.get(dev)
+    if buf is None or buf.numel() < n:
+        _PARTIALS.pop(dev, None)
+        buf = torch.empty(n, dtype=torch.float32, device=dev)
+        _PARTIALS[dev] = buf
+    return buf[:n]
+
+
 def _bmm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     if a.is_cuda and a.dtype != torch.float32:
+        out = _partials(a.device, a.shape[0] * a.shape[1] * b.shape[2]).view(
+            a.shape[0], a.shape[1], b.shape[2])
+        try:
+            return torch.bmm(a, b, out_dtype=torch.float32, out=out)
+        except (RuntimeError, TypeError):
+            pass
         try:
             return torch.bmm(a, b, out_dtype=torch.float32)
         except (RuntimeError, TypeError):
@@ -33,11 +54,28 @@ def _bmm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     return torch.bmm(a, b).float()
 
 
-def wgrad(x: torch.Tensor, g: torch.Tensor, rows_per_chunk: int = 1 << 18) -> torch.Tensor:
-    """``x^T @ g`` in fp32 for tall ``x [L, K]``, ``g [L, N]`` (row-contiguous)."""
+def _wgrad_rows_per_chunk(L: int, K: int, N: int, budget: int = 2 << 30) -> int:
+    """Chunk rows for the split-K batch: small chunks (many independent [K, N] products)
+    measured fastest on MI355X at L = 111M (K = N = 256: 2^14 rows 20.6 ms, 2^16 27.2 ms,
+    2^18 30.0 ms; benchmarks/bench_wgrad.py), bounded so the fp32 partials stay under
+    ``budget`` bytes."""
+    c = 1 << 14
+    while (L // c) * K * N * 4 > budget:
+        c *= 2
+    return c
+
+
+def wgrad(x: torch.Tensor, g: torch.Tensor, rows_per_chunk: int = 0) -> torch.Tensor:
+    """``x^T @ g`` in fp32 for tall ``x [L, K]``, ``g [L, N]`` (row-contiguous).
+    ``rows_per_chunk`` 0 = size-aware default. The wider operand goes first (the library
+    kernel it selects streams that operand once: K=128, N=256 19.3 ms -> ~14.6 ms)."""
     L = x.shape[0]
     if L == 0:
         return torch.zeros(x.shape[1], g.shape[1], dtype=torch.float32, device=x.device)
+    if x.is_cuda and x.shape[1] < g.shape[1]:
+        return wgrad(g, x, rows_per_chunk).t()
+    if rows_per_chunk <= 0:
+        rows_per_chunk = _wgrad_rows_per_chunk(L, x.shape[1], g.shape[1])
     nb = L // rows_per_chunk
     if not x.is_cuda or nb < 2 or not (x.is_contiguous() and g.is_contiguous()):
         return mm_f32(x.t(), g)
