@@ -124,7 +124,11 @@ class _LinearFn(torch.autograd.Function):
             dx = (g2 @ W.to(g2.dtype)).reshape(x.shape)
         if ctx.needs_input_grad[1]:
             if g2.is_cuda:
-                dW = wgrad(g2, x2.contiguous(), _auto_rows_per_chunk(g2.shape[0]))
+                # >= 8M rows (R-GCN relation linears): the 2^14-row split-K default
+                # (1/8 MAG240M step 378 -> 357 ms); fewer rows (GraphCast, 1-2M): >= 4096
+                # rows x <= 128 chunks (50.5 -> 46.4 ms)
+                L2 = g2.shape[0]
+                dW = wgrad(g2, x2.contiguous(), 0 if L2 >= 1 << 23 else _auto_rows_per_chunk(L2))
             else:
                 dW = g2.t().to(torch.float64 if g2.dtype == torch.float64 else torch.float32) @ \
                     x2.to(torch.float64 if g2.dtype == torch.float64 else torch.float32)
