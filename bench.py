@@ -7,17 +7,28 @@ partition of a synthetic graph with the papers100M shape: 111,059,956 nodes,
 1,615,685,872 directed edges symmetrised to ~3.23B messages per layer, 128 features,
 172 classes), RCCL all-to-all-v halo exchange overlapped with interior aggregation.
 
-A step = forward over ALL vertices (3 SAGE-mean layers, hidden 256, bf16 compute, fp32
-master weights) + masked cross-entropy on the train split + backward + gradient
-all-reduce + Adam step (the reference's epoch, experiments/OGB/main.py:129-158).
+A step is the reference's full-graph epoch (experiments/OGB/main.py:129-184):
+  forward of ALL 3 SAGE-mean layers over ALL vertices (hidden 256, bf16 compute with fp32
+  accumulation, fp32 master weights) -> masked cross-entropy on the train split, and
+  validation/test accuracy from the SAME forward -> backward -> gradient all-reduce ->
+  Adam step.
+The output layer's backward uses only the train rows' nonzero gradient (A[train, :]^T):
+exact (the dense backward multiplies zeros), counted as what it aggregates.
 
-    edges_per_s = num_layers * E_msg / epoch_s     (E_msg = symmetrised message edges)
+    value = edges_per_s = num_layers * E_msg / step_s      (BASELINE.md §2 definition)
+    edges_aggregated_per_step = nonzeros actually aggregated, forward + backward
 
+Secondary measurements in the same JSON line (unless --no-extra):
+  * "structureless": the same step on a --global-frac 1.0 graph (uniformly random
+    endpoints: no locality for any cache to exploit);
+  * "train_rows_only": the step with the output layer aggregated only at the train rows
+    (not a full-graph forward; labelled, never the headline).
 The whole graph is fixed as N grows (strong scaling). Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -44,18 +55,31 @@ def parse():
     ap.add_argument("--hidden", type=int, default=256)
     ap.add_argument("--layers", type=int, default=3)
     ap.add_argument("--lr", type=float, default=1e-3)
-    ap.add_argument("--global-frac", type=float, default=0.05)
+    ap.add_argument("--dtype", choices=("bf16", "fp32"), default="bf16",
+                    help="compute/storage dtype of features and activations (weights are "
+                         "fp32 masters either way)")
+    ap.add_argument("--global-frac", type=float, default=0.05,
+                    help="fraction of uniformly random (non-local) edges of the headline "
+                         "graph; the rest join ids within +-window")
     ap.add_argument("--window", type=int, default=1 << 14)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--restrict-last", action="store_true",
+                    help="headline = train-rows-only step (output layer aggregated at the "
+                         "train rows only); NOT a full-graph step, for A/B only")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the structureless-graph and train-rows-only measurements")
+    ap.add_argument("--extra-steps", type=int, default=3)
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--rehearse-world", type=int, default=0,
                     help="single process: run rank --rehearse-rank of a W-way partition with "
                          "a loopback halo exchange (per-rank compute + memory; no peers)")
     ap.add_argument("--rehearse-rank", type=int, default=0)
     ap.add_argument("--profile-ops", default="",
-                    help="after the timed steps, profile one extra step with "
-                         "torch.profiler and write the per-op device-time table here")
+                    help="after the timed steps, profile one extra step (every rank runs it) "
+                         "with torch.profiler; rank 0 writes the per-op device-time table")
+    ap.add_argument("--metrics-jsonl", default=os.environ.get("DGRAPH_METRICS_JSONL", ""),
+                    help="append one metrics record per measured phase (rank 0)")
     return ap.parse_args()
 
 
@@ -64,120 +88,251 @@ def log(rank, *a):
         print("[bench]", *a, file=sys.stderr, flush=True)
 
 
-def _profile_one_step(step, path):
-    """Per-aten-op device time of one (untimed) step, grouped by input shape."""
+def _profile_one_step(step, path, rank):
+    """Per-aten-op device time of one (untimed) step, grouped by input shape. Every rank
+    runs the step (its collectives must match); rank 0 writes the table."""
     from torch.profiler import ProfilerActivity, profile
 
     with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA],
                  record_shapes=True) as prof:
         step()
         torch.cuda.synchronize()
-    ka = prof.key_averages(group_by_input_shape=True)
-    with open(path, "w") as f:
-        f.write(ka.table(sort_by="self_cuda_time_total", row_limit=60, max_name_column_width=60,
-                         max_shapes_column_width=90))
+    if rank == 0:
+        ka = prof.key_averages(group_by_input_shape=True)
+        with open(path, "w") as f:
+            f.write(ka.table(sort_by="self_cuda_time_total", row_limit=60,
+                             max_name_column_width=60, max_shapes_column_width=90))
+
+
+class Job:
+    """One graph + data + model + optimizer on this rank (built collectively)."""
+
+    def __init__(self, args, comm, dev, global_frac: float, dtype):
+        from dgraph_amd.data.synthetic import (SHAPES, SPLIT_TEST, SPLIT_TRAIN, SPLIT_VALID,
+                                               build_partition, node_data)
+        from dgraph_amd.models.sage import GraphSAGE
+        from dgraph_amd.parallel.dist_graph import DistGraph
+        from dgraph_amd.parallel.grad_sync import GradSync
+
+        self.args, self.dev = args, dev
+        self.rank, self.world = comm.get_rank(), comm.get_world_size()
+        shape = SHAPES[args.shape]
+        if args.scale != 1.0:
+            shape = shape.scaled(args.scale)
+        self.shape = shape
+        self.global_frac = global_frac
+        t0 = time.time()
+        self.rehearse = args.rehearse_world > 1 and self.world == 1
+        p_rank, p_world = ((args.rehearse_rank, args.rehearse_world) if self.rehearse
+                           else (self.rank, self.world))
+        self.p_rank, self.p_world = p_rank, p_world
+        part = build_partition(shape, p_rank, p_world, dev, seed=args.seed,
+                               global_frac=global_frac, window=args.window,
+                               rehearse=self.rehearse)
+        csr = part["csr"]
+        if p_world == 1:
+            csr.num_cols = part["L"]
+        self.L, self.H = part["L"], part["H"]
+        self.graph = DistGraph(csr, part["L"], part["H"], part["send_local_idx"],
+                               part["send_splits"],
+                               # the synthetic graph is symmetrised, so the interior
+                               # (local x local) block is symmetric at every W: its
+                               # transpose is never materialised
+                               part["recv_splits"], comm.group, symmetric=True,
+                               overlap=not args.no_overlap)
+        del part, csr
+        self.graph.prepare_backward()
+        self.x, y, split = node_data(shape, p_rank,
+                                     _offsets(shape.num_nodes, p_world), dev, seed=args.seed,
+                                     dtype=dtype, return_split=True)
+        self.train_idx = torch.nonzero(split == SPLIT_TRAIN, as_tuple=True)[0]
+        self.y_train = y[self.train_idx]
+        ev = split == SPLIT_VALID
+        ev |= split == SPLIT_TEST
+        self.eval_idx = torch.nonzero(ev, as_tuple=True)[0]
+        self.y_eval = y[self.eval_idx]
+        self.eval_is_val = (split[self.eval_idx] == SPLIT_VALID)
+        del y, split, ev
+        cnt = torch.tensor([self.graph.nnz, self.train_idx.numel(), self.H,
+                            int(self.eval_is_val.sum()),
+                            self.eval_idx.numel()], dtype=torch.long, device=dev)
+        if self.world > 1:
+            dist.all_reduce(cnt)
+        self.E_msg, self.n_train, self.halo_total, self.n_val, n_eval = (
+            int(v) for v in cnt.tolist())
+        self.n_test = n_eval - self.n_val
+        self.build_s = time.time() - t0
+        torch.manual_seed(args.seed)
+        self.model = GraphSAGE(shape.num_features, args.hidden, shape.num_classes,
+                               args.layers).to(dev)
+        self.opt = torch.optim.Adam(self.model.parameters(), lr=args.lr,
+                                    fused=dev.type == "cuda")
+        self.sync = GradSync(self.model.parameters(), group=None) if self.world > 1 else None
+        self.inv_n = 1.0 / max(self.n_train, 1)
+        self.correct = torch.zeros(2, dtype=torch.long, device=dev)  # val, test
+
+    def step(self, restrict_last: bool = False):
+        import torch.nn.functional as Fn
+
+        g = self.graph
+        if restrict_last:
+            logits = self.model(self.x, g, out_rows=self.train_idx, restrict_last=True)
+        else:
+            logits, ev = self.model(self.x, g, out_rows=self.train_idx,
+                                    eval_rows=self.eval_idx)
+            # validation/test accuracy from the same forward (device counters, no sync)
+            hit = ev.argmax(1) == self.y_eval
+            self.correct[0] = (hit & self.eval_is_val).sum()
+            self.correct[1] = (hit & ~self.eval_is_val).sum()
+        loss = Fn.cross_entropy(logits.float(), self.y_train, reduction="sum") * self.inv_n
+        loss.backward()
+        if self.sync is not None:
+            self.sync.all_reduce()
+        self.opt.step()
+        self.opt.zero_grad(set_to_none=True)
+        return loss
+
+    def halo_stats(self):
+        from dgraph_amd.utils.diagnostics import halo_stats
+
+        if self.world == 1 and not self.rehearse:
+            return {}
+        fb = self.args.hidden * self.x.element_size()
+        st = halo_stats(self.graph, fb)
+        keep = ("max_pairwise_bytes", "max_rank_send_bytes", "xgmi_bound_ms")
+        return {k: st[k] for k in keep if k in st}
+
+    def free(self):
+        for k in ("graph", "x", "model", "opt", "sync", "train_idx", "y_train", "eval_idx",
+                  "y_eval", "eval_is_val"):
+            setattr(self, k, None)
+
+
+def _offsets(n, w):
+    from dgraph_amd.data.synthetic import contiguous_offsets
+
+    return contiguous_offsets(n, w)
+
+
+def barrier_sync(world, dev):
+    if world > 1:
+        dist.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+
+
+def timed(job: Job, steps: int, warmup: int, restrict_last: bool, verbose: bool = False):
+    """W untimed warmup steps, then K steps bracketed by barrier + synchronize; returns
+    (ms_per_step as the MAX over ranks, mean loss of the last step summed over ranks,
+     edges aggregated per step summed over ranks)."""
+    world, dev = job.world, job.dev
+    for i in range(warmup):
+        l = job.step(restrict_last)
+        if verbose:
+            log(job.rank, f"warmup {i} loss {float(l.detach()):.4f}")
+    barrier_sync(world, dev)
+    e0 = job.graph.edges_aggregated
+    t_start = time.perf_counter()
+    l = None
+    for _ in range(steps):
+        l = job.step(restrict_last)
+    barrier_sync(world, dev)
+    elapsed = time.perf_counter() - t_start
+    e1 = job.graph.edges_aggregated
+    red = torch.tensor([elapsed * 1000.0 / max(steps, 1)], dtype=torch.float64, device=dev)
+    tot = torch.tensor([float(l.detach()) if l is not None else 0.0,
+                        (e1 - e0) / max(steps, 1)], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(red, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tot)  # each rank holds its share of the global mean loss
+    return float(red.item()), float(tot[0].item()), float(tot[1].item())
 
 
 def main():
     args = parse()
     from dgraph_amd import Communicator
-    from dgraph_amd.data.synthetic import SHAPES, build_partition, node_data
-    from dgraph_amd.models.sage import GraphSAGE
-    from dgraph_amd.parallel.dist_graph import DistGraph
-    from dgraph_amd.parallel.grad_sync import GradSync
+    from dgraph_amd.utils.config import RunConfig
+    from dgraph_amd.utils.metrics import ExperimentLogger
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world != args.gpus:
-        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env != args.gpus:
+        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world_env}",
+              file=sys.stderr)
+    cfg = RunConfig.from_env()  # DGRAPH_<SECTION>_<FIELD> overrides (kernel knobs etc.)
+    cfg.model.hidden, cfg.model.num_layers, cfg.model.dtype = args.hidden, args.layers, args.dtype
+    cfg.data.dataset, cfg.data.global_frac = args.shape, args.global_frac
     comm = Communicator.init_process_group("nccl")
     rank, world = comm.get_rank(), comm.get_world_size()
     dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() \
         else torch.device("cpu")
-    shape = SHAPES[args.shape]
-    if args.scale != 1.0:
-        shape = shape.scaled(args.scale)
+    if dev.type == "cuda":
+        cfg.apply()
+    dtype = torch.bfloat16 if (args.dtype == "bf16" and dev.type == "cuda") else torch.float32
+    mlog = ExperimentLogger(os.path.dirname(args.metrics_jsonl) or ".", args.shape, world) \
+        if args.metrics_jsonl else None
 
-    t0 = time.time()
-    rehearse = args.rehearse_world > 1 and world == 1
-    p_rank, p_world = (args.rehearse_rank, args.rehearse_world) if rehearse else (rank, world)
-    part = build_partition(shape, p_rank, p_world, dev, seed=args.seed,
-                           global_frac=args.global_frac, window=args.window, rehearse=rehearse)
-    csr = part["csr"]
-    if p_world == 1:
-        csr.num_cols = part["L"]
-    graph = DistGraph(csr, part["L"], part["H"], part["send_local_idx"], part["send_splits"],
-                      # the synthetic graph is symmetrised, so the interior (local x local)
-                      # block is symmetric at every W: its transpose is never materialised
-                      part["recv_splits"], comm.group, symmetric=True,
-                      overlap=not args.no_overlap)
-    graph.prepare_backward()
-    dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
-    x, y, train = node_data(shape, p_rank, part["offsets"], dev, seed=args.seed, dtype=dtype)
-    train_idx = torch.nonzero(train, as_tuple=True)[0]
-    y_train = y[train_idx]
-    del y, train
-    e_local = torch.tensor([graph.interior.nnz + (graph.halo.nnz if graph.halo else 0),
-                            train_idx.numel(), part["H"]], dtype=torch.long, device=dev)
-    if world > 1:
-        dist.all_reduce(e_local)
-    E_msg, n_train, halo_total = (int(v) for v in e_local.tolist())
-    log(rank, f"graph built in {time.time() - t0:.1f}s: V={shape.num_nodes} E_msg={E_msg} "
-              f"halo_rows_total={halo_total} train={n_train}")
-
-    torch.manual_seed(args.seed)
-    model = GraphSAGE(shape.num_features, args.hidden, shape.num_classes, args.layers).to(dev)
-    opt = torch.optim.Adam(model.parameters(), lr=args.lr,
-                           fused=dev.type == "cuda")
-    sync = GradSync(model.parameters(), group=None) if world > 1 else None
-    inv_n = 1.0 / max(n_train, 1)
-
-    def step():
-        # all-vertex forward; logits of the train split leave the fused stack
-        logits = model(x, graph, out_rows=train_idx).float()
-        loss = torch.nn.functional.cross_entropy(logits, y_train, reduction="sum") * inv_n
-        loss.backward()
-        if sync is not None:
-            sync.all_reduce()
-        opt.step()
-        opt.zero_grad(set_to_none=True)
-        return loss
-
-    def barrier_sync():
-        if world > 1:
-            dist.barrier()
-        if dev.type == "cuda":
-            torch.cuda.synchronize()
-
-    for i in range(args.warmup):
-        l = step()
-        if args.verbose:
-            log(rank, f"warmup {i} loss {float(l.detach()):.4f}")
-    barrier_sync()
+    job = Job(args, comm, dev, args.global_frac, dtype)
+    log(rank, f"graph built in {job.build_s:.1f}s: V={job.shape.num_nodes} E_msg={job.E_msg} "
+              f"halo_rows_total={job.halo_total} train={job.n_train} val={job.n_val} "
+              f"test={job.n_test}")
+    head_restrict = args.restrict_last
     if dev.type == "cuda":
         torch.cuda.reset_peak_memory_stats()
-    t_start = time.perf_counter()
-    for _ in range(args.steps):
-        l = step()
-    barrier_sync()
-    elapsed = time.perf_counter() - t_start
-    if args.profile_ops and rank == 0:
-        _profile_one_step(step, args.profile_ops)
-    ms = torch.tensor([elapsed * 1000.0 / max(args.steps, 1)], dtype=torch.float64,
-                      device=dev)
-    if world > 1:
-        dist.all_reduce(ms, op=dist.ReduceOp.MAX)
-    ms_per_step = float(ms.item())
-    lt = l.detach().reshape(1).double()
-    if world > 1:
-        dist.all_reduce(lt)  # each rank holds its share of the global mean loss
-    final_loss = float(lt.item())
+    ms, final_loss, e_step = timed(job, args.steps, args.warmup, head_restrict, args.verbose)
     peak_gb = torch.cuda.max_memory_allocated() / 1e9 if dev.type == "cuda" else 0.0
-    edges_per_s = args.layers * E_msg / (ms_per_step / 1000.0)
-    if rehearse:
+    corr = job.correct.clone()
+    if world > 1:
+        dist.all_reduce(corr)
+    val_acc = float(corr[0]) / max(job.n_val, 1)
+    test_acc = float(corr[1]) / max(job.n_test, 1)
+    halo = job.halo_stats()
+    if args.profile_ops:
+        _profile_one_step(lambda: job.step(head_restrict), args.profile_ops, rank)
+    E_msg, n_train, halo_total = job.E_msg, job.n_train, job.halo_total
+    shape = job.shape
+    edges_per_s = args.layers * E_msg / (ms / 1000.0)
+    if mlog is not None:
+        mlog.metrics(phase="headline", epoch_ms=ms, edges_per_s=edges_per_s,
+                     edges_aggregated_per_step=e_step, loss=final_loss, val_acc=val_acc,
+                     test_acc=test_acc, peak_hbm_gb=peak_gb, **halo)
+
+    extra = {}
+    if not args.no_extra and not job.rehearse:
+        ks = max(args.extra_steps, 1)
+        if not head_restrict:
+            t_ms, _, t_e = timed(job, ks, 1, True)
+            extra["train_rows_only"] = {
+                "ms_per_step": t_ms, "edges_aggregated_per_step": t_e,
+                "note": "output layer aggregated at the train rows only (not a full-graph "
+                        "forward; no val/test predictions)"}
+        job.free()
+        del job
+        gc.collect()
+        if dev.type == "cuda":
+            torch.cuda.empty_cache()
+        sjob = Job(args, comm, dev, 1.0, dtype)
+        s_ms, s_loss, s_e = timed(sjob, ks, 1, head_restrict)
+        extra["structureless"] = {
+            "global_frac": 1.0, "ms_per_step": s_ms,
+            "edges_per_s": args.layers * sjob.E_msg / (s_ms / 1000.0),
+            "edges_aggregated_per_step": s_e, "E_msg": sjob.E_msg,
+            "halo_rows_total": sjob.halo_total, "steps": ks, "warmup": 1,
+            "final_loss": s_loss, **sjob.halo_stats()}
+        if mlog is not None:
+            mlog.metrics(phase="structureless", **extra["structureless"])
+        sjob.free()
+        del sjob
+    else:
+        job.free()
+
+    if args.rehearse_world > 1 and world == 1:
         # not a whole-job number: one rank's compute with a loopback exchange
-        print(json.dumps({"rehearsal": True, "rank": p_rank, "world": p_world,
-                          "ms_per_step_compute_loopback": ms_per_step, "L": part["L"],
-                          "H": part["H"], "E_local": E_msg, "peak_mem_gb": round(peak_gb, 2),
+        print(json.dumps({"rehearsal": True, "rank": args.rehearse_rank,
+                          "world": args.rehearse_world,
+                          "ms_per_step_compute_loopback": ms, "E_local": E_msg,
+                          "halo_rows": halo_total, "peak_mem_gb": round(peak_gb, 2),
+                          "dtype": args.dtype, "global_frac": args.global_frac,
+                          "restrict_last": head_restrict,
                           "final_loss_local": final_loss}), flush=True)
     elif rank == 0:
         rec = {
@@ -187,16 +342,16 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": ms_per_step,
-            "epoch_ms": ms_per_step,
+            "ms_per_step": ms,
+            "epoch_ms": ms,
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "bf16" if dtype == torch.bfloat16 else "fp32",
+            "dtype": args.dtype if dev.type == "cuda" else "fp32",
             "data": (f"synthetic {shape.name}-shaped graph (V={shape.num_nodes}, "
                      f"directed={shape.num_directed_edges}, symmetrised E_msg={E_msg}, "
                      f"global_frac={args.global_frac}, window={args.window}), random "
-                     f"features/labels, random-init weights"),
+                     f"features/labels/splits, random-init weights"),
             "config": {
                 "model": f"GraphSAGE-mean {args.layers}-layer hidden {args.hidden}",
                 "global_batch": shape.num_nodes,
@@ -208,9 +363,20 @@ def main():
                 "E_msg": E_msg,
                 "halo_rows_total": halo_total,
                 "train_nodes": n_train,
+                "step": ("train-rows-only output layer" if head_restrict else
+                         "full-graph forward (all vertices, all layers) + val/test accuracy "
+                         "from the same forward + backward + allreduce + Adam"),
+                "precision": ("bf16 storage/compute, fp32 accumulate, fp32 master weights"
+                              if dtype == torch.bfloat16 else "fp32"),
             },
+            "edges_aggregated_per_step": e_step,
+            "edges_aggregated_per_s": e_step / (ms / 1000.0),
             "final_loss": final_loss,
+            "val_acc": val_acc,
+            "test_acc": test_acc,
             "peak_mem_gb_rank0": round(peak_gb, 2),
+            **({"halo": halo} if halo else {}),
+            **extra,
         }
         print(json.dumps(rec), flush=True)
     comm.destroy()

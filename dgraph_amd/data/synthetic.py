@@ -38,20 +38,26 @@ class GraphShape:
     num_features: int
     num_classes: int
     train_frac: float
+    val_frac: float = 0.0
+    test_frac: float = 0.0
 
     def scaled(self, factor: float) -> "GraphShape":
         return GraphShape(f"{self.name}@{factor:g}", max(int(self.num_nodes * factor), 16),
                           max(int(self.num_directed_edges * factor), 16), self.num_features,
-                          self.num_classes, self.train_frac)
+                          self.num_classes, self.train_frac, self.val_frac, self.test_frac)
 
 
 SHAPES = {
-    # OGB public specs (SURVEY.md App. D "External dataset sizes")
-    "ogbn-arxiv": GraphShape("ogbn-arxiv", 169_343, 1_166_243, 128, 40, 0.537),
-    "ogbn-products": GraphShape("ogbn-products", 2_449_029, 61_859_140, 100, 47, 0.08),
+    # OGB public specs (SURVEY.md App. D "External dataset sizes"); split fractions are the
+    # official split sizes / num_nodes (arxiv 90,941/29,799/48,603; products
+    # 196,615/39,323/2,213,091; papers100M 1,207,179/125,265/214,338)
+    "ogbn-arxiv": GraphShape("ogbn-arxiv", 169_343, 1_166_243, 128, 40, 0.537, 0.176, 0.287),
+    "ogbn-products": GraphShape("ogbn-products", 2_449_029, 61_859_140, 100, 47, 0.08,
+                                0.0161, 0.9037),
     "ogbn-papers100M": GraphShape("ogbn-papers100M", 111_059_956, 1_615_685_872, 128, 172,
-                                  0.0109),
-    "ogbn-proteins": GraphShape("ogbn-proteins", 132_534, 39_561_252, 8, 112, 0.65),
+                                  0.0109, 0.00113, 0.00193),
+    "ogbn-proteins": GraphShape("ogbn-proteins", 132_534, 39_561_252, 8, 112, 0.65, 0.16,
+                                0.19),
 }
 
 
@@ -243,15 +249,24 @@ def build_partition(shape: GraphShape, rank: int, world_size: int, device, seed:
                 recv_splits=recv_splits, offsets=offsets)
 
 
+SPLIT_TRAIN, SPLIT_VALID, SPLIT_TEST, SPLIT_NONE = 0, 1, 2, 3
+
+
 def node_data(shape: GraphShape, rank: int, offsets: List[int], device, seed: int = 0,
-              dtype=torch.bfloat16):
+              dtype=torch.bfloat16, return_split: bool = False):
     """Random features [L, F] (dtype), labels [L] and a train mask for owned vertices,
-    seeded per global vertex block so results do not depend on the world size."""
+    seeded per global vertex block so results do not depend on the world size.
+
+    ``return_split=True`` returns an int8 split code per vertex instead of the train mask
+    (SPLIT_TRAIN / SPLIT_VALID / SPLIT_TEST / SPLIT_NONE at the shape's split fractions;
+    the train set is the same as the mask's)."""
     lo, hi = offsets[rank], offsets[rank + 1]
     L = hi - lo
     x = torch.empty(L, shape.num_features, device=device, dtype=dtype)
     y = torch.empty(L, dtype=torch.int64, device=device)
-    train = torch.empty(L, dtype=torch.bool, device=device)
+    train = torch.empty(L, dtype=torch.int8 if return_split else torch.bool, device=device)
+    tf, vf = shape.train_frac, shape.train_frac + shape.val_frac
+    sf = vf + shape.test_frac
     C = 1 << 20  # global vertex chunks: values depend on the vertex id, not on W
     g = torch.Generator(device=device)
     for c in range(lo // C, (hi + C - 1) // C):
@@ -259,7 +274,14 @@ def node_data(shape: GraphShape, rank: int, offsets: List[int], device, seed: in
         g.manual_seed(_mix(seed, 0x6E6F646573, c))
         xc = torch.randn(b - a, shape.num_features, generator=g, device=device)
         yc = torch.randint(0, shape.num_classes, (b - a,), generator=g, device=device)
-        tc = torch.rand(b - a, generator=g, device=device) < shape.train_frac
+        u = torch.rand(b - a, generator=g, device=device)
+        if return_split:
+            tc = torch.full_like(u, SPLIT_NONE, dtype=torch.int8)
+            tc[u < sf] = SPLIT_TEST
+            tc[u < vf] = SPLIT_VALID
+            tc[u < tf] = SPLIT_TRAIN
+        else:
+            tc = u < tf
         s, e = max(a, lo), min(b, hi)
         x[s - lo:e - lo] = xc[s - a:e - a].to(dtype)
         y[s - lo:e - lo] = yc[s - a:e - a]

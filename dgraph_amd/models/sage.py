@@ -256,10 +256,22 @@ class SAGEStackFn(Function):
     """
 
     @staticmethod
-    def forward(ctx, x0, graph: DistGraph, specs, out_rows, ws_obj, *params):
+    def forward(ctx, x0, graph: DistGraph, specs, out_rows, ws_obj, restrict_last,
+                eval_rows, *params):
+        """Returns ``(logits[out_rows] or all logits, logits[eval_rows])``; the second output
+        is not differentiable (validation/test predictions from the SAME forward, as the
+        reference's epoch does, experiments/OGB/main.py:140-184).
+
+        ``restrict_last``: with ``out_rows`` and a project-first output layer, aggregate
+        only the loss rows in that layer (A[rows, :] z) instead of all vertices. Exact for
+        the returned rows, but the other vertices get no logits, so it is incompatible with
+        ``eval_rows`` and is NOT a full-graph forward (bench.py reports it separately)."""
         # workspace slots are used on the training path (row-subset output); a full
         # output must own its storage, so that path allocates
         use_ws = ws_obj is not None and out_rows is not None
+        if restrict_last and eval_rows is not None:
+            raise ValueError("restrict_last computes only the loss rows; eval_rows need the "
+                             "full output layer")
         n = len(specs)
         L = x0.shape[0]
         dt = x0.dtype
@@ -293,7 +305,7 @@ class SAGEStackFn(Function):
             if fused and relu:
                 mask = torch.empty(tile32_mask_words(L, Fo), dtype=torch.int64,
                                    device=h.device)
-            if last and pf and not relu and out_rows is not None:
+            if last and pf and not relu and out_rows is not None and restrict_last:
                 # only the loss rows leave the node: y[rows] = A[rows, :] (h Wn) +
                 # h[rows] Ws + b — the row-restricted SpMM reads ~|rows|/L of the edges
                 # and receives only the halo rows those rows touch
@@ -351,16 +363,21 @@ class SAGEStackFn(Function):
         ctx.save_for_backward(*params)
         ctx.out_rows = out_rows
         C = dims[-1]
+        if eval_rows is not None:
+            ev = h.index_select(0, eval_rows)[:, :C].contiguous()
+        else:
+            ev = h.new_zeros(0, C)
+        ctx.mark_non_differentiable(ev)
         if out_rows is not None:
             # only the requested rows leave the node, so autograd never holds a dense
             # [V, C] output gradient (a project-first last layer computed just those rows)
-            if h.shape[0] == out_rows.numel() and specs[-1][1] and not specs[-1][0]:
-                return h[:, :C].contiguous() if C != h.shape[1] else h
-            return h.index_select(0, out_rows)[:, :C].contiguous()
-        return h[:, :C] if C != h.shape[1] else h
+            if restrict_last and specs[-1][1] and not specs[-1][0]:
+                return (h[:, :C].contiguous() if C != h.shape[1] else h), ev
+            return h.index_select(0, out_rows)[:, :C].contiguous(), ev
+        return (h[:, :C] if C != h.shape[1] else h), ev
 
     @staticmethod
-    def backward(ctx, gy):
+    def backward(ctx, gy, _g_eval=None):
         params = ctx.saved_tensors
         graph: DistGraph = ctx.graph
         acts, masks, specs, dims_true = ctx.acts, ctx.masks, ctx.specs, ctx.dims
@@ -518,7 +535,7 @@ class SAGEStackFn(Function):
             g = dx
             if i == 0:
                 dx0 = dx
-        return (dx0, None, None, None, None, *grads)
+        return (dx0, None, None, None, None, None, None, *grads)
 
 
 class GraphSAGE(nn.Module):
@@ -540,21 +557,34 @@ class GraphSAGE(nn.Module):
         self._workspace = SageWorkspace()
 
     def forward(self, x: torch.Tensor, graph: DistGraph,
-                out_rows: Optional[torch.Tensor] = None) -> torch.Tensor:
+                out_rows: Optional[torch.Tensor] = None,
+                eval_rows: Optional[torch.Tensor] = None,
+                restrict_last: bool = False):
         """Logits for all local vertices, or only for ``out_rows`` (e.g. the train split:
-        the full last layer is still computed, but no dense [V, C] gradient is held)."""
+        the full last layer is still computed, but no dense [V, C] gradient is held).
+
+        With ``eval_rows`` the call returns ``(logits, eval_logits)``: the logits of the
+        validation/test vertices from the same full-graph forward (no gradient).
+        ``restrict_last=True`` aggregates only ``out_rows`` in a project-first output layer
+        (train-rows-only step; not a full-graph forward, see :class:`SAGEStackFn`)."""
         if self.dropout == 0 or not self.training:
             specs = tuple((l.relu, l.project_first()) for l in self.layers)
             params = []
             for l in self.layers:
                 params += [l.w_self, l.w_neigh, l.bias]
             ws = self._workspace if (self.training and torch.is_grad_enabled()) else None
-            return SAGEStackFn.apply(x, graph, specs, out_rows, ws, *params)
+            out, ev = SAGEStackFn.apply(x, graph, specs, out_rows, ws,
+                                        bool(restrict_last and out_rows is not None),
+                                        eval_rows, *params)
+            return out if eval_rows is None else (out, ev)
         for i, layer in enumerate(self.layers):
             x = layer(x, graph)
             if self.dropout > 0 and self.training and i < len(self.layers) - 1:
                 x = Fn.dropout(x, self.dropout, training=True)
-        return x if out_rows is None else x.index_select(0, out_rows)
+        out = x if out_rows is None else x.index_select(0, out_rows)
+        if eval_rows is None:
+            return out
+        return out, x.index_select(0, eval_rows).detach()
 
     def num_message_edges(self, graph: DistGraph) -> int:
         """Directed message edges aggregated per layer on this rank (``E_msg``)."""

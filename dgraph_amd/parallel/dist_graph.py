@@ -50,6 +50,9 @@ class DistGraph:
         self._restrict_cache = {}
         self._restrict_fwd_cache = {}
         self._static_cache = {}
+        # edges (nonzeros) aggregated by every call so far, forward and transposed:
+        # bench.py reports the per-step delta as ``edges_aggregated_per_step``
+        self.edges_aggregated = 0
         if self.H > 0 or (send_local_idx is not None and send_local_idx.numel() > 0):
             self.interior, self.halo = csr.split_columns(self.L)
             self.interior.symmetric = symmetric
@@ -73,6 +76,11 @@ class DistGraph:
     @property
     def device(self):
         return self.interior.device
+
+    @property
+    def nnz(self) -> int:
+        """Message edges aggregated at this rank's vertices (interior + halo)."""
+        return self.interior.nnz + (self.halo.nnz if self.halo is not None else 0)
 
     @staticmethod
     def from_pattern(cp, num_nbr_rows: Optional[int] = None, group=None,
@@ -107,6 +115,7 @@ class DistGraph:
         """Mean (or sum) over in-neighbours, local and halo. ``static=True`` marks ``x``
         as a read-only input whose halo rows may be exchanged once and reused."""
         rs = self.inv_deg if mean else None
+        self.edges_aggregated += self.nnz
         if self.halo is None:
             return K.spmm(self.interior.rowptr, self.interior.col, x, out, row_scale=rs)
         if static:
@@ -153,6 +162,7 @@ class DistGraph:
         """Transposed aggregation (the backward of :meth:`aggregate`). ``scratch``: an
         optional free buffer (any shape, same dtype as ``g``) for the pre-scaled path."""
         cs = self.inv_deg if mean else None
+        self.edges_aggregated += self.nnz
         g = g.contiguous()
         it = self.interior if self.interior.symmetric else self.interior.transpose()
         if self.halo is None:
@@ -232,6 +242,7 @@ class DistGraph:
         it, cs_rows, sub = self._restricted(rows)
         cs = cs_rows if mean else None
         g_rows = g_rows.contiguous()
+        self.edges_aggregated += it.nnz + (sub[0].nnz if sub is not None else 0)
         if sub is None:
             return K.spmm(it.rowptr, it.col, g_rows, out, col_scale=cs)
         ht_nz, a2a_sub, st = sub[:3]
@@ -277,6 +288,7 @@ class DistGraph:
         is collective (sub-plan exchange, shared with :meth:`aggregate_T_rows`)."""
         ir, rs, hsub = self._restricted_fwd(rows)
         rsc = rs if mean else None
+        self.edges_aggregated += ir.nnz + (hsub[0].nnz if hsub is not None else 0)
         if hsub is None:
             return K.spmm(ir.rowptr, ir.col, x, out, row_scale=rsc)
         hr, a2a_f, recv_local = hsub

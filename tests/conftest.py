@@ -42,6 +42,8 @@ def _worker(rank, world_size, port, fn, args, q):
     try:
         import torch.distributed as dist
 
+        # W ranks share the container's CPUs: one intra-op pool each, sized to fit
+        torch.set_num_threads(max(1, (os.cpu_count() or 8) // max(world_size, 1)))
         dist.init_process_group("gloo", rank=rank, world_size=world_size)
         torch.manual_seed(0)
         fn(rank, world_size, *args)

@@ -174,7 +174,7 @@ def _random_pattern_exchange(rank, world, symmetric):
     assert torch.equal(lv[le[:, 0]], mine[:, 0])
 
 
-@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 @pytest.mark.parametrize("symmetric", [True, False])
 def test_pattern_any_partition_any_graph(ranks, world, symmetric):
     """Request-based builder is correct for round-robin/random placements and for

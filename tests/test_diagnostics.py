@@ -84,7 +84,7 @@ def _straggler_and_stats(rank, world):
     dist.barrier()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_straggler_exchange_and_halo_stats(ranks, world):
     ranks(_straggler_and_stats, world)
 

@@ -119,6 +119,6 @@ def _gcn_dist(rank, world):
         comm.destroy()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_comm_aware_gcn_distributed(ranks, world):
     ranks(_gcn_dist, world)

@@ -137,10 +137,10 @@ def _gc_dist(rank, world, out_dir):
 
 def test_graphcast_distributed_equivalence(ranks, tmp_path):
     d = str(tmp_path)
-    for w in (1, 2, 3):
+    for w in (1, 2, 3, 8):
         ranks(_gc_dist, w, d)
     r1 = torch.load(f"{d}/gc_w1.pt", weights_only=True)
-    for w in (2, 3):
+    for w in (2, 3, 8):
         rw = torch.load(f"{d}/gc_w{w}.pt", weights_only=True)
         torch.testing.assert_close(rw["out"], r1["out"])
         torch.testing.assert_close(rw["loss"], r1["loss"])

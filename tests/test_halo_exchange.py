@@ -74,7 +74,7 @@ def _pattern_offline(E, part, r, world):
     return key % V
 
 
-@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_halo_exchange_nccl(ranks, world):
     ranks(_halo, world, "nccl")
 

@@ -57,7 +57,7 @@ def _plan_fields(rank, world):
     assert mu["total"] > 0 and mu["unit"] == "KB"
 
 
-@pytest.mark.parametrize("world", [1, 2, 4])
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
 def test_plan_fields(ranks, world):
     if world == 1:
         _plan_fields(0, 1)
@@ -112,7 +112,7 @@ def _gather_scatter(rank, world, dtype):
         comm.destroy()
 
 
-@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_gather_scatter_fwd_bwd(ranks, world):
     ranks(_gather_scatter, world, torch.float32)
 

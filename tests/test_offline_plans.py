@@ -28,7 +28,7 @@ def _compare(rank, world, tmpdir):
         save_patterns(build_all_patterns_offline(E, part, world), tmpdir, "g")
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_offline_patterns_match_collective(ranks, world, tmp_path):
     ranks(_compare, world, str(tmp_path))
     E, part = _graph()

@@ -62,7 +62,7 @@ def _bn_dist(rank, world):
     torch.testing.assert_close(bn.running_var[0], ref.running_var)
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_sync_bn_distributed(ranks, world):
     ranks(_bn_dist, world)
 
@@ -170,8 +170,9 @@ def test_rgat_distributed_equivalence(ranks, tmp_path):
     ranks(_rgat_dist, 1, d)
     ranks(_rgat_dist, 2, d)
     ranks(_rgat_dist, 3, d)
+    ranks(_rgat_dist, 8, d)
     r1 = torch.load(f"{d}/rgat_w1.pt", weights_only=True)
-    for w in (2, 3):
+    for w in (2, 3, 8):
         rw = torch.load(f"{d}/rgat_w{w}.pt", weights_only=True)
         torch.testing.assert_close(rw["out"], r1["out"])
         torch.testing.assert_close(rw["loss"], r1["loss"])

@@ -28,7 +28,7 @@ def test_layer_plan_prunes_to_target():
     assert need3[0] == {0, 1, 2} and sorted(rels3[0]) == [0, 1, 2, 3, 4]
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_generator_partitions_the_w1_graph(world):
     full, offs1 = build_relation_csrs(SHAPE, 0, 1, "cpu", global_frac=0.2, window=64)
     for rid, (s, d) in enumerate(EDGE_TYPES):
@@ -121,7 +121,7 @@ def _train(rank, world, steps, out):
         torch.save(torch.tensor(losses), out)
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_distributed_training_matches_single_rank(ranks, tmp_path, world):
     _train(0, 1, 3, tmp_path / "w1.pt")
     ranks(_train, world, 3, str(tmp_path / "wn.pt"))

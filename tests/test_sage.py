@@ -109,7 +109,7 @@ def _train_losses(rank, world, steps, out, hidden=32):
         torch.save(torch.tensor(losses), out)
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 @pytest.mark.parametrize("hidden", [32, 64])
 def test_distributed_training_matches_single_rank(ranks, tmp_path, world, hidden):
     """Halo-overlapped DistGraph training on W ranks follows the same loss curve as W=1.
