@@ -27,6 +27,23 @@ from ..ops import kernels as K
 from ..ops.csr import CSR, IndexMap
 
 
+def _cache_lookup(cache: dict, rows: torch.Tensor):
+    """Plan-cache hit for the row-index tensor ``rows``: the SAME live tensor object (a
+    weak reference, never the address, which a freed tensor's successor can reuse) at the
+    same version counter (an in-place edit of ``rows`` misses). Building a sub-plan on a
+    miss is collective, so the key must not depend on allocator state that can differ
+    between ranks."""
+    ref = cache.get("ref")
+    if ref is not None and ref() is rows and cache.get("version") == rows._version:
+        return cache["plan"]
+    return None
+
+
+def _cache_store(cache: dict, rows: torch.Tensor, plan) -> None:
+    cache.clear()
+    cache.update(ref=weakref.ref(rows), version=rows._version, plan=plan)
+
+
 class DistGraph:
     def __init__(
         self,
@@ -195,8 +212,7 @@ class DistGraph:
         neighbour a loss row (A[rows, halo]^T restricted to its nonzero rows) with a
         matching sub-plan of the reverse exchange, so the owners receive just those rows
         instead of all H (built once, collectively: two small all-to-alls)."""
-        key = (rows.data_ptr(), rows.numel(), str(rows.device))
-        hit = self._restrict_cache.get(key)
+        hit = _cache_lookup(self._restrict_cache, rows)
         if hit is not None:
             return hit
         it = self.interior.select_rows(rows).transpose()
@@ -229,7 +245,7 @@ class DistGraph:
             sub = (ht_nz, AllToAllV(cnt_l, peer_l, self.a2a.group),
                    IndexMap(recv_local, self.L).transpose_csr(), nz, recv_local)
         hit = (it, cs, sub)
-        self._restrict_cache = {key: hit}  # one loss-row set at a time
+        _cache_store(self._restrict_cache, rows, hit)  # one loss-row set at a time
         return hit
 
     def aggregate_T_rows(self, g_rows: torch.Tensor, rows: torch.Tensor, mean: bool = True,
@@ -260,8 +276,7 @@ class DistGraph:
         the halo columns renumbered onto the contributing halo rows only, plus the
         forward sub-plan (owners send just those rows: the reverse of the backward
         sub-plan)."""
-        key = (rows.data_ptr(), rows.numel(), str(rows.device))
-        hit = self._restrict_fwd_cache.get(key)
+        hit = _cache_lookup(self._restrict_fwd_cache, rows)
         if hit is not None:
             return hit
         ir = self.interior.select_rows(rows)
@@ -277,7 +292,7 @@ class DistGraph:
                      max(int(nz.numel()), 1))
             hsub = (hr, a2a_sub.reversed(), recv_local.to(self.send_map.idx.dtype))
         hit = (ir, rs, hsub)
-        self._restrict_fwd_cache = {key: hit}
+        _cache_store(self._restrict_fwd_cache, rows, hit)
         return hit
 
     def aggregate_rows(self, x: torch.Tensor, rows: torch.Tensor, mean: bool = True,

@@ -166,3 +166,33 @@ def _static_halo(rank, world):
 
 def test_static_feature_halo_cached(ranks):
     ranks(_static_halo, 2)
+
+
+@pytest.mark.parametrize("classes", [40, 172])
+def test_eval_rows_and_restricted_last_layer(classes):
+    """The full-graph step returns validation/test logits from the same forward
+    (``eval_rows``), and the train-rows-only variant (``restrict_last``) produces the same
+    loss-row logits and gradients as the full output layer."""
+    p, g, A = _graph()
+    x, _, tr = node_data(SHAPE, 0, p["offsets"], "cpu", dtype=torch.float32)
+    rows = torch.nonzero(tr).squeeze(1)
+    ev_rows = torch.nonzero(~tr).squeeze(1)[::3]
+    res = {}
+    for restrict in (False, True):
+        torch.manual_seed(0)
+        m = GraphSAGE(SHAPE.num_features, 64, classes, 3)
+        if restrict:
+            out = m(x, g, out_rows=rows, restrict_last=True)
+            ev = None
+        else:
+            out, ev = m(x, g, out_rows=rows, eval_rows=ev_rows)
+            assert not ev.requires_grad
+        out.square().mean().backward()
+        res[restrict] = (out.detach(), ev, [q.grad.clone() for q in m.parameters()], m)
+    full = _dense_forward(res[False][3], x, A).detach()
+    torch.testing.assert_close(res[False][1], full[ev_rows], atol=1e-5, rtol=1e-4)
+    torch.testing.assert_close(res[True][0], res[False][0], atol=1e-5, rtol=1e-4)
+    for a, b in zip(res[True][2], res[False][2]):
+        torch.testing.assert_close(a, b, atol=1e-6, rtol=1e-4)
+    with pytest.raises(ValueError):
+        res[True][3](x, g, out_rows=rows, eval_rows=ev_rows, restrict_last=True)
