@@ -540,7 +540,14 @@ void set_spmm_config_op(int64_t variant, int64_t xcd, int64_t pass_cols) {
                           static_cast<int>(pass_cols));
 }
 
+void set_dual_gemm_variant_op(int64_t variant) {
+  dgraph::set_dual_gemm_variant(static_cast<int>(variant));
+}
+int64_t get_dual_gemm_variant_op() { return dgraph::get_dual_gemm_variant(); }
+
 TORCH_LIBRARY(dgraph_amd, m) {
+  m.def("set_dual_gemm_variant(int variant) -> ()", &set_dual_gemm_variant_op);
+  m.def("get_dual_gemm_variant() -> int", &get_dual_gemm_variant_op);
   m.def("set_spmm_config(int variant, int xcd, int pass_cols=-1) -> ()", &set_spmm_config_op);
   m.def("bias_relu_pack(Tensor(a!) y, Tensor? bias, Tensor(b!)? bits, bool relu) -> ()");
   m.def("relu_mask_bwd(Tensor(a!) g, Tensor bits) -> ()");

@@ -305,7 +305,14 @@ hipError_t by_nc1(int nc1, int nc2, const void* A1, int64_t lda1, const void* B1
   }
 }
 
+int g_dual_gemm_variant = 2;
+
 }  // namespace
+
+void set_dual_gemm_variant(int variant) {
+  g_dual_gemm_variant = (variant == 1 || variant == 2) ? variant : 2;
+}
+int get_dual_gemm_variant() { return g_dual_gemm_variant; }
 
 bool dual_gemm_supported(int64_t N, int64_t K1, int64_t K2) {
   auto okk = [](int64_t k) { return k == 128 || k == 192 || k == 256; };
@@ -318,6 +325,9 @@ hipError_t dual_gemm(const void* A1, int64_t lda1, const void* B1t, int64_t K1, 
                      uint64_t* mask_out, const uint64_t* mask_in, bool relu, hipStream_t st) {
   if (M <= 0) return hipSuccess;
   if (!dual_gemm_supported(N, K1, K2)) return hipErrorInvalidValue;
+  if (g_dual_gemm_variant == 2 && dual_gemm_bs_supported(N, K1, K2))
+    return dual_gemm_bs(A1, lda1, B1t, K1, A2, lda2, B2t, K2, bias, cin, ldc, out, ldo, M, N,
+                        mask_out, mask_in, relu, st);
   const int nc1 = static_cast<int>(K1 / kBK), nc2 = static_cast<int>(K2 / kBK);
   switch (N) {
     case 128: return by_nc1<4>(nc1, nc2, A1, lda1, B1t, A2, lda2, B2t, bias, cin, ldc, out, ldo, mask_out, mask_in, M, relu, st);

@@ -136,5 +136,16 @@ hipError_t dual_gemm(const void* A1, int64_t lda1, const void* B1t, int64_t K1, 
                      int64_t lda2, const void* B2t, int64_t K2, const float* bias,
                      const void* cin, int64_t ldc, void* out, int64_t ldo, int64_t M, int64_t N,
                      uint64_t* mask_out, const uint64_t* mask_in, bool relu, hipStream_t st);
+// B-stationary variant (dual_gemm_bs.hip): same contract; A read from HBM once.
+// Supports K1 + K2 in {192, 256, 512}; other shapes run the column-half kernel.
+bool dual_gemm_bs_supported(int64_t N, int64_t K1, int64_t K2);
+hipError_t dual_gemm_bs(const void* A1, int64_t lda1, const void* B1t, int64_t K1,
+                        const void* A2, int64_t lda2, const void* B2t, int64_t K2,
+                        const float* bias, const void* cin, int64_t ldc, void* out, int64_t ldo,
+                        int64_t M, int64_t N, uint64_t* mask_out, const uint64_t* mask_in,
+                        bool relu, hipStream_t st);
+// 1 = column-half kernel (dual_gemm.hip), 2 = B-stationary (default); < 0 restores it
+void set_dual_gemm_variant(int variant);
+int get_dual_gemm_variant();
 
 }  // namespace dgraph

@@ -460,8 +460,24 @@ def test_linear_split_k_grads(rows):
 @pytest.mark.parametrize("M", [1, 300, 256 * 3, 70001])
 @pytest.mark.parametrize("N,K1,K2", [(256, 128, 128), (256, 256, 256), (256, 192, 192),
                                       (192, 256, 0), (128, 192, 256)])
-@pytest.mark.parametrize("mode", ["relu", "plain", "cin_maskin"])
-def test_dual_gemm(M, N, K1, K2, mode):
+@pytest.mark.parametrize("mode", ["relu", "plain", "cin_maskin", "cin_inplace"])
+@pytest.mark.parametrize("variant", [1, 2])
+def test_dual_gemm(M, N, K1, K2, mode, variant):
+    """Both dual-GEMM kernels (1: column-half, B^T in LDS; 2: B-stationary in VGPRs, A
+    streamed once through LDS) against an fp32 reference of the same op."""
+    from dgraph_amd.ops.dense import dual_gemm, tile32_mask_words
+
+    from dgraph_amd import _native
+
+    ops = _native.ops()
+    ops.set_dual_gemm_variant(variant)
+    try:
+        _dual_gemm_case(M, N, K1, K2, mode)
+    finally:
+        ops.set_dual_gemm_variant(2)
+
+
+def _dual_gemm_case(M, N, K1, K2, mode):
     from dgraph_amd.ops.dense import dual_gemm, tile32_mask_words
 
     g = torch.Generator().manual_seed(M + N + K1)
@@ -490,6 +506,13 @@ def test_dual_gemm(M, N, K1, K2, mode):
     elif mode == "plain":
         out = dual_gemm(d(A1), d(B1.t().contiguous()), **kw)
         torch.testing.assert_close(out.float().cpu(), ref, atol=3e-2, rtol=2e-2)
+    elif mode == "cin_inplace":
+        # the SAGE project-first output layer: out = A1 B1 + bias + out (cin aliases out)
+        cin = torch.randn(M, N, generator=g).to(torch.bfloat16)
+        buf = d(cin).clone()
+        out = dual_gemm(d(A1), d(B1.t().contiguous()), cin=buf, out=buf, **kw)
+        assert out.data_ptr() == buf.data_ptr()
+        torch.testing.assert_close(out.float().cpu(), ref + cin.float(), atol=3e-2, rtol=2e-2)
     else:
         cin = torch.randn(M, N, generator=g).to(torch.bfloat16)
         keep = torch.rand(M, N, generator=g) > 0.4
