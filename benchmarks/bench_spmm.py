@@ -25,8 +25,13 @@ def main():
     ap.add_argument("--global-frac", type=float, default=0.05)
     ap.add_argument("--window", type=int, default=1 << 14)
     ap.add_argument("--variants", default="2:2:128,4:0:128,4:2:64",
-                    help="comma list of variant:row_map:pass_cols")
+                    help="comma list of variant:row_map:pass_cols[:hub_cap] (hub_cap > 0: "
+                         "hub-row split at that degree)")
     ap.add_argument("--slices", default="1")
+    ap.add_argument("--powerlaw", type=float, default=0.0,
+                    help="> 0: instead of the shaped generator, a power-law in-degree graph: "
+                         "row = floor(V u^a) for u ~ U(0,1) (a = 6: the top row holds ~5%% "
+                         "of all entries), uniform columns, E_msg entries")
     ap.add_argument("--mean", default="row", choices=["row", "col"],
                     help="mean as a row scale (forward) or a column scale (transposed)")
     a = ap.parse_args()
@@ -37,8 +42,27 @@ def main():
     ops = _native.ops()
     dev = torch.device("cuda", 0)
     shape = SHAPES[a.shape] if a.scale == 1.0 else SHAPES[a.shape].scaled(a.scale)
-    p = build_partition(shape, 0, 1, dev, global_frac=a.global_frac, window=a.window)
+    if a.powerlaw > 0:
+        from dgraph_amd.ops.csr import CSR
+
+        V, E = shape.num_nodes, 2 * shape.num_directed_edges
+        gen = torch.Generator(device=dev).manual_seed(0)
+        rows = (torch.rand(E, generator=gen, device=dev) ** a.powerlaw * V).long()
+        rows.clamp_(max=V - 1)
+        rows, _ = torch.sort(rows)
+        cols = torch.randint(0, V, (E,), generator=gen, device=dev, dtype=torch.int32)
+        csr = CSR.from_coo(rows, cols, V, V, keep_perm=False)
+        del rows, cols
+        p = {"csr": csr, "L": V}
+    else:
+        p = build_partition(shape, 0, 1, dev, global_frac=a.global_frac, window=a.window)
     csr = p["csr"]
+    deg = csr.degree()
+    q = torch.quantile(deg[:: max(1, deg.numel() // (1 << 22))].float(),
+                       torch.tensor([0.5, 0.99, 0.9999], device=dev))
+    print(f"[spmm] rows={csr.num_rows} nnz={csr.nnz} degree median/p99/p99.99/max = "
+          f"{q.tolist()} / {int(deg.max())}; rows > 256: {int((deg > 256).sum())}, "
+          f"> 4096: {int((deg > 4096).sum())}", flush=True)
     inv = csr.inv_degree()
     sc = {"row_scale": inv} if a.mean == "row" else {"col_scale": inv}
     variants = [tuple(int(v) for v in s.split(":")) for s in a.variants.split(",")]
@@ -50,11 +74,12 @@ def main():
         ref = None
         for r in range(a.rounds + 1):
             for v in variants:
-                ops.set_spmm_config(*v)
+                ops.set_spmm_config(*v[:3])
+                sp = csr.hub_split(v[3]) if len(v) > 3 else None
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 torch.cuda.synchronize()
                 s.record()
-                K.spmm(csr.rowptr, csr.col, x, out, **sc)
+                K.spmm(csr.rowptr, csr.col, x, out, split=sp, **sc)
                 e.record()
                 torch.cuda.synchronize()
                 if r > 0:
@@ -69,7 +94,7 @@ def main():
         # feature-sliced execution (narrower gathered rows -> smaller per-XCD working set)
         for s, v in [(int(sv), v) for sv in a.slices.split(",") for v in variants
                      if int(sv) > 1 and F % int(sv) == 0]:
-            ops.set_spmm_config(*v)
+            ops.set_spmm_config(*v[:3])
             ts = []
             w = F // s
             for r in range(a.rounds + 1):
@@ -90,8 +115,8 @@ def main():
                   flush=True)
         for v in variants:
             ms = statistics.median(times[v])
-            res[f"F{F}_v{v[0]}_xcd{v[1]}"] = {"ms": round(ms, 3),
-                                              "TBps": round(nbytes / ms / 1e9, 3)}
+            res[f"F{F}_" + "_".join(str(t) for t in v)] = {"ms": round(ms, 3),
+                                                          "TBps": round(nbytes / ms / 1e9, 3)}
             print(f"F={F:4d} variant={v} window={a.window}: {ms:8.2f} ms  "
                   f"{nbytes / ms / 1e9:6.2f} TB/s effective", flush=True)
         del x, out, ref

@@ -56,7 +56,7 @@ const float* opt_f32(const c10::optional<at::Tensor>& t, const at::Tensor& ref,
 void spmm(const at::Tensor& rowptr, const at::Tensor& col, const c10::optional<at::Tensor>& ew,
           const c10::optional<at::Tensor>& col_scale,
           const c10::optional<at::Tensor>& row_scale, const at::Tensor& x,
-          const at::Tensor& out, int64_t heads, int64_t head_dim, double beta) {
+          const at::Tensor& out, int64_t heads, int64_t head_dim, double beta, int64_t cap) {
   check_dev(x, x, "x");
   check_dev(rowptr, x, "rowptr");
   check_dev(col, x, "col");
@@ -81,7 +81,61 @@ void spmm(const at::Tensor& rowptr, const at::Tensor& col, const c10::optional<a
                         col.data_ptr(), ewp, static_cast<int>(heads),
                         static_cast<int>(head_dim), csp, rsp, x.data_ptr(), x.stride(0),
                         out.data_ptr(), out.stride(0), nrows, F, static_cast<float>(beta),
-                        cur_stream(x)));
+                        cur_stream(x), cap));
+}
+
+// hub-row splitting passes (see kernels.h): fp32 partial sums of the hub-row tails, then
+// their fixed-order reduction into the output rows
+void spmm_hub_partials_op(const at::Tensor& seg_beg, const at::Tensor& seg_end,
+                          const at::Tensor& col, const c10::optional<at::Tensor>& ew,
+                          const c10::optional<at::Tensor>& col_scale, const at::Tensor& x,
+                          const at::Tensor& partials) {
+  check_dev(x, x, "x");
+  check_dev(seg_beg, x, "seg_beg");
+  check_dev(seg_end, x, "seg_end");
+  check_dev(col, x, "col");
+  check_dev(partials, x, "partials");
+  check_rows(x, "x");
+  TORCH_CHECK(seg_beg.scalar_type() == at::kLong && seg_end.scalar_type() == at::kLong &&
+                  seg_beg.is_contiguous() && seg_end.is_contiguous() &&
+                  seg_beg.numel() == seg_end.numel(),
+              "seg_beg/seg_end must be contiguous int64 of equal length");
+  TORCH_CHECK(partials.scalar_type() == at::kFloat && partials.is_contiguous() &&
+                  partials.dim() == 2 && partials.size(0) >= seg_beg.numel() &&
+                  partials.size(1) == x.size(1),
+              "partials must be contiguous float32 [nseg, F]");
+  TORCH_CHECK(col.is_contiguous(), "col must be contiguous");
+  const float* ewp = opt_f32(ew, x, "edge_weight");
+  if (ewp) TORCH_CHECK(ew->numel() == col.numel(), "edge_weight must be [E] (one head)");
+  const float* csp = opt_f32(col_scale, x, "col_scale");
+  c10::DeviceGuard g(x.device());
+  DG_HIP_CHECK(spmm_hub_partials(dtype_of(x), itype_of(col), seg_beg.data_ptr<int64_t>(),
+                                 seg_end.data_ptr<int64_t>(), col.data_ptr(), ewp, csp,
+                                 x.data_ptr(), x.stride(0), partials.data_ptr<float>(),
+                                 seg_beg.numel(), static_cast<int>(x.size(1)), cur_stream(x)));
+}
+
+void spmm_hub_reduce_op(const at::Tensor& partials, const at::Tensor& hub_seg_ptr,
+                        const at::Tensor& hub_rows, const c10::optional<at::Tensor>& row_scale,
+                        const at::Tensor& out) {
+  check_dev(out, out, "out");
+  check_dev(partials, out, "partials");
+  check_dev(hub_seg_ptr, out, "hub_seg_ptr");
+  check_dev(hub_rows, out, "hub_rows");
+  check_rows(out, "out");
+  TORCH_CHECK(partials.scalar_type() == at::kFloat && partials.is_contiguous() &&
+                  partials.dim() == 2 && partials.size(1) == out.size(1),
+              "partials must be contiguous float32 [nseg, F]");
+  TORCH_CHECK(hub_seg_ptr.scalar_type() == at::kLong && hub_rows.scalar_type() == at::kLong &&
+                  hub_seg_ptr.is_contiguous() && hub_rows.is_contiguous() &&
+                  hub_seg_ptr.numel() == hub_rows.numel() + 1,
+              "hub_seg_ptr [nhub+1] / hub_rows [nhub] must be contiguous int64");
+  const float* rsp = opt_f32(row_scale, out, "row_scale");
+  c10::DeviceGuard g(out.device());
+  DG_HIP_CHECK(spmm_hub_reduce(dtype_of(out), partials.data_ptr<float>(),
+                               hub_seg_ptr.data_ptr<int64_t>(), hub_rows.data_ptr<int64_t>(),
+                               rsp, out.data_ptr(), out.stride(0), hub_rows.numel(),
+                               static_cast<int>(out.size(1)), cur_stream(out)));
 }
 
 void copy_rows_op(const at::Tensor& x, const c10::optional<at::Tensor>& src_idx,
@@ -570,7 +624,12 @@ TORCH_LIBRARY(dgraph_amd, m) {
         "Tensor(a!) out, int act) -> ()");
   m.def(
       "spmm(Tensor rowptr, Tensor col, Tensor? edge_weight, Tensor? col_scale, "
-      "Tensor? row_scale, Tensor x, Tensor(a!) out, int heads, int head_dim, float beta) -> ()");
+      "Tensor? row_scale, Tensor x, Tensor(a!) out, int heads, int head_dim, float beta, "
+      "int cap=0) -> ()");
+  m.def("spmm_hub_partials(Tensor seg_beg, Tensor seg_end, Tensor col, Tensor? edge_weight, "
+        "Tensor? col_scale, Tensor x, Tensor(a!) partials) -> ()");
+  m.def("spmm_hub_reduce(Tensor partials, Tensor hub_seg_ptr, Tensor hub_rows, "
+        "Tensor? row_scale, Tensor(a!) out) -> ()");
   m.def("copy_rows(Tensor x, Tensor? src_idx, Tensor? dst_idx, Tensor(a!) out, "
         "bool accumulate) -> ()");
   m.def("masked_gather_rows(Tensor x, Tensor idx, Tensor mask, int value, Tensor(a!) out) -> ()");
@@ -580,6 +639,8 @@ TORCH_LIBRARY(dgraph_amd, m) {
 
 TORCH_LIBRARY_IMPL(dgraph_amd, CUDA, m) {
   m.impl("spmm", &dgraph::spmm);
+  m.impl("spmm_hub_partials", &dgraph::spmm_hub_partials_op);
+  m.impl("spmm_hub_reduce", &dgraph::spmm_hub_reduce_op);
   m.impl("copy_rows", &dgraph::copy_rows_op);
   m.impl("masked_gather_rows", &dgraph::masked_gather_rows_op);
   m.impl("edge_softmax_fwd", &dgraph::edge_softmax_fwd_op);

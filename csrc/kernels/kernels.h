@@ -31,7 +31,23 @@ void set_spmm_config(int variant, int xcd, int pass_cols);
 hipError_t spmm_csr(DType dt, IType it, const int64_t* rowptr, const void* col,
                     const float* ew, int heads, int head_dim, const float* col_scale,
                     const float* row_scale, const void* x, int64_t ldx, void* out,
-                    int64_t ldo, int64_t nrows, int F, float beta, hipStream_t stream);
+                    int64_t ldo, int64_t nrows, int F, float beta, hipStream_t stream,
+                    int64_t cap = 0);
+
+// Hub-row splitting (rows whose degree exceeds `cap` are aggregated in three steps):
+//   1. spmm_csr(..., cap): every row sums at most its first `cap` entries;
+//   2. spmm_hub_partials: segment i = entries [seg_beg[i], seg_end[i]) of one hub row's tail
+//      (<= cap entries each), summed (weights as in spmm_csr, one head) into fp32
+//      partials[i, :F];
+//   3. spmm_hub_reduce: out[hub_rows[h]] += row_scale * sum of partials[hub_seg_ptr[h] ..
+//      hub_seg_ptr[h+1]) in segment order (deterministic; no atomics).
+hipError_t spmm_hub_partials(DType dt, IType it, const int64_t* seg_beg,
+                             const int64_t* seg_end, const void* col, const float* ew,
+                             const float* col_scale, const void* x, int64_t ldx,
+                             float* partials, int64_t nseg, int F, hipStream_t stream);
+hipError_t spmm_hub_reduce(DType dt, const float* partials, const int64_t* hub_seg_ptr,
+                           const int64_t* hub_rows, const float* row_scale, void* out,
+                           int64_t ldo, int64_t nhub, int F, hipStream_t stream);
 
 // ---------------------------------------------------------------------------
 // Row copy with optional source and destination index (K4/K7/K8 replacement, K-new-1).

@@ -24,7 +24,7 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(
     const float* __restrict__ ew, int heads, int head_dim,
     const float* __restrict__ col_scale, const float* __restrict__ row_scale,
     const T* __restrict__ x, int64_t ldx, T* __restrict__ out, int64_t ldo,
-    int64_t nrows, int F, float beta) {
+    int64_t nrows, int F, float beta, int64_t cap) {
   constexpr int G = kWave / LPR;  // lane groups per wave = neighbour rows per step
   const int lane = threadIdx.x & (kWave - 1);
   const int g = lane / LPR;
@@ -34,7 +34,8 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(
 
   for (int64_t r = wave; r < nrows; r += nwaves) {
     const int64_t s = rowptr[r];
-    const int64_t e = rowptr[r + 1];
+    const int64_t e1 = rowptr[r + 1];
+    const int64_t e = (cap > 0 && e1 - s > cap) ? s + cap : e1;
     for (int fc = 0; fc < F; fc += LPR * VEC) {
       const int f = fc + l * VEC;
       const bool active = f < F;
@@ -113,7 +114,7 @@ __global__ __launch_bounds__(256) void spmm_csr_v2_kernel(
     const float* __restrict__ ew, int heads, int head_dim,
     const float* __restrict__ col_scale, const float* __restrict__ row_scale,
     const T* __restrict__ x, int64_t ldx, T* __restrict__ out, int64_t ldo,
-    int64_t nrows, int F, float beta) {
+    int64_t nrows, int F, float beta, int64_t cap) {
   constexpr int G = kWave / LPR;
   const int lane = threadIdx.x & (kWave - 1);
   const int g = lane / LPR;
@@ -137,7 +138,8 @@ __global__ __launch_bounds__(256) void spmm_csr_v2_kernel(
   const bool multi_head = heads > 1;
   for (int64_t r = r0; r < rend; r += rstep) {
     const int64_t s = rowptr[r];
-    const int64_t e = rowptr[r + 1];
+    const int64_t e1 = rowptr[r + 1];
+    const int64_t e = (cap > 0 && e1 - s > cap) ? s + cap : e1;
     for (int fc = 0; fc < F; fc += LPR * VEC) {
       const int f = fc + l * VEC;
       const bool active = f < F;
@@ -258,7 +260,7 @@ __global__ __launch_bounds__(256, (LPR <= 8 ? 6 : 1)) void spmm_bf16_rowgroup_ke
     const int64_t* __restrict__ rowptr, const IdxT* __restrict__ col,
     const float* __restrict__ ew, const float* __restrict__ col_scale,
     const float* __restrict__ row_scale, const uint16_t* __restrict__ x, int64_t ldx,
-    uint16_t* __restrict__ out, int64_t ldo, int64_t nrows, int F, float beta) {
+    uint16_t* __restrict__ out, int64_t ldo, int64_t nrows, int F, float beta, int cap) {
   constexpr int VEC = 8;
   constexpr int G = kWave / LPR;
   constexpr int U = LPR < 8 ? LPR : 8;  // neighbour rows in flight per lane per batch
@@ -292,7 +294,10 @@ __global__ __launch_bounds__(256, (LPR <= 8 ? 6 : 1)) void spmm_bf16_rowgroup_ke
     const int64_t r = q * G + g;
     const bool has_row = r < nrows;
     const int64_t s = has_row ? rowptr[r] : 0;
-    const int deg = has_row ? static_cast<int>(rowptr[r + 1] - s) : 0;
+    const int64_t deg1 = has_row ? rowptr[r + 1] - s : 0;
+    // hub rows (degree > cap) aggregate their first cap entries here; the rest is summed
+    // by spmm_hub_partials / spmm_hub_reduce (hub-row splitting)
+    const int deg = static_cast<int>(deg1 > cap ? cap : deg1);
     int maxdeg = deg;
 #pragma unroll
     for (int off = LPR; off < kWave; off <<= 1) {
@@ -400,7 +405,8 @@ template <typename IdxT>
 hipError_t launch_rowgroup(const int64_t* rowptr, const IdxT* col, const float* ew,
                            const float* cs, const float* rs, const uint16_t* x, int64_t ldx,
                            uint16_t* out, int64_t ldo, int64_t nrows, int F, float beta,
-                           bool xcd_mode, hipStream_t st) {
+                           bool xcd_mode, int64_t cap, hipStream_t st) {
+  const int icap = (cap > 0 && cap < (int64_t(1) << 30)) ? static_cast<int>(cap) : (1 << 30);
   // one pass covers LPR * 8 columns; the caller splits wider rows into passes
   const int lanes = (F + 7) / 8;
   const int LPR = lanes <= 4 ? 4 : lanes <= 8 ? 8 : lanes <= 16 ? 16 : lanes <= 32 ? 32 : 64;
@@ -416,10 +422,12 @@ hipError_t launch_rowgroup(const int64_t* rowptr, const IdxT* col, const float* 
   if (LPR == LPR_ && wmode == W_) {                                                          \
     if (xcd)                                                                                 \
       hipLaunchKernelGGL((spmm_bf16_rowgroup_kernel<IdxT, LPR_, W_, true>), grid, block, 0,  \
-                         st, rowptr, col, ew, cs, rs, x, ldx, out, ldo, nrows, F, beta);     \
+                         st, rowptr, col, ew, cs, rs, x, ldx, out, ldo, nrows, F, beta,      \
+                         icap);                                                              \
     else                                                                                     \
       hipLaunchKernelGGL((spmm_bf16_rowgroup_kernel<IdxT, LPR_, W_, false>), grid, block, 0, \
-                         st, rowptr, col, ew, cs, rs, x, ldx, out, ldo, nrows, F, beta);     \
+                         st, rowptr, col, ew, cs, rs, x, ldx, out, ldo, nrows, F, beta,      \
+                         icap);                                                              \
     return hipGetLastError();                                                                \
   }
 #define DG_RG(LPR_) DG_RG_W(LPR_, 0) DG_RG_W(LPR_, 1) DG_RG_W(LPR_, 2) DG_RG_W(LPR_, 3)
@@ -455,7 +463,8 @@ int g_spmm_pass_cols = kSpmmDefaultPassCols;  // bf16 rows wider than this run a
 template <typename T, typename IdxT, int VEC>
 hipError_t launch_lpr(const int64_t* rowptr, const IdxT* col, const float* ew, int heads,
                       int head_dim, const float* cs, const float* rs, const T* x, int64_t ldx,
-                      T* out, int64_t ldo, int64_t nrows, int F, float beta, hipStream_t st) {
+                      T* out, int64_t ldo, int64_t nrows, int F, float beta, int64_t cap,
+                      hipStream_t st) {
   const int lanes_needed = (F + VEC - 1) / VEC;
   int64_t blocks = cap_blocks((nrows + 3) / 4, 256 * 32);
   if (g_spmm_xcd == 3) blocks = (nrows + 3) / 4;  // in-order, one row per wave, no chunking
@@ -475,11 +484,11 @@ hipError_t launch_lpr(const int64_t* rowptr, const IdxT* col, const float* ew, i
   if (xcd)                                                                                 \
     hipLaunchKernelGGL((spmm_csr_v2_kernel<T, IdxT, VEC, LPR_, U_, true>), grid, block, 0, \
                        st, rowptr, col, ew, heads, head_dim, cs, rs, x, ldx, out, ldo,     \
-                       nrows, F, beta);                                                    \
+                       nrows, F, beta, cap);                                               \
   else                                                                                     \
     hipLaunchKernelGGL((spmm_csr_v2_kernel<T, IdxT, VEC, LPR_, U_, false>), grid, block,   \
                        0, st, rowptr, col, ew, heads, head_dim, cs, rs, x, ldx, out, ldo,  \
-                       nrows, F, beta);                                                    \
+                       nrows, F, beta, cap);                                               \
   return hipGetLastError();
     if (lanes_needed <= 4) { DG_V2(4, 2) }
     if (lanes_needed <= 8) { DG_V2(8, 2) }
@@ -490,7 +499,8 @@ hipError_t launch_lpr(const int64_t* rowptr, const IdxT* col, const float* ew, i
   }
 #define DG_SPMM_CASE(LPR_)                                                               \
   hipLaunchKernelGGL((spmm_csr_kernel<T, IdxT, VEC, LPR_>), grid, block, 0, st, rowptr, \
-                     col, ew, heads, head_dim, cs, rs, x, ldx, out, ldo, nrows, F, beta); \
+                     col, ew, heads, head_dim, cs, rs, x, ldx, out, ldo, nrows, F, beta,  \
+                     cap);                                                                \
   return hipGetLastError();
   if (lanes_needed <= 4) { DG_SPMM_CASE(4) }
   if (lanes_needed <= 8) { DG_SPMM_CASE(8) }
@@ -507,7 +517,8 @@ inline bool aligned(const void* p, int bytes) {
 template <typename T, typename IdxT>
 hipError_t launch_vec(const int64_t* rowptr, const IdxT* col, const float* ew, int heads,
                       int head_dim, const float* cs, const float* rs, const T* x, int64_t ldx,
-                      T* out, int64_t ldo, int64_t nrows, int F, float beta, hipStream_t st) {
+                      T* out, int64_t ldo, int64_t nrows, int F, float beta, int64_t cap,
+                      hipStream_t st) {
   // Widest vector that divides the row, both leading dimensions, the head
   // size and both base pointers.
   constexpr int kMaxVec = 16 / sizeof(T);
@@ -517,15 +528,129 @@ hipError_t launch_vec(const int64_t* rowptr, const IdxT* col, const float* ew, i
   };
   if (ok(kMaxVec))
     return launch_lpr<T, IdxT, kMaxVec>(rowptr, col, ew, heads, head_dim, cs, rs, x, ldx, out,
-                                        ldo, nrows, F, beta, st);
+                                        ldo, nrows, F, beta, cap, st);
   if (ok(4))
     return launch_lpr<T, IdxT, 4>(rowptr, col, ew, heads, head_dim, cs, rs, x, ldx, out, ldo,
-                                  nrows, F, beta, st);
+                                  nrows, F, beta, cap, st);
   return launch_lpr<T, IdxT, 1>(rowptr, col, ew, heads, head_dim, cs, rs, x, ldx, out, ldo,
-                                nrows, F, beta, st);
+                                nrows, F, beta, cap, st);
 }
 
 }  // namespace
+
+// ---------------------------------------------------------------------------
+// Hub-row splitting. A power-law graph has rows whose degree is 10^3-10^5 x the mean
+// (the structureless papers100M-shaped graph: ~150K at the top hub). In the row-group
+// kernel such a row keeps its whole wave (and the G-1 rows sharing it) iterating long
+// after the rest of the grid is done. Rows are therefore capped at `cap` entries in the
+// main pass, and the tails are cut into segments of <= cap entries that run as
+// independent waves (fp32 partial sums), then added to their rows in a fixed order.
+template <typename T, typename IdxT, int VEC>
+__global__ __launch_bounds__(256) void hub_partials_kernel(
+    const int64_t* __restrict__ seg_beg, const int64_t* __restrict__ seg_end,
+    const IdxT* __restrict__ col, const float* __restrict__ ew,
+    const float* __restrict__ col_scale, const T* __restrict__ x, int64_t ldx,
+    float* __restrict__ part, int64_t nseg, int F) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t w = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  if (w >= nseg) return;  // wave-uniform
+  const int64_t s = seg_beg[w], e = seg_end[w];
+  for (int fc = 0; fc < F; fc += kWave * VEC) {
+    const int f = fc + lane * VEC;
+    const bool active = f < F;
+    float acc[VEC];
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) acc[i] = 0.f;
+    for (int64_t base = s; base < e; base += kWave) {
+      const int n = (e - base) < kWave ? static_cast<int>(e - base) : kWave;
+      IdxT my_c = IdxT(0);
+      float my_w = 0.f;
+      if (lane < n) {
+        my_c = col[base + lane];
+        my_w = ew ? ew[base + lane] : 1.f;
+        if (col_scale) my_w *= col_scale[my_c];
+      }
+      for (int u0 = 0; u0 < n; u0 += 4) {  // n is wave-uniform: shuffles see every lane
+        float v[4][VEC];
+        float wu[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int src = u0 + k < n ? u0 + k : 0;
+          const int64_t c = static_cast<int64_t>(__shfl(my_c, src, kWave));
+          wu[k] = u0 + k < n ? __shfl(my_w, src, kWave) : 0.f;
+          load_vec_f32<T, VEC>(x + c * ldx + (active ? f : 0), v[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+          for (int i = 0; i < VEC; ++i) acc[i] = fmaf(wu[k], v[k][i], acc[i]);
+      }
+    }
+    if (active) {
+      float* o = part + w * F + f;
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) o[i] = acc[i];
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void hub_reduce_kernel(
+    const float* __restrict__ part, const int64_t* __restrict__ hub_seg_ptr,
+    const int64_t* __restrict__ hub_rows, const float* __restrict__ row_scale,
+    T* __restrict__ out, int64_t ldo, int64_t nhub, int F) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t h = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  if (h >= nhub) return;
+  const int64_t r = hub_rows[h];
+  const int64_t p0 = hub_seg_ptr[h], p1 = hub_seg_ptr[h + 1];
+  const float rs = row_scale ? row_scale[r] : 1.f;
+  for (int f = lane; f < F; f += kWave) {
+    float acc = 0.f;
+    for (int64_t i = p0; i < p1; ++i) acc += part[i * F + f];  // segment order
+    T* o = out + r * ldo + f;
+    *o = Elem<T>::from_f32(fmaf(rs, acc, Elem<T>::to_f32(*o)));
+  }
+}
+
+hipError_t spmm_hub_partials(DType dt, IType it, const int64_t* seg_beg,
+                             const int64_t* seg_end, const void* col, const float* ew,
+                             const float* col_scale, const void* x, int64_t ldx,
+                             float* partials, int64_t nseg, int F, hipStream_t stream) {
+  if (nseg <= 0 || F <= 0) return hipSuccess;
+  const int64_t blocks = (nseg + 3) / 4;
+  if (blocks > 0x7fffffff) return hipErrorInvalidValue;
+  dim3 grid(static_cast<unsigned>(blocks)), block(256);
+#define DG_HP(T_, I_, V_)                                                                   \
+  hipLaunchKernelGGL((hub_partials_kernel<T_, I_, V_>), grid, block, 0, stream, seg_beg,  \
+                     seg_end, static_cast<const I_*>(col), ew, col_scale,                  \
+                     static_cast<const T_*>(x), ldx, partials, nseg, F);                   \
+  return hipGetLastError();
+  if (dt == DType::BF16) {
+    if (it == IType::I32) { DG_HP(uint16_t, int32_t, 4) }
+    DG_HP(uint16_t, int64_t, 4)
+  }
+  if (it == IType::I32) { DG_HP(float, int32_t, 2) }
+  DG_HP(float, int64_t, 2)
+#undef DG_HP
+}
+
+hipError_t spmm_hub_reduce(DType dt, const float* partials, const int64_t* hub_seg_ptr,
+                           const int64_t* hub_rows, const float* row_scale, void* out,
+                           int64_t ldo, int64_t nhub, int F, hipStream_t stream) {
+  if (nhub <= 0 || F <= 0) return hipSuccess;
+  const int64_t blocks = (nhub + 3) / 4;
+  dim3 grid(static_cast<unsigned>(blocks)), block(256);
+  if (dt == DType::BF16)
+    hipLaunchKernelGGL((hub_reduce_kernel<uint16_t>), grid, block, 0, stream, partials,
+                       hub_seg_ptr, hub_rows, row_scale, static_cast<uint16_t*>(out), ldo,
+                       nhub, F);
+  else
+    hipLaunchKernelGGL((hub_reduce_kernel<float>), grid, block, 0, stream, partials,
+                       hub_seg_ptr, hub_rows, row_scale, static_cast<float*>(out), ldo, nhub,
+                       F);
+  return hipGetLastError();
+}
 
 void set_spmm_config(int variant, int xcd, int pass_cols) {
   if (variant < 0) {  // restore the defaults
@@ -542,13 +667,14 @@ void set_spmm_config(int variant, int xcd, int pass_cols) {
 hipError_t spmm_csr(DType dt, IType it, const int64_t* rowptr, const void* col,
                     const float* ew, int heads, int head_dim, const float* col_scale,
                     const float* row_scale, const void* x, int64_t ldx, void* out,
-                    int64_t ldo, int64_t nrows, int F, float beta, hipStream_t stream) {
+                    int64_t ldo, int64_t nrows, int F, float beta, hipStream_t stream,
+                    int64_t cap) {
   if (nrows <= 0 || F <= 0) return hipSuccess;
   if (heads < 1) heads = 1;
   if (head_dim < 1) head_dim = F;
 #define DG_ARGS(T, I)                                                                   \
   rowptr, static_cast<const I*>(col), ew, heads, head_dim, col_scale, row_scale,        \
-      static_cast<const T*>(x), ldx, static_cast<T*>(out), ldo, nrows, F, beta, stream
+      static_cast<const T*>(x), ldx, static_cast<T*>(out), ldo, nrows, F, beta, cap, stream
   if (dt == DType::F32) {
     if (it == IType::I32) return launch_vec<float, int32_t>(DG_ARGS(float, int32_t));
     return launch_vec<float, int64_t>(DG_ARGS(float, int64_t));
@@ -564,9 +690,11 @@ hipError_t spmm_csr(DType dt, IType it, const int64_t* rowptr, const void* col,
       auto* op = static_cast<uint16_t*>(out) + c0;
       hipError_t err = it == IType::I32
           ? launch_rowgroup<int32_t>(rowptr, static_cast<const int32_t*>(col), ew, col_scale,
-                                     row_scale, xp, ldx, op, ldo, nrows, w, beta, xcd, stream)
+                                     row_scale, xp, ldx, op, ldo, nrows, w, beta, xcd, cap,
+                                     stream)
           : launch_rowgroup<int64_t>(rowptr, static_cast<const int64_t*>(col), ew, col_scale,
-                                     row_scale, xp, ldx, op, ldo, nrows, w, beta, xcd, stream);
+                                     row_scale, xp, ldx, op, ldo, nrows, w, beta, xcd, cap,
+                                     stream);
       if (err != hipSuccess) return err;
     }
     return hipSuccess;
@@ -581,10 +709,10 @@ hipError_t spmm_csr(DType dt, IType it, const int64_t* rowptr, const void* col,
       hipError_t err = it == IType::I32
           ? launch_vec<uint16_t, int32_t>(rowptr, static_cast<const int32_t*>(col), ew, 1, pc,
                                           col_scale, row_scale, xp, ldx, op, ldo, nrows, pc,
-                                          beta, stream)
+                                          beta, cap, stream)
           : launch_vec<uint16_t, int64_t>(rowptr, static_cast<const int64_t*>(col), ew, 1, pc,
                                           col_scale, row_scale, xp, ldx, op, ldo, nrows, pc,
-                                          beta, stream);
+                                          beta, cap, stream);
       if (err != hipSuccess) return err;
     }
     return hipSuccess;

@@ -32,6 +32,22 @@ def _rowptr_from_sorted_rows(rows_sorted: torch.Tensor, num_rows: int) -> torch.
     return rowptr
 
 
+@dataclass(frozen=True)
+class HubSplit:
+    """Hub-row split of a CSR (see :meth:`CSR.hub_split`): ``hub_rows[h]`` owns segments
+    ``hub_seg_ptr[h] .. hub_seg_ptr[h+1]``; segment ``i`` is ``col[seg_beg[i]:seg_end[i]]``."""
+
+    cap: int
+    hub_rows: torch.Tensor
+    hub_seg_ptr: torch.Tensor
+    seg_beg: torch.Tensor
+    seg_end: torch.Tensor
+
+    @property
+    def num_segments(self) -> int:
+        return self.seg_beg.numel()
+
+
 @dataclass
 class CSR:
     """A sparse [num_rows, num_cols] pattern in CSR form.
@@ -48,6 +64,7 @@ class CSR:
     symmetric: bool = False
     _transpose: Optional["CSR"] = field(default=None, repr=False)
     _inv_deg: Optional[torch.Tensor] = field(default=None, repr=False)
+    _hub: Optional[tuple] = field(default=None, repr=False)
 
     @property
     def num_rows(self) -> int:
@@ -69,6 +86,37 @@ class CSR:
         if self._inv_deg is None:
             self._inv_deg = (1.0 / self.degree().clamp(min=1).float()).contiguous()
         return self._inv_deg
+
+    def hub_split(self, cap: int) -> Optional["HubSplit"]:
+        """Hub-row split for the native SpMM (cached per ``cap``): rows with more than
+        ``cap`` entries keep their first ``cap`` in the main pass; their tails are cut into
+        segments of at most ``cap`` entries (ranges of THIS csr's ``col``, no copy) that are
+        summed as independent waves and added back in segment order. ``None`` when no row
+        exceeds ``cap`` (or ``cap <= 0``)."""
+        if cap <= 0:
+            return None
+        if self._hub is not None and self._hub[0] == cap:
+            return self._hub[1]
+        deg = self.degree()
+        hub_rows = torch.nonzero(deg > cap).reshape(-1)
+        split = None
+        if hub_rows.numel() > 0:
+            nh = hub_rows.numel()
+            tail = deg[hub_rows] - cap
+            nseg = torch.div(tail + cap - 1, cap, rounding_mode="floor")
+            seg_ptr = torch.zeros(nh + 1, dtype=torch.long, device=self.device)
+            torch.cumsum(nseg, 0, out=seg_ptr[1:])
+            S = int(seg_ptr[-1].item())
+            seg_hub = torch.repeat_interleave(torch.arange(nh, device=self.device), nseg,
+                                              output_size=S)
+            k = torch.arange(S, device=self.device) - seg_ptr[seg_hub]
+            start = self.rowptr[hub_rows][seg_hub]
+            beg = start + cap + k * cap
+            end = torch.minimum(beg + cap, self.rowptr[hub_rows + 1][seg_hub])
+            split = HubSplit(int(cap), hub_rows.contiguous(), seg_ptr, beg.contiguous(),
+                             end.contiguous())
+        self._hub = (cap, split)
+        return split
 
     def row_ids(self) -> torch.Tensor:
         return torch.repeat_interleave(

@@ -41,21 +41,39 @@ def spmm(
     row_scale: Optional[torch.Tensor] = None,
     heads: int = 1,
     beta: float = 0.0,
+    split=None,
 ) -> torch.Tensor:
-    """CSR aggregation ``out[r] = row_scale[r]*sum_j w_j*col_scale[c_j]*x[c_j] + beta*out[r]``."""
+    """CSR aggregation ``out[r] = row_scale[r]*sum_j w_j*col_scale[c_j]*x[c_j] + beta*out[r]``.
+
+    ``split``: a :class:`~dgraph_amd.ops.csr.HubSplit` of this CSR (one head only): hub
+    rows sum their first ``split.cap`` entries in the main pass and their tails in
+    independent segment waves, added back in a fixed order (same result; no wave is held
+    by a 10^5-degree row)."""
     R = rowptr.numel() - 1
     F = x.shape[1]
     if out is None:
         out = torch.empty(R, F, dtype=x.dtype, device=x.device)
         beta = 0.0
     heads = max(int(heads), 1)
+    if split is not None and heads != 1:
+        split = None
+    cap = split.cap if split is not None else 0
+    ew, cs, rs = _f32(edge_weight), _f32(col_scale), _f32(row_scale)
     if _native_ok(x):
-        _native.ops().spmm(
-            rowptr, col, _f32(edge_weight), _f32(col_scale), _f32(row_scale), x, out,
-            heads, F // heads, float(beta),
-        )
+        ops = _native.ops()
+        ops.spmm(rowptr, col, ew, cs, rs, x, out, heads, F // heads, float(beta), cap)
+        if split is not None:
+            part = torch.empty(split.num_segments, F, dtype=torch.float32, device=x.device)
+            ops.spmm_hub_partials(split.seg_beg, split.seg_end, col, ew, cs, x, part)
+            ops.spmm_hub_reduce(part, split.hub_seg_ptr, split.hub_rows, rs, out)
         return out
-    return _ref.spmm(rowptr, col, x, out, edge_weight, col_scale, row_scale, heads, beta)
+    _ref.spmm(rowptr, col, x, out, edge_weight, col_scale, row_scale, heads, beta, cap)
+    if split is not None:
+        part = torch.empty(split.num_segments, F, dtype=torch.float32, device=x.device)
+        _ref.spmm_hub_partials(split.seg_beg, split.seg_end, col, x, part, edge_weight,
+                               col_scale)
+        _ref.spmm_hub_reduce(part, split.hub_seg_ptr, split.hub_rows, out, row_scale)
+    return out
 
 
 def copy_rows(

@@ -26,11 +26,20 @@ def spmm(
     row_scale: Optional[torch.Tensor] = None,
     heads: int = 1,
     beta: float = 0.0,
+    cap: int = 0,
 ) -> torch.Tensor:
+    """``cap > 0``: every row sums only its first ``cap`` entries (hub-split main pass)."""
     R = rowptr.numel() - 1
     F = x.shape[1]
     col = col.long()
     rows = _row_ids(rowptr)
+    keep = None
+    if cap > 0 and col.numel() > 0:
+        slot = torch.arange(col.numel(), device=col.device) - rowptr[:-1].long()[rows]
+        keep = slot < cap
+        col, rows = col[keep], rows[keep]
+        if edge_weight is not None:
+            edge_weight = edge_weight.reshape(keep.numel(), -1)[keep]
     adt = torch.float64 if x.dtype == torch.float64 else torch.float32
     vals = x.to(adt)[col]
     if edge_weight is not None:
@@ -46,6 +55,44 @@ def spmm(
     if beta != 0.0:
         acc = acc + beta * out[:R].to(adt)
     out[:R].copy_(acc.to(out.dtype))
+    return out
+
+
+def spmm_hub_partials(seg_beg, seg_end, col, x, partials, edge_weight=None, col_scale=None):
+    """fp32 sums of the hub-tail segments ``col[seg_beg[i]:seg_end[i]]`` (cf. kernels.h)."""
+    lens = seg_end - seg_beg
+    S = seg_beg.numel()
+    if S == 0:
+        return partials
+    seg = torch.repeat_interleave(torch.arange(S, device=col.device), lens)
+    off = torch.zeros(S + 1, dtype=torch.long, device=col.device)
+    torch.cumsum(lens, 0, out=off[1:])
+    pos = seg_beg[seg] + (torch.arange(seg.numel(), device=col.device) - off[:-1][seg])
+    c = col.long()[pos]
+    vals = x.float()[c]
+    w = torch.ones(pos.numel(), device=col.device)
+    if edge_weight is not None:
+        w = w * edge_weight.reshape(-1).float()[pos]
+    if col_scale is not None:
+        w = w * col_scale.float()[c]
+    acc = torch.zeros(S, x.shape[1], device=x.device)
+    acc.index_add_(0, seg, vals * w.unsqueeze(1))
+    partials[:S].copy_(acc)
+    return partials
+
+
+def spmm_hub_reduce(partials, hub_seg_ptr, hub_rows, out, row_scale=None):
+    """``out[hub_rows[h]] += row_scale * sum of the hub's segment partials`` (in order)."""
+    nh = hub_rows.numel()
+    if nh == 0:
+        return out
+    cnt = hub_seg_ptr[1:] - hub_seg_ptr[:-1]
+    owner = torch.repeat_interleave(torch.arange(nh, device=out.device), cnt)
+    acc = torch.zeros(nh, out.shape[1], device=out.device)
+    acc.index_add_(0, owner, partials[: owner.numel()].float())
+    if row_scale is not None:
+        acc = acc * row_scale.float()[hub_rows].unsqueeze(1)
+    out[hub_rows] = (out[hub_rows].float() + acc).to(out.dtype)
     return out
 
 

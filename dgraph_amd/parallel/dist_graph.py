@@ -15,6 +15,7 @@ serialised every exchange with compute and synced the host per exchange (§3.2 n
 """
 from __future__ import annotations
 
+import os
 import weakref
 from dataclasses import dataclass
 from typing import List, Optional
@@ -25,6 +26,15 @@ from torch.autograd import Function
 from ..comm.alltoallv import AllToAllV
 from ..ops import kernels as K
 from ..ops.csr import CSR, IndexMap
+
+
+# Hub-row split threshold for the SpMM (ops.csr.CSR.hub_split): rows with more entries
+# run their tails as separate segment waves. 0 disables.
+SPMM_HUB_CAP = int(os.environ.get("DGRAPH_SPMM_HUB_CAP", "2048"))
+
+
+def _hs(csr: CSR):
+    return csr.hub_split(SPMM_HUB_CAP) if SPMM_HUB_CAP > 0 else None
 
 
 def _cache_lookup(cache: dict, rows: torch.Tensor):
@@ -134,19 +144,24 @@ class DistGraph:
         rs = self.inv_deg if mean else None
         self.edges_aggregated += self.nnz
         if self.halo is None:
-            return K.spmm(self.interior.rowptr, self.interior.col, x, out, row_scale=rs)
+            return K.spmm(self.interior.rowptr, self.interior.col, x, out, row_scale=rs,
+                          split=_hs(self.interior))
         if static:
             recv = self._static_halo(x)
-            out = K.spmm(self.interior.rowptr, self.interior.col, x, out, row_scale=rs)
-            K.spmm(self.halo.rowptr, self.halo.col, recv, out, row_scale=rs, beta=1.0)
+            out = K.spmm(self.interior.rowptr, self.interior.col, x, out, row_scale=rs,
+                         split=_hs(self.interior))
+            K.spmm(self.halo.rowptr, self.halo.col, recv, out, row_scale=rs, beta=1.0,
+                   split=_hs(self.halo))
             return out
         send = K.gather_rows(x, self.send_map.idx)
         recv, work = self.a2a(send, async_op=True)
         if not self.overlap:
             work.wait()
-        out = K.spmm(self.interior.rowptr, self.interior.col, x, out, row_scale=rs)
+        out = K.spmm(self.interior.rowptr, self.interior.col, x, out, row_scale=rs,
+                     split=_hs(self.interior))
         work.wait()
-        K.spmm(self.halo.rowptr, self.halo.col, recv, out, row_scale=rs, beta=1.0)
+        K.spmm(self.halo.rowptr, self.halo.col, recv, out, row_scale=rs, beta=1.0,
+               split=_hs(self.halo))
         return out
 
     @staticmethod
@@ -159,7 +174,7 @@ class DistGraph:
         rows, F = g.shape
         S = 0 if scratch is None else min(F, (scratch.numel() // max(rows, 1)) // 64 * 64)
         if S < 64 or g.dtype != torch.bfloat16 or not g.is_cuda:
-            return K.spmm(csr.rowptr, csr.col, g, out, col_scale=cs)
+            return K.spmm(csr.rowptr, csr.col, g, out, col_scale=cs, split=_hs(csr))
         if out is None:
             out = torch.empty(csr.num_rows, F, dtype=g.dtype, device=g.device)
         aligned = g.data_ptr() % 16 == 0 and scratch.data_ptr() % 16 == 0 and F % 8 == 0
@@ -170,7 +185,7 @@ class DistGraph:
                 K.row_scale_cols(g[:, c0:c0 + w], cs, buf)
             else:
                 torch.mul(g[:, c0:c0 + w], cs.unsqueeze(1), out=buf)
-            K.spmm(csr.rowptr, csr.col, buf, out[:, c0:c0 + w])
+            K.spmm(csr.rowptr, csr.col, buf, out[:, c0:c0 + w], split=_hs(csr))
         return out
 
     def aggregate_T(self, g: torch.Tensor, mean: bool = True,
@@ -185,19 +200,19 @@ class DistGraph:
         if self.halo is None:
             if cs is not None and scratch is not None:
                 return self._spmm_col_scaled(it, g, cs, out, scratch.reshape(-1))
-            return K.spmm(it.rowptr, it.col, g, out, col_scale=cs)
+            return K.spmm(it.rowptr, it.col, g, out, col_scale=cs, split=_hs(it))
         ht = self.halo.transpose()
-        hg = K.spmm(ht.rowptr, ht.col, g, col_scale=cs)
+        hg = K.spmm(ht.rowptr, ht.col, g, col_scale=cs, split=_hs(ht))
         sg, work = self.a2a_rev(hg, async_op=True)
         if not self.overlap:
             work.wait()
         if cs is not None and scratch is not None:
             out = self._spmm_col_scaled(it, g, cs, out, scratch.reshape(-1))
         else:
-            out = K.spmm(it.rowptr, it.col, g, out, col_scale=cs)
+            out = K.spmm(it.rowptr, it.col, g, out, col_scale=cs, split=_hs(it))
         work.wait()
         st = self.send_map.transpose_csr()
-        K.spmm(st.rowptr, st.col, sg, out, beta=1.0)
+        K.spmm(st.rowptr, st.col, sg, out, beta=1.0, split=_hs(st))
         return out
 
     def _peers(self) -> bool:
@@ -260,15 +275,15 @@ class DistGraph:
         g_rows = g_rows.contiguous()
         self.edges_aggregated += it.nnz + (sub[0].nnz if sub is not None else 0)
         if sub is None:
-            return K.spmm(it.rowptr, it.col, g_rows, out, col_scale=cs)
+            return K.spmm(it.rowptr, it.col, g_rows, out, col_scale=cs, split=_hs(it))
         ht_nz, a2a_sub, st = sub[:3]
-        hg = K.spmm(ht_nz.rowptr, ht_nz.col, g_rows, col_scale=cs)
+        hg = K.spmm(ht_nz.rowptr, ht_nz.col, g_rows, col_scale=cs, split=_hs(ht_nz))
         sg, work = a2a_sub(hg, async_op=True)
         if not self.overlap:
             work.wait()
-        out = K.spmm(it.rowptr, it.col, g_rows, out, col_scale=cs)
+        out = K.spmm(it.rowptr, it.col, g_rows, out, col_scale=cs, split=_hs(it))
         work.wait()
-        K.spmm(st.rowptr, st.col, sg, out, beta=1.0)
+        K.spmm(st.rowptr, st.col, sg, out, beta=1.0, split=_hs(st))
         return out
 
     def _restricted_fwd(self, rows: torch.Tensor):
@@ -305,23 +320,26 @@ class DistGraph:
         rsc = rs if mean else None
         self.edges_aggregated += ir.nnz + (hsub[0].nnz if hsub is not None else 0)
         if hsub is None:
-            return K.spmm(ir.rowptr, ir.col, x, out, row_scale=rsc)
+            return K.spmm(ir.rowptr, ir.col, x, out, row_scale=rsc, split=_hs(ir))
         hr, a2a_f, recv_local = hsub
         recv, work = a2a_f(K.gather_rows(x, recv_local), async_op=True)
         if not self.overlap:
             work.wait()
-        out = K.spmm(ir.rowptr, ir.col, x, out, row_scale=rsc)
+        out = K.spmm(ir.rowptr, ir.col, x, out, row_scale=rsc, split=_hs(ir))
         work.wait()
-        K.spmm(hr.rowptr, hr.col, recv, out, row_scale=rsc, beta=1.0)
+        K.spmm(hr.rowptr, hr.col, recv, out, row_scale=rsc, beta=1.0, split=_hs(hr))
         return out
 
     def prepare_backward(self):
-        """Build the cached transposes eagerly (outside any timed region)."""
+        """Build the cached transposes and hub-row splits eagerly (outside any timed
+        region)."""
+        csrs = [self.interior]
         if not self.interior.symmetric:
-            self.interior.transpose()
+            csrs.append(self.interior.transpose())
         if self.halo is not None:
-            self.halo.transpose()
-            self.send_map.transpose_csr()
+            csrs += [self.halo, self.halo.transpose(), self.send_map.transpose_csr()]
+        for c in csrs:
+            _hs(c)
         return self
 
     def memory_bytes(self) -> int:
