@@ -46,6 +46,12 @@ def ensure_process_group(backend: Optional[str] = None, **kwargs) -> None:
         dev = default_device()
         torch.cuda.set_device(dev)
         kw["device_id"] = dev
+        if "pg_options" not in kwargs and os.environ.get("DGRAPH_PG_HIGH_PRIORITY", "1") == "1":
+            # RCCL kernels on a high-priority stream: the halo exchange overlaps the
+            # interior SpMM, and at equal priority the SpMM's waves fill every CU first
+            opts = dist.ProcessGroupNCCL.Options()
+            opts.is_high_priority_stream = True
+            kw["pg_options"] = opts
     if "RANK" in os.environ and "WORLD_SIZE" in os.environ:
         dist.init_process_group(**kw, **kwargs)
     else:

@@ -476,12 +476,18 @@ class SAGEStackFn(Function):
             fuse_dx = _bwd_fused(specs, dims, i, need_dx, g)
             mask_in = prev[1] if (fuse_dx and isinstance(prev, tuple)) else None
             g_masked = mask_in is not None
-            grads[3 * i] = wgrad(x, g)[:r_in, :r_out].to(ws.dtype)
-            if b is not None:
-                grads[3 * i + 2] = col_sum_f32(g)[:r_out].to(b.dtype)
+
+            def self_grads(i=i, x=x, g=g, ws=ws, b=b, r_in=r_in, r_out=r_out):
+                # W_self / bias gradients need no aggregation: on a multi-GPU graph they
+                # run while the layer's reverse halo exchange is on the links
+                grads[3 * i] = wgrad(x, g)[:r_in, :r_out].to(ws.dtype)
+                if b is not None:
+                    grads[3 * i + 2] = col_sum_f32(g)[:r_out].to(b.dtype)
+
             dx = None
             if pf:
-                dz = graph.aggregate_T(g, mean=True, out=V("tmp_b", dims[i + 1]))
+                dz = graph.aggregate_T(g, mean=True, out=V("tmp_b", dims[i + 1]),
+                                       overlap=self_grads)
                 grads[3 * i + 1] = wgrad(x, dz)[:r_in, :r_out].to(wn.dtype)
                 if need_dx:
                     if fuse_dx:
@@ -500,7 +506,7 @@ class SAGEStackFn(Function):
                 scratch = ws_obj.slots["tmp_b" if u_name == "tmp_a" else "tmp_a"] \
                     if use_ws and i < n - 1 else None
                 u = graph.aggregate_T(g, mean=True, out=V(u_name, dims[i + 1]),
-                                      scratch=scratch)
+                                      scratch=scratch, overlap=self_grads)
                 del scratch
                 grads[3 * i + 1] = wgrad(x, u)[:r_in, :r_out].to(wn.dtype)
                 if fuse_dx:
@@ -513,6 +519,7 @@ class SAGEStackFn(Function):
                     dx.addmm_(u, wn_.t())
                 del u
             else:
+                self_grads()
                 # tmp_a may still hold g for the last layer: recompute into tmp_b then
                 a_name = "tmp_b" if (i == n - 1 and ctx.out_rows is not None) else "tmp_a"
                 if i == 0 and ctx.keep0:

@@ -66,6 +66,7 @@ class DistGraph:
         group=None,
         symmetric: bool = False,
         overlap: bool = True,
+        chunk_bytes: Optional[int] = None,
     ):
         assert csr.num_rows == num_local, "CSR rows must be the local vertices"
         assert csr.num_cols == num_local + num_halo
@@ -74,6 +75,9 @@ class DistGraph:
         self.inv_deg = csr.inv_degree()
         self.symmetric = symmetric
         self.overlap = overlap
+        # per-peer message size above which an exchange is cut into column chunks
+        self.chunk_bytes = int(os.environ.get("DGRAPH_HALO_CHUNK_BYTES", str(32 << 20))) \
+            if chunk_bytes is None else int(chunk_bytes)
         self._restrict_cache = {}
         self._restrict_fwd_cache = {}
         self._static_cache = {}
@@ -153,16 +157,39 @@ class DistGraph:
             K.spmm(self.halo.rowptr, self.halo.col, recv, out, row_scale=rs, beta=1.0,
                    split=_hs(self.halo))
             return out
-        send = K.gather_rows(x, self.send_map.idx)
-        recv, work = self.a2a(send, async_op=True)
-        if not self.overlap:
+        if out is None:
+            out = torch.empty(self.L, x.shape[1], dtype=x.dtype, device=x.device)
+        # column chunks: chunk k's halo SpMM runs while chunk k+1 is on the links
+        pend = []
+        for c0, c1 in self._col_chunks(self.a2a, x.shape[1], x.element_size()):
+            xc = x if (c0, c1) == (0, x.shape[1]) else x[:, c0:c1]
+            recv, work = self.a2a(K.gather_rows(xc, self.send_map.idx), async_op=True)
+            if not self.overlap:
+                work.wait()
+            pend.append((c0, c1, recv, work))
+        K.spmm(self.interior.rowptr, self.interior.col, x, out, row_scale=rs,
+               split=_hs(self.interior))
+        for c0, c1, recv, work in pend:
             work.wait()
-        out = K.spmm(self.interior.rowptr, self.interior.col, x, out, row_scale=rs,
-                     split=_hs(self.interior))
-        work.wait()
-        K.spmm(self.halo.rowptr, self.halo.col, recv, out, row_scale=rs, beta=1.0,
-               split=_hs(self.halo))
+            oc = out if (c0, c1) == (0, x.shape[1]) else out[:, c0:c1]
+            K.spmm(self.halo.rowptr, self.halo.col, recv, oc, row_scale=rs, beta=1.0,
+                   split=_hs(self.halo))
         return out
+
+    def _col_chunks(self, a2a, F: int, esize: int):
+        """Column ranges of one exchange: a single range unless the largest per-peer
+        message exceeds 2 x ``chunk_bytes``; then chunks of whole 64-column blocks, each
+        per-peer message of a chunk >= ``chunk_bytes`` / 2 (RCCL's per-call cost stays
+        negligible; xGMI is point-to-point, so a peer message is one link's load)."""
+        cb = self.chunk_bytes
+        peer = max(max(a2a.send_splits, default=0), max(a2a.recv_splits, default=0))
+        per_peer = peer * F * esize
+        if cb <= 0 or per_peer <= 2 * cb or F < 128:
+            return [(0, F)]
+        n = min(-(-per_peer // cb), F // 64)
+        w = -(-F // n)
+        w = -(-w // 64) * 64
+        return [(c, min(c + w, F)) for c in range(0, F, w)]
 
     @staticmethod
     def _spmm_col_scaled(csr: CSR, g: torch.Tensor, cs: torch.Tensor, out, scratch):
@@ -190,29 +217,44 @@ class DistGraph:
 
     def aggregate_T(self, g: torch.Tensor, mean: bool = True,
                     out: Optional[torch.Tensor] = None,
-                    scratch: Optional[torch.Tensor] = None) -> torch.Tensor:
+                    scratch: Optional[torch.Tensor] = None, overlap=None) -> torch.Tensor:
         """Transposed aggregation (the backward of :meth:`aggregate`). ``scratch``: an
-        optional free buffer (any shape, same dtype as ``g``) for the pre-scaled path."""
+        optional free buffer (any shape, same dtype as ``g``) for the pre-scaled path.
+        ``overlap``: a callable of independent work, run after the reverse exchange and
+        the interior SpMM are issued and before the exchange is waited for."""
         cs = self.inv_deg if mean else None
         self.edges_aggregated += self.nnz
         g = g.contiguous()
         it = self.interior if self.interior.symmetric else self.interior.transpose()
         if self.halo is None:
             if cs is not None and scratch is not None:
-                return self._spmm_col_scaled(it, g, cs, out, scratch.reshape(-1))
-            return K.spmm(it.rowptr, it.col, g, out, col_scale=cs, split=_hs(it))
+                out = self._spmm_col_scaled(it, g, cs, out, scratch.reshape(-1))
+            else:
+                out = K.spmm(it.rowptr, it.col, g, out, col_scale=cs, split=_hs(it))
+            if overlap is not None:
+                overlap()
+            return out
         ht = self.halo.transpose()
-        hg = K.spmm(ht.rowptr, ht.col, g, col_scale=cs, split=_hs(ht))
-        sg, work = self.a2a_rev(hg, async_op=True)
-        if not self.overlap:
-            work.wait()
+        F = g.shape[1]
+        pend = []
+        for c0, c1 in self._col_chunks(self.a2a_rev, F, g.element_size()):
+            gc = g if (c0, c1) == (0, F) else g[:, c0:c1]
+            hg = K.spmm(ht.rowptr, ht.col, gc, col_scale=cs, split=_hs(ht))
+            sg, work = self.a2a_rev(hg, async_op=True)
+            if not self.overlap:
+                work.wait()
+            pend.append((c0, c1, sg, work))
         if cs is not None and scratch is not None:
             out = self._spmm_col_scaled(it, g, cs, out, scratch.reshape(-1))
         else:
             out = K.spmm(it.rowptr, it.col, g, out, col_scale=cs, split=_hs(it))
-        work.wait()
+        if overlap is not None:
+            overlap()  # independent work queued behind the exchange (e.g. a weight grad)
         st = self.send_map.transpose_csr()
-        K.spmm(st.rowptr, st.col, sg, out, beta=1.0, split=_hs(st))
+        for c0, c1, sg, work in pend:
+            work.wait()
+            oc = out if (c0, c1) == (0, F) else out[:, c0:c1]
+            K.spmm(st.rowptr, st.col, sg, oc, beta=1.0, split=_hs(st))
         return out
 
     def _peers(self) -> bool:

@@ -14,7 +14,7 @@ from conftest import run_ranks
 
 
 def _args(**kw):
-    a = argparse.Namespace(shape="ogbn-papers100M", scale=2e-5, hidden=64, layers=3, lr=1e-2,
+    a = argparse.Namespace(shape="ogbn-papers100M", scale=2e-5, hidden=128, layers=3, lr=1e-2,
                            dtype="fp32", global_frac=0.05, window=64, seed=0,
                            no_overlap=False, rehearse_world=0, rehearse_rank=0)
     for k, v in kw.items():
@@ -47,8 +47,16 @@ def _run_job(rank, world, out, steps, global_frac, restrict):
 
 
 @pytest.mark.parametrize("world", [2, 8])
-@pytest.mark.parametrize("global_frac,restrict", [(0.05, False), (1.0, False), (0.05, True)])
-def test_bench_step_matches_single_rank(tmp_path, world, global_frac, restrict):
+@pytest.mark.parametrize("global_frac,restrict,chunked", [(0.05, False, False),
+                                                          (1.0, False, False),
+                                                          (0.05, True, False),
+                                                          (1.0, False, True)])
+def test_bench_step_matches_single_rank(tmp_path, monkeypatch, world, global_frac, restrict,
+                                        chunked):
+    """``chunked``: every halo exchange of width >= 128 is cut into 64-column chunks
+    (DGRAPH_HALO_CHUNK_BYTES tiny), exercising the chunk pipeline of DistGraph."""
+    if chunked:
+        monkeypatch.setenv("DGRAPH_HALO_CHUNK_BYTES", "64")
     steps = 3
     _run_job(0, 1, tmp_path / "w1.pt", steps, global_frac, restrict)
     run_ranks(_run_job, world, str(tmp_path / "wn.pt"), steps, global_frac, restrict,
