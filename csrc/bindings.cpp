@@ -56,7 +56,8 @@ const float* opt_f32(const c10::optional<at::Tensor>& t, const at::Tensor& ref,
 void spmm(const at::Tensor& rowptr, const at::Tensor& col, const c10::optional<at::Tensor>& ew,
           const c10::optional<at::Tensor>& col_scale,
           const c10::optional<at::Tensor>& row_scale, const at::Tensor& x,
-          const at::Tensor& out, int64_t heads, int64_t head_dim, double beta, int64_t cap) {
+          const at::Tensor& out, int64_t heads, int64_t head_dim, double beta, int64_t cap,
+          const c10::optional<at::Tensor>& row_map) {
   check_dev(x, x, "x");
   check_dev(rowptr, x, "rowptr");
   check_dev(col, x, "col");
@@ -69,7 +70,16 @@ void spmm(const at::Tensor& rowptr, const at::Tensor& col, const c10::optional<a
   TORCH_CHECK(x.scalar_type() == out.scalar_type(), "x/out dtype mismatch");
   TORCH_CHECK(x.size(1) == out.size(1), "x/out feature mismatch");
   const int64_t nrows = rowptr.numel() - 1;
-  TORCH_CHECK(out.size(0) >= nrows, "out has fewer rows than the CSR");
+  const int64_t* rmap = nullptr;
+  if (row_map.has_value() && row_map->defined()) {
+    check_dev(*row_map, x, "row_map");
+    TORCH_CHECK(row_map->scalar_type() == at::kLong && row_map->is_contiguous() &&
+                    row_map->numel() == nrows,
+                "row_map must be contiguous int64 [nrows]");
+    rmap = row_map->data_ptr<int64_t>();
+  } else {
+    TORCH_CHECK(out.size(0) >= nrows, "out has fewer rows than the CSR");
+  }
   const float* ewp = opt_f32(ew, x, "edge_weight");
   if (ewp) TORCH_CHECK(ew->numel() == col.numel() * std::max<int64_t>(heads, 1),
                        "edge_weight must be [E, heads]");
@@ -81,7 +91,7 @@ void spmm(const at::Tensor& rowptr, const at::Tensor& col, const c10::optional<a
                         col.data_ptr(), ewp, static_cast<int>(heads),
                         static_cast<int>(head_dim), csp, rsp, x.data_ptr(), x.stride(0),
                         out.data_ptr(), out.stride(0), nrows, F, static_cast<float>(beta),
-                        cur_stream(x), cap));
+                        cur_stream(x), cap, rmap));
 }
 
 // hub-row splitting passes (see kernels.h): fp32 partial sums of the hub-row tails, then
@@ -625,7 +635,7 @@ TORCH_LIBRARY(dgraph_amd, m) {
   m.def(
       "spmm(Tensor rowptr, Tensor col, Tensor? edge_weight, Tensor? col_scale, "
       "Tensor? row_scale, Tensor x, Tensor(a!) out, int heads, int head_dim, float beta, "
-      "int cap=0) -> ()");
+      "int cap=0, Tensor? row_map=None) -> ()");
   m.def("spmm_hub_partials(Tensor seg_beg, Tensor seg_end, Tensor col, Tensor? edge_weight, "
         "Tensor? col_scale, Tensor x, Tensor(a!) partials) -> ()");
   m.def("spmm_hub_reduce(Tensor partials, Tensor hub_seg_ptr, Tensor hub_rows, "

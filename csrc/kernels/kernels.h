@@ -32,7 +32,9 @@ hipError_t spmm_csr(DType dt, IType it, const int64_t* rowptr, const void* col,
                     const float* ew, int heads, int head_dim, const float* col_scale,
                     const float* row_scale, const void* x, int64_t ldx, void* out,
                     int64_t ldo, int64_t nrows, int F, float beta, hipStream_t stream,
-                    int64_t cap = 0);
+                    int64_t cap = 0, const int64_t* row_map = nullptr);
+// row_map (optional, int64 [nrows]): CSR row r writes output row row_map[r] and reads
+// row_scale[row_map[r]] (a row-compacted CSR that skips empty rows).
 
 // Hub-row splitting (rows whose degree exceeds `cap` are aggregated in three steps):
 //   1. spmm_csr(..., cap): every row sums at most its first `cap` entries;

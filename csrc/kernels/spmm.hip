@@ -24,7 +24,8 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(
     const float* __restrict__ ew, int heads, int head_dim,
     const float* __restrict__ col_scale, const float* __restrict__ row_scale,
     const T* __restrict__ x, int64_t ldx, T* __restrict__ out, int64_t ldo,
-    int64_t nrows, int F, float beta, int64_t cap) {
+    int64_t nrows, int F, float beta, int64_t cap,
+    const int64_t* __restrict__ row_map) {
   constexpr int G = kWave / LPR;  // lane groups per wave = neighbour rows per step
   const int lane = threadIdx.x & (kWave - 1);
   const int g = lane / LPR;
@@ -85,8 +86,9 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(
         for (int i = 0; i < VEC; ++i) acc[i] += __shfl_xor(acc[i], off, kWave);
 
       if (g == 0 && active) {
-        const float rs = row_scale ? row_scale[r] : 1.f;
-        T* o = out + r * ldo + f;
+        const int64_t orow = row_map ? row_map[r] : r;  // compacted CSR: output row
+        const float rs = row_scale ? row_scale[orow] : 1.f;
+        T* o = out + orow * ldo + f;
         if (beta != 0.f) {
           float old[VEC];
           load_vec_f32<T, VEC>(o, old);
@@ -114,7 +116,8 @@ __global__ __launch_bounds__(256) void spmm_csr_v2_kernel(
     const float* __restrict__ ew, int heads, int head_dim,
     const float* __restrict__ col_scale, const float* __restrict__ row_scale,
     const T* __restrict__ x, int64_t ldx, T* __restrict__ out, int64_t ldo,
-    int64_t nrows, int F, float beta, int64_t cap) {
+    int64_t nrows, int F, float beta, int64_t cap,
+    const int64_t* __restrict__ row_map) {
   constexpr int G = kWave / LPR;
   const int lane = threadIdx.x & (kWave - 1);
   const int g = lane / LPR;
@@ -199,8 +202,9 @@ __global__ __launch_bounds__(256) void spmm_csr_v2_kernel(
 #pragma unroll
         for (int i = 0; i < VEC; ++i) acc[i] += __shfl_xor(acc[i], off, kWave);
       if (g == 0 && active) {
-        const float rs = row_scale ? row_scale[r] : 1.f;
-        T* o = out + r * ldo + f;
+        const int64_t orow = row_map ? row_map[r] : r;  // compacted CSR: output row
+        const float rs = row_scale ? row_scale[orow] : 1.f;
+        T* o = out + orow * ldo + f;
         if (beta != 0.f) {
           float old[VEC];
           load_vec_f32<T, VEC>(o, old);
@@ -260,7 +264,8 @@ __global__ __launch_bounds__(256, (LPR <= 8 ? 6 : 1)) void spmm_bf16_rowgroup_ke
     const int64_t* __restrict__ rowptr, const IdxT* __restrict__ col,
     const float* __restrict__ ew, const float* __restrict__ col_scale,
     const float* __restrict__ row_scale, const uint16_t* __restrict__ x, int64_t ldx,
-    uint16_t* __restrict__ out, int64_t ldo, int64_t nrows, int F, float beta, int cap) {
+    uint16_t* __restrict__ out, int64_t ldo, int64_t nrows, int F, float beta, int cap,
+    const int64_t* __restrict__ row_map) {
   constexpr int VEC = 8;
   constexpr int G = kWave / LPR;
   constexpr int U = LPR < 8 ? LPR : 8;  // neighbour rows in flight per lane per batch
@@ -378,8 +383,9 @@ __global__ __launch_bounds__(256, (LPR <= 8 ? 6 : 1)) void spmm_bf16_rowgroup_ke
       my_c = nx_c;
     }
     if (has_row && active) {
-      const float rs = row_scale ? row_scale[r] : 1.f;
-      uint16_t* o = out + r * ldo + f;
+      const int64_t orow = row_map ? row_map[r] : r;  // compacted CSR: output row
+      const float rs = row_scale ? row_scale[orow] : 1.f;
+      uint16_t* o = out + orow * ldo + f;
       float res[VEC];
       if (beta != 0.f) {
         float old[VEC];
@@ -405,7 +411,8 @@ template <typename IdxT>
 hipError_t launch_rowgroup(const int64_t* rowptr, const IdxT* col, const float* ew,
                            const float* cs, const float* rs, const uint16_t* x, int64_t ldx,
                            uint16_t* out, int64_t ldo, int64_t nrows, int F, float beta,
-                           bool xcd_mode, int64_t cap, hipStream_t st) {
+                           bool xcd_mode, int64_t cap, const int64_t* row_map,
+                           hipStream_t st) {
   const int icap = (cap > 0 && cap < (int64_t(1) << 30)) ? static_cast<int>(cap) : (1 << 30);
   // one pass covers LPR * 8 columns; the caller splits wider rows into passes
   const int lanes = (F + 7) / 8;
@@ -423,11 +430,11 @@ hipError_t launch_rowgroup(const int64_t* rowptr, const IdxT* col, const float* 
     if (xcd)                                                                                 \
       hipLaunchKernelGGL((spmm_bf16_rowgroup_kernel<IdxT, LPR_, W_, true>), grid, block, 0,  \
                          st, rowptr, col, ew, cs, rs, x, ldx, out, ldo, nrows, F, beta,      \
-                         icap);                                                              \
+                         icap, row_map);                                                     \
     else                                                                                     \
       hipLaunchKernelGGL((spmm_bf16_rowgroup_kernel<IdxT, LPR_, W_, false>), grid, block, 0, \
                          st, rowptr, col, ew, cs, rs, x, ldx, out, ldo, nrows, F, beta,      \
-                         icap);                                                              \
+                         icap, row_map);                                                     \
     return hipGetLastError();                                                                \
   }
 #define DG_RG(LPR_) DG_RG_W(LPR_, 0) DG_RG_W(LPR_, 1) DG_RG_W(LPR_, 2) DG_RG_W(LPR_, 3)
@@ -464,7 +471,7 @@ template <typename T, typename IdxT, int VEC>
 hipError_t launch_lpr(const int64_t* rowptr, const IdxT* col, const float* ew, int heads,
                       int head_dim, const float* cs, const float* rs, const T* x, int64_t ldx,
                       T* out, int64_t ldo, int64_t nrows, int F, float beta, int64_t cap,
-                      hipStream_t st) {
+                      const int64_t* row_map, hipStream_t st) {
   const int lanes_needed = (F + VEC - 1) / VEC;
   int64_t blocks = cap_blocks((nrows + 3) / 4, 256 * 32);
   if (g_spmm_xcd == 3) blocks = (nrows + 3) / 4;  // in-order, one row per wave, no chunking
@@ -484,11 +491,11 @@ hipError_t launch_lpr(const int64_t* rowptr, const IdxT* col, const float* ew, i
   if (xcd)                                                                                 \
     hipLaunchKernelGGL((spmm_csr_v2_kernel<T, IdxT, VEC, LPR_, U_, true>), grid, block, 0, \
                        st, rowptr, col, ew, heads, head_dim, cs, rs, x, ldx, out, ldo,     \
-                       nrows, F, beta, cap);                                               \
+                       nrows, F, beta, cap, row_map);                                      \
   else                                                                                     \
     hipLaunchKernelGGL((spmm_csr_v2_kernel<T, IdxT, VEC, LPR_, U_, false>), grid, block,   \
                        0, st, rowptr, col, ew, heads, head_dim, cs, rs, x, ldx, out, ldo,  \
-                       nrows, F, beta, cap);                                               \
+                       nrows, F, beta, cap, row_map);                                      \
   return hipGetLastError();
     if (lanes_needed <= 4) { DG_V2(4, 2) }
     if (lanes_needed <= 8) { DG_V2(8, 2) }
@@ -500,7 +507,7 @@ hipError_t launch_lpr(const int64_t* rowptr, const IdxT* col, const float* ew, i
 #define DG_SPMM_CASE(LPR_)                                                               \
   hipLaunchKernelGGL((spmm_csr_kernel<T, IdxT, VEC, LPR_>), grid, block, 0, st, rowptr, \
                      col, ew, heads, head_dim, cs, rs, x, ldx, out, ldo, nrows, F, beta,  \
-                     cap);                                                                \
+                     cap, row_map);                                                       \
   return hipGetLastError();
   if (lanes_needed <= 4) { DG_SPMM_CASE(4) }
   if (lanes_needed <= 8) { DG_SPMM_CASE(8) }
@@ -518,7 +525,7 @@ template <typename T, typename IdxT>
 hipError_t launch_vec(const int64_t* rowptr, const IdxT* col, const float* ew, int heads,
                       int head_dim, const float* cs, const float* rs, const T* x, int64_t ldx,
                       T* out, int64_t ldo, int64_t nrows, int F, float beta, int64_t cap,
-                      hipStream_t st) {
+                      const int64_t* row_map, hipStream_t st) {
   // Widest vector that divides the row, both leading dimensions, the head
   // size and both base pointers.
   constexpr int kMaxVec = 16 / sizeof(T);
@@ -528,12 +535,12 @@ hipError_t launch_vec(const int64_t* rowptr, const IdxT* col, const float* ew, i
   };
   if (ok(kMaxVec))
     return launch_lpr<T, IdxT, kMaxVec>(rowptr, col, ew, heads, head_dim, cs, rs, x, ldx, out,
-                                        ldo, nrows, F, beta, cap, st);
+                                        ldo, nrows, F, beta, cap, row_map, st);
   if (ok(4))
     return launch_lpr<T, IdxT, 4>(rowptr, col, ew, heads, head_dim, cs, rs, x, ldx, out, ldo,
-                                  nrows, F, beta, cap, st);
+                                  nrows, F, beta, cap, row_map, st);
   return launch_lpr<T, IdxT, 1>(rowptr, col, ew, heads, head_dim, cs, rs, x, ldx, out, ldo,
-                                nrows, F, beta, cap, st);
+                                nrows, F, beta, cap, row_map, st);
 }
 
 }  // namespace
@@ -668,13 +675,13 @@ hipError_t spmm_csr(DType dt, IType it, const int64_t* rowptr, const void* col,
                     const float* ew, int heads, int head_dim, const float* col_scale,
                     const float* row_scale, const void* x, int64_t ldx, void* out,
                     int64_t ldo, int64_t nrows, int F, float beta, hipStream_t stream,
-                    int64_t cap) {
+                    int64_t cap, const int64_t* row_map) {
   if (nrows <= 0 || F <= 0) return hipSuccess;
   if (heads < 1) heads = 1;
   if (head_dim < 1) head_dim = F;
 #define DG_ARGS(T, I)                                                                   \
   rowptr, static_cast<const I*>(col), ew, heads, head_dim, col_scale, row_scale,        \
-      static_cast<const T*>(x), ldx, static_cast<T*>(out), ldo, nrows, F, beta, cap, stream
+      static_cast<const T*>(x), ldx, static_cast<T*>(out), ldo, nrows, F, beta, cap, row_map, stream
   if (dt == DType::F32) {
     if (it == IType::I32) return launch_vec<float, int32_t>(DG_ARGS(float, int32_t));
     return launch_vec<float, int64_t>(DG_ARGS(float, int64_t));
@@ -691,10 +698,10 @@ hipError_t spmm_csr(DType dt, IType it, const int64_t* rowptr, const void* col,
       hipError_t err = it == IType::I32
           ? launch_rowgroup<int32_t>(rowptr, static_cast<const int32_t*>(col), ew, col_scale,
                                      row_scale, xp, ldx, op, ldo, nrows, w, beta, xcd, cap,
-                                     stream)
+                                     row_map, stream)
           : launch_rowgroup<int64_t>(rowptr, static_cast<const int64_t*>(col), ew, col_scale,
                                      row_scale, xp, ldx, op, ldo, nrows, w, beta, xcd, cap,
-                                     stream);
+                                     row_map, stream);
       if (err != hipSuccess) return err;
     }
     return hipSuccess;
@@ -709,10 +716,10 @@ hipError_t spmm_csr(DType dt, IType it, const int64_t* rowptr, const void* col,
       hipError_t err = it == IType::I32
           ? launch_vec<uint16_t, int32_t>(rowptr, static_cast<const int32_t*>(col), ew, 1, pc,
                                           col_scale, row_scale, xp, ldx, op, ldo, nrows, pc,
-                                          beta, cap, stream)
+                                          beta, cap, row_map, stream)
           : launch_vec<uint16_t, int64_t>(rowptr, static_cast<const int64_t*>(col), ew, 1, pc,
                                           col_scale, row_scale, xp, ldx, op, ldo, nrows, pc,
-                                          beta, cap, stream);
+                                          beta, cap, row_map, stream);
       if (err != hipSuccess) return err;
     }
     return hipSuccess;

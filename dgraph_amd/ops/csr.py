@@ -65,6 +65,9 @@ class CSR:
     _transpose: Optional["CSR"] = field(default=None, repr=False)
     _inv_deg: Optional[torch.Tensor] = field(default=None, repr=False)
     _hub: Optional[tuple] = field(default=None, repr=False)
+    # row-compacted CSR (see compact_rows): CSR row r is output row row_map[r]
+    row_map: Optional[torch.Tensor] = None
+    _compact: Optional["CSR"] = field(default=None, repr=False)
 
     @property
     def num_rows(self) -> int:
@@ -113,10 +116,25 @@ class CSR:
             start = self.rowptr[hub_rows][seg_hub]
             beg = start + cap + k * cap
             end = torch.minimum(beg + cap, self.rowptr[hub_rows + 1][seg_hub])
-            split = HubSplit(int(cap), hub_rows.contiguous(), seg_ptr, beg.contiguous(),
+            out_rows = hub_rows if self.row_map is None else self.row_map[hub_rows]
+            split = HubSplit(int(cap), out_rows.contiguous(), seg_ptr, beg.contiguous(),
                              end.contiguous())
         self._hub = (cap, split)
         return split
+
+    def compact_rows(self) -> "CSR":
+        """The same entries over the non-empty rows only, with ``row_map`` giving each
+        row's output row (cached). For the halo / segment-sum blocks of a partition, where
+        a pass with ``beta=1`` would otherwise read and rewrite every output row, also the
+        ~30-60 % with no entry. The ``col`` array is shared (no copy)."""
+        if self.row_map is not None:
+            return self
+        if self._compact is None:
+            nz = torch.nonzero(self.degree() > 0).reshape(-1)
+            rowptr = torch.cat([self.rowptr[nz], self.rowptr[-1:]]).contiguous()
+            self._compact = CSR(rowptr, self.col, self.num_cols, self.perm, False, None, None,
+                                row_map=nz.contiguous())
+        return self._compact
 
     def row_ids(self) -> torch.Tensor:
         return torch.repeat_interleave(
@@ -135,6 +153,7 @@ class CSR:
             self.symmetric,
             None,
             None if self._inv_deg is None else self._inv_deg.to(device),
+            row_map=None if self.row_map is None else self.row_map.to(device),
         )
 
     def to(self, device) -> "CSR":

@@ -42,15 +42,21 @@ def spmm(
     heads: int = 1,
     beta: float = 0.0,
     split=None,
+    row_map: Optional[torch.Tensor] = None,
 ) -> torch.Tensor:
     """CSR aggregation ``out[r] = row_scale[r]*sum_j w_j*col_scale[c_j]*x[c_j] + beta*out[r]``.
 
     ``split``: a :class:`~dgraph_amd.ops.csr.HubSplit` of this CSR (one head only): hub
     rows sum their first ``split.cap`` entries in the main pass and their tails in
     independent segment waves, added back in a fixed order (same result; no wave is held
-    by a 10^5-degree row)."""
+    by a 10^5-degree row).
+
+    ``row_map``: CSR row r is output row ``row_map[r]`` (a row-compacted CSR,
+    :meth:`~dgraph_amd.ops.csr.CSR.compact_rows`); ``out`` must then be given."""
     R = rowptr.numel() - 1
     F = x.shape[1]
+    if row_map is not None and out is None:
+        raise ValueError("spmm: row_map needs an explicit out")
     if out is None:
         out = torch.empty(R, F, dtype=x.dtype, device=x.device)
         beta = 0.0
@@ -61,13 +67,21 @@ def spmm(
     ew, cs, rs = _f32(edge_weight), _f32(col_scale), _f32(row_scale)
     if _native_ok(x):
         ops = _native.ops()
-        ops.spmm(rowptr, col, ew, cs, rs, x, out, heads, F // heads, float(beta), cap)
+        ops.spmm(rowptr, col, ew, cs, rs, x, out, heads, F // heads, float(beta), cap,
+                 row_map)
         if split is not None:
             part = torch.empty(split.num_segments, F, dtype=torch.float32, device=x.device)
             ops.spmm_hub_partials(split.seg_beg, split.seg_end, col, ew, cs, x, part)
             ops.spmm_hub_reduce(part, split.hub_seg_ptr, split.hub_rows, rs, out)
         return out
-    _ref.spmm(rowptr, col, x, out, edge_weight, col_scale, row_scale, heads, beta, cap)
+    if row_map is not None:
+        rs_c = None if row_scale is None else row_scale[row_map]
+        tmp = out[row_map] if beta != 0.0 else torch.empty(R, F, dtype=out.dtype,
+                                                            device=out.device)
+        _ref.spmm(rowptr, col, x, tmp, edge_weight, col_scale, rs_c, heads, beta, cap)
+        out[row_map] = tmp
+    else:
+        _ref.spmm(rowptr, col, x, out, edge_weight, col_scale, row_scale, heads, beta, cap)
     if split is not None:
         part = torch.empty(split.num_segments, F, dtype=torch.float32, device=x.device)
         _ref.spmm_hub_partials(split.seg_beg, split.seg_end, col, x, part, edge_weight,

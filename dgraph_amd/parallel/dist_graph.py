@@ -154,8 +154,9 @@ class DistGraph:
             recv = self._static_halo(x)
             out = K.spmm(self.interior.rowptr, self.interior.col, x, out, row_scale=rs,
                          split=_hs(self.interior))
-            K.spmm(self.halo.rowptr, self.halo.col, recv, out, row_scale=rs, beta=1.0,
-                   split=_hs(self.halo))
+            hc = self.halo.compact_rows()
+            K.spmm(hc.rowptr, hc.col, recv, out, row_scale=rs, beta=1.0, split=_hs(hc),
+                   row_map=hc.row_map)
             return out
         if out is None:
             out = torch.empty(self.L, x.shape[1], dtype=x.dtype, device=x.device)
@@ -169,11 +170,12 @@ class DistGraph:
             pend.append((c0, c1, recv, work))
         K.spmm(self.interior.rowptr, self.interior.col, x, out, row_scale=rs,
                split=_hs(self.interior))
+        hc = self.halo.compact_rows()
         for c0, c1, recv, work in pend:
             work.wait()
             oc = out if (c0, c1) == (0, x.shape[1]) else out[:, c0:c1]
-            K.spmm(self.halo.rowptr, self.halo.col, recv, oc, row_scale=rs, beta=1.0,
-                   split=_hs(self.halo))
+            K.spmm(hc.rowptr, hc.col, recv, oc, row_scale=rs, beta=1.0, split=_hs(hc),
+                   row_map=hc.row_map)
         return out
 
     def _col_chunks(self, a2a, F: int, esize: int):
@@ -250,11 +252,11 @@ class DistGraph:
             out = K.spmm(it.rowptr, it.col, g, out, col_scale=cs, split=_hs(it))
         if overlap is not None:
             overlap()  # independent work queued behind the exchange (e.g. a weight grad)
-        st = self.send_map.transpose_csr()
+        st = self.send_map.transpose_csr().compact_rows()
         for c0, c1, sg, work in pend:
             work.wait()
             oc = out if (c0, c1) == (0, F) else out[:, c0:c1]
-            K.spmm(st.rowptr, st.col, sg, oc, beta=1.0, split=_hs(st))
+            K.spmm(st.rowptr, st.col, sg, oc, beta=1.0, split=_hs(st), row_map=st.row_map)
         return out
 
     def _peers(self) -> bool:
@@ -379,7 +381,8 @@ class DistGraph:
         if not self.interior.symmetric:
             csrs.append(self.interior.transpose())
         if self.halo is not None:
-            csrs += [self.halo, self.halo.transpose(), self.send_map.transpose_csr()]
+            csrs += [self.halo.compact_rows(), self.halo.transpose(),
+                     self.send_map.transpose_csr().compact_rows()]
         for c in csrs:
             _hs(c)
         return self

@@ -12,6 +12,8 @@ def _powerlaw_csr(n=3000, nnz=60000, seed=0, device="cpu"):
     g = torch.Generator().manual_seed(seed)
     u = torch.rand(nnz, generator=g)
     rows = (u ** 3 * n).long().clamp(max=n - 1)  # heavy skew: row 0 gets ~n^(1/3) share
+    rows = rows[rows % 7 != 3]  # and some empty rows (row compaction)
+    nnz = rows.numel()
     cols = torch.randint(0, n, (nnz,), generator=g)
     return CSR.from_coo(rows, cols, n, n).to(device)
 
@@ -52,7 +54,7 @@ def test_split_metadata_covers_every_entry_once():
     assert csr.hub_split(10 ** 9) is None
 
 
-def _check(device, dtype, cap, weighted, beta, F):
+def _check(device, dtype, cap, weighted, beta, F, compact=False):
     csr = _powerlaw_csr(device=device)
     g = torch.Generator().manual_seed(cap + F)
     x = torch.randn(csr.num_cols, F, generator=g).to(device=device, dtype=dtype)
@@ -60,11 +62,20 @@ def _check(device, dtype, cap, weighted, beta, F):
     cs = (torch.rand(csr.num_cols, generator=g) + 0.5).to(device) if weighted else None
     rs = csr.inv_degree()
     out0 = torch.randn(csr.num_rows, F, generator=g).to(device=device, dtype=dtype)
-    sp = csr.hub_split(cap)
     out = out0.clone()
-    K.spmm(csr.rowptr, csr.col, x, out, edge_weight=ew, col_scale=cs, row_scale=rs,
-           beta=beta, split=sp)
+    if compact:
+        # row-compacted CSR (empty rows skipped): the empty rows keep beta * out0
+        cc = csr.compact_rows()
+        assert cc.num_rows < csr.num_rows and cc.col is csr.col
+        K.spmm(cc.rowptr, cc.col, x, out, edge_weight=ew, col_scale=cs, row_scale=rs,
+               beta=beta, split=cc.hub_split(cap), row_map=cc.row_map)
+    else:
+        K.spmm(csr.rowptr, csr.col, x, out, edge_weight=ew, col_scale=cs, row_scale=rs,
+               beta=beta, split=csr.hub_split(cap))
     ref = _dense_ref(csr, x, ew, cs, rs, beta, out0)
+    if compact and beta == 0.0:
+        empty = (csr.degree() == 0).cpu()
+        ref[empty] = out0.double().cpu()[empty]
     tol = 1e-5 if dtype == torch.float32 else 2e-2
     torch.testing.assert_close(out.double().cpu(), ref, atol=tol, rtol=tol)
 
@@ -72,8 +83,9 @@ def _check(device, dtype, cap, weighted, beta, F):
 @pytest.mark.parametrize("cap", [16, 64, 1000])
 @pytest.mark.parametrize("weighted", [False, True])
 @pytest.mark.parametrize("beta", [0.0, 1.0])
-def test_split_spmm_cpu(cap, weighted, beta):
-    _check("cpu", torch.float32, cap, weighted, beta, 24)
+@pytest.mark.parametrize("compact", [False, True])
+def test_split_spmm_cpu(cap, weighted, beta, compact):
+    _check("cpu", torch.float32, cap, weighted, beta, 24, compact)
 
 
 @pytest.mark.gpu
@@ -82,5 +94,6 @@ def test_split_spmm_cpu(cap, weighted, beta):
 @pytest.mark.parametrize("beta", [0.0, 1.0])
 @pytest.mark.parametrize("dtype,F", [(torch.bfloat16, 128), (torch.bfloat16, 256),
                                      (torch.bfloat16, 40), (torch.float32, 64)])
-def test_split_spmm_gpu(cap, weighted, beta, dtype, F):
-    _check("cuda", dtype, cap, weighted, beta, F)
+@pytest.mark.parametrize("compact", [False, True])
+def test_split_spmm_gpu(cap, weighted, beta, dtype, F, compact):
+    _check("cuda", dtype, cap, weighted, beta, F, compact)
