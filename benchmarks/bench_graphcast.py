@@ -73,15 +73,26 @@ def main():
         x, y = (t.to(dev, dt) for t in ds[0])
         model = DGraphCast(cfg, comm).to(dev, dt)
         gs = GradSync(model.parameters())
-        opt = torch.optim.Adam(model.parameters(), lr=1e-4, fused=True)
+        if dt == torch.float32:
+            opt = torch.optim.Adam(model.parameters(), lr=1e-4, fused=True)
+            masters = None
+        else:
+            # bf16 compute, fp32 master weights + Adam state (the trainer's scheme)
+            from dgraph_amd.utils.master_weights import MasterWeights
+
+            masters = MasterWeights(model, lambda ps: torch.optim.Adam(ps, lr=1e-4, fused=True))
+            opt = masters.optimizer
 
         def step():
-            opt.zero_grad(set_to_none=True)
+            model.zero_grad(set_to_none=True)
             out = model(x, pg)
             loss = ((out.float() - y.float()) ** 2).mean()
             loss.backward()
             gs.all_reduce()
-            opt.step()
+            if masters is not None:
+                masters.step()
+            else:
+                opt.step()
             return loss
 
         for _ in range(a.warmup):
@@ -94,6 +105,8 @@ def main():
         ms = (time.perf_counter() - t) * 1e3 / a.steps
         edges = a.layers * g.m2m[0].size + g.g2m[0].size + g.m2g[0].size
         result = {"metric": "graphcast_step_ms", "ms_per_step": ms,
+                  "precision": "bf16 compute, fp32 master weights" if masters is not None
+                  else "fp32",
                   "edge_updates_per_s": edges / (ms / 1e3), "loss": float(loss),
                   "peak_mem_gb": torch.cuda.max_memory_allocated() / 1e9}
     else:

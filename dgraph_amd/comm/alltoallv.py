@@ -16,8 +16,15 @@ from typing import List, Optional, Sequence
 import torch
 import torch.distributed as dist
 
-# "torch": ProcessGroupNCCL (RCCL through torch.distributed); "native": the C++ RCCL
-# plan executor (comm/rccl_exec.py). Both are RCCL over xGMI; GPU tensors only.
+# Transport of the halo all-to-all-v. Default "torch": ProcessGroupNCCL, i.e. RCCL through
+# torch.distributed on a high-priority stream (comm/groups.py). Decision (round 2): both
+# paths issue the same RCCL grouped send/recv kernels over the same xGMI links, so the
+# data movement is identical; the PG path additionally carries the NCCL watchdog /
+# timeout / async error handling that failure detection (§5.3) relies on, costs no
+# second communicator (RCCL buffers per peer and channel), and is the one exercised by
+# the W = 2..8 equivalence tests. "native" (comm/rccl_exec.py: a private communicator,
+# several tensors per group call, completion as a HIP event) stays selectable with
+# DGRAPH_A2A_IMPL=native for A/B runs on a multi-GPU node (benchmarks/bench_comm.py).
 A2A_IMPL = os.environ.get("DGRAPH_A2A_IMPL", "torch")
 
 
@@ -43,10 +50,12 @@ class CommStats:
     calls = 0
     bytes_sent = 0
     bytes_recv = 0
+    peer_bytes_sent: dict = {}  # group-local peer rank -> bytes sent to it
 
     @classmethod
     def reset(cls):
         cls.calls = cls.bytes_sent = cls.bytes_recv = 0
+        cls.peer_bytes_sent = {}
 
 
 class AllToAllV:
@@ -76,6 +85,10 @@ class AllToAllV:
         CommStats.calls += 1
         CommStats.bytes_sent += self.total_send * row_bytes
         CommStats.bytes_recv += self.total_recv * row_bytes
+        pb = CommStats.peer_bytes_sent
+        for p, n in enumerate(self.send_splits):
+            if n:
+                pb[p] = pb.get(p, 0) + n * row_bytes
         from .faults import FaultInjector
 
         if FaultInjector.active():

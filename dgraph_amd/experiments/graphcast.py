@@ -30,8 +30,10 @@ from ..data.graphcast_graph import build_global_graph, partition_graphcast_graph
 from ..data.weather import SyntheticWeatherDataset
 from ..models.graphcast import Config, DGraphCast
 from ..parallel.grad_sync import GradSync
+from ..utils.master_weights import MasterWeights
 from ..utils.metrics import print_on_rank_zero
 from ..utils.timing import TimingReport
+from ..utils.trainer import RunSupport, add_run_args, build_config
 
 
 def make_scheduler(optimizer, tc):
@@ -55,7 +57,7 @@ def _device() -> torch.device:
 
 class GraphCastTrainer:
     def __init__(self, comm, cfg: Optional[Config] = None, dtype: torch.dtype = torch.float32,
-                 checkpoint_dir: Optional[str] = None, global_graph=None):
+                 checkpoint_dir: Optional[str] = None, global_graph=None, support=None):
         self.comm = comm
         self.cfg = cfg or Config()
         self.device = _device()
@@ -74,8 +76,16 @@ class GraphCastTrainer:
         torch.manual_seed(0)
         self.model = DGraphCast(self.cfg, comm).to(self.device, dtype)
         self.sync = GradSync(self.model.parameters())
-        self.optimizer = torch.optim.Adam(self.model.parameters(), lr=self.cfg.training.lr)
+        lr = self.cfg.training.lr
+        self.masters = None
+        if dtype != torch.float32:
+            # bf16 compute, fp32 master weights + optimizer state (utils/master_weights.py)
+            self.masters = MasterWeights(self.model, lambda ps: torch.optim.Adam(ps, lr=lr))
+            self.optimizer = self.masters.optimizer
+        else:
+            self.optimizer = torch.optim.Adam(self.model.parameters(), lr=lr)
         self.scheduler = make_scheduler(self.optimizer, self.cfg.training)
+        self.support = support
         n = torch.tensor([float(self.graph.num_local_grid * self.cfg.model.output_grid_dim)],
                          device=self.device)
         if self.psize > 1:
@@ -102,7 +112,10 @@ class GraphCastTrainer:
                 if p.grad is not None:
                     p.grad.div_(self.num_replicas)
         torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.cfg.training.grad_clip_norm)
-        self.optimizer.step()
+        if self.masters is not None:
+            self.masters.step()
+        else:
+            self.optimizer.step()
         self.scheduler.step()
         self.iter += 1
         lv = loss.detach()
@@ -110,10 +123,18 @@ class GraphCastTrainer:
             dist.all_reduce(lv, group=self.comm.group)
         return float(lv)
 
+    def _ckpt_model(self):
+        return self.masters if self.masters is not None else self.model
+
     def train(self, iters: int) -> float:
         last = float("nan")
-        for _ in range(iters):
+        sup = self.support
+        if sup is not None:
+            self.iter = sup.resume(self._ckpt_model(), self.optimizer, self.scheduler)
+        while self.iter < iters:
             x, y = self.sample(self.iter)
+            if sup is not None:
+                sup.begin_epoch()
             t0 = time.perf_counter()
             last = self.step(x, y)
             if self.device.type == "cuda":
@@ -121,18 +142,29 @@ class GraphCastTrainer:
             ms = (time.perf_counter() - t0) * 1e3
             self.history.append({"iter": self.iter, "loss": last, "ms": ms})
             print_on_rank_zero(f"iter {self.iter:5d} | loss {last:.5f} | {ms:.1f} ms")
+            if sup is not None:  # one metrics record / checkpoint slot per iteration
+                sup.end_epoch(self.iter - 1, self._ckpt_model(), self.optimizer,
+                              self.scheduler, epoch_ms=ms, loss=last)
             if (self.checkpoint_dir and self.iter % self.cfg.training.save_freq == 0
                     and self.comm.get_rank() == 0):
                 os.makedirs(self.checkpoint_dir, exist_ok=True)
                 torch.save(self.model.state_dict(),
                            os.path.join(self.checkpoint_dir, f"model_{self.iter}.pth"))
+        if sup is not None:
+            sup.finish(self.iter - 1, self._ckpt_model(), self.optimizer, self.scheduler)
         return last
 
 
 def main(backend: str = "nccl", procs_per_graph: int = -1, iters: int = 10,
          mesh_level: int = 6, grid: str = "721x1440", hidden_dim: int = 128,
          processor_layers: int = 4, channels: int = 73, dtype: str = "fp32",
-         checkpoint_dir: Optional[str] = None, test_run: bool = False):
+         checkpoint_dir: Optional[str] = None, test_run: bool = False, run_args=None,
+         log_dir: str = "logs"):
+    rcfg = build_config(getattr(run_args, "config", ()), comm__backend=backend,
+                        comm__ranks_per_graph=procs_per_graph, model__name="graphcast",
+                        model__hidden=hidden_dim, model__num_layers=processor_layers,
+                        model__dtype=dtype, train__epochs=iters, train__log_dir=log_dir,
+                        data__dataset=f"graphcast-{grid}-level{mesh_level}")
     cfg = Config()
     cfg.model.mesh_level = mesh_level
     cfg.model.hidden_dim = hidden_dim
@@ -143,8 +175,12 @@ def main(backend: str = "nccl", procs_per_graph: int = -1, iters: int = 10,
     comm = Communicator.init_process_group(backend, ranks_per_graph=procs_per_graph)
     if not TimingReport._is_initialized:
         TimingReport.init(comm)
+    support = None
+    if run_args is not None:
+        support = RunSupport(run_args, rcfg, rcfg.data.dataset, comm.get_world_size(),
+                             log_dir, _device())
     tr = GraphCastTrainer(comm, cfg, torch.bfloat16 if dtype == "bf16" else torch.float32,
-                          checkpoint_dir)
+                          checkpoint_dir, support=support)
     last = tr.train(1 if test_run else iters)
     return tr, last
 
@@ -160,9 +196,13 @@ def cli(argv=None):
     p.add_argument("--processor_layers", type=int, default=4)
     p.add_argument("--channels", type=int, default=73)
     p.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
-    p.add_argument("--checkpoint_dir", default=None)
     p.add_argument("--test_run", action="store_true")
-    main(**vars(p.parse_args(argv)))
+    p.add_argument("--log_dir", default="logs")
+    add_run_args(p)  # --checkpoint_dir: model_{iter}.pth (reference layout) + resumable state
+    a = p.parse_args(argv)
+    run_keys = ("config", "resume", "checkpoint_every", "metrics_jsonl", "checkpoint_dir")
+    kw = {k: v for k, v in vars(a).items() if k not in run_keys}
+    main(**kw, checkpoint_dir=a.checkpoint_dir or None, run_args=a)
     Communicator.instance().destroy()
 
 

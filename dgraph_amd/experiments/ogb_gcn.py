@@ -33,6 +33,7 @@ from ..parallel.halo import HaloExchange
 from ..utils.metrics import (calculate_accuracy, dist_print_ephemeral, make_experiment_log,
                              write_experiment_log)
 from ..utils.timing import TimingReport, region
+from ..utils.trainer import RunSupport, add_run_args, build_config
 
 NUM_CLASSES = {"arxiv": 40, "products": 47, "papers100M": 172, "proteins": 112}
 
@@ -74,7 +75,7 @@ def visualize_trajectories(traj: np.ndarray, title: str, path: str, rank: int = 
 
 def run_experiment(dataset: DGraphOGBDataset, comm, lr: float, epochs: int, log_prefix: str,
                    hidden_dims: int = 256, num_classes: int = 40, device=None,
-                   dtype: str = "fp32", seed: int = 0):
+                   dtype: str = "fp32", seed: int = 0, support: Optional[RunSupport] = None):
     device = device or _device()
     rank = comm.get_rank()
     x, y, cp = dataset[0]
@@ -99,10 +100,22 @@ def run_experiment(dataset: DGraphOGBDataset, comm, lr: float, epochs: int, log_
     n_train = torch.tensor([float(masks["train_mask"].sum())], device=device)
     if world > 1:
         torch.distributed.all_reduce(n_train, group=comm.group)
-    for epoch in range(epochs):
+    # message edges per epoch (2 propagation layers over every rank's local edge list)
+    le = getattr(cp, "local_edge_list", None)
+    n_edges = torch.tensor([float(le.shape[0]) if le is not None else 0.0], device=device)
+    if world > 1:
+        torch.distributed.all_reduce(n_edges, group=comm.group)
+    edges_per_epoch = 2 * int(n_edges.item())
+    start = support.resume(model, opt) if support is not None else 0
+    epoch = start - 1
+    nan = float("nan")  # resumed runs: the epochs before the checkpoint are not re-logged
+    tl, vl, va = [nan] * start, [nan] * start, [nan] * start
+    for epoch in range(start, epochs):
         model.train()
         comm.barrier()
         _sync(device)
+        if support is not None:
+            support.begin_epoch()
         t0 = time.perf_counter()
         opt.zero_grad(set_to_none=True)
         with region("forward"):
@@ -134,6 +147,11 @@ def run_experiment(dataset: DGraphOGBDataset, comm, lr: float, epochs: int, log_
         write_experiment_log(str(float(vloss)), f"{log_prefix}_validation_loss.log", rank)
         write_experiment_log(f"Validation Accuracy: {vacc:.2f}",
                              f"{log_prefix}_validation_accuracy.log", rank)
+        if support is not None:
+            support.end_epoch(epoch, model, opt, epoch_ms=ms, edges=edges_per_epoch,
+                              loss=float(lt), val_loss=float(vloss), val_acc=vacc)
+    if support is not None:
+        support.finish(epoch, model, opt)
     model.eval()
     with torch.no_grad():
         out = fwd()
@@ -148,7 +166,7 @@ def run_experiment(dataset: DGraphOGBDataset, comm, lr: float, epochs: int, log_
     make_experiment_log(f"{log_prefix}_training_times.log", rank)
     for t in times:
         write_experiment_log(str(t), f"{log_prefix}_training_times.log", rank)
-    avg = float(np.mean(times[1:])) if len(times) > 1 else float(times[0])
+    avg = float(np.mean(times[1:])) if len(times) > 1 else float(times[0]) if times else 0.0
     make_experiment_log(f"{log_prefix}_runtime_experiment.log", rank)
     write_experiment_log(f"Average time per epoch (excl. first): {avg:.4f} ms",
                          f"{log_prefix}_runtime_experiment.log", rank)
@@ -160,10 +178,14 @@ def run_experiment(dataset: DGraphOGBDataset, comm, lr: float, epochs: int, log_
 def main(backend: str = "nccl", dataset: str = "arxiv", epochs: int = 10, lr: float = 1e-3,
          runs: int = 1, hidden_dims: int = 256, log_dir: str = "logs",
          node_rank_placement_file: Optional[str] = None, root_dir: Optional[str] = None,
-         dtype: str = "fp32", synthetic_scale: float = 1.0):
+         dtype: str = "fp32", synthetic_scale: float = 1.0, run_args=None):
     if dataset not in NUM_CLASSES:
         raise ValueError(f"Unsupported dataset '{dataset}'. Choose from {list(NUM_CLASSES)}")
-    comm = Communicator.init_process_group(backend.lower())
+    cfg = build_config(getattr(run_args, "config", ()), comm__backend=backend,
+                       model__name="gcn", model__hidden=hidden_dims, model__dtype=dtype,
+                       train__epochs=epochs, train__lr=lr, train__log_dir=log_dir,
+                       data__dataset=dataset, data__scale=synthetic_scale)
+    comm = Communicator.init_process_group(cfg.comm.backend.lower())
     rank, world = comm.get_rank(), comm.get_world_size()
     device = _device()
     if not TimingReport._is_initialized:
@@ -178,11 +200,14 @@ def main(backend: str = "nccl", dataset: str = "arxiv", epochs: int = 10, lr: fl
     tr = np.zeros((runs, epochs))
     vl = np.zeros((runs, epochs))
     va = np.zeros((runs, epochs))
+    support = None
+    if run_args is not None:
+        support = RunSupport(run_args, cfg, dataset, world, log_dir, device)
     for run in range(runs):
         prefix = f"{log_dir}/{dataset}_world{world}_run{run}"
         tr[run], vl[run], va[run] = run_experiment(
             ds, comm, lr, epochs, prefix, hidden_dims, NUM_CLASSES[dataset], device, dtype,
-            seed=run)
+            seed=run, support=support if run == 0 else None)
     TimingReport.resolve()
     if rank == 0:
         TimingReport.dump(f"{log_dir}/{dataset}_timing_report_world{world}.json")
@@ -206,8 +231,11 @@ def cli(argv=None):
     p.add_argument("--root_dir", default=None)
     p.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
     p.add_argument("--synthetic_scale", type=float, default=1.0)
+    add_run_args(p)
     a = p.parse_args(argv)
-    main(**vars(a))
+    run_keys = ("config", "resume", "checkpoint_dir", "checkpoint_every", "metrics_jsonl")
+    kw = {k: v for k, v in vars(a).items() if k not in run_keys}
+    main(**kw, run_args=a)
     Communicator.instance().destroy()
 
 

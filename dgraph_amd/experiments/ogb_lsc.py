@@ -29,6 +29,7 @@ from ..models.rgat import CommAwareRGAT
 from ..models.rgcn import CommAwareRGCN
 from ..parallel.grad_sync import GradSync
 from ..utils.metrics import print_on_rank_zero
+from ..utils.trainer import RunSupport, add_run_args, build_config
 
 
 @dataclass
@@ -68,7 +69,8 @@ def _device() -> torch.device:
 
 class Trainer:
     def __init__(self, dataset, comm, model_config: ModelConfig = None,
-                 training_config: TrainingConfig = None, device=None, seed: int = 0):
+                 training_config: TrainingConfig = None, device=None, seed: int = 0,
+                 support=None):
         self.dataset = dataset
         self.comm = comm
         self.model_config = model_config or ModelConfig()
@@ -95,6 +97,7 @@ class Trainer:
         self.scheduler = torch.optim.lr_scheduler.StepLR(self.optimizer, tc.lr_step_size,
                                                          tc.lr_gamma)
         self.history = []
+        self.support = support  # utils.trainer.RunSupport: resume / metrics / checkpoints
 
     def prepare_data(self):
         self.dataset = self.dataset.to(self.device)
@@ -110,7 +113,12 @@ class Trainer:
         target = self.dataset.get_target("train").to(self.device)
         n_glob = GetGlobalVal(target.numel(), self.comm.group, self.device)
         loss_val = 0.0
-        for epoch in range(1, (epochs or self.training_config.epochs) + 1):
+        sup = self.support
+        start = sup.resume(self.model, self.optimizer, self.scheduler) if sup else 0
+        last = start - 1
+        for epoch in range(start + 1, (epochs or self.training_config.epochs) + 1):
+            if sup:
+                sup.begin_epoch()
             t0 = time.perf_counter()
             self.optimizer.zero_grad(set_to_none=True)
             out = self._forward()
@@ -123,6 +131,12 @@ class Trainer:
             ms = (time.perf_counter() - t0) * 1e3
             self.history.append({"epoch": epoch, "loss": loss_val, "ms": ms})
             print_on_rank_zero(f"Epoch {epoch:03d} | loss {loss_val:.4f} | {ms:.1f} ms")
+            last = epoch - 1
+            if sup:  # 0-based epochs in the metrics stream and checkpoints
+                sup.end_epoch(last, self.model, self.optimizer, self.scheduler, epoch_ms=ms,
+                              loss=loss_val, lr=self.scheduler.get_last_lr()[0])
+        if sup:
+            sup.finish(last, self.model, self.optimizer, self.scheduler)
         return loss_val
 
     @torch.no_grad()
@@ -144,11 +158,17 @@ def main(comm_type: str = "nccl", dataset: str = "synthetic", num_papers: int = 
          num_authors: int = 512, num_institutions: int = 16, num_features: int = 16,
          num_classes: int = 153, epochs: int = 100, hidden_channels: int = 2,
          num_layers: int = 2, heads: int = 1, dropout: float = 0.5, lr: float = 1e-4,
-         data_dir: str = "data/MAG240M", cache_dir: str = None, model: str = "rgat"):
+         data_dir: str = "data/MAG240M", cache_dir: str = None, model: str = "rgat",
+         run_args=None, log_dir: str = "logs"):
     if dataset not in ("synthetic", "mag240m"):
         raise ValueError(f"Invalid dataset: {dataset}")
     if comm_type not in ("nccl", "nvshmem", "rocshmem", "gloo", "mpi"):
         raise ValueError(f"Invalid comm_type: {comm_type}")
+    rcfg = build_config(getattr(run_args, "config", ()), comm__backend=comm_type,
+                        model__name=model, model__hidden=hidden_channels,
+                        model__num_layers=num_layers, model__dropout=dropout,
+                        train__epochs=epochs, train__lr=lr, train__log_dir=log_dir,
+                        data__dataset=dataset)
     comm = Communicator.init_process_group(comm_type)
     if dataset == "synthetic":
         cfg = SyntheticDatasetConfig(num_papers=num_papers, num_authors=num_authors,
@@ -157,10 +177,14 @@ def main(comm_type: str = "nccl", dataset: str = "synthetic", num_papers: int = 
         ds = SyntheticHeterogeneousDataset(cfg, comm, cache_dir=cache_dir)
     else:
         ds = DGraph_MAG240M_Dataset(comm, data_dir=data_dir)
+    support = None
+    if run_args is not None:
+        support = RunSupport(run_args, rcfg, f"ogblsc-{dataset}-{model}",
+                             comm.get_world_size(), log_dir, _device())
     trainer = Trainer(ds, comm, ModelConfig(hidden_channels=hidden_channels,
                                             num_layers=num_layers, heads=heads,
                                             dropout=dropout, model=model),
-                      TrainingConfig(epochs=epochs, lr=lr))
+                      TrainingConfig(epochs=epochs, lr=lr), support=support)
     trainer.prepare_data()
     final = trainer.train()
     accs = trainer.evaluate()
@@ -178,9 +202,13 @@ def cli(argv=None):
                                ("hidden_channels", int, 2), ("num_layers", int, 2),
                                ("heads", int, 1), ("dropout", float, 0.5),
                                ("lr", float, 1e-4), ("data_dir", str, "data/MAG240M"),
-                               ("cache_dir", str, None), ("model", str, "rgat")]:
+                               ("cache_dir", str, None), ("model", str, "rgat"),
+                               ("log_dir", str, "logs")]:
         p.add_argument(f"--{name}", type=typ, default=default)
-    main(**vars(p.parse_args(argv)))
+    add_run_args(p)
+    a = p.parse_args(argv)
+    run_keys = ("config", "resume", "checkpoint_dir", "checkpoint_every", "metrics_jsonl")
+    main(**{k: v for k, v in vars(a).items() if k not in run_keys}, run_args=a)
     Communicator.instance().destroy()
 
 

@@ -29,6 +29,9 @@ class KernelConfig:
     spmm_variant: int = 4
     spmm_row_map: int = 0  # 0 grid-stride / in-order, 1-2 XCD-chunked, 3 in-order (v2)
     spmm_pass_cols: int = 128
+    spmm_hub_cap: int = 2048        # hub-row split degree (0: off)
+    dual_gemm_variant: int = 2      # 1 column-half (B^T in LDS), 2 B-stationary
+    halo_chunk_bytes: int = 32 << 20  # per-peer message size that triggers chunking
     deterministic: bool = True      # segment sums only, no float atomics
 
 
@@ -87,10 +90,15 @@ class RunConfig:
         """Push the kernel settings into the native library."""
         from .. import _native
 
+        from ..parallel import dist_graph
+
         if _native.available():
             _native.ops().set_spmm_config(self.kernels.spmm_variant,
                                           self.kernels.spmm_row_map,
                                           self.kernels.spmm_pass_cols)
+            _native.ops().set_dual_gemm_variant(self.kernels.dual_gemm_variant)
+        dist_graph.SPMM_HUB_CAP = int(self.kernels.spmm_hub_cap)
+        os.environ["DGRAPH_HALO_CHUNK_BYTES"] = str(int(self.kernels.halo_chunk_bytes))
         os.environ["DGRAPH_SHMEM_TRANSPORT"] = self.comm.shmem_transport
         return self
 
