@@ -30,13 +30,23 @@ _PARTIALS: dict = {}
 def _partials(dev: torch.device, n: int) -> torch.Tensor:
     """Resident fp32 workspace for the split-K partial products, grown on demand and kept:
     allocating ~2 GB per call next to a 269 GB working set made the caching allocator
-    free and re-map blocks (184 ms of host time per wgrad, profiles/)."""
-    buf = _PARTIALS.get(dev)
+    free and re-map blocks (184 ms of host time per wgrad, profiles/). Keyed by (device,
+    current stream): a wgrad issued on a side stream gets its own buffer, so two streams
+    never race on one workspace. :func:`release_workspace` frees them."""
+    key = (dev, torch.cuda.current_stream(dev).cuda_stream if dev.type == "cuda" else 0)
+    buf = _PARTIALS.get(key)
     if buf is None or buf.numel() < n:
-        _PARTIALS.pop(dev, None)
+        # drop the old buffer BEFORE allocating the larger one (peak = new, not old + new)
+        buf = None
+        _PARTIALS.pop(key, None)
         buf = torch.empty(n, dtype=torch.float32, device=dev)
-        _PARTIALS[dev] = buf
+        _PARTIALS[key] = buf
     return buf[:n]
+
+
+def release_workspace() -> None:
+    """Free the resident split-K workspaces (e.g. before a memory-hungry phase)."""
+    _PARTIALS.clear()
 
 
 def _bmm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:

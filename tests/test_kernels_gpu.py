@@ -605,3 +605,24 @@ def test_row_scale_cols(dtype, F, c0, w):
     K.row_scale_cols(g[:, c0:c0 + w], s, out)
     ref = (g[:, c0:c0 + w].float() * s.unsqueeze(1)).to(dtype)
     torch.testing.assert_close(out.float(), ref.float(), atol=0, rtol=0)
+
+
+@pytest.mark.parametrize("L", [(1 << 23) - 777, (1 << 23) + 12345, 300_001])
+@pytest.mark.parametrize("K,N", [(256, 128), (128, 256), (64, 64)])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_wgrad_matches_fp32_reference(L, K, N, dtype):
+    """Split-K batched weight gradient (dense.wgrad) vs ``x.float().t() @ g.float()``:
+    just below / above the 2^23-row chunking switch of the linear layers, a remainder
+    tail (L not a multiple of the chunk), the swapped K < N order, bf16 and fp32."""
+    from dgraph_amd.ops.dense import _auto_rows_per_chunk, release_workspace, wgrad
+
+    gen = torch.Generator(device="cuda").manual_seed(L + K)
+    x = torch.randn(L, K, device="cuda", generator=gen).to(dtype)
+    g = torch.randn(L, N, device="cuda", generator=gen).to(dtype)
+    ref = x.double().t() @ g.double()
+    for rpc in (0, _auto_rows_per_chunk(L)):
+        out = wgrad(x, g, rpc)
+        assert out.dtype == torch.float32 and out.shape == (K, N)
+        # sums over L ~ 1e7 products: compare on the scale of sqrt(L)
+        torch.testing.assert_close(out.double(), ref, atol=2e-3 * L ** 0.5, rtol=1e-3)
+    release_workspace()
