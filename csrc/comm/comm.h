@@ -17,4 +17,12 @@ hipError_t heap_put_rows(DType dt, const uint64_t* peer_base, int64_t dst_off,
                          const int64_t* row_peer, const int64_t* row_dst, const void* src,
                          int64_t ld_src, int64_t ld_dst, int64_t n, int F, hipStream_t st);
 
+// stream-ordered completion flags (see symheap.hip): signal stores `epoch` into
+// flags[me] of every peer's heap at flag_off (system-scope release); wait spins on the
+// local flags[q] for every peer q until >= epoch (bounded; *timed_out = 1 on give-up)
+hipError_t heap_signal(const uint64_t* peer_base, int64_t flag_off, int me, int world,
+                       uint64_t epoch, bool self_too, hipStream_t st);
+hipError_t heap_wait(const uint64_t* flags, int me, int world, uint64_t epoch,
+                     int64_t max_spins, bool self_too, int* timed_out, hipStream_t st);
+
 }  // namespace dgraph

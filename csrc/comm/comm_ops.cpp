@@ -127,6 +127,30 @@ void heap_put_rows_op(const at::Tensor& table, int64_t dst_off, const at::Tensor
                              static_cast<int>(src.size(1)), cur_stream(src)));
 }
 
+void heap_signal_op(const at::Tensor& table, int64_t flag_off, int64_t me, int64_t world,
+                    int64_t epoch, bool self_too) {
+  TORCH_CHECK(table.is_cuda() && table.scalar_type() == at::kLong && table.numel() == world,
+              "table must be the int64 GPU peer table of the group");
+  c10::DeviceGuard g(table.device());
+  DG_HIP_CHECK(heap_signal(reinterpret_cast<const uint64_t*>(table.data_ptr()), flag_off,
+                           static_cast<int>(me), static_cast<int>(world),
+                           static_cast<uint64_t>(epoch), self_too, cur_stream(table)));
+}
+
+void heap_wait_op(const at::Tensor& flags, int64_t me, int64_t world, int64_t epoch,
+                  int64_t max_spins, bool self_too, const at::Tensor& timed_out) {
+  TORCH_CHECK(flags.is_cuda() && flags.scalar_type() == at::kLong && flags.numel() >= world &&
+                  flags.is_contiguous(),
+              "flags must be a contiguous int64 GPU tensor of >= world words");
+  TORCH_CHECK(timed_out.is_cuda() && timed_out.scalar_type() == at::kInt,
+              "timed_out must be an int32 GPU tensor");
+  c10::DeviceGuard g(flags.device());
+  DG_HIP_CHECK(heap_wait(reinterpret_cast<const uint64_t*>(flags.data_ptr()),
+                         static_cast<int>(me), static_cast<int>(world),
+                         static_cast<uint64_t>(epoch), max_spins, self_too,
+                         timed_out.data_ptr<int>(), cur_stream(flags)));
+}
+
 // ------------------------------------------------------------------ RCCL executor
 struct CommEntry {
   ncclComm_t comm;
@@ -259,6 +283,12 @@ TORCH_LIBRARY_FRAGMENT(dgraph_amd, m) {
   m.def("heap_put_rows(Tensor table, int dst_off, Tensor row_peer, Tensor row_dst, Tensor src, "
         "int ld_dst) -> ()",
         &dgraph::heap_put_rows_op);
+  m.def("heap_signal(Tensor table, int flag_off, int me, int world, int epoch, "
+        "bool self_too) -> ()",
+        &dgraph::heap_signal_op);
+  m.def("heap_wait(Tensor flags, int me, int world, int epoch, int max_spins, bool self_too, "
+        "Tensor(a!) timed_out) -> ()",
+        &dgraph::heap_wait_op);
   m.def("rccl_unique_id() -> Tensor", &dgraph::rccl_unique_id);
   m.def("rccl_comm_init(Tensor uid, int world, int rank, int device) -> int",
         &dgraph::rccl_comm_init);

@@ -69,6 +69,43 @@ __global__ __launch_bounds__(256) void heap_put_rows_kernel(
   __threadfence_system();
 }
 
+// ---------------------------------------------------------------------------------------
+// Stream-ordered completion (the nvshmemx_quiet_on_stream / barrier_all_on_stream /
+// signal_wait_until counterpart). Each rank's heap starts with flag words
+// flags[kind][W] (uint64). A producer, after its put/copy kernels on the same stream,
+// runs heap_signal: lane p stores `epoch` into flags[kind][me] of peer p's heap with a
+// system-scope RELEASE (the data stores of the earlier kernels on this stream were
+// retired before this kernel started, and each put block ended with a system fence). A
+// consumer runs heap_wait: lane q spins on its OWN heap's flags[kind][q] with a
+// system-scope ACQUIRE until it reaches `epoch` (monotonic epochs: no reset races).
+// All flag traffic is vector memory (global atomics), never scalar. The spin is bounded:
+// after max_spins polls (with s_sleep) the lane gives up, sets *timed_out and exits, so
+// the grid always drains (the host raises on the flag).
+__global__ __launch_bounds__(64) void heap_signal_kernel(const uint64_t* __restrict__ peer_base,
+                                                         int64_t flag_off, int me, int world,
+                                                         uint64_t epoch, int self_too) {
+  const int p = threadIdx.x;
+  if (p >= world || (p == me && !self_too)) return;
+  uint64_t* f = reinterpret_cast<uint64_t*>(peer_base[p] + flag_off) + me;
+  __hip_atomic_store(f, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(64) void heap_wait_kernel(const uint64_t* __restrict__ flags,
+                                                       int me, int world, uint64_t epoch,
+                                                       int64_t max_spins, int self_too,
+                                                       int* __restrict__ timed_out) {
+  const int q = threadIdx.x;
+  if (q >= world || (q == me && !self_too)) return;
+  int64_t spins = 0;
+  while (__hip_atomic_load(flags + q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
+    if (++spins >= max_spins) {
+      __hip_atomic_store(timed_out, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
 inline int pick_lpr(int lanes) {
   return lanes <= 4 ? 4 : lanes <= 8 ? 8 : lanes <= 16 ? 16 : lanes <= 32 ? 32 : 64;
 }
@@ -122,6 +159,22 @@ hipError_t launch_put(const uint64_t* pb, int64_t off, const int64_t* rp, const 
 }
 
 }  // namespace
+
+hipError_t heap_signal(const uint64_t* peer_base, int64_t flag_off, int me, int world,
+                       uint64_t epoch, bool self_too, hipStream_t st) {
+  if (world <= 0 || world > 64) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(heap_signal_kernel, dim3(1), dim3(64), 0, st, peer_base, flag_off, me,
+                     world, epoch, self_too ? 1 : 0);
+  return hipGetLastError();
+}
+
+hipError_t heap_wait(const uint64_t* flags, int me, int world, uint64_t epoch,
+                     int64_t max_spins, bool self_too, int* timed_out, hipStream_t st) {
+  if (world <= 0 || world > 64) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(heap_wait_kernel, dim3(1), dim3(64), 0, st, flags, me, world, epoch,
+                     max_spins, self_too ? 1 : 0, timed_out);
+  return hipGetLastError();
+}
 
 hipError_t heap_get_rows(DType dt, const uint64_t* peer_base, int64_t base_off,
                          const int64_t* owner, const int64_t* row, void* out, int64_t ld_src,

@@ -6,7 +6,8 @@ rocSHMEM is not installed in this image, so the symmetric heap is the native HIP
 heap in ``csrc/comm/symheap.hip`` (:class:`dgraph_amd.comm.symheap.SymmetricHeap`):
 every rank maps every peer's heap over xGMI, remote rows are read with wave64 16-byte
 peer loads (the K15 remote get) and written with peer stores at ``remote_offsets`` (put),
-completion is a stream drain plus a group barrier. Sizes are agreed as the max over ranks
+one-sided scatter puts pre-summed rows into per-source slots of the owner's heap (summed
+there in a fixed order), and completion is stream-ordered (device-side signal / wait). Sizes are agreed as the max over ranks
 (fixing the reference's mismatched collective ``nvshmem_malloc`` sizes, D4).
 
 When the heap cannot be used (host tensors, a single process spanning several nodes, or
@@ -105,6 +106,12 @@ class ROCSHMEMBackendEngine(BackendEngine):
     def scatter(self, x, indices, rank_mappings, num_output_rows, *args, **kwargs):
         from ..parallel import index_ops
 
+        x3 = x if x.dim() == 3 else x.unsqueeze(0)
+        h = self.heap() if x3.is_cuda else None
+        if h is not None:
+            # one-sided: pre-summed rows put into the owners' slots, fixed-order add there
+            return h.scatter_add(x3[0], indices.reshape(-1), rank_mappings.reshape(-1),
+                                 int(num_output_rows)).unsqueeze(0)
         return index_ops.g1_scatter_local(x, indices, rank_mappings, num_output_rows,
                                           self.get_rank(), self.get_world_size(),
                                           self._g1_cache, self.group)

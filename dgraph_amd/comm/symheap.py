@@ -9,16 +9,28 @@ publishes its IPC handle, and maps every peer heap. Tensors carved from the heap
 collective bump allocator: all ranks allocate in the same order), so a peer's copy of a
 symmetric tensor is ``peer_base[p] + offset``. Native kernels (csrc/comm/symheap.hip) then
 
-* read remote rows directly over xGMI (:meth:`remote_gather`, the K15 ``dist_get``), and
-* write rows into peers' receive buffers at ``remote_offsets`` (:meth:`put_rows`).
+* read remote rows directly over xGMI (:meth:`remote_gather`, the K15 ``dist_get``),
+* write rows into peers' receive buffers at ``remote_offsets`` (:meth:`put_rows`), and
+* scatter-add rows into peers' symmetric outputs (:meth:`scatter_add`, the ``dist_put`` of
+  torch_nvshmem_p2p.cu:96-164) — deterministically: each rank pre-aggregates its rows per
+  (destination rank, row), puts the partial sums into a per-source slot of the owner's
+  heap, and the owner adds the slots with a fixed-order segment sum (no float atomics; the
+  reference's CAS loop made the sum order, and so the bits, run-dependent).
 
-Completion is host-ordered: drain the current stream, then a process-group barrier
-(:meth:`barrier`). Accumulating remote puts (the reference's CAS-loop ``dist_put``) go through
-the two-sided scatter path instead of remote atomics.
+Completion is STREAM-ORDERED and device-side (no host sync on the data path; the
+reference used nvshmemx_quiet_on_stream / barrier_all_on_stream, torch_nvshmem_p2p.cu:
+149,162,366-376): the heap starts with flag words, a producer kernel is followed on the
+same stream by ``heap_signal`` (system-scope release of a monotonic epoch into every peer's
+flag) and a consumer waits with ``heap_wait`` (system-scope acquire spin, bounded).
+:meth:`barrier_stream` is the device-side barrier; :meth:`barrier` additionally drains the
+host (start-up / tear-down only). Tensors gathered repeatedly are registered once
+(:meth:`register`: a persistent heap copy, refreshed when the tensor's version changes), so
+the steady state has no per-call negotiation, staging allocation or host barrier.
 """
 from __future__ import annotations
 
 import os
+import weakref
 from typing import Dict, Optional, Sequence, Tuple
 
 import torch
@@ -27,6 +39,12 @@ import torch.distributed as dist
 from .. import _native
 
 _ALIGN = 256
+# flag words at the start of every heap: kind k, source rank q -> word k * 64 + q
+_MAX_W = 64
+_READY, _DONE, _BAR, _PUT, _PUTDONE, _SC, _SCDONE = range(7)
+_NKINDS = 8
+_FLAG_BYTES = _NKINDS * _MAX_W * 8
+_MAX_SPINS = int(os.environ.get("DGRAPH_SHMEM_MAX_SPINS", str(1 << 23)))  # ~10 s bound
 
 
 def _group_rank(group) -> Tuple[int, int]:
@@ -72,9 +90,30 @@ class SymmetricHeap:
                 ptrs.append(ptr)
         self.peer_ptrs = ptrs
         self.table = torch.tensor(ptrs, dtype=torch.int64, device=dev)
-        self._cursor = 0
+        if self.world > _MAX_W:
+            raise ValueError(f"symmetric heap supports up to {_MAX_W} ranks per group")
+        # flag words (zeroed before any peer can signal: the init barrier below)
+        self.flags = self.local[:_FLAG_BYTES].view(torch.int64).view(_NKINDS, _MAX_W)
+        self.flags.zero_()
+        self._epoch = [0] * _NKINDS
+        self._timed_out = torch.zeros(1, dtype=torch.int32, device=dev)
+        self._cursor = _FLAG_BYTES
         self._allocs: Dict[int, Tuple[int, int]] = {}  # data_ptr -> (offset, nbytes)
         self._put_cache: Dict[tuple, Tuple[torch.Tensor, torch.Tensor]] = {}
+        self._registered: Dict[int, dict] = {}  # id(tensor) -> registration
+        self._scatter_plans: Dict[tuple, "_ScatterPlan"] = {}
+        # Device-side completion needs every rank's kernels to run concurrently (one GPU
+        # per rank). Ranks sharing one GPU (the 2-process-on-one-GPU test harness) are
+        # time-sliced between processes, so a spinning wait could starve the peer whose
+        # signal it awaits: such groups complete through the host instead (same data
+        # path, host barriers). DGRAPH_SHMEM_COMPLETION=device|host overrides.
+        mode = os.environ.get("DGRAPH_SHMEM_COMPLETION", "auto")
+        if mode == "auto":
+            uid = str(getattr(torch.cuda.get_device_properties(dev), "uuid", "")) \
+                if dev.type == "cuda" else ""
+            ids = _allgather_obj((os.uname().nodename, uid, dev.index), group)
+            mode = "host" if len(set(ids)) < len(ids) else "device"
+        self.device_completion = mode == "device"
         self.barrier()
 
     # ------------------------------------------------------------------ lifecycle
@@ -95,11 +134,51 @@ class SymmetricHeap:
         self.table = None
 
     def barrier(self) -> None:
-        """All prior heap traffic of every rank is complete and visible."""
+        """Host-level: all prior heap traffic of every rank is complete and visible
+        (start-up / tear-down; the data path uses :meth:`barrier_stream`)."""
         if self.local is not None and self.local.is_cuda:
             torch.cuda.current_stream(self.device).synchronize()
+            self.check()
         if dist.is_initialized() and self.world > 1:
             dist.barrier(group=self.group)
+
+    # ------------------------------------------------------------------ device completion
+    def _flag_off(self, kind: int) -> int:
+        return kind * _MAX_W * 8
+
+    def signal(self, kind: int, epoch: int, self_too: bool = False) -> None:
+        """Stream-ordered: after this stream's earlier kernels, store ``epoch`` into
+        ``flags[kind][me]`` of every peer's heap (system-scope release)."""
+        if self.world > 1 or self_too:
+            _native.ops().heap_signal(self.table, self._flag_off(kind), self.rank,
+                                      self.world, int(epoch), bool(self_too))
+
+    def wait(self, kind: int, epoch: int, self_too: bool = False) -> None:
+        """Stream-ordered: later kernels on this stream start once every peer q has
+        signalled ``flags[kind][q] >= epoch`` (bounded spin; see :meth:`check`)."""
+        if self.world > 1 or self_too:
+            _native.ops().heap_wait(self.flags[kind], self.rank, self.world, int(epoch),
+                                    _MAX_SPINS, bool(self_too), self._timed_out)
+
+    def next_epoch(self, kind: int) -> int:
+        self._epoch[kind] += 1
+        return self._epoch[kind]
+
+    def barrier_stream(self) -> None:
+        """Device-side barrier of the group (nvshmemx_barrier_all_on_stream): no host sync;
+        the stream proceeds once every peer's stream reached its barrier_stream."""
+        if not self.device_completion:
+            self.barrier()
+            return
+        e = self.next_epoch(_BAR)
+        self.signal(_BAR, e)
+        self.wait(_BAR, e)
+
+    def check(self) -> None:
+        """Raise if a device-side wait gave up (a peer never signalled). Host sync."""
+        if self._timed_out is not None and int(self._timed_out.item()) != 0:
+            raise RuntimeError("symmetric heap: a device-side wait timed out (a peer did not "
+                               "reach the matching signal; see DGRAPH_SHMEM_MAX_SPINS)")
 
     # ------------------------------------------------------------------ allocation
     def alloc_tensor(self, size, dtype: torch.dtype) -> torch.Tensor:
@@ -121,9 +200,11 @@ class SymmetricHeap:
 
     def reset(self) -> None:
         """Release every symmetric tensor (collective)."""
-        self._cursor = 0
+        self._cursor = _FLAG_BYTES
         self._allocs.clear()
         self._put_cache.clear()
+        self._registered.clear()
+        self._scatter_plans.clear()
 
     def owns(self, t: torch.Tensor) -> bool:
         if self.local is None or not t.is_cuda or t.device != self.local.device:
@@ -137,34 +218,71 @@ class SymmetricHeap:
         return t.data_ptr() - self.local.data_ptr()
 
     # ------------------------------------------------------------------ one-sided ops
+    def register(self, x: torch.Tensor) -> torch.Tensor:
+        """Collective (first call for a tensor): a persistent symmetric copy of ``x``
+        ([N_r, F], per-rank N may differ; the slot is sized for the largest). Later
+        :meth:`remote_gather` calls on the same tensor reuse it; an in-place update of
+        ``x`` (version change) is re-copied into the same slot without renegotiation."""
+        F = x.shape[-1]
+        x2 = x.reshape(-1, F)
+        n_max = max(_allgather_obj(int(x2.shape[0]), self.group))
+        slot = self.alloc_tensor((max(n_max, 1), F), x2.dtype)
+        slot[: x2.shape[0]].copy_(x2)
+        ent = {"ref": weakref.ref(x), "version": x._version, "slot": slot, "rows": x2.shape[0]}
+        self._registered[id(x)] = ent
+        return slot
+
+    def _slot_for(self, x: torch.Tensor) -> torch.Tensor:
+        if self.owns(x):
+            return x.reshape(-1, x.shape[-1])
+        ent = self._registered.get(id(x))
+        if ent is None or ent["ref"]() is not x:
+            return self.register(x)
+        if ent["version"] != x._version:
+            # readers of the previous epoch must be done with the slot before it changes
+            if self.device_completion:
+                self.wait(_DONE, self._epoch[_DONE])
+            ent["slot"][: ent["rows"]].copy_(x.reshape(-1, x.shape[-1]))
+            ent["version"] = x._version
+        return ent["slot"]
+
     def remote_gather(self, x: torch.Tensor, indices: torch.Tensor,
                       owners: torch.Tensor) -> torch.Tensor:
         """``out[i] = x_on_rank[owners[i]][indices[i]]`` — the local-form G1 gather.
 
-        ``x`` ([N_r, F], per-rank row counts may differ) is staged into a symmetric slot
-        sized for the largest N_r, then every output row is fetched straight from its
-        owner's heap.
+        Stream-ordered one-sided get: every rank publishes its (registered or heap-resident)
+        rows with a READY signal, waits for its peers' READY, reads the rows straight from
+        the owners' heaps over xGMI, and releases the slots with a DONE signal. No host
+        synchronisation after the first (registering) call for a tensor.
         """
         F = x.shape[-1]
-        x2 = x.reshape(-1, F)
-        n_max = max(_allgather_obj(int(x2.shape[0]), self.group))
-        mark = self._cursor
-        stage = self.alloc_tensor((max(n_max, 1), F), x2.dtype)
-        stage[: x2.shape[0]].copy_(x2)
-        self.barrier()  # every rank has staged its rows
-        out = torch.empty(indices.numel(), F, dtype=x2.dtype, device=x2.device)
+        slot = self._slot_for(x)
+        if self.device_completion:
+            e = self.next_epoch(_READY)
+            self.signal(_READY, e)
+            self.wait(_READY, e)
+        else:
+            self.barrier()  # every owner has (re)written its slot
+        out = torch.empty(indices.numel(), F, dtype=x.dtype, device=x.device)
         if out.numel():
-            _native.ops().heap_get_rows(self.table, self.offset_of(stage),
+            _native.ops().heap_get_rows(self.table, self.offset_of(slot),
                                         owners.reshape(-1).long().contiguous(),
-                                        indices.reshape(-1).long().contiguous(), out, F)
-        self.barrier()  # nobody reuses the staging slot while peers still read it
-        self._release_to(mark)
+                                        indices.reshape(-1).long().contiguous(), out,
+                                        slot.stride(0))
+        if self.device_completion:
+            d = self.next_epoch(_DONE)
+            self.signal(_DONE, d)
+        else:
+            self.barrier()  # nobody rewrites a slot while peers still read it
         return out
 
     def put_rows(self, send: torch.Tensor, recv: torch.Tensor, send_splits: Sequence[int],
                  remote_offsets: Sequence[int]) -> None:
         """Rows ``send[so_p : so_p + n_p]`` land in peer ``p``'s ``recv`` at row
-        ``remote_offsets[p]`` (``recv`` must be a symmetric tensor). Synchronous."""
+        ``remote_offsets[p]`` (``recv`` must be a symmetric tensor). Stream-ordered:
+        kernels issued after this call on the current stream see every peer's rows in
+        ``recv``; a peer's rows of the previous call are not overwritten before that peer
+        has entered this call (its reads of them were issued before)."""
         F = send.shape[-1]
         s2 = send.reshape(-1, F).contiguous()
         key = (tuple(int(v) for v in send_splits), tuple(int(v) for v in remote_offsets))
@@ -177,15 +295,119 @@ class SymmetricHeap:
             pos = torch.arange(peers.numel()) - so[peers] + starts[peers]
             idx = (peers.to(s2.device), pos.to(s2.device))
             self._put_cache[key] = idx
+        if not self.device_completion:
+            self.barrier()
+            if s2.shape[0]:
+                _native.ops().heap_put_rows(self.table, self.offset_of(recv), idx[0], idx[1],
+                                            s2, recv.reshape(-1, F).stride(0))
+            self.barrier()
+            return
+        # the previous epoch's receivers are done with their recv (they entered this call)
+        prev = self._epoch[_PUT]
+        self.signal(_PUTDONE, prev)
+        self.wait(_PUTDONE, prev)
         if s2.shape[0]:
             _native.ops().heap_put_rows(self.table, self.offset_of(recv), idx[0], idx[1], s2,
                                         recv.reshape(-1, F).stride(0))
-        self.barrier()
+        e = self.next_epoch(_PUT)
+        self.signal(_PUT, e)
+        self.wait(_PUT, e)  # every peer's rows have landed in my recv
+
+    def scatter_add(self, x: torch.Tensor, indices: torch.Tensor, owners: torch.Tensor,
+                    num_output_rows: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """One-sided scatter-add (the reference's ``dist_put``):
+        ``out_on_rank[owners[i]][indices[i]] += x[i]``; returns this rank's ``out``
+        ([num_output_rows, F], zero-initialised when not given).
+
+        Deterministic: rows are pre-summed locally per (owner, row), put as one block per
+        owner into this rank's slot range of the owner's symmetric receive area, and every
+        owner adds its slots with a fixed-order segment sum. The plan (slot layout and the
+        owners' segment-sum CSR) is built once per index tensor pair — collectively, so all
+        ranks must pass their index tensors consistently (same objects, unmodified) to hit
+        it — after which a call is two local SpMMs, one put kernel and the completion
+        signals: no host synchronisation."""
+        from ..ops import kernels as K
+
+        F = x.shape[-1]
+        x2 = x.reshape(-1, F).contiguous()
+        plan = self._scatter_plan(indices, owners, int(num_output_rows), F, x2.dtype)
+        if out is None:
+            out = torch.zeros(int(num_output_rows), F, dtype=x2.dtype, device=x2.device)
+        agg = K.spmm(plan.pre.rowptr, plan.pre.col, x2) if plan.pre.nnz else \
+            x2.new_zeros(0, F)
+        self.put_rows(agg, plan.slot, plan.send_splits, plan.remote_offsets)
+        post = plan.post
+        if post.nnz:
+            o2 = out.reshape(-1, F)
+            K.spmm(post.rowptr, post.col, plan.slot, o2, beta=1.0, row_map=post.row_map)
+        return out
+
+    def _scatter_plan(self, indices, owners, n_out: int, F: int, dtype) -> "_ScatterPlan":
+        key = (id(indices), id(owners), n_out, F, dtype)
+        plan = self._scatter_plans.get(key)
+        if plan is not None and plan.matches(indices, owners):
+            return plan
+        plan = _ScatterPlan(self, indices, owners, n_out, F, dtype)
+        self._scatter_plans[key] = plan
+        return plan
 
     def _release_to(self, mark: int) -> None:
         self._cursor = mark
         for p in [p for p, (o, _) in self._allocs.items() if o >= mark]:
             del self._allocs[p]
+
+
+class _ScatterPlan:
+    """Slot layout of one :meth:`SymmetricHeap.scatter_add` pattern (built collectively)."""
+
+    def __init__(self, heap: SymmetricHeap, indices, owners, n_out: int, F: int, dtype):
+        from ..ops.csr import CSR
+        from ..plan.pattern import _alltoall_counts, _alltoallv_ids
+
+        self.refs = (weakref.ref(indices), weakref.ref(owners))
+        self.versions = (indices._version, owners._version)
+        dev = heap.device
+        W = heap.world
+        idx = indices.reshape(-1).to(dev).long()
+        dst = owners.reshape(-1).to(dev).long()
+        n = idx.numel()
+        # (owner, row) key: rows index the OWNER's output, so the radix is this rank's
+        # largest target row + 1 (not its own n_out)
+        M = int(idx.max().item()) + 1 if n else 1
+        key = dst * M + idx
+        uniq, inv = (torch.unique(key, sorted=True, return_inverse=True) if n else
+                     (key, key))
+        U = uniq.numel()
+        # local pre-aggregation: unique (owner, row) u <- the input rows that target it
+        self.pre = CSR.from_coo(inv, torch.arange(n, device=dev), U, max(n, 1))
+        udst = torch.div(uniq, M, rounding_mode="floor")
+        uidx = uniq - udst * M
+        counts = torch.bincount(udst, minlength=W) if U else torch.zeros(W, dtype=torch.long,
+                                                                          device=dev)
+        group = heap.group
+        peer_counts = _alltoall_counts(counts, group) if W > 1 else counts.clone()
+        self.send_splits = [int(v) for v in counts.tolist()]
+        recv_splits = [int(v) for v in peer_counts.tolist()]
+        recv_idx = _alltoallv_ids(uidx, self.send_splits, recv_splits, group) if W > 1 \
+            else uidx
+        R = sum(recv_splits)
+        r_max = max(_allgather_obj(R, group))
+        # my rows land in owner p's slots at p's prefix over its sources
+        prefix = torch.zeros(W, dtype=torch.long, device=dev)
+        if W > 1:
+            prefix[1:] = torch.cumsum(peer_counts, 0)[:-1]
+            remote = _alltoall_counts(prefix, group)
+        else:
+            remote = prefix
+        self.remote_offsets = [int(v) for v in remote.tolist()]
+        self.slot = heap.alloc_tensor((max(r_max, 1), F), dtype)
+        # owner side: output row <- slot positions, source-major (fixed summation order)
+        self.post = CSR.from_coo(recv_idx.to(dev).long(), torch.arange(R, device=dev), n_out,
+                                 max(r_max, 1)).compact_rows()
+
+    def matches(self, indices, owners) -> bool:
+        return (self.refs[0]() is indices and self.refs[1]() is owners
+                and self.versions == (indices._version, owners._version))
 
 
 class NVSHMEMP2P:
@@ -255,6 +477,20 @@ class NVSHMEMP2P:
         dst.reshape(-1, int(num_features))[: out.shape[0]].copy_(out)
 
     @staticmethod
+    def dist_put(src, dst, indices, rank_mappings, bs, num_input_rows, num_features,
+                 num_output_rows) -> None:
+        """``dst_on[rank_mappings[i]][0, indices[i]] += src[0, i]`` (batch size 1); ``dst``
+        is this rank's output (symmetric or not). Deterministic one-sided scatter-add
+        (:meth:`SymmetricHeap.scatter_add`), stream-ordered."""
+        assert int(bs) == 1, "batch size must be 1"
+        F = int(num_features)
+        out = dst.reshape(-1, F)[: int(num_output_rows)]
+        NVSHMEMP2P._h().scatter_add(src.reshape(-1, F)[: int(num_input_rows)],
+                                    indices.reshape(-1)[: int(num_input_rows)],
+                                    rank_mappings.reshape(-1)[: int(num_input_rows)],
+                                    int(num_output_rows), out=out)
+
+    @staticmethod
     def get_max(val: int) -> int:
         h = NVSHMEMP2P._h()
         return max(_allgather_obj(int(val), h.group))
@@ -265,4 +501,5 @@ class NVSHMEMP2P:
 
     @staticmethod
     def barrier_stream() -> None:
-        NVSHMEMP2P._h().barrier()
+        """Device-side barrier on the current stream (no host sync)."""
+        NVSHMEMP2P._h().barrier_stream()

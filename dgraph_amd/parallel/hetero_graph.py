@@ -149,11 +149,11 @@ class SourceGraph:
         local = gids - off[owners]
         F = x.shape[1]
         out = torch.empty(gids.numel(), F, dtype=x.dtype, device=x.device)
-        heap.barrier()  # every owner has written its features
+        heap.barrier_stream()  # every owner's writes of x are visible (device-side)
         if out.numel():
             _native.ops().heap_get_rows(heap.table, heap.offset_of(x), owners, local, out,
                                         x.stride(0))
-        heap.barrier()
+        heap.barrier_stream()  # no owner overwrites x while peers still read it
         return out
 
     # ------------------------------------------------------------------ forward / adjoint

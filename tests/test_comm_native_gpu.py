@@ -62,6 +62,49 @@ def _heap_body(rank, world):
     NVSHMEMP2P.dist_get(xs[rank].to(dev).unsqueeze(0), dst, rows.to(dev).unsqueeze(0),
                         owners.to(dev).unsqueeze(0), 1, n_rows[rank], F, E)
     torch.testing.assert_close(dst[0].cpu(), ref, rtol=0, atol=0)
+    # ---- registered tensor: the second gather reuses the heap slot (no renegotiation);
+    # an in-place update is re-copied (version counter), all stream-ordered
+    xr = xs[rank].to(dev)
+    o1 = heap.remote_gather(xr, rows.to(dev), owners.to(dev))
+    cursor = heap._cursor
+    o2 = heap.remote_gather(xr, rows.to(dev), owners.to(dev))
+    assert heap._cursor == cursor, "registered gather must not allocate"
+    torch.testing.assert_close(o2.cpu(), ref, rtol=0, atol=0)
+    xr.add_(1.0)
+    o3 = heap.remote_gather(xr, rows.to(dev), owners.to(dev))
+    torch.testing.assert_close(o3.cpu(), ref + 1.0, rtol=0, atol=0)
+    del o1
+    # ---- device-side barrier (no host sync) and the timeout flag stays clear
+    for _ in range(3):
+        heap.barrier_stream()
+    heap.check()
+    # ---- one-sided scatter-add (dist_put): deterministic, vs a dense reference
+    n_out = [50 + 7 * r for r in range(world)]
+    g2 = torch.Generator().manual_seed(100 + rank)
+    E2 = 700
+    dst_r = torch.randint(0, world, (E2,), generator=g2)
+    dst_i = torch.tensor([int(torch.randint(0, n_out[o], (1,), generator=g2)) for o in dst_r])
+    vals = torch.randn(E2, F, generator=g2)
+    di, dr = dst_i.to(dev), dst_r.to(dev)
+    out_a = heap.scatter_add(vals.to(dev), di, dr, n_out[rank])
+    out_b = heap.scatter_add(vals.to(dev), di, dr, n_out[rank])  # cached plan, same bits
+    assert torch.equal(out_a, out_b)
+    # dense reference: every rank's contributions (regenerated from the seeds)
+    ref_out = torch.zeros(n_out[rank], F, dtype=torch.float64)
+    for q in range(world):
+        gq = torch.Generator().manual_seed(100 + q)
+        rq = torch.randint(0, world, (E2,), generator=gq)
+        iq = torch.tensor([int(torch.randint(0, n_out[o], (1,), generator=gq)) for o in rq])
+        vq = torch.randn(E2, F, generator=gq).double()
+        m = rq == rank
+        ref_out.index_add_(0, iq[m], vq[m])
+    torch.testing.assert_close(out_a.double().cpu(), ref_out, atol=1e-4, rtol=1e-5)
+    # facade: dist_put accumulates into a given output
+    acc = torch.ones(1, n_out[rank], F, device=dev)
+    NVSHMEMP2P.dist_put(vals.to(dev).unsqueeze(0), acc, di.unsqueeze(0), dr.unsqueeze(0), 1,
+                        E2, F, n_out[rank])
+    torch.testing.assert_close(acc[0].double().cpu(), ref_out + 1.0, atol=1e-4, rtol=1e-5)
+    heap.check()
     NVSHMEMP2P.finalize()
     dist.barrier()
 
@@ -102,3 +145,52 @@ def test_rccl_executor_self_exchange():
         assert float(t.sum()) == 4096.0
     finally:
         ex.close()
+
+
+def test_device_signal_wait_two_streams():
+    """Stream-ordered one-sided completion with real concurrency: two "ranks" as two HIP
+    streams of one process, each with its own heap (peer table = both heaps). Every round
+    each rank (1) acknowledges the previous round's receive (PUTDONE) and waits for the
+    peer's acknowledgement, (2) puts its rows into the peer's receive slot, (3) signals PUT
+    and waits for the peer's PUT, (4) copies what it received — all without a host sync.
+    The copies must show exactly the peer's rows of that round, and no wait may time out.
+    (Across processes sharing one GPU the kernels are time-sliced, so there the heap
+    completes through the host; see SymmetricHeap.device_completion.)"""
+    from dgraph_amd import _native
+
+    ops = _native.ops()
+    dev = torch.device("cuda", 0)
+    nb = 1 << 20
+    heaps = [ops.heap_alloc(nb, 0), ops.heap_alloc(nb, 0)]
+    table = torch.tensor([ops.tensor_ptr(h) for h in heaps], dtype=torch.int64, device=dev)
+    flags = [h[:4096].view(torch.int64).view(8, 64) for h in heaps]
+    for f in flags:
+        f.zero_()
+    PUT, PUTDONE = 3, 4
+    off_put, off_done = PUT * 64 * 8, PUTDONE * 64 * 8
+    data_off = 4096
+    R, F, rounds = 300, 24, 40
+    recv = [h[data_off:data_off + R * F * 4].view(torch.float32).view(R, F) for h in heaps]
+    timed_out = torch.zeros(1, dtype=torch.int32, device=dev)
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    got = [torch.empty(rounds, R, F, device=dev) for _ in range(2)]
+    srcs = [[torch.full((R, F), float(100 * it + r), device=dev) for it in range(rounds)]
+            for r in range(2)]
+    torch.cuda.synchronize()
+    row_dst = torch.arange(R, dtype=torch.int64, device=dev)
+    for it in range(rounds):
+        for r in range(2):
+            peer = 1 - r
+            with torch.cuda.stream(streams[r]):
+                ops.heap_signal(table, off_done, r, 2, it, False)
+                ops.heap_wait(flags[r][PUTDONE], r, 2, it, 1 << 24, False, timed_out)
+                row_peer = torch.full((R,), peer, dtype=torch.int64, device=dev)
+                ops.heap_put_rows(table, data_off, row_peer, row_dst, srcs[r][it], F)
+                ops.heap_signal(table, off_put, r, 2, it + 1, False)
+                ops.heap_wait(flags[r][PUT], r, 2, it + 1, 1 << 24, False, timed_out)
+                got[r][it].copy_(recv[r])
+    torch.cuda.synchronize()
+    assert int(timed_out.item()) == 0
+    for r in range(2):
+        exp = torch.stack([torch.full((R, F), float(100 * it + (1 - r))) for it in range(rounds)])
+        assert torch.equal(got[r].cpu(), exp)
