@@ -30,14 +30,26 @@ def main():
     ap.add_argument("--grid", default="721x1440")
     ap.add_argument("--hidden", type=int, default=128)
     ap.add_argument("--layers", type=int, default=4)
-    ap.add_argument("--channels", type=int, default=73)
+    ap.add_argument("--channels", type=int, default=None,
+                    help="grid channels (default: by --channel-config)")
+    ap.add_argument("--channel-config", default="reference-73",
+                    choices=["reference-73", "era5-37"],
+                    help="reference-73: the reference's 73 climate channels "
+                         "(graphcast_config.py:42); era5-37: ERA5 on 37 pressure levels, "
+                         "6 atmospheric variables x 37 + 5 surface = 227 channels "
+                         "(BASELINE config 5)")
+    ap.add_argument("--profile-ops", default="",
+                    help="torch.profiler per-op device-time table of one step -> PATH")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--reference-mesh-edges", action="store_true",
-                    help="carry every multimesh edge twice, as the reference's graph does "
-                         "(655 320 processor edges at level 6 instead of 327 660)")
+    ap.add_argument("--dedup-mesh-edges", action="store_true",
+                    help="one processor edge per multimesh edge pair (327 660 at level 6); "
+                         "default: the reference's graph, every multimesh edge carried twice "
+                         "(655 320, experiments/GraphCast/tests/test_single_graph_data.py)")
     a = ap.parse_args()
+    if a.channels is None:
+        a.channels = 73 if a.channel_config == "reference-73" else 6 * 37 + 5
 
     import torch.distributed as dist
 
@@ -53,7 +65,7 @@ def main():
     dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     t0 = time.perf_counter()
     g = build_global_graph(a.mesh_level, tuple(int(v) for v in a.grid.split("x")),
-                           duplicate_mesh_edges=a.reference_mesh_edges)
+                           duplicate_mesh_edges=not a.dedup_mesh_edges)
     pg = partition_graphcast_graph(g, rank, W, group=comm.group).to(dev)
     build_s = time.perf_counter() - t0
     cfg = Config()
@@ -104,7 +116,21 @@ def main():
         sync()
         ms = (time.perf_counter() - t) * 1e3 / a.steps
         edges = a.layers * g.m2m[0].size + g.g2m[0].size + g.m2g[0].size
+        if a.profile_ops and rank == 0:
+            from torch.profiler import ProfilerActivity, profile
+
+            with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA],
+                         record_shapes=True) as prof:
+                step()
+                sync()
+            with open(a.profile_ops, "w") as f:
+                f.write(prof.key_averages(group_by_input_shape=True).table(
+                    sort_by="self_cuda_time_total", row_limit=40, max_name_column_width=60,
+                    max_shapes_column_width=80))
         result = {"metric": "graphcast_step_ms", "ms_per_step": ms,
+                  "channels": a.channels, "channel_config": a.channel_config,
+                  "mesh_edges": int(g.m2m[0].size), "duplicate_mesh_edges":
+                  not a.dedup_mesh_edges,
                   "precision": "bf16 compute, fp32 master weights" if masters is not None
                   else "fp32",
                   "edge_updates_per_s": edges / (ms / 1e3), "loss": float(loss),

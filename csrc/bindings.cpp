@@ -474,7 +474,8 @@ const float* bn_vec(const c10::optional<at::Tensor>& t, const at::Tensor& x, con
 at::Tensor bn_reduce_op(const at::Tensor& x, const c10::optional<at::Tensor>& dy,
                         const at::Tensor& center, const c10::optional<at::Tensor>& rstd,
                         const c10::optional<at::Tensor>& gamma,
-                        const c10::optional<at::Tensor>& beta, bool relu, int64_t mode) {
+                        const c10::optional<at::Tensor>& beta, bool relu, int64_t mode,
+                        double drop_p, int64_t seed) {
   check_dev(x, x, "x");
   check_rows(x, "x");
   TORCH_CHECK(mode == 0 || mode == 1, "bn_reduce: mode 0 (stats) or 1 (backward)");
@@ -496,7 +497,8 @@ at::Tensor bn_reduce_op(const at::Tensor& x, const c10::optional<at::Tensor>& dy
                          N, static_cast<int>(F), bn_vec(center, x, "center"),
                          bn_vec(rstd, x, "rstd"), bn_vec(gamma, x, "gamma"),
                          bn_vec(beta, x, "beta"), relu, partial.data_ptr<float>(), nb,
-                         out.data_ptr<double>(), cur_stream(x)));
+                         out.data_ptr<double>(), cur_stream(x), static_cast<float>(drop_p),
+                         static_cast<uint64_t>(seed)));
   return out;
 }
 
@@ -504,7 +506,8 @@ at::Tensor bn_apply_op(const at::Tensor& x, const c10::optional<at::Tensor>& dy,
                        const at::Tensor& mean, const at::Tensor& rstd,
                        const c10::optional<at::Tensor>& gamma,
                        const c10::optional<at::Tensor>& beta, const c10::optional<at::Tensor>& c1,
-                       const c10::optional<at::Tensor>& c2, bool relu, int64_t mode) {
+                       const c10::optional<at::Tensor>& c2, bool relu, int64_t mode,
+                       double drop_p, int64_t seed) {
   check_dev(x, x, "x");
   check_rows(x, "x");
   TORCH_CHECK(mode == 0 || mode == 1, "bn_apply: mode 0 (forward) or 1 (backward)");
@@ -522,7 +525,8 @@ at::Tensor bn_apply_op(const at::Tensor& x, const c10::optional<at::Tensor>& dy,
                         out.data_ptr(), out.stride(0), x.size(0), static_cast<int>(x.size(1)),
                         bn_vec(mean, x, "mean"), bn_vec(rstd, x, "rstd"),
                         bn_vec(gamma, x, "gamma"), bn_vec(beta, x, "beta"), bn_vec(c1, x, "c1"),
-                        bn_vec(c2, x, "c2"), relu, cur_stream(x)));
+                        bn_vec(c2, x, "c2"), relu, cur_stream(x), static_cast<float>(drop_p),
+                        static_cast<uint64_t>(seed)));
   return out;
 }
 
@@ -624,9 +628,9 @@ TORCH_LIBRARY(dgraph_amd, m) {
   m.def("layer_norm_bwd(Tensor dy, Tensor x, Tensor mean, Tensor rstd, Tensor? gamma) -> "
         "(Tensor, Tensor, Tensor)");
   m.def("bn_reduce(Tensor x, Tensor? dy, Tensor center, Tensor? rstd, Tensor? gamma, "
-        "Tensor? beta, bool relu, int mode) -> Tensor");
+        "Tensor? beta, bool relu, int mode, float drop_p=0., int seed=0) -> Tensor");
   m.def("bn_apply(Tensor x, Tensor? dy, Tensor mean, Tensor rstd, Tensor? gamma, Tensor? beta, "
-        "Tensor? c1, Tensor? c2, bool relu, int mode) -> Tensor");
+        "Tensor? c1, Tensor? c2, bool relu, int mode, float drop_p=0., int seed=0) -> Tensor");
   m.def("dual_gemm(Tensor A1, Tensor B1t, Tensor? A2, Tensor? B2t, Tensor? bias, Tensor? cin, "
         "Tensor(a!) out, Tensor(b!)? mask_out, Tensor? mask_in, bool relu) -> ()");
   m.def("tile32_mask_words(int M, int N) -> int", &tile32_mask_words_op);

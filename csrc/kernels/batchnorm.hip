@@ -10,8 +10,13 @@
 //   bn_reduce mode 1 (backward):    P[b] = ( sum dy', sum dy' * xhat )
 //                                    dy' = dy * [y > 0] when the ReLU is fused
 //   bn_finalize: out[k][f] = sum_b P[b][k][f] in a fixed order, in fp64 (deterministic)
-//   bn_apply mode 0 (forward):      y  = act((x - mean) * rstd * g + b)
+//   bn_apply mode 0 (forward):      y  = drop(act((x - mean) * rstd * g + b))
 //   bn_apply mode 1 (backward):     dx = (dy' - c1 - xhat * c2) * rstd * g
+//
+// Fused dropout (drop_thresh > 0): element (r, c) is kept iff hash(seed, r * F + c) >=
+// drop_thresh (= p * 2^32), kept values scaled by 1/(1-p). The mask is a pure function of
+// (seed, index), so the backward kernels regenerate it (dy' = dy * keep / (1-p) first):
+// no mask tensor, no separate dropout / masked-scale passes over [N, F].
 //
 // Mapping: a row of F elements is covered by LPR lanes with VEC-element (16-byte) vectors;
 // a wave holds 64/LPR rows, a block 4 waves; blocks stride over row groups (grid.x) and
@@ -43,7 +48,22 @@ struct BNArgs {
   const float* c2;
   float* partial;  // [gridDim.x][2][F]
   bool relu;
+  uint32_t drop_thresh;  // 0: no dropout
+  float keep_scale;
+  uint32_t seed_lo, seed_hi;
 };
+
+// counter-based keep decision (murmur3 fmix32 of the element index mixed with the seed)
+__device__ __forceinline__ bool dropout_keep(const BNArgs& a, int64_t idx) {
+  uint32_t h = static_cast<uint32_t>(idx) ^ a.seed_lo;
+  h ^= (static_cast<uint32_t>(static_cast<uint64_t>(idx) >> 32) + a.seed_hi) * 0x9E3779B1u;
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h >= a.drop_thresh;
+}
 
 template <int VEC>
 __device__ __forceinline__ void load_param(const float* p, int col, float (&o)[VEC],
@@ -103,10 +123,20 @@ __global__ __launch_bounds__(256) void bn_kernel(BNArgs a) {
           float v = fmaf((x[i] - mean[i]) * rstd[i], g[i], b[i]);
           y[i] = a.relu ? fmaxf(v, 0.f) : v;
         }
+        if (a.drop_thresh) {
+#pragma unroll
+          for (int i = 0; i < VEC; ++i)
+            y[i] = dropout_keep(a, r * a.F + col + i) ? y[i] * a.keep_scale : 0.f;
+        }
         store_vec_f32<T, VEC>(O + r * a.ldo + col, y);
       } else {
         float d[VEC];
         load_vec_f32<T, VEC>(DY + r * a.ldy + col, d);
+        if (a.drop_thresh) {
+#pragma unroll
+          for (int i = 0; i < VEC; ++i)
+            d[i] = dropout_keep(a, r * a.F + col + i) ? d[i] * a.keep_scale : 0.f;
+        }
 #pragma unroll
         for (int i = 0; i < VEC; ++i) {
           const float xh = (x[i] - mean[i]) * rstd[i];
@@ -206,13 +236,29 @@ int bn_reduce_blocks(int64_t N) {
   return static_cast<int>(b < 1 ? 1 : (b > 1024 ? 1024 : b));
 }
 
+// dropout parameters of a fused BN pass: keep probability 1 - p, 64-bit seed
+static void set_dropout(BNArgs& a, float p, uint64_t seed) {
+  if (p > 0.f && p < 1.f) {
+    const double t = static_cast<double>(p) * 4294967296.0;
+    a.drop_thresh = t >= 4294967295.0 ? 4294967295u : static_cast<uint32_t>(t < 1.0 ? 1.0 : t);
+    a.keep_scale = 1.f / (1.f - p);
+  } else {
+    a.drop_thresh = 0;
+    a.keep_scale = 1.f;
+  }
+  a.seed_lo = static_cast<uint32_t>(seed);
+  a.seed_hi = static_cast<uint32_t>(seed >> 32);
+}
+
 hipError_t bn_reduce(DType dt, int mode, const void* x, int64_t ldx, const void* dy,
                      int64_t ldy, int64_t N, int F, const float* shift_or_mean,
                      const float* rstd, const float* gamma, const float* beta, bool relu,
-                     float* partial, int nblocks, double* out, hipStream_t st) {
+                     float* partial, int nblocks, double* out, hipStream_t st, float drop_p,
+                     uint64_t seed) {
   if (F <= 0) return hipSuccess;
   BNArgs a{x, ldx, dy, ldy, nullptr, 0, N < 0 ? 0 : N, F, shift_or_mean, rstd, gamma, beta,
-           nullptr, nullptr, partial, relu};
+           nullptr, nullptr, partial, relu, 0, 1.f, 0, 0};
+  if (mode == 1) set_dropout(a, drop_p, seed);
   hipError_t e = mode == 0 ? dispatch<0>(dt, a, nblocks, st) : dispatch<1>(dt, a, nblocks, st);
   if (e != hipSuccess) return e;
   const int n2 = 2 * F;
@@ -224,9 +270,11 @@ hipError_t bn_reduce(DType dt, int mode, const void* x, int64_t ldx, const void*
 hipError_t bn_apply(DType dt, int mode, const void* x, int64_t ldx, const void* dy,
                     int64_t ldy, void* out, int64_t ldo, int64_t N, int F, const float* mean,
                     const float* rstd, const float* gamma, const float* beta, const float* c1,
-                    const float* c2, bool relu, hipStream_t st) {
+                    const float* c2, bool relu, hipStream_t st, float drop_p, uint64_t seed) {
   if (N <= 0 || F <= 0) return hipSuccess;
-  BNArgs a{x, ldx, dy, ldy, out, ldo, N, F, mean, rstd, gamma, beta, c1, c2, nullptr, relu};
+  BNArgs a{x, ldx, dy, ldy, out, ldo, N, F, mean, rstd, gamma, beta, c1, c2, nullptr, relu,
+           0, 1.f, 0, 0};
+  set_dropout(a, drop_p, seed);
   return mode == 0 ? dispatch<2>(dt, a, 0, st) : dispatch<3>(dt, a, 0, st);
 }
 

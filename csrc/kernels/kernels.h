@@ -135,11 +135,15 @@ int bn_reduce_blocks(int64_t N);
 hipError_t bn_reduce(DType dt, int mode, const void* x, int64_t ldx, const void* dy,
                      int64_t ldy, int64_t N, int F, const float* center, const float* rstd,
                      const float* gamma, const float* beta, bool relu, float* partial,
-                     int nblocks, double* out, hipStream_t st);
+                     int nblocks, double* out, hipStream_t st, float drop_p = 0.f,
+                     uint64_t seed = 0);
+// drop_p > 0: dropout fused after the activation (forward) / regenerated from (seed,
+// element index) on dy (backward, both the reduce and the apply pass)
 hipError_t bn_apply(DType dt, int mode, const void* x, int64_t ldx, const void* dy,
                     int64_t ldy, void* out, int64_t ldo, int64_t N, int F, const float* mean,
                     const float* rstd, const float* gamma, const float* beta, const float* c1,
-                    const float* c2, bool relu, hipStream_t st);
+                    const float* c2, bool relu, hipStream_t st, float drop_p = 0.f,
+                    uint64_t seed = 0);
 
 // ---------------------------------------------------------------------------
 // Fused tall-skinny MFMA dual GEMM (dual_gemm.hip), bf16 in / fp32 accumulate:

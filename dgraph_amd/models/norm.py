@@ -101,8 +101,13 @@ class _SyncBNFn(Function):
 
     @staticmethod
     def forward(ctx, x, gamma, beta, eps: float, group, recompute: bool, box: list,
-                relu: bool = False):
+                relu: bool = False, drop_p: float = 0.0):
         N, mean, var = global_moments(x, group)
+        # dropout fused after the activation: the keep mask is a function of (seed, element
+        # index) that the backward regenerates (native kernels and reference alike)
+        seed = int(torch.randint(0, 1 << 62, (1,), dtype=torch.int64).item()) \
+            if drop_p > 0 else 0
+        ctx.drop = (float(drop_p), seed)
         box.append(N)
         rstd = torch.rsqrt(var + eps)
         ctx.group, ctx.N, ctx.relu = group, N, relu
@@ -112,7 +117,8 @@ class _SyncBNFn(Function):
         ctx.native = _native_ok(x)
         g, b = _vec(gamma), _vec(beta)
         if ctx.native:
-            y = _ops().bn_apply(x, None, mean, rstd, g, b, None, None, relu, 0)
+            y = _ops().bn_apply(x, None, mean, rstd, g, b, None, None, relu, 0, float(drop_p),
+                                seed)
             ctx.save_for_backward(x, mean, rstd, g, b)
             return y, mean, var
         ctx.recompute = recompute
@@ -122,6 +128,9 @@ class _SyncBNFn(Function):
             y = y * g.to(mean.dtype) + b.to(mean.dtype)
         if relu:
             y = torch.relu(y)
+        if drop_p > 0:
+            y = y * dropout_keep_mask(seed, *x.shape, x.device, drop_p).to(y.dtype) / \
+                (1.0 - drop_p)
         ctx.save_for_backward(x if recompute else xhat, mean, rstd, g, b)
         return y.to(x.dtype), mean, var
 
@@ -130,16 +139,20 @@ class _SyncBNFn(Function):
         saved, mean, rstd, g, b = ctx.saved_tensors
         F = mean.numel()
         Nf = max(ctx.N, 1.0)
+        p, seed = ctx.drop
         if ctx.native:
             x = saved
             dy = dy.to(x.dtype)
             if dy.stride(1) != 1 or dy.shape != x.shape:
                 dy = dy.contiguous()
-            s = _ops().bn_reduce(x, dy, mean, rstd, g, b, ctx.relu, 1).float()
+            s = _ops().bn_reduce(x, dy, mean, rstd, g, b, ctx.relu, 1, p, seed).float()
             sum_dy, sum_dy_xhat = s[0], s[1]
         else:
             xhat = (saved.to(mean.dtype) - mean) * rstd if ctx.recompute else saved
             dyf = dy.to(mean.dtype)
+            if p > 0:
+                dyf = dyf * dropout_keep_mask(seed, *dyf.shape, dyf.device, p).to(dyf.dtype) / \
+                    (1.0 - p)
             if ctx.relu:
                 pre = xhat * g.to(mean.dtype) + b.to(mean.dtype) if g is not None else xhat
                 dyf = dyf * (pre > 0)
@@ -155,13 +168,32 @@ class _SyncBNFn(Function):
         m_dy, m_dyx = glob[:F] / Nf, glob[F:] / Nf
         if ctx.native:
             dx = _ops().bn_apply(saved, dy, mean, rstd, g, b, m_dy.contiguous(),
-                                 m_dyx.contiguous(), ctx.relu, 1)
+                                 m_dyx.contiguous(), ctx.relu, 1, p, seed)
         else:
             dx = (dyf - m_dy - xhat * m_dyx) * rstd
             if g is not None:
                 dx = dx * g.to(mean.dtype)
             dx = dx.to(dy.dtype)
-        return dx, dgamma, dbeta, None, None, None, None, None
+        return dx, dgamma, dbeta, None, None, None, None, None, None
+
+
+def dropout_keep_mask(seed: int, N: int, F: int, device=None, p: float = 0.0) -> torch.Tensor:
+    """The fused-dropout keep mask of the native BN kernels (csrc/kernels/batchnorm.hip
+    ``dropout_keep``): keep (r, c) iff fmix32 of the element index r * F + c mixed with the
+    64-bit seed is >= p * 2^32. A pure function of (seed, index): forward and backward (and
+    the CPU reference and the GPU kernels) agree bit for bit."""
+    M = 0xFFFFFFFF
+    idx = torch.arange(N * F, dtype=torch.int64, device=device)
+    lo, hi = idx & M, idx >> 32
+    h = lo ^ (seed & M)
+    h = h ^ ((((hi + (seed >> 32)) & M) * 0x9E3779B1) & M)
+    h = h ^ (h >> 16)
+    h = (h * 0x85EBCA6B) & M
+    h = h ^ (h >> 13)
+    h = (h * 0xC2B2AE35) & M
+    h = h ^ (h >> 16)
+    t = min(max(int(p * 4294967296.0), 1), 0xFFFFFFFF) if p > 0 else 0
+    return (h >= t).view(N, F)
 
 
 class DistributedBatchNorm1D(nn.Module):
@@ -190,8 +222,10 @@ class DistributedBatchNorm1D(nn.Module):
         self.recompute = recompute
         self.group = group
 
-    def forward(self, x: torch.Tensor, relu: bool = False) -> torch.Tensor:
-        """``BN(x)``, or ``relu(BN(x))`` fused into the same kernels when ``relu``."""
+    def forward(self, x: torch.Tensor, relu: bool = False, dropout: float = 0.0) -> torch.Tensor:
+        """``BN(x)``, or ``relu(BN(x))`` fused into the same kernels when ``relu``; in
+        training, ``dropout`` > 0 applies dropout after the activation in the same pass
+        (mask regenerated in backward, never stored)."""
         squeeze = False
         if x.dim() == 3:
             if x.size(0) != 1:
@@ -202,7 +236,8 @@ class DistributedBatchNorm1D(nn.Module):
         if self.training or not self.track_running_stats:
             box: list = []
             y, mean, var = _SyncBNFn.apply(x, self.gamma, self.beta, self.eps, self.group,
-                                           self.recompute, box, relu)
+                                           self.recompute, box, relu,
+                                           float(dropout) if self.training else 0.0)
             if self.training and self.track_running_stats:
                 with torch.no_grad():
                     self.num_batches_tracked += 1

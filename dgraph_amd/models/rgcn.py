@@ -107,12 +107,13 @@ class CommAwareRGCN(nn.Module):
 
     def _head(self, h: torch.Tensor) -> torch.Tensor:
         lin1, bn, _, drop, lin2 = self.mlp
-        t = bn(self._lin(lin1, h), relu=True)
-        return self._lin(lin2, drop(t))
+        t = bn(self._lin(lin1, h), relu=True, dropout=drop.p)  # BN + ReLU + dropout fused
+        return self._lin(lin2, t)
 
     def _finish(self, l: int, t: torch.Tensor) -> torch.Tensor:
-        t = self.bns[l](t, relu=True)  # BN + ReLU fused (native kernels on GPU)
-        return F.dropout(t, self.dropout, self.training)
+        # BN + ReLU + dropout in one pass (native kernels on GPU; the dropout mask is
+        # regenerated from a seed in backward: no mask tensor, no masked-scale pass)
+        return self.bns[l](t, relu=True, dropout=self.dropout)
 
     def forward(self, xs, graph, edge_types=None) -> torch.Tensor:
         """``forward(xs, HeteroGraph)`` (hot path), or the RelationGraph path with either

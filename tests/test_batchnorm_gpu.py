@@ -81,3 +81,44 @@ def test_empty_rows():
     x = torch.zeros(0, 16, device=DEV, dtype=torch.bfloat16)
     n, mean, var = _local_moments(x)
     assert n == 0 and mean.numel() == 16
+
+
+@pytest.mark.parametrize("F", [7, 153, 256])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("p", [0.1, 0.5])
+def test_fused_dropout_matches_reference(F, dtype, p):
+    """BN + ReLU + dropout in the native kernels (mask regenerated from the seed in the
+    backward reduce and apply passes) vs an fp64 reference using the same counter-based
+    mask (models/norm.dropout_keep_mask): forward values, keep fraction, dx, dgamma, dbeta."""
+    from dgraph_amd.models.norm import dropout_keep_mask
+
+    torch.manual_seed(5)
+    x = _data(3001, F, dtype, seed=F + 7)
+    bn = DistributedBatchNorm1D(F).to(DEV)
+    with torch.no_grad():
+        bn.gamma.uniform_(0.5, 1.5)
+        bn.beta.uniform_(-0.5, 0.5)
+    xg = x.clone().requires_grad_(True)
+    torch.manual_seed(11)
+    y = bn(xg, relu=True, dropout=p)
+    torch.manual_seed(11)
+    seed = int(torch.randint(0, 1 << 62, (1,), dtype=torch.int64).item())  # the same draw
+    keep = dropout_keep_mask(seed, x.shape[0], F, "cpu", p).double()
+    frac = float(keep.mean())
+    assert abs(frac - (1 - p)) < 0.03, frac
+    dy = torch.randn(y.shape, generator=torch.Generator().manual_seed(3)).to(dtype).to(DEV)
+    y.backward(dy)
+    ref = torch.nn.BatchNorm1d(F, eps=bn.eps).double()
+    with torch.no_grad():
+        ref.weight.copy_(bn.gamma.detach().reshape(-1).double().cpu())
+        ref.bias.copy_(bn.beta.detach().reshape(-1).double().cpu())
+    xr = x.detach().cpu().double().requires_grad_(True)
+    yr = torch.relu(ref(xr)) * keep / (1 - p)
+    yr.backward(dy.cpu().double())
+    tol = dict(atol=6e-2, rtol=3e-2) if dtype == torch.bfloat16 else dict(atol=5e-4, rtol=5e-4)
+    torch.testing.assert_close(y.detach().cpu().double(), yr.detach(), **tol)
+    torch.testing.assert_close(xg.grad.cpu().double(), xr.grad, **tol)
+    torch.testing.assert_close(bn.gamma.grad.reshape(-1).cpu().double(), ref.weight.grad,
+                               atol=tol["atol"] * 40, rtol=tol["rtol"])
+    torch.testing.assert_close(bn.beta.grad.reshape(-1).cpu().double(), ref.bias.grad,
+                               atol=tol["atol"] * 40, rtol=tol["rtol"])
