@@ -293,46 +293,10 @@ def derive_features_by_mean(src_feats_global: torch.Tensor, edges: torch.Tensor,
     return aggregate(src_feats_global, csr, reduce="mean")
 
 
-class DGraph_MAG240M_Dataset(DistributedHeteroGraphDataset):  # noqa: N801 - reference name
-    """Real MAG240M via ``ogb.lsc.MAG240MDataset`` (MAG240M_dataset.py:116-320).
-
-    Contiguous per-type blocks; paper features are the real 768-d fp16 features read
-    row-range-wise from the memory map when ``real_features=True`` (the reference replaced
-    them by ``randn(n, 1)``), author / institution features are then derived by mean
-    aggregation. Needs the ``ogb`` package and the dataset on disk (not available offline
-    here: construction raises ImportError)."""
-
-    def __init__(self, comm, data_dir: str = "data/MAG240M", real_features: bool = False,
-                 num_features: int = 1, cache_dir: Optional[str] = None):
-        try:
-            from ogb.lsc import MAG240MDataset  # type: ignore
-        except ImportError as e:
-            raise ImportError("DGraph_MAG240M_Dataset needs the `ogb` package and the "
-                              "MAG240M files; use SyntheticHeterogeneousDataset") from e
-        rank, W = comm.get_rank(), comm.get_world_size()
-        ds = MAG240MDataset(root=data_dir)
-        counts = [ds.num_papers, ds.num_authors, ds.num_institutions]
-        offsets = {t: get_vertex_offsets(n, W) for t, n in enumerate(counts)}
-        split = {"train": torch.from_numpy(ds.get_idx_split("train")).long(),
-                 "val": torch.from_numpy(ds.get_idx_split("valid")).long(),
-                 "test": torch.from_numpy(ds.get_idx_split("test-dev")).long()}
-        labels = torch.from_numpy(ds.paper_label).nan_to_num(0).long()
-        p2p = torch.from_numpy(ds.edge_index("paper", "cites", "paper")).long()
-        p2p = torch.cat([p2p, p2p.flip(0)], dim=1)
-        a2p = torch.from_numpy(ds.edge_index("author", "writes", "paper")).long()
-        a2i = torch.from_numpy(ds.edge_index("author", "institution")).long()
-        feats = []
-        g = _generator(0)
-        for t, n in enumerate(counts):
-            lo, hi = int(offsets[t][rank]), int(offsets[t][rank + 1])
-            if t == 0 and real_features:
-                feats.append(torch.from_numpy(ds.paper_feat[lo:hi]).float())
-            else:
-                feats.append(torch.randn(hi - lo, num_features, generator=g))
-        rel_edges = {(0, 0): p2p, (0, 1): a2p.flip(0), (1, 0): a2p, (1, 2): a2i,
-                     (2, 1): a2i.flip(0)}
-        group = getattr(comm, "group", None)
-        rels = [build_relation_graph(rel_edges[et], et[0], et[1], offsets, rank, W, group)
-                for et in EDGE_TYPES]
-        super().__init__(rank, W, feats[0].shape[1], ds.num_classes, feats, offsets, labels,
-                         split, rels)
+def __getattr__(name):
+    # The real-MAG240M dataset reads the on-disk layout directly (no ``ogb``):
+    # data/mag240m.py (imported lazily: it builds on this module).
+    if name == "DGraph_MAG240M_Dataset":
+        from .mag240m import DGraph_MAG240M_Dataset
+        return DGraph_MAG240M_Dataset
+    raise AttributeError(name)

@@ -111,3 +111,60 @@ def test_synthetic_shape_counts():
     p = build_partition(shape, 0, 1, "cpu")
     assert p["csr"].nnz == 2 * shape.num_directed_edges
     assert p["L"] == shape.num_nodes
+
+
+def _community_graph(k=4, n=25, p_in=0.4, n_bridge=6, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    es = []
+    for c in range(k):
+        pairs = torch.combinations(torch.arange(n), 2)
+        keep = torch.rand(pairs.shape[0], generator=g) < p_in
+        es.append(pairs[keep].t() + c * n)
+    es.append(torch.randint(0, k * n, (2, n_bridge), generator=g))
+    ei = torch.cat(es, 1)
+    return k * n, ei[:, ei[0] != ei[1]]
+
+
+def _dlp_worker(rank, world, parts):
+    import torch.distributed as dist
+
+    from dgraph_amd.data.partition import distributed_label_propagation
+
+    V, ei = _community_graph()
+    init = torch.randint(0, parts, (V,), generator=torch.Generator().manual_seed(3))
+    # this rank owns adjacency rows [lo, hi) (both directions), global column ids
+    lo, hi = rank * V // world, (rank + 1) * V // world
+    rows = torch.cat([ei[0], ei[1]])
+    cols = torch.cat([ei[1], ei[0]])
+    m = (rows >= lo) & (rows < hi)
+    r, c = rows[m] - lo, cols[m]
+    o = torch.argsort(r * V + c)
+    r, c = r[o], c[o]
+    rowptr = torch.zeros(hi - lo + 1, dtype=torch.long)
+    rowptr[1:] = torch.cumsum(torch.bincount(r, minlength=hi - lo), 0)
+    part = distributed_label_propagation(rowptr, c, lo, V, parts, rounds=30, imbalance=0.1,
+                                         init=init, seed=1)
+    got = [torch.empty_like(part) for _ in range(world)]
+    dist.all_gather(got, part)
+    assert all(torch.equal(x, part) for x in got), "part vectors diverged across ranks"
+    s0 = partition_stats(ei, init, parts, symmetric=True)
+    s1 = partition_stats(ei, part, parts, symmetric=True)
+    assert s1["edge_cut_frac"] < 0.5 * s0["edge_cut_frac"], (s0["edge_cut_frac"], s1["edge_cut_frac"])
+    assert s1["imbalance"] <= 1.1 + 1e-6
+    assert s1["halo_rows_total"] < s0["halo_rows_total"]
+
+
+@pytest.mark.parametrize("world", [1, 2, 4])
+def test_distributed_label_propagation(world):
+    from conftest import run_ranks
+
+    run_ranks(_dlp_worker, world, 4)
+
+
+def test_partition_stats_symmetric_matches_concatenated():
+    V, ei = _community_graph()
+    part = torch.randint(0, 3, (V,), generator=torch.Generator().manual_seed(5))
+    a = partition_stats(ei, part, 3, symmetric=True)
+    b = partition_stats(torch.cat([ei, ei.flip(0)], 1), part, 3)
+    assert a["edge_cut_frac"] == b["edge_cut_frac"]
+    assert torch.equal(a["pair_matrix"], b["pair_matrix"])
