@@ -10,6 +10,7 @@
 #include <torch/library.h>
 
 #include "check.h"
+#include "host/plan_check.h"
 #include "kernels/kernels.h"
 
 namespace dgraph {
@@ -447,7 +448,9 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> layer_norm_bwd_op(
               "mean/rstd must be fp32 [N]");
   const float* gp = opt_f32(gamma, x, "gamma");
   auto dx = at::empty_like(x);
-  const int64_t nb = std::max<int64_t>(1, std::min<int64_t>(1024, (N + 255) / 256));
+  // 4096 blocks x 4 waves keeps ~16 waves per CU streaming; the [nb, 2, F] fp32 partials
+  // (4 MB at F = 128) are summed in a fixed order below
+  const int64_t nb = std::max<int64_t>(1, std::min<int64_t>(4096, (N + 255) / 256));
   auto partial = at::empty({nb, 2, F}, x.options().dtype(at::kFloat));
   c10::DeviceGuard g(x.device());
   DG_HIP_CHECK(layer_norm_bwd(dtype_of(x), dy.data_ptr(), x.data_ptr(), mean.data_ptr<float>(),
@@ -613,9 +616,61 @@ void set_dual_gemm_variant_op(int64_t variant) {
 }
 int64_t get_dual_gemm_variant_op() { return dgraph::get_dual_gemm_variant(); }
 
+// --- host-side plan validation (csrc/host/plan_check.*; DGRAPH_CHECK_PLANS=1) ----------
+namespace {
+at::Tensor host_i64(const at::Tensor& t) { return t.to(at::kCPU, at::kLong).contiguous(); }
+
+void raise_if_bad(const dgraph::host::CheckResult& r, const char* what) {
+  TORCH_CHECK(r.ok, what, ": ", r.what, " (at index ", r.where, ")");
+}
+}  // namespace
+
+void validate_csr_op(const at::Tensor& rowptr, const at::Tensor& col, int64_t ncols) {
+  const at::Tensor rp = host_i64(rowptr);
+  TORCH_CHECK(col.scalar_type() == at::kInt || col.scalar_type() == at::kLong,
+              "validate_csr: col must be int32 or int64");
+  const at::Tensor c = col.to(at::kCPU).contiguous();
+  raise_if_bad(dgraph::host::check_csr(rp.data_ptr<int64_t>(), rp.numel() - 1, c.data_ptr(),
+                                       static_cast<int>(c.element_size()), c.numel(), ncols),
+               "validate_csr");
+}
+
+void validate_row_map_op(const at::Tensor& row_map, int64_t nrows_out) {
+  const at::Tensor m = host_i64(row_map);
+  raise_if_bad(dgraph::host::check_row_map(m.data_ptr<int64_t>(), m.numel(), nrows_out),
+               "validate_row_map");
+}
+
+void validate_hub_split_op(const at::Tensor& rowptr, const at::Tensor& seg_row,
+                           const at::Tensor& seg_lo, const at::Tensor& seg_hi, int64_t head) {
+  const at::Tensor rp = host_i64(rowptr), r = host_i64(seg_row), lo = host_i64(seg_lo),
+                   hi = host_i64(seg_hi);
+  TORCH_CHECK(r.numel() == lo.numel() && r.numel() == hi.numel(), "segment arrays differ");
+  raise_if_bad(dgraph::host::check_hub_split(rp.data_ptr<int64_t>(), rp.numel() - 1,
+                                             r.data_ptr<int64_t>(), lo.data_ptr<int64_t>(),
+                                             hi.data_ptr<int64_t>(), r.numel(), head),
+               "validate_hub_split");
+}
+
+void validate_splits_op(const at::Tensor& send, const at::Tensor& recv, int64_t total_send,
+                        int64_t total_recv) {
+  const at::Tensor s = host_i64(send), r = host_i64(recv);
+  TORCH_CHECK(s.numel() == r.numel(), "split vectors differ in length");
+  raise_if_bad(dgraph::host::check_splits(s.data_ptr<int64_t>(), r.data_ptr<int64_t>(),
+                                          static_cast<int>(s.numel()), total_send, total_recv),
+               "validate_splits");
+}
+
 TORCH_LIBRARY(dgraph_amd, m) {
   m.def("set_dual_gemm_variant(int variant) -> ()", &set_dual_gemm_variant_op);
   m.def("get_dual_gemm_variant() -> int", &get_dual_gemm_variant_op);
+  m.def("validate_csr(Tensor rowptr, Tensor col, int ncols) -> ()", &validate_csr_op);
+  m.def("validate_row_map(Tensor row_map, int nrows_out) -> ()", &validate_row_map_op);
+  m.def("validate_hub_split(Tensor rowptr, Tensor seg_row, Tensor seg_lo, Tensor seg_hi, "
+        "int head=0) -> ()",
+        &validate_hub_split_op);
+  m.def("validate_splits(Tensor send, Tensor recv, int total_send, int total_recv) -> ()",
+        &validate_splits_op);
   m.def("set_spmm_config(int variant, int xcd, int pass_cols=-1) -> ()", &set_spmm_config_op);
   m.def("bias_relu_pack(Tensor(a!) y, Tensor? bias, Tensor(b!)? bits, bool relu) -> ()");
   m.def("relu_mask_bwd(Tensor(a!) g, Tensor bits) -> ()");

@@ -30,6 +30,19 @@ __global__ __launch_bounds__(256) void layer_norm_fwd_kernel(
   const int64_t wave = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
   const float invF = 1.f / static_cast<float>(F);
+  // a lane owns the same columns in every row: gamma / beta live in registers for the
+  // whole grid-stride loop (per-row per-element loads made the kernel issue-bound)
+  float ga[CH][VEC], be[CH][VEC];
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int f = (c * LPR + l) * VEC;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      const bool in = gamma != nullptr && f + i < F;
+      ga[c][i] = in ? gamma[f + i] : 1.f;
+      be[c][i] = in ? beta[f + i] : 0.f;
+    }
+  }
   for (int64_t base = wave * G; base < N; base += nwaves * G) {
     const int64_t r = base + g;
     const bool valid = r < N;
@@ -78,8 +91,7 @@ __global__ __launch_bounds__(256) void layer_norm_fwd_kernel(
       if constexpr (RES) load_vec_f32<T, VEC>(res + r * F + f, rr);
 #pragma unroll
       for (int i = 0; i < VEC; ++i) {
-        float t = (v[c][i] - mu) * rs;
-        if (gamma) t = t * gamma[f + i] + beta[f + i];
+        float t = (v[c][i] - mu) * rs * ga[c][i] + be[c][i];
         if constexpr (RES) t += rr[i];
         o[i] = t;
       }
@@ -102,11 +114,16 @@ __global__ __launch_bounds__(256) void layer_norm_bwd_kernel(
   const int64_t wave = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
   const float invF = 1.f / static_cast<float>(F);
-  float dg[CH][VEC], db[CH][VEC];
+  float dg[CH][VEC], db[CH][VEC], ga[CH][VEC];
 #pragma unroll
-  for (int c = 0; c < CH; ++c)
+  for (int c = 0; c < CH; ++c) {
+    const int f = (c * LPR + l) * VEC;
 #pragma unroll
-    for (int i = 0; i < VEC; ++i) dg[c][i] = db[c][i] = 0.f;
+    for (int i = 0; i < VEC; ++i) {
+      dg[c][i] = db[c][i] = 0.f;
+      ga[c][i] = (gamma != nullptr && f + i < F) ? gamma[f + i] : 1.f;
+    }
+  }
   for (int64_t base = wave * G; base < N; base += nwaves * G) {
     const int64_t r = base + g;
     const bool valid = r < N;
@@ -126,7 +143,7 @@ __global__ __launch_bounds__(256) void layer_norm_bwd_kernel(
           xh[c][i] = (xv[i] - mu) * rs;
           dg[c][i] += gy[c][i] * xh[c][i];
           db[c][i] += gy[c][i];
-          const float d = gamma ? gy[c][i] * gamma[f + i] : gy[c][i];
+          const float d = gy[c][i] * ga[c][i];
           gy[c][i] = d;  // now dxhat
           s1 += d;
           s2 += d * xh[c][i];

@@ -68,6 +68,7 @@ def _common_flags():
 
 def _sources():
     srcs = sorted(CSRC.rglob("*.hip")) + sorted(CSRC.rglob("*.cpp"))
+    srcs = [s for s in srcs if not s.name.startswith("test_")]  # host test drivers (main())
     headers = sorted(CSRC.rglob("*.h")) + sorted(CSRC.rglob("*.hpp"))
     return srcs, headers
 

@@ -99,18 +99,70 @@ class PlanError(ValueError):
     pass
 
 
+def _native_ops():
+    """The native host checkers (csrc/host/plan_check.cpp) when the library is loaded."""
+    try:
+        from .. import _native
+
+        if _native.load():
+            ops = _native.ops()
+            return ops if hasattr(ops, "validate_csr") else None
+    except Exception:  # noqa: BLE001 - fall back to the torch checks
+        pass
+    return None
+
+
+def _raise_native(fn, *args) -> None:
+    try:
+        fn(*args)
+    except RuntimeError as e:
+        raise PlanError(str(e).split("\n")[0]) from None
+
+
 def _check_csr(csr, name: str, num_rows: int, num_cols: int) -> None:
     rp, col = csr.rowptr, csr.col
     if rp.numel() != num_rows + 1:
         raise PlanError(f"{name}: rowptr has {rp.numel()} entries, expected {num_rows + 1}")
-    if int(rp[0]) != 0 or int(rp[-1]) != col.numel():
-        raise PlanError(f"{name}: rowptr must start at 0 and end at nnz={col.numel()}")
-    if rp.numel() > 1 and bool((rp[1:] < rp[:-1]).any()):
-        raise PlanError(f"{name}: rowptr is not monotone")
-    if col.numel():
-        lo, hi = int(col.min()), int(col.max())
-        if lo < 0 or hi >= num_cols:
-            raise PlanError(f"{name}: column ids span [{lo}, {hi}], outside [0, {num_cols})")
+    ops = _native_ops()
+    if ops is not None:  # multi-threaded host scan (and the sanitized code path)
+        _raise_native(ops.validate_csr, rp, col, int(num_cols))
+    else:
+        if int(rp[0]) != 0 or int(rp[-1]) != col.numel():
+            raise PlanError(f"{name}: rowptr must start at 0 and end at nnz={col.numel()}")
+        if rp.numel() > 1 and bool((rp[1:] < rp[:-1]).any()):
+            raise PlanError(f"{name}: rowptr is not monotone")
+        if col.numel():
+            lo, hi = int(col.min()), int(col.max())
+            if lo < 0 or hi >= num_cols:
+                raise PlanError(f"{name}: column ids span [{lo}, {hi}], outside [0, {num_cols})")
+    _check_derived(csr, name, num_rows, ops)
+
+
+def _check_derived(csr, name: str, num_rows: int, ops) -> None:
+    """Row-compacted copies (row_map: a duplicated output row would be a write race) and
+    hub splits (segments must tile each hub row exactly) cached on ``csr``."""
+    comp = getattr(csr, "_compact", None)
+    if comp is not None and comp.row_map is not None:
+        rm = comp.row_map
+        if ops is not None:
+            _raise_native(ops.validate_row_map, rm, int(num_rows))
+        elif rm.numel():
+            if int(rm.min()) < 0 or int(rm.max()) >= num_rows:
+                raise PlanError(f"{name}: row_map outside [0, {num_rows})")
+            if torch.unique(rm).numel() != rm.numel():
+                raise PlanError(f"{name}: row_map repeats an output row (write race)")
+    hub = getattr(csr, "_hub", None)
+    hub = hub[1] if hub else None  # cached as (cap, HubSplit or None)
+    if hub is not None and ops is not None and hub.num_segments:
+        # hub_rows are OUTPUT rows; the segments index this CSR's rows
+        rows = torch.nonzero(csr.degree() > hub.cap).reshape(-1)
+        out = rows if csr.row_map is None else csr.row_map[rows]
+        if not torch.equal(out.cpu().long(), hub.hub_rows.cpu().long()):
+            raise PlanError(f"{name}: hub rows do not match the rows longer than {hub.cap}")
+        seg_row = torch.repeat_interleave(rows.long(),
+                                          (hub.hub_seg_ptr[1:] - hub.hub_seg_ptr[:-1]).long())
+        _raise_native(ops.validate_hub_split, csr.rowptr, seg_row, hub.seg_beg, hub.seg_end,
+                      int(hub.cap))
 
 
 def validate_graph(graph) -> None:
@@ -128,6 +180,10 @@ def validate_graph(graph) -> None:
             raise PlanError(f"recv splits sum {graph.a2a.total_recv} != halo rows {H}")
         if graph.a2a.total_send != idx.numel():
             raise PlanError(f"send splits sum {graph.a2a.total_send} != {idx.numel()} rows")
+        ops = _native_ops()
+        if ops is not None:
+            _raise_native(ops.validate_splits, torch.tensor(list(graph.a2a.send_splits)),
+                          torch.tensor(list(graph.a2a.recv_splits)), idx.numel(), H)
         if dist.is_available() and dist.is_initialized():
             # every peer's send count to me equals my recv count from it
             dev = idx.device if idx.is_cuda else torch.device("cpu")
