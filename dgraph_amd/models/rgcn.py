@@ -32,6 +32,7 @@ import torch.nn.functional as F
 
 from ..ops.aggregate import aggregate
 from ..ops.dense import linear as _dense_linear
+from ..ops.dense import linear_sum
 from ..parallel.hetero_graph import SourceGraph, source_aggregate
 from .norm import DistributedBatchNorm1D
 
@@ -131,7 +132,11 @@ class CommAwareRGCN(nn.Module):
         need, rels = layer_plan(ets, self.num_layers, self.target, avail)
         h = dict(xs)
         for l in range(self.num_layers):
-            tmp = {t: self._lin(self.skips[l], h[t]) for t in sorted(need[l])}
+            tmp = {t: self._lin(self.skips[l], h[t]) for t in sorted(need[l])} if l == 0 else {}
+            # layers > 0: skip + one linear per relation summed by ONE fused op per
+            # destination type (the MFMA dual GEMM chains the running sum: no per-term
+            # outputs, no elementwise adds)
+            terms = {t: [(h[t], self.skips[l].weight)] for t in sorted(need[l])} if l else {}
             by_src: Dict[int, List[int]] = {}
             for r in rels[l]:
                 by_src.setdefault(ets[r][0], []).append(r)
@@ -154,8 +159,9 @@ class CommAwareRGCN(nn.Module):
                     spec = [(r, 0, h[s].shape[1]) for r in rs]
                     outs = source_aggregate(h[s], sg, spec)
                     for r, o in zip(rs, outs):
-                        d = ets[r][1]
-                        tmp[d] = tmp[d].add_(self._lin(self.convs[l][r], o))
+                        terms[ets[r][1]].append((o, self.convs[l][r].weight))
+            for t, tl in terms.items():
+                tmp[t] = linear_sum(tl, self.skips[l].bias)
             h = {t: self._finish(l, v) for t, v in tmp.items()}
         return self._head(h[self.target])
 

@@ -151,7 +151,7 @@ class _LinearFn(torch.autograd.Function):
 def linear(x: torch.Tensor, W: torch.Tensor, b=None) -> torch.Tensor:
     """Drop-in for ``F.linear`` with a tall-skinny-aware backward."""
     if torch.is_autocast_enabled() and x.is_cuda:
-        dt = torch.get_autocast_gpu_dtype()
+        dt = torch.get_autocast_dtype("cuda")
         x, W = x.to(dt), W.to(dt)
         b = None if b is None else b.to(dt)
     return _LinearFn.apply(x, W, b)
@@ -186,3 +186,89 @@ def dual_gemm(A1: torch.Tensor, B1t: torch.Tensor, A2=None, B2t=None, bias=None,
 def dual_gemm_shape_ok(N: int, K1: int, K2: int = 0) -> bool:
     ks = (128, 192, 256)
     return N in ks and K1 in ks and (K2 == 0 or K2 in ks)
+
+
+def _native_linear_sum_ok(xs, Ws, acc) -> bool:
+    N = Ws[0].shape[0]
+    if not (xs[0].is_cuda and all(x.dtype == torch.bfloat16 for x in xs)):
+        return False
+    if acc is not None and (acc.dtype != torch.bfloat16 or not acc.is_contiguous()
+                            or acc.shape != (xs[0].shape[0], N)):
+        return False
+    return all(x.dim() == 2 and x.is_contiguous() and W.shape[0] == N
+               and dual_gemm_shape_ok(N, x.shape[1]) for x, W in zip(xs, Ws))
+
+
+class _LinearSumFn(torch.autograd.Function):
+    """``y = sum_i x_i W_i^T + b (+ acc)`` (R-GCN: skip + one linear per relation into the
+    same destination). On the GPU the terms go through the native MFMA dual GEMM two at a
+    time, chaining the running sum through its ``cin`` input, so the per-term outputs and
+    the elementwise adds never touch HBM; backward: ``dx_i = g W_i`` on the same kernel,
+    split-K ``dW_i``, native column-sum ``db``, ``dacc = g``."""
+
+    @staticmethod
+    def forward(ctx, b, acc, *flat):
+        xs, Ws = list(flat[0::2]), list(flat[1::2])
+        ctx.save_for_backward(*flat)
+        ctx.has_b, ctx.has_acc = b is not None, acc is not None
+        ctx.native = _native_linear_sum_ok(xs, Ws, acc)
+        if ctx.native:
+            out = torch.empty(xs[0].shape[0], Ws[0].shape[0], dtype=xs[0].dtype,
+                              device=xs[0].device)
+            cin = acc
+            for k in range(0, len(xs), 2):
+                two = k + 1 < len(xs)
+                dual_gemm(xs[k], Ws[k].to(xs[k].dtype), xs[k + 1] if two else None,
+                          Ws[k + 1].to(xs[k].dtype) if two else None,
+                          bias=b if k == 0 else None, cin=cin, out=out)
+                cin = out
+            return out
+        out = torch.nn.functional.linear(xs[0], Ws[0], b)
+        for x, W in zip(xs[1:], Ws[1:]):
+            out = out + torch.nn.functional.linear(x, W)
+        return out if acc is None else out + acc
+
+    @staticmethod
+    def backward(ctx, g):
+        flat = ctx.saved_tensors
+        xs, Ws = flat[0::2], flat[1::2]
+        g = g.contiguous()
+        grads = []
+        for i, (x, W) in enumerate(zip(xs, Ws)):
+            dx = dW = None
+            if ctx.needs_input_grad[2 + 2 * i]:
+                if ctx.native and dual_gemm_shape_ok(x.shape[1], W.shape[0]):
+                    dx = dual_gemm(g, W.to(g.dtype).t().contiguous())
+                else:
+                    dx = g @ W.to(g.dtype)
+            if ctx.needs_input_grad[3 + 2 * i]:
+                if g.is_cuda:
+                    L = g.shape[0]
+                    dW = wgrad(g, x, 0 if L >= 1 << 23 else _auto_rows_per_chunk(L))
+                else:
+                    adt = torch.float64 if g.dtype == torch.float64 else torch.float32
+                    dW = g.t().to(adt) @ x.to(adt)
+                dW = dW.to(W.dtype)
+            grads += [dx, dW]
+        db = None
+        if ctx.has_b and ctx.needs_input_grad[0]:
+            db = col_sum_f32(g) if g.is_cuda else \
+                g.to(torch.float64 if g.dtype == torch.float64 else torch.float32).sum(0)
+        dacc = g if ctx.has_acc and ctx.needs_input_grad[1] else None
+        return (db, dacc, *grads)
+
+
+def linear_sum(terms, b=None, acc=None) -> torch.Tensor:
+    """``sum_i x_i W_i^T + b (+ acc)`` for ``terms = [(x_i, W_i), ...]`` (see
+    :class:`_LinearSumFn`)."""
+    xs = [x for x, _ in terms]
+    Ws = [W for _, W in terms]
+    if torch.is_autocast_enabled() and xs[0].is_cuda:
+        dt = torch.get_autocast_dtype("cuda")
+        xs = [x.to(dt) for x in xs]
+        Ws = [W.to(dt) for W in Ws]
+        b = None if b is None else b.to(dt)
+        acc = None if acc is None else acc.to(dt)
+    flat = [t for pair in zip(xs, Ws) for t in pair]
+    out = _LinearSumFn.apply(b, acc, *flat)
+    return out
