@@ -230,10 +230,18 @@ class DGraph_MAG240M_Dataset(DistributedHeteroGraphDataset):  # noqa: N801 - ref
     @staticmethod
     def _relations(files, comm, offsets, rank, W, data_dir, cached):
         path = cached or DGraph_MAG240M_Dataset.plan_path(data_dir, rank, W)
+        # fingerprint of what the plans depend on (sizes, world, rank, per-type ownership):
+        # a file written for another partition or world size is rebuilt, not trusted
+        meta = torch.cat([torch.tensor([files.num_papers, files.num_authors,
+                                        files.num_institutions, W, rank])]
+                         + [offsets[t].long() for t in range(3)])
         if osp.exists(path):
             d = torch.load(path, weights_only=True)
-            return [RelationGraph.from_state_dict(d[PLAN_KEYS[et]]) for et in EDGE_TYPES]
-        if cached:
+            if "_meta" not in d or torch.equal(d["_meta"], meta):
+                return [RelationGraph.from_state_dict(d[PLAN_KEYS[et]]) for et in EDGE_TYPES]
+            if cached:
+                raise ValueError(f"{cached}: plans were built for another partition/world size")
+        elif cached:
             raise FileNotFoundError(cached)
         def load(*k):
             return torch.from_numpy(np.array(files.edge_index(*k), dtype=np.int64))
@@ -247,5 +255,7 @@ class DGraph_MAG240M_Dataset(DistributedHeteroGraphDataset):  # noqa: N801 - ref
         group = getattr(comm, "group", None)
         rels = [build_relation_graph(rel_edges[et], et[0], et[1], offsets, rank, W, group)
                 for et in EDGE_TYPES]
-        torch.save({PLAN_KEYS[et]: r.state_dict() for et, r in zip(EDGE_TYPES, rels)}, path)
+        d = {PLAN_KEYS[et]: r.state_dict() for et, r in zip(EDGE_TYPES, rels)}
+        d["_meta"] = meta
+        torch.save(d, path)
         return rels

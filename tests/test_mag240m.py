@@ -142,3 +142,20 @@ def _mag_dist(rank, world, d):
 def test_dataset_distributed(tmp_path, ranks, world):
     d = make_fake_mag(str(tmp_path))
     ranks(_mag_dist, world, d)
+
+
+def test_stale_plan_file_is_rebuilt(tmp_path):
+    from dgraph_amd.data import mag240m
+
+    d = make_fake_mag(str(tmp_path))
+    mag240m.DGraph_MAG240M_Dataset(_Comm(), data_dir=d)
+    path = os.path.join(d, "MAG240M_dataset_rank_0_of_1_comm_plans.pt")
+    blob = torch.load(path, weights_only=True)
+    blob["_meta"][0] += 1  # pretend it was written for another graph
+    torch.save(blob, path)
+    with pytest.raises(ValueError):
+        mag240m.DGraph_MAG240M_Dataset(_Comm(), data_dir=d, cached_comm_plans=path)
+    ds = mag240m.DGraph_MAG240M_Dataset(_Comm(), data_dir=d)  # default path: rebuilt
+    assert torch.equal(torch.load(path, weights_only=True)["_meta"][:3],
+                       torch.tensor([NP, NA, NI]))
+    assert ds.num_relations == 5
