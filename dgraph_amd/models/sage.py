@@ -319,7 +319,11 @@ class SAGEStackFn(Function):
                 h = y_rows
                 break
             if pf:
-                z = torch.mm(h, wn_, out=V("tmp_a", Fo))
+                z = V("tmp_a", Fo)
+                if fused:  # the projection on the same streaming MFMA kernel
+                    dual_gemm(h, wn_.t().contiguous(), out=z)
+                else:
+                    torch.mm(h, wn_, out=z)
                 graph.aggregate(z, mean=True, out=y)
                 del z
                 if fused:

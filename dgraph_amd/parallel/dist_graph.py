@@ -315,17 +315,30 @@ class DistGraph:
         back only the halo rows that carry a contribution, with exactly the result of the
         dense call. The first call for a row set is collective (sub-plan exchange)."""
         it, cs_rows, sub = self._restricted(rows)
-        cs = cs_rows if mean else None
         g_rows = g_rows.contiguous()
+        if mean:
+            # the column scale applies to the |rows| gradient rows: scale them once (a
+            # 1 %-of-V pass) instead of gathering a per-edge scale inside the SpMM
+            g_rows = (g_rows.float() * cs_rows.unsqueeze(1)).to(g_rows.dtype) \
+                if g_rows.dtype != torch.float64 else g_rows * cs_rows.unsqueeze(1)
         self.edges_aggregated += it.nnz + (sub[0].nnz if sub is not None else 0)
+        # A[rows, :]^T touches only the ~30 % of vertices adjacent to a loss row: run the
+        # SpMM over those rows (row-compacted, output row map) and zero-fill the rest,
+        # instead of walking all V rows of a 1 %-dense transposed block
+        itc = it.compact_rows()
+        if out is None:
+            out = torch.empty(it.num_rows, g_rows.shape[1], dtype=g_rows.dtype,
+                              device=g_rows.device)
+        out.zero_()
         if sub is None:
-            return K.spmm(it.rowptr, it.col, g_rows, out, col_scale=cs, split=_hs(it))
+            K.spmm(itc.rowptr, itc.col, g_rows, out, split=_hs(itc), row_map=itc.row_map)
+            return out
         ht_nz, a2a_sub, st = sub[:3]
-        hg = K.spmm(ht_nz.rowptr, ht_nz.col, g_rows, col_scale=cs, split=_hs(ht_nz))
+        hg = K.spmm(ht_nz.rowptr, ht_nz.col, g_rows, split=_hs(ht_nz))
         sg, work = a2a_sub(hg, async_op=True)
         if not self.overlap:
             work.wait()
-        out = K.spmm(it.rowptr, it.col, g_rows, out, col_scale=cs, split=_hs(it))
+        K.spmm(itc.rowptr, itc.col, g_rows, out, split=_hs(itc), row_map=itc.row_map)
         work.wait()
         K.spmm(st.rowptr, st.col, sg, out, beta=1.0, split=_hs(st))
         return out

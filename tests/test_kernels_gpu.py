@@ -556,9 +556,9 @@ def test_sage_stack_fused_dual_gemm_matches_unfused(monkeypatch):
         loss = out.float().square().mean()
         loss.backward()
         res[fused] = (out.float().cpu(), [q.grad.cpu() for q in m.parameters()], len(calls))
-    # 3 full-row forward combines (the output layer is computed for every vertex) +
-    # 2 backward input-gradient combines
-    assert res[True][2] == 5 and res[False][2] == 0
+    # 3 full-row forward combines (the output layer is computed for every vertex) + the
+    # project-first output layer's projection + 2 backward input-gradient combines
+    assert res[True][2] == 6 and res[False][2] == 0
     torch.testing.assert_close(res[True][0], res[False][0], atol=5e-2, rtol=5e-2)
     for a, b in zip(res[True][1], res[False][1]):
         rel = (a - b).norm() / b.norm().clamp_min(1e-12)
