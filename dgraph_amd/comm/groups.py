@@ -31,11 +31,12 @@ def default_device() -> torch.device:
     return torch.device("cpu")
 
 
-def ensure_process_group(backend: Optional[str] = None, **kwargs) -> None:
+def ensure_process_group(backend: Optional[str] = None, **kwargs) -> bool:
     """Initialise the default process group if needed (env:// rendezvous, or a private
-    single-rank store when no launcher variables are present)."""
+    single-rank store when no launcher variables are present). Returns True when this call
+    created it (the caller then owns its teardown)."""
     if dist.is_initialized():
-        return
+        return False
     if backend is None or backend == "auto":
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     if backend == "nccl" and not torch.cuda.is_available():
@@ -57,6 +58,7 @@ def ensure_process_group(backend: Optional[str] = None, **kwargs) -> None:
     else:
         store = dist.HashStore()
         dist.init_process_group(store=store, rank=0, world_size=1, **kw, **kwargs)
+    return True
 
 
 @dataclass

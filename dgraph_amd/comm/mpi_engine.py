@@ -53,7 +53,7 @@ class MPIBackendEngine(BackendEngine):
         if mw is not None and "RANK" not in os.environ:
             os.environ["RANK"], os.environ["WORLD_SIZE"] = str(mw[0]), str(mw[1])
             os.environ.setdefault("LOCAL_RANK", str(mw[0]))
-        ensure_process_group(kwargs.pop("backend", None), **kwargs)
+        self._owns_pg = ensure_process_group(kwargs.pop("backend", None), **kwargs)
         if dist.get_backend() != "gloo" and dist.get_world_size() > 1:
             self._cpu_group = dist.new_group(backend="gloo")
         MPIBackendEngine._is_initialized = True
@@ -114,3 +114,6 @@ class MPIBackendEngine(BackendEngine):
     def destroy(self) -> None:
         MPIBackendEngine._is_initialized = False
         self._g1_cache.clear()
+        if getattr(self, "_owns_pg", False) and dist.is_initialized():
+            self._owns_pg = False
+            dist.destroy_process_group()

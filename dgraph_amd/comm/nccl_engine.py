@@ -39,7 +39,7 @@ class NCCLBackendEngine(BackendEngine):
     # ------------------------------------------------------------------ setup
     def init_process_group(self, ranks_per_graph: int = -1, *args, **kwargs):
         backend = kwargs.pop("backend", None)
-        ensure_process_group(backend or "nccl", **kwargs)
+        NCCLBackendEngine._owns_pg = ensure_process_group(backend or "nccl", **kwargs)
         NCCLBackendEngine._groups = make_partition_groups(ranks_per_graph)
         NCCLBackendEngine._is_initialized = True
 
@@ -145,3 +145,8 @@ class NCCLBackendEngine(BackendEngine):
         NCCLBackendEngine._is_initialized = False
         NCCLBackendEngine._groups = None
         self._g1_cache.clear()
+        if getattr(NCCLBackendEngine, "_owns_pg", False) and dist.is_initialized():
+            # the engine created the process group: tear it down (RCCL communicators
+            # included) instead of leaving it to interpreter exit
+            NCCLBackendEngine._owns_pg = False
+            dist.destroy_process_group()

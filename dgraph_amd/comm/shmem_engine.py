@@ -40,7 +40,7 @@ class ROCSHMEMBackendEngine(BackendEngine):
         self.init_process_group(ranks_per_graph, **kwargs)
 
     def init_process_group(self, ranks_per_graph: int = -1, **kwargs):
-        ensure_process_group(kwargs.pop("backend", None), **kwargs)
+        self._owns_pg = ensure_process_group(kwargs.pop("backend", None), **kwargs)
         self._groups = make_partition_groups(ranks_per_graph)
         ROCSHMEMBackendEngine._ranks_per_graph = self._groups.ranks_per_graph
         ROCSHMEMBackendEngine._partition_num = self._groups.partition_id
@@ -137,6 +137,9 @@ class ROCSHMEMBackendEngine(BackendEngine):
     def destroy(self) -> None:
         self.finalize()
         self._g1_cache.clear()
+        if getattr(self, "_owns_pg", False) and dist.is_initialized():
+            self._owns_pg = False
+            dist.destroy_process_group()
 
 
 # API-compatibility alias (reference backend name "nvshmem")
