@@ -95,3 +95,32 @@ def test_rgcn_training_with_fused_dropout_is_bitwise_deterministic():
 
 def test_rgcn_training_with_dropout_is_deterministic_on_cpu():
     _assert_bitwise(_rgcn_run(device="cpu"), _rgcn_run(device="cpu"))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_segment_sum_vs_atomic_scatter(dtype):
+    """the atomic scatter-add the reference used (K6-K8, here torch's
+    index_add_) and the library's sorted-destination segment sum agree numerically; the
+    segment sum is bitwise reproducible, the atomic path need not be."""
+    from dgraph_amd import _native
+    from dgraph_amd.ops import kernels as K
+    from dgraph_amd.ops.csr import CSR
+
+    assert _native.load(), "native library missing"
+    dev = torch.device("cuda", 0)
+    g = torch.Generator().manual_seed(11)
+    V, E, F = 200_000, 4_000_000, 128
+    src = torch.randint(0, V, (E,), generator=g)
+    dst = (torch.rand(E, generator=g) ** 3 * V).long()  # skewed: hot destinations
+    x = torch.randn(V, F, generator=g).to(dev, dtype)
+    csr = CSR.from_coo(dst.to(dev), src.to(dev), V, V)
+    seg = [K.spmm(csr.rowptr, csr.col, x) for _ in range(3)]
+    assert all(torch.equal(seg[0], s) for s in seg[1:]), "segment sum must be reproducible"
+    acc = torch.zeros(V, F, device=dev, dtype=torch.float32)
+    acc.index_add_(0, dst.to(dev), x.float()[src.to(dev)])  # atomics, fp32
+    ref = torch.zeros(V, F, dtype=torch.float64)
+    ref.index_add_(0, dst, x.double().cpu()[src])
+    tol = 1e-4 if dtype == torch.float32 else 2e-2
+    torch.testing.assert_close(seg[0].double().cpu(), ref, atol=tol * 10, rtol=tol)
+    torch.testing.assert_close(acc.double().cpu(), ref, atol=1e-3, rtol=1e-4)
