@@ -121,6 +121,8 @@ def test_segment_sum_vs_atomic_scatter(dtype):
     acc.index_add_(0, dst.to(dev), x.float()[src.to(dev)])  # atomics, fp32
     ref = torch.zeros(V, F, dtype=torch.float64)
     ref.index_add_(0, dst, x.double().cpu()[src])
-    tol = 1e-4 if dtype == torch.float32 else 2e-2
-    torch.testing.assert_close(seg[0].double().cpu(), ref, atol=tol * 10, rtol=tol)
-    torch.testing.assert_close(acc.double().cpu(), ref, atol=1e-3, rtol=1e-4)
+    # row 0 is the hottest destination (~7e4 entries): fp32 accumulation of that many
+    # terms drifts by ~1e-3 absolute whatever the summation order
+    tol = 1e-3 if dtype == torch.float32 else 2e-2
+    torch.testing.assert_close(seg[0].double().cpu(), ref, atol=tol * 5, rtol=tol)
+    torch.testing.assert_close(acc.double().cpu(), ref, atol=5e-3, rtol=1e-3)
