@@ -78,6 +78,10 @@ def parse():
     ap.add_argument("--profile-ops", default="",
                     help="after the timed steps, profile one extra step (every rank runs it) "
                          "with torch.profiler; rank 0 writes the per-op device-time table")
+    ap.add_argument("--cuda-graph", action="store_true",
+                    help="capture the whole step (forward, backward, sync, Adam) into a HIP "
+                         "graph after the first eager warmup step and replay it "
+                         "(dgraph_amd.utils.graphed; for launch-bound small shapes)")
     ap.add_argument("--metrics-jsonl", default=os.environ.get("DGRAPH_METRICS_JSONL", ""),
                     help="append one metrics record per measured phase (rank 0)")
     return ap.parse_args()
@@ -167,6 +171,13 @@ class Job:
                                args.layers).to(dev)
         self.opt = torch.optim.Adam(self.model.parameters(), lr=args.lr,
                                     fused=dev.type == "cuda")
+        self.steppers = {}
+        if getattr(args, "cuda_graph", False) and dev.type == "cuda":
+            from dgraph_amd.utils.graphed import GraphedStep, make_capturable
+
+            make_capturable(self.opt)
+            self.steppers = {r: GraphedStep(lambda r=r: self.step(r), warmup=1)
+                             for r in (False, True)}
         self.sync = GradSync(self.model.parameters(), group=None) if self.world > 1 else None
         self.inv_n = 1.0 / max(self.n_train, 1)
         self.correct = torch.zeros(2, dtype=torch.long, device=dev)  # val, test
@@ -191,6 +202,10 @@ class Job:
         self.opt.step()
         self.opt.zero_grad(set_to_none=True)
         return loss
+
+    def stepper(self, restrict_last: bool):
+        """The step as a callable: eager, or captured once and replayed (--cuda-graph)."""
+        return self.steppers.get(restrict_last) or (lambda: self.step(restrict_last))
 
     def halo_stats(self):
         from dgraph_amd.utils.diagnostics import halo_stats
@@ -226,8 +241,13 @@ def timed(job: Job, steps: int, warmup: int, restrict_last: bool, verbose: bool 
     (ms_per_step as the MAX over ranks, mean loss of the last step summed over ranks,
      edges aggregated per step summed over ranks)."""
     world, dev = job.world, job.dev
+    stepf = job.stepper(restrict_last)
+    e_eager = None  # edges of one step, counted on the host while the step's Python runs
     for i in range(warmup):
-        l = job.step(restrict_last)
+        ea = job.graph.edges_aggregated
+        l = stepf()
+        if e_eager is None:
+            e_eager = job.graph.edges_aggregated - ea
         if verbose:
             log(job.rank, f"warmup {i} loss {float(l.detach()):.4f}")
     barrier_sync(world, dev)
@@ -235,10 +255,14 @@ def timed(job: Job, steps: int, warmup: int, restrict_last: bool, verbose: bool 
     t_start = time.perf_counter()
     l = None
     for _ in range(steps):
-        l = job.step(restrict_last)
+        l = stepf()
     barrier_sync(world, dev)
     elapsed = time.perf_counter() - t_start
     e1 = job.graph.edges_aggregated
+    if job.steppers and e_eager is not None:
+        # graph replays run no Python, so the host counter did not move: every replay
+        # aggregates what the captured (eager-equivalent) step did
+        e1 = e0 + e_eager * steps
     red = torch.tensor([elapsed * 1000.0 / max(steps, 1)], dtype=torch.float64, device=dev)
     tot = torch.tensor([float(l.detach()) if l is not None else 0.0,
                         (e1 - e0) / max(steps, 1)], dtype=torch.float64, device=dev)
@@ -366,6 +390,7 @@ def main():
                 "step": ("train-rows-only output layer" if head_restrict else
                          "full-graph forward (all vertices, all layers) + val/test accuracy "
                          "from the same forward + backward + allreduce + Adam"),
+                "launch": "HIP graph replay" if args.cuda_graph else "eager",
                 "precision": ("bf16 storage/compute, fp32 accumulate, fp32 master weights"
                               if dtype == torch.bfloat16 else "fp32"),
             },

@@ -43,6 +43,9 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--cuda-graph", action="store_true",
+                    help="--mode step: capture the whole step into a HIP graph after one "
+                         "eager step and replay it (dgraph_amd.utils.graphed)")
     ap.add_argument("--dedup-mesh-edges", action="store_true",
                     help="one processor edge per multimesh edge pair (327 660 at level 6); "
                          "default: the reference's graph, every multimesh edge carried twice "
@@ -107,12 +110,18 @@ def main():
                 opt.step()
             return loss
 
+        run = step
+        if a.cuda_graph:
+            from dgraph_amd.utils.graphed import GraphedStep, make_capturable
+
+            make_capturable(opt)
+            run = GraphedStep(step, warmup=1)
         for _ in range(a.warmup):
-            step()
+            run()
         sync()
         t = time.perf_counter()
         for _ in range(a.steps):
-            loss = step()
+            loss = run()
         sync()
         ms = (time.perf_counter() - t) * 1e3 / a.steps
         edges = a.layers * g.m2m[0].size + g.g2m[0].size + g.m2g[0].size
@@ -131,6 +140,7 @@ def main():
                   "channels": a.channels, "channel_config": a.channel_config,
                   "mesh_edges": int(g.m2m[0].size), "duplicate_mesh_edges":
                   not a.dedup_mesh_edges,
+                  "launch": "HIP graph replay" if a.cuda_graph else "eager",
                   "precision": "bf16 compute, fp32 master weights" if masters is not None
                   else "fp32",
                   "edge_updates_per_s": edges / (ms / 1e3), "loss": float(loss),

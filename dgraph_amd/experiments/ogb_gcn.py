@@ -75,7 +75,8 @@ def visualize_trajectories(traj: np.ndarray, title: str, path: str, rank: int = 
 
 def run_experiment(dataset: DGraphOGBDataset, comm, lr: float, epochs: int, log_prefix: str,
                    hidden_dims: int = 256, num_classes: int = 40, device=None,
-                   dtype: str = "fp32", seed: int = 0, support: Optional[RunSupport] = None):
+                   dtype: str = "fp32", seed: int = 0, support: Optional[RunSupport] = None,
+                   cuda_graph: bool = False):
     device = device or _device()
     rank = comm.get_rank()
     x, y, cp = dataset[0]
@@ -89,6 +90,13 @@ def run_experiment(dataset: DGraphOGBDataset, comm, lr: float, epochs: int, log_
     sync = GradSync(model.parameters(), group=comm.group)
     opt = torch.optim.Adam(model.parameters(), lr=lr)
     amp = dtype == "bf16"
+    graphed = None
+    if cuda_graph and device.type == "cuda":
+        # whole-step HIP graph: one launch per epoch instead of hundreds (the arxiv-shaped
+        # step is launch-bound); the TimingReport regions are not recorded in this mode
+        from dgraph_amd.utils.graphed import GraphedStep, make_capturable
+
+        make_capturable(opt)
 
     def fwd():
         with torch.autocast(device.type, dtype=torch.bfloat16, enabled=amp):
@@ -106,6 +114,33 @@ def run_experiment(dataset: DGraphOGBDataset, comm, lr: float, epochs: int, log_
     if world > 1:
         torch.distributed.all_reduce(n_edges, group=comm.group)
     edges_per_epoch = 2 * int(n_edges.item())
+    tm = masks["train_mask"]
+
+    def train_step():
+        opt.zero_grad(set_to_none=True)
+        out = fwd()
+        # global mean over all ranks' training vertices (the reference averaged per rank)
+        loss = F.cross_entropy(out[tm], y[tm].reshape(-1), reduction="sum") / n_train
+        loss.backward()
+        sync.all_reduce()
+        opt.step()
+        return loss, out
+
+    if cuda_graph and device.type == "cuda":
+        # masked indexing syncs on the mask's count: capture with precomputed indices
+        ti = torch.nonzero(tm.reshape(-1)).reshape(-1)
+        yt = y[ti].reshape(-1)
+
+        def train_step():  # noqa: F811
+            opt.zero_grad(set_to_none=True)
+            out = fwd()
+            loss = F.cross_entropy(out.index_select(0, ti), yt, reduction="sum") / n_train
+            loss.backward()
+            sync.all_reduce()
+            opt.step()
+            return loss, out
+
+        graphed = GraphedStep(train_step, warmup=1)
     start = support.resume(model, opt) if support is not None else 0
     epoch = start - 1
     nan = float("nan")  # resumed runs: the epochs before the checkpoint are not re-logged
@@ -117,16 +152,18 @@ def run_experiment(dataset: DGraphOGBDataset, comm, lr: float, epochs: int, log_
         if support is not None:
             support.begin_epoch()
         t0 = time.perf_counter()
-        opt.zero_grad(set_to_none=True)
-        with region("forward"):
-            out = fwd()
-        tm = masks["train_mask"]
-        # global mean over all ranks' training vertices (the reference averaged per rank)
-        loss = F.cross_entropy(out[tm], y[tm].reshape(-1), reduction="sum") / n_train
-        with region("backward"):
-            loss.backward()
-        sync.all_reduce()
-        opt.step()
+        if graphed is not None:
+            loss, out = graphed()
+        else:
+            opt.zero_grad(set_to_none=True)
+            with region("forward"):
+                out = fwd()
+            # global mean over all ranks' training vertices (the reference averaged per rank)
+            loss = F.cross_entropy(out[tm], y[tm].reshape(-1), reduction="sum") / n_train
+            with region("backward"):
+                loss.backward()
+            sync.all_reduce()
+            opt.step()
         comm.barrier()
         _sync(device)
         ms = (time.perf_counter() - t0) * 1e3
@@ -178,7 +215,8 @@ def run_experiment(dataset: DGraphOGBDataset, comm, lr: float, epochs: int, log_
 def main(backend: str = "nccl", dataset: str = "arxiv", epochs: int = 10, lr: float = 1e-3,
          runs: int = 1, hidden_dims: int = 256, log_dir: str = "logs",
          node_rank_placement_file: Optional[str] = None, root_dir: Optional[str] = None,
-         dtype: str = "fp32", synthetic_scale: float = 1.0, run_args=None):
+         dtype: str = "fp32", synthetic_scale: float = 1.0, cuda_graph: bool = False,
+         run_args=None):
     if dataset not in NUM_CLASSES:
         raise ValueError(f"Unsupported dataset '{dataset}'. Choose from {list(NUM_CLASSES)}")
     cfg = build_config(getattr(run_args, "config", ()), comm__backend=backend,
@@ -207,7 +245,7 @@ def main(backend: str = "nccl", dataset: str = "arxiv", epochs: int = 10, lr: fl
         prefix = f"{log_dir}/{dataset}_world{world}_run{run}"
         tr[run], vl[run], va[run] = run_experiment(
             ds, comm, lr, epochs, prefix, hidden_dims, NUM_CLASSES[dataset], device, dtype,
-            seed=run, support=support if run == 0 else None)
+            seed=run, support=support if run == 0 else None, cuda_graph=cuda_graph)
     TimingReport.resolve()
     if rank == 0:
         TimingReport.dump(f"{log_dir}/{dataset}_timing_report_world{world}.json")
@@ -231,6 +269,8 @@ def cli(argv=None):
     p.add_argument("--root_dir", default=None)
     p.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
     p.add_argument("--synthetic_scale", type=float, default=1.0)
+    p.add_argument("--cuda_graph", action="store_true",
+                   help="capture the training step into a HIP graph and replay it")
     add_run_args(p)
     a = p.parse_args(argv)
     run_keys = ("config", "resume", "checkpoint_dir", "checkpoint_every", "metrics_jsonl")

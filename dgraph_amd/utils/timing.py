@@ -28,6 +28,10 @@ class _Pending:
         self.t0 = t0
 
 
+def _capturing() -> bool:
+    return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+
+
 class TimingReport:
     _timers: Dict[str, List] = {}
     _communicator = None
@@ -73,6 +77,8 @@ class TimingReport:
     @staticmethod
     def start(name: str):
         TimingReport._check()
+        if _capturing():
+            return  # inside a HIP-graph capture: events would belong to the graph
         if TimingReport._sync and TimingReport._communicator is not None:
             TimingReport._communicator.barrier()
         lst = TimingReport._timers.setdefault(name, [])
@@ -88,6 +94,8 @@ class TimingReport:
     @staticmethod
     def stop(name: str):
         TimingReport._check()
+        if _capturing():
+            return None
         lst = TimingReport._timers.get(name)
         if not lst or not isinstance(lst[-1], _Pending):
             raise ValueError(f"No timer started for {name}")
