@@ -78,6 +78,11 @@ def parse():
     ap.add_argument("--profile-ops", default="",
                     help="after the timed steps, profile one extra step (every rank runs it) "
                          "with torch.profiler; rank 0 writes the per-op device-time table")
+    ap.add_argument("--halo-recompute", choices=("auto", "on", "off"), default="auto",
+                    help="W>1: compute the first hidden layer for the halo vertices too, so "
+                         "layer 2 exchanges nothing forward or backward "
+                         "(parallel/halo_recompute.py); auto = on when every rank's halo "
+                         "is smaller than its partition")
     ap.add_argument("--cuda-graph", action="store_true",
                     help="capture the whole step (forward, backward, sync, Adam) into a HIP "
                          "graph after the first eager warmup step and replay it "
@@ -144,8 +149,28 @@ class Job:
                                # transpose is never materialised
                                part["recv_splits"], comm.group, symmetric=True,
                                overlap=not args.no_overlap)
+        halo_gids = part["halo_gids"]
         del part, csr
         self.graph.prepare_backward()
+        self.recompute = False
+        mode = getattr(args, "halo_recompute", "off")
+        if p_world > 1 and mode != "off" and args.layers >= 3:
+            want = torch.tensor([1 if (mode == "on" or self.H < self.L) else 0],
+                                dtype=torch.long, device=dev)
+            if self.world > 1:
+                dist.all_reduce(want, op=dist.ReduceOp.MIN)  # one decision for all ranks
+            if int(want) == 1:
+                from dgraph_amd.data.synthetic import build_rows_csr
+                from dgraph_amd.parallel.halo_recompute import HaloRecompute
+
+                rows_csr = build_rows_csr(shape, halo_gids, dev, seed=args.seed,
+                                          global_frac=global_frac, window=args.window)
+                self.graph.recompute = HaloRecompute(
+                    self.graph, rows_csr, halo_gids, _offsets(shape.num_nodes, p_world),
+                    p_rank, comm.group, rehearse=self.rehearse)
+                del rows_csr
+                self.recompute = True
+        del halo_gids
         self.x, y, split = node_data(shape, p_rank,
                                      _offsets(shape.num_nodes, p_world), dev, seed=args.seed,
                                      dtype=dtype, return_split=True)
@@ -313,6 +338,7 @@ def main():
     if args.profile_ops:
         _profile_one_step(lambda: job.step(head_restrict), args.profile_ops, rank)
     E_msg, n_train, halo_total = job.E_msg, job.n_train, job.halo_total
+    job_recompute = job.recompute
     shape = job.shape
     edges_per_s = args.layers * E_msg / (ms / 1000.0)
     if mlog is not None:
@@ -356,6 +382,7 @@ def main():
                           "ms_per_step_compute_loopback": ms, "E_local": E_msg,
                           "halo_rows": halo_total, "peak_mem_gb": round(peak_gb, 2),
                           "dtype": args.dtype, "global_frac": args.global_frac,
+                          "halo_recompute": job_recompute,
                           "restrict_last": head_restrict,
                           "final_loss_local": final_loss}), flush=True)
     elif rank == 0:
@@ -380,7 +407,9 @@ def main():
                 "model": f"GraphSAGE-mean {args.layers}-layer hidden {args.hidden}",
                 "global_batch": shape.num_nodes,
                 "seq_len": None,
-                "parallelism": f"graph-partition{world} (RCCL all-to-all-v halo) + dp-allreduce",
+                "parallelism": f"graph-partition{world} (RCCL all-to-all-v halo"
+                               + (", layer-1 halo recomputed" if job_recompute else "")
+                               + ") + dp-allreduce",
                 "dataset_shape": shape.name,
                 "num_layers": args.layers,
                 "hidden": args.hidden,
@@ -391,6 +420,7 @@ def main():
                          "full-graph forward (all vertices, all layers) + val/test accuracy "
                          "from the same forward + backward + allreduce + Adam"),
                 "launch": "HIP graph replay" if args.cuda_graph else "eager",
+                "halo_recompute": job_recompute,
                 "precision": ("bf16 storage/compute, fp32 accumulate, fp32 master weights"
                               if dtype == torch.bfloat16 else "fp32"),
             },

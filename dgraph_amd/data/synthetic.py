@@ -170,6 +170,37 @@ def build_local_csr(
     return CSR(rowptr, col, shape.num_nodes, None, symmetric=False), L, off
 
 
+def build_rows_csr(shape: GraphShape, row_gids: torch.Tensor, device, seed: int = 0,
+                   global_frac: float = 0.05, window: int = 1 << 14) -> CSR:
+    """CSR of the symmetrised graph restricted to an arbitrary sorted set of vertices
+    ``row_gids`` (e.g. a rank's halo vertices, for halo recomputation); columns are GLOBAL
+    ids. The same streaming generator as :func:`build_local_csr`, so each row holds
+    exactly the entries (and the (row, col) order) its owner's CSR holds."""
+    V = shape.num_nodes
+    R = row_gids.numel()
+    member = torch.zeros(V, dtype=torch.bool, device=device)
+    member[row_gids] = True
+    cdt = torch.int32 if V < 2**31 else torch.int64
+    keys = []
+    E = shape.num_directed_edges
+    for k in range(0, (E + _CHUNK - 1) // _CHUNK):
+        n = min(_CHUNK, E - k * _CHUNK)
+        s_, d_ = _chunk_edges(shape, k, n, seed, global_frac, window, device)
+        for rows, cols in ((d_, s_), (s_, d_)):
+            m = member[rows]
+            r = torch.searchsorted(row_gids, rows[m])
+            keys.append(r * V + cols[m])
+        del s_, d_
+    key = torch.sort(torch.cat(keys)).values if keys else \
+        torch.zeros(0, dtype=torch.int64, device=device)
+    del keys
+    r = torch.div(key, V, rounding_mode="floor")
+    col = (key - r * V).to(cdt)
+    rowptr = torch.zeros(R + 1, dtype=torch.int64, device=device)
+    torch.cumsum(torch.bincount(r, minlength=R), 0, out=rowptr[1:])
+    return CSR(rowptr, col, V, None, symmetric=False)
+
+
 def localize_columns(csr: CSR, rank: int, offsets: List[int]):
     """Relabel global column ids: owned -> [0, L), remote -> L + position in the halo
     (sorted by global id == (owner, id) under contiguous ownership). Returns

@@ -196,8 +196,12 @@ class SageWorkspace:
     # masks, weight-gradient partials and allocator slack)
     AGG0_HEADROOM = 24 << 30
 
-    def prepare(self, L: int, dims, pf_flags, dtype, device, keep_agg0: bool = False):
-        key = (L, tuple(dims), tuple(pf_flags), dtype, str(device), keep_agg0)
+    def prepare(self, L: int, dims, pf_flags, dtype, device, keep_agg0: bool = False,
+                rows0: Optional[int] = None):
+        """``rows0``: rows of the first layer's output and aggregate when they exceed
+        ``L`` (halo recomputation: owned + padding + halo rows)."""
+        rows0 = L if rows0 is None else int(rows0)
+        key = (L, tuple(dims), tuple(pf_flags), dtype, str(device), keep_agg0, rows0)
         if key == self.key:
             return
         self.slots = {}
@@ -206,18 +210,22 @@ class SageWorkspace:
         wa = max([C] + [(dims[i + 1] if pf_flags[i] else dims[i]) for i in range(n)])
         wb = max([C] + [dims[i + 1] for i in range(n) if pf_flags[i]])
         for i in range(1, n):
-            self.slots[f"act{i}"] = torch.empty(L * dims[i], dtype=dtype, device=device)
-        self.slots["tmp_a"] = torch.empty(L * wa, dtype=dtype, device=device)
+            self.slots[f"act{i}"] = torch.empty((rows0 if i == 1 else L) * dims[i],
+                                                dtype=dtype, device=device)
+        na = L * wa
+        if rows0 > L:  # layer-0 aggregate and layer-1 u over the extended rows
+            na = max(na, rows0 * max(dims[0], dims[2] if n > 2 else 0))
+        self.slots["tmp_a"] = torch.empty(na, dtype=dtype, device=device)
         self.slots["tmp_b"] = torch.empty(L * wb, dtype=dtype, device=device)
         if keep_agg0 and not pf_flags[0]:
             # layer 0's aggregate A x0 kept for its weight gradient (saves one SpMM per
             # step) when it fits next to the other slots (multi-GPU shards; not 1-GPU
             # papers100M, which needs ~263 GB without it)
-            need = L * dims[0] * torch.empty((), dtype=dtype).element_size()
+            need = rows0 * dims[0] * torch.empty((), dtype=dtype).element_size()
             free = torch.cuda.mem_get_info(device)[0] if torch.device(device).type == "cuda" \
                 else need + (64 << 30)  # host memory: treated as ample
             if free - need >= self.AGG0_HEADROOM:
-                self.slots["agg0"] = torch.empty(L * dims[0], dtype=dtype, device=device)
+                self.slots["agg0"] = torch.empty(rows0 * dims[0], dtype=dtype, device=device)
         self.key = key
 
     def has(self, name: str) -> bool:
@@ -280,22 +288,38 @@ class SAGEStackFn(Function):
         # vector loads in the SpMM and the ReLU-mask kernels); pads stay exactly zero
         dims_p = [dims[0]] + [_pad_width(d) for d in dims[1:]]
         pf_flags = [pf for (_, pf) in specs]
+        # halo recomputation (parallel/halo_recompute.py): layer 0 runs on the owned AND
+        # halo rows, layer 1 reads its halo rows locally (no exchange either way)
+        rc = getattr(graph, "recompute", None)
+        if rc is not None and not (n >= 3 and not pf_flags[0] and not pf_flags[1]
+                                   and not x0.requires_grad and out_rows is not None
+                                   and dims_p[2] <= 2 * dims_p[1]):
+            rc = None
+        L1 = rc.L1 if rc is not None else L
         if use_ws:
             ws_obj.prepare(L, dims_p, pf_flags, dt, x0.device,
-                           keep_agg0=not x0.requires_grad)
+                           keep_agg0=not x0.requires_grad, rows0=L1)
             ws_obj.generation += 1
         keep0 = use_ws and ws_obj.has("agg0") and not pf_flags[0] and not x0.requires_grad
         V = (lambda name, F: ws_obj.view(name, L, F)) if use_ws else \
             (lambda name, F: torch.empty(L, F, dtype=dt, device=x0.device))
+        V1 = (lambda name, F: ws_obj.view(name, L1, F)) if use_ws else \
+            (lambda name, F: torch.empty(L1, F, dtype=dt, device=x0.device))
         acts = [x0]
         masks = []
         h = x0
+        X_ext = None
+        if rc is not None:
+            X_ext = rc.inputs(x0)
+            h = X_ext[:L1]
+            acts = [h]
         for i, (relu, pf) in enumerate(specs):
             ws, wn, b = _padded(params, i, dims_p, dt)
             ws_, wn_ = ws, wn
             last = i == n - 1
             Fi, Fo = dims_p[i], dims_p[i + 1]
-            y = V("tmp_b" if last else f"act{i + 1}", Fo)
+            rows_i = L1 if (rc is not None and i == 0) else L
+            y = (V1 if rows_i != L else V)("tmp_b" if last else f"act{i + 1}", Fo)
             # one MFMA dual GEMM for the whole combine (+ bias, ReLU, 1-bit mask) when the
             # shape is supported and, for a ReLU layer, the backward consumer of its mask
             # (layer i + 1's input-gradient GEMM) is fused too (same "tile32" mask layout)
@@ -303,7 +327,7 @@ class SAGEStackFn(Function):
                 not relu or (i + 1 < n and _bwd_fused(specs, dims_p, i + 1, True, h)))
             mask = None
             if fused and relu:
-                mask = torch.empty(tile32_mask_words(L, Fo), dtype=torch.int64,
+                mask = torch.empty(tile32_mask_words(rows_i, Fo), dtype=torch.int64,
                                    device=h.device)
             if last and pf and not relu and out_rows is not None and restrict_last:
                 # only the loss rows leave the node: y[rows] = A[rows, :] (h Wn) +
@@ -333,10 +357,18 @@ class SAGEStackFn(Function):
                     y.addmm_(h, ws_)
             else:
                 slot = "agg0" if (i == 0 and keep0) else "tmp_a"
-                # layer 0 aggregates the input features: read-only without grad, so
-                # their halo rows are exchanged once and kept (DistGraph._static_halo)
-                a = graph.aggregate(h, mean=True, out=V(slot, Fi),
-                                    static=i == 0 and not x0.requires_grad)
+                if rc is not None and i == 0:
+                    a = rc.aggregate0(X_ext, V1(slot, Fi))
+                elif rc is not None and i == 1:
+                    # the halo rows of h1 were computed here: no exchange
+                    a = graph.aggregate(h[:L], mean=True, out=V(slot, Fi),
+                                        halo_rows=h[rc.Lp:rc.L1])
+                    h = h[:L]
+                else:
+                    # layer 0 aggregates the input features: read-only without grad, so
+                    # their halo rows are exchanged once and kept (DistGraph._static_halo)
+                    a = graph.aggregate(h, mean=True, out=V(slot, Fi),
+                                        static=i == 0 and not x0.requires_grad)
                 if fused:
                     dual_gemm(h, ws_.t().contiguous(), a, wn_.t().contiguous(), bias=b, out=y,
                               relu=relu, mask_out=mask)
@@ -363,6 +395,7 @@ class SAGEStackFn(Function):
         ctx.acts, ctx.masks = acts, masks
         ctx.x0_requires_grad = x0.requires_grad
         ctx.ws, ctx.use_ws, ctx.keep0 = ws_obj, use_ws, keep0
+        ctx.rc, ctx.X_ext = rc, X_ext
         ctx.gen = ws_obj.generation if use_ws else None
         ctx.save_for_backward(*params)
         ctx.out_rows = out_rows
@@ -394,8 +427,15 @@ class SAGEStackFn(Function):
         n = len(specs)
         x0 = acts[0]
         L, dt = x0.shape[0], x0.dtype
+        rc, X_ext = ctx.rc, ctx.X_ext
+        ctx.X_ext = None
+        if rc is not None:
+            L = rc.L  # acts[0] holds the L1 extended first-layer rows
+        L1 = rc.L1 if rc is not None else L
         V = (lambda name, F: ws_obj.view(name, L, F)) if use_ws else \
             (lambda name, F: torch.empty(L, F, dtype=dt, device=x0.device))
+        V1 = (lambda name, F: ws_obj.view(name, L1, F)) if use_ws else \
+            (lambda name, F: torch.empty(L1, F, dtype=dt, device=x0.device))
         C, Cp = dims_true[-1], dims[-1]
         gyp = gy.to(dt)
         if Cp != C:
@@ -481,7 +521,10 @@ class SAGEStackFn(Function):
             mask_in = prev[1] if (fuse_dx and isinstance(prev, tuple)) else None
             g_masked = mask_in is not None
 
-            def self_grads(i=i, x=x, g=g, ws=ws, b=b, r_in=r_in, r_out=r_out):
+            ext1 = rc is not None and i == 1  # x has the L1 extended rows, g the owned L
+            xs = x[:L] if ext1 else x
+
+            def self_grads(i=i, x=xs, g=g, ws=ws, b=b, r_in=r_in, r_out=r_out):
                 # W_self / bias gradients need no aggregation: on a multi-GPU graph they
                 # run while the layer's reverse halo exchange is on the links
                 grads[3 * i] = wgrad(x, g)[:r_in, :r_out].to(ws.dtype)
@@ -501,6 +544,38 @@ class SAGEStackFn(Function):
                         dx = torch.mm(g, ws_.t(), out=x) if recyclable else g @ ws_.t()
                         dx.addmm_(dz, wn_.t())
                 del dz
+            elif ext1:
+                # halo recomputation: u = A^T g over the owned AND halo rows of h1 (the
+                # halo part stays here instead of going to the owners), then
+                #   dW_neigh = h1_ext^T u,  dh1[own] = g Ws^T + u[own] Wn^T,
+                #   dh1[halo] = u[halo] Wn^T   (masked by layer 0's ReLU bits)
+                Lp = rc.Lp
+                F2 = dims[i + 1]
+                u = V1("tmp_a", F2)
+                if Lp > L:
+                    u[L:Lp].zero_()
+                scratch = ws_obj.slots["tmp_b"] if use_ws else None
+                graph.aggregate_T(g, mean=True, out=u[:L], scratch=scratch,
+                                  overlap=self_grads, halo_out=u[Lp:L1])
+                del scratch
+                grads[3 * i + 1] = wgrad(x, u)[:r_in, :r_out].to(wn.dtype)
+                if fuse_dx:
+                    # the L1-row tile32 mask: owned rows are its first tiles, the halo rows
+                    # start at tile Lp / 32 (Lp is a multiple of the 256-row mask group)
+                    w_own = tile32_mask_words(L, dims[i])
+                    w0, wh = tile32_mask_words(Lp, dims[i]), tile32_mask_words(L1 - Lp, dims[i])
+                    dual_gemm(g, ws_, u[:L], wn_, out=x[:L],
+                              mask_in=None if mask_in is None else mask_in[:w_own])
+                    dual_gemm(u[Lp:L1], wn_, out=x[Lp:L1],
+                              mask_in=None if mask_in is None else mask_in[w0:w0 + wh])
+                else:
+                    torch.mm(g, ws_.t(), out=x[:L])
+                    x[:L].addmm_(u[:L], wn_.t())
+                    torch.mm(u[Lp:L1], wn_.t(), out=x[Lp:L1])
+                if Lp > L:
+                    x[L:Lp].zero_()
+                dx = x
+                del u
             elif need_dx and dims[i + 1] <= 2 * dims[i]:
                 # u = A^T g gives both gradients with ONE SpMM at F_out:
                 #   dW_neigh = (A h)^T g = h^T u,   dh = g W_self^T + u W_neigh^T
@@ -526,15 +601,19 @@ class SAGEStackFn(Function):
                 self_grads()
                 # tmp_a may still hold g for the last layer: recompute into tmp_b then
                 a_name = "tmp_b" if (i == n - 1 and ctx.out_rows is not None) else "tmp_a"
+                V0 = V1 if (rc is not None and i == 0) else V
                 if i == 0 and ctx.keep0:
-                    a_buf = a = V("agg0", dims[0])  # kept by forward: no recompute
+                    a_buf = a = V0("agg0", dims[0])  # kept by forward: no recompute
                 elif i == n - 1 and ctx.out_rows is not None and dims[i] > dims[-1]:
                     a_buf = torch.empty(L, dims[i], dtype=dt, device=x.device)
                 else:
-                    a_buf = V(a_name, dims[i])
+                    a_buf = V0(a_name, dims[i])
                 if not (i == 0 and ctx.keep0):
-                    a = graph.aggregate(x, mean=True, out=a_buf,
-                                        static=i == 0 and not ctx.x0_requires_grad)
+                    if rc is not None and i == 0:
+                        a = rc.aggregate0(X_ext, a_buf)
+                    else:
+                        a = graph.aggregate(x, mean=True, out=a_buf,
+                                            static=i == 0 and not ctx.x0_requires_grad)
                 grads[3 * i + 1] = wgrad(a, g)[:r_in, :r_out].to(wn.dtype)
                 if need_dx:
                     t = torch.mm(g, wn_.t(), out=a)

@@ -142,16 +142,19 @@ class DistGraph:
         return c["recv"]
 
     def aggregate(self, x: torch.Tensor, mean: bool = True,
-                  out: Optional[torch.Tensor] = None, static: bool = False) -> torch.Tensor:
+                  out: Optional[torch.Tensor] = None, static: bool = False,
+                  halo_rows: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Mean (or sum) over in-neighbours, local and halo. ``static=True`` marks ``x``
-        as a read-only input whose halo rows may be exchanged once and reused."""
+        as a read-only input whose halo rows may be exchanged once and reused.
+        ``halo_rows``: the halo rows' values ``[H, F]`` computed on this rank (halo
+        recomputation, :mod:`~dgraph_amd.parallel.halo_recompute`): no exchange."""
         rs = self.inv_deg if mean else None
         self.edges_aggregated += self.nnz
         if self.halo is None:
             return K.spmm(self.interior.rowptr, self.interior.col, x, out, row_scale=rs,
                           split=_hs(self.interior))
-        if static:
-            recv = self._static_halo(x)
+        if static or halo_rows is not None:
+            recv = self._static_halo(x) if halo_rows is None else halo_rows
             out = K.spmm(self.interior.rowptr, self.interior.col, x, out, row_scale=rs,
                          split=_hs(self.interior))
             hc = self.halo.compact_rows()
@@ -219,15 +222,29 @@ class DistGraph:
 
     def aggregate_T(self, g: torch.Tensor, mean: bool = True,
                     out: Optional[torch.Tensor] = None,
-                    scratch: Optional[torch.Tensor] = None, overlap=None) -> torch.Tensor:
+                    scratch: Optional[torch.Tensor] = None, overlap=None,
+                    halo_out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Transposed aggregation (the backward of :meth:`aggregate`). ``scratch``: an
         optional free buffer (any shape, same dtype as ``g``) for the pre-scaled path.
         ``overlap``: a callable of independent work, run after the reverse exchange and
-        the interior SpMM are issued and before the exchange is waited for."""
+        the interior SpMM are issued and before the exchange is waited for.
+        ``halo_out``: ``[H, F]`` buffer that receives the halo rows' gradient, which then
+        stays on this rank (halo recomputation: the rows were computed here) — no
+        exchange, no owner-side segment sum."""
         cs = self.inv_deg if mean else None
         self.edges_aggregated += self.nnz
         g = g.contiguous()
         it = self.interior if self.interior.symmetric else self.interior.transpose()
+        if halo_out is not None and self.halo is not None:
+            K.spmm(self.halo.transpose().rowptr, self.halo.transpose().col, g, halo_out,
+                   col_scale=cs, split=_hs(self.halo.transpose()))
+            if cs is not None and scratch is not None:
+                out = self._spmm_col_scaled(it, g, cs, out, scratch.reshape(-1))
+            else:
+                out = K.spmm(it.rowptr, it.col, g, out, col_scale=cs, split=_hs(it))
+            if overlap is not None:
+                overlap()
+            return out
         if self.halo is None:
             if cs is not None and scratch is not None:
                 out = self._spmm_col_scaled(it, g, cs, out, scratch.reshape(-1))

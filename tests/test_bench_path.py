@@ -22,21 +22,25 @@ def _args(**kw):
     return a
 
 
-def _run_job(rank, world, out, steps, global_frac, restrict):
+def _run_job(rank, world, out, steps, global_frac, restrict, recompute="off"):
     import torch.distributed as dist
 
     import bench
 
     comm = types.SimpleNamespace(get_rank=lambda: rank, get_world_size=lambda: world,
                                  group=None)
-    job = bench.Job(_args(global_frac=global_frac), comm, torch.device("cpu"), global_frac,
-                    torch.float32)
+    job = bench.Job(_args(global_frac=global_frac, halo_recompute=recompute), comm,
+                    torch.device("cpu"), global_frac, torch.float32)
+    if recompute == "on" and world > 1:
+        assert job.recompute and job.graph.recompute is not None
     losses = []
     for _ in range(steps):
         loss = job.step(restrict).detach().clone()
         if world > 1:
             dist.all_reduce(loss)
         losses.append(float(loss))
+    if recompute == "on" and world > 1:
+        assert job.graph.recompute._cache, "the recompute path did not run"
     corr = job.correct.clone()
     if world > 1:
         dist.all_reduce(corr)
@@ -69,4 +73,26 @@ def test_bench_step_matches_single_rank(tmp_path, monkeypatch, world, global_fra
         torch.testing.assert_close(p, q, atol=1e-5, rtol=1e-4)
     if not restrict:
         # the last step's forward ran before its update: identical weights on entry
+        assert torch.equal(a["correct"], b["correct"])
+
+
+@pytest.mark.parametrize("world,global_frac,restrict", [(2, 0.05, False), (2, 1.0, False),
+                                                        (4, 0.05, False), (4, 0.05, True),
+                                                        (8, 0.05, False)])
+def test_bench_step_halo_recompute_matches_single_rank(tmp_path, world, global_frac,
+                                                       restrict):
+    """Halo recomputation (parallel/halo_recompute.py): the first hidden layer computed
+    for the halo rows on every rank, layer 2 exchanging nothing, reproduces W=1."""
+    steps = 3
+    _run_job(0, 1, tmp_path / "w1.pt", steps, global_frac, restrict)
+    run_ranks(_run_job, world, str(tmp_path / "wn.pt"), steps, global_frac, restrict, "on",
+              timeout=600)
+    a = torch.load(tmp_path / "w1.pt", weights_only=True)
+    b = torch.load(tmp_path / "wn.pt", weights_only=True)
+    torch.testing.assert_close(a["losses"], b["losses"], atol=1e-5, rtol=1e-5)
+    # the first layer's weight gradient sums the halo rows' share in another order (each
+    # rank adds its own uses of a row): fp32 reassociation, amplified by Adam's 1/sqrt(v)
+    for p, q in zip(a["params"], b["params"]):
+        torch.testing.assert_close(p, q, atol=5e-5, rtol=1e-3)
+    if not restrict:
         assert torch.equal(a["correct"], b["correct"])
