@@ -28,6 +28,7 @@ from torch.autograd import Function
 
 from .. import _native
 from ..ops import kernels as K
+from ..parallel import halo_recompute as _hr
 from ..ops.dense import (col_sum_f32, dual_gemm, dual_gemm_shape_ok, mm_f32,  # noqa: F401
                          tile32_mask_words, wgrad)
 from ..parallel.dist_graph import DistGraph
@@ -361,8 +362,11 @@ class SAGEStackFn(Function):
                     a = rc.aggregate0(X_ext, V1(slot, Fi))
                 elif rc is not None and i == 1:
                     # the halo rows of h1 were computed here: no exchange
-                    a = graph.aggregate(h[:L], mean=True, out=V(slot, Fi),
-                                        halo_rows=h[rc.Lp:rc.L1])
+                    if _hr.MERGED:
+                        a = rc.aggregate_owned(h, V(slot, Fi))
+                    else:
+                        a = graph.aggregate(h[:L], mean=True, out=V(slot, Fi),
+                                            halo_rows=h[rc.Lp:rc.L1])
                     h = h[:L]
                 else:
                     # layer 0 aggregates the input features: read-only without grad, so

@@ -30,6 +30,7 @@ Reference: no equivalent (the reference always exchanges every layer,
 """
 from __future__ import annotations
 
+import os
 import weakref
 from typing import List, Optional
 
@@ -39,6 +40,10 @@ from ..comm.alltoallv import AllToAllV
 from ..ops import kernels as K
 from ..ops.csr import CSR
 from .dist_graph import DistGraph, _hs
+
+# owned rows aggregated in one pass over the merged (interior + halo) CSR; 0 = the
+# interior pass + a beta=1 halo pass (DGRAPH_RECOMPUTE_MERGED)
+MERGED = os.environ.get("DGRAPH_RECOMPUTE_MERGED", "1") != "0"
 
 
 class HaloRecompute:
@@ -98,6 +103,53 @@ class HaloRecompute:
         self.send_idx2 = send_idx.to(torch.int32 if L < 2**31 else torch.int64)
         self.a2a2 = AllToAllV(send_splits, recv_splits, group)
         self._cache = {}
+        self._merged: Optional[CSR] = None
+
+    def merged(self) -> CSR:
+        """The owned rows' full neighbourhoods in the extended column layout (interior
+        columns as they are, halo column j -> ``Lp + j``), built once. With the halo rows
+        local, layers 0 and 1 aggregate the owned rows in ONE SpMM pass over it: no second
+        (``beta=1``) pass that re-reads and re-writes every row with a halo neighbour.
+        Row entries: the interior ones, then the halo ones (fixed order)."""
+        if self._merged is None:
+            g = self.graph
+            it, ht = g.interior, g.halo
+            L, Lp = self.L, self.Lp
+            dev = it.device
+            di, dh = it.degree(), ht.degree()
+            rowptr = torch.zeros(L + 1, dtype=torch.long, device=dev)
+            torch.cumsum(di + dh, 0, out=rowptr[1:])
+            nnz = int(rowptr[-1])
+            ncols = self.L1
+            col = torch.empty(nnz, dtype=torch.int32 if ncols < 2**31 else torch.int64,
+                              device=dev)
+            # row chunks of <= ~2^26 entries: bounded int64 temporaries at 1e9+ entries
+            step = max(1, int(L * (1 << 26) // max(nnz, 1)))
+            for r0 in range(0, L, step):
+                r1 = min(L, r0 + step)
+                rr = torch.arange(r0, r1, device=dev)
+                for part, deg, base, shift in ((it, di, 0, 0), (ht, dh, 1, Lp)):
+                    a, b = int(part.rowptr[r0]), int(part.rowptr[r1])
+                    if b == a:
+                        continue
+                    rows = torch.repeat_interleave(rr, deg[r0:r1], output_size=b - a)
+                    pos = torch.arange(a, b, device=dev) - part.rowptr[rows] + rowptr[rows]
+                    if base:
+                        pos += di[rows]
+                    col[pos] = (part.col[a:b].long() + shift).to(col.dtype)
+                    del rows, pos
+            self._merged = CSR(rowptr, col, ncols, None, symmetric=False)
+        return self._merged
+
+    def aggregate_owned(self, h_ext: torch.Tensor, out: torch.Tensor,
+                        mean: bool = True) -> torch.Tensor:
+        """Neighbour mean of the owned rows over an extended-layout input (rows
+        ``[0, L)`` owned, ``[Lp, Lp + H)`` halo): one pass over :meth:`merged`."""
+        g = self.graph
+        m = self.merged()
+        g.edges_aggregated += m.nnz
+        return K.spmm(m.rowptr, m.col, h_ext, out, row_scale=g.inv_deg if mean else None,
+                      split=_hs(m))
 
     @property
     def nnz(self) -> int:
@@ -126,7 +178,10 @@ class HaloRecompute:
         through their own neighbourhood lists."""
         g = self.graph
         L, Lp, L1 = self.L, self.Lp, self.L1
-        g.aggregate(X[:L], mean=mean, out=out[:L], halo_rows=X[Lp:L1])
+        if MERGED:
+            self.aggregate_owned(X, out[:L], mean=mean)
+        else:
+            g.aggregate(X[:L], mean=mean, out=out[:L], halo_rows=X[Lp:L1])
         if Lp > L:
             out[L:Lp].zero_()
         K.spmm(self.csr.rowptr, self.csr.col, X, out[Lp:L1],
