@@ -240,7 +240,21 @@ class Job:
         fb = self.args.hidden * self.x.element_size()
         st = halo_stats(self.graph, fb)
         keep = ("max_pairwise_bytes", "max_rank_send_bytes", "xgmi_bound_ms")
-        return {k: st[k] for k in keep if k in st}
+        out = {k: st[k] for k in keep if k in st}
+        # full-width exchanges of one training step (the output layer's restricted
+        # backward exchange, ~1 % of rows, not counted): hidden-layer halos forward and
+        # backward, the projected output layer forward; only the latter with recompute
+        from dgraph_amd.models.sage import _pad_width
+
+        c_out = _pad_width(self.shape.num_classes)
+        widths = [c_out] if self.recompute else \
+            [self.args.hidden] * (self.args.layers - 2) + [c_out] + \
+            [self.args.hidden] * (self.args.layers - 2)
+        out["exchange_widths_per_step"] = widths
+        if "max_pairwise_bytes" in out:
+            rows = out["max_pairwise_bytes"] / fb
+            out["max_pairwise_bytes_per_step"] = rows * sum(widths) * self.x.element_size()
+        return out
 
     def free(self):
         for k in ("graph", "x", "model", "opt", "sync", "train_idx", "y_train", "eval_idx",
