@@ -305,6 +305,37 @@ void row_scale_cols_op(const at::Tensor& x, const at::Tensor& s, const at::Tenso
                               static_cast<int>(x.size(1)), cur_stream(x)));
 }
 
+// row_scale_cols on bf16 + the column sums of the unscaled x into partial[:, 0:w] (a
+// column slice of a [nblocks, F] fp32 partials tensor; the caller sums over dim 0)
+void row_scale_colsum_op(const at::Tensor& x, const at::Tensor& s, const at::Tensor& out,
+                         const at::Tensor& partial) {
+  check_dev(x, x, "x");
+  check_dev(x, out, "out");
+  check_dev(x, s, "s");
+  check_dev(x, partial, "partial");
+  TORCH_CHECK(x.dim() == 2 && out.dim() == 2 && x.sizes() == out.sizes(), "shape mismatch");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && out.scalar_type() == at::kBFloat16,
+              "row_scale_colsum is bf16");
+  TORCH_CHECK(s.scalar_type() == at::kFloat && s.is_contiguous() && s.numel() == x.size(0),
+              "s must be contiguous fp32 [rows]");
+  TORCH_CHECK(x.stride(1) == 1 && out.stride(1) == 1, "rows must be unit-stride");
+  TORCH_CHECK(x.size(1) % 8 == 0 && x.size(1) <= 256 && x.stride(0) % 8 == 0 &&
+                  out.stride(0) % 8 == 0,
+              "row_scale_colsum needs 16-B vectors and width <= 256");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0,
+              "row_scale_colsum needs 16-B aligned x/out");
+  TORCH_CHECK(partial.scalar_type() == at::kFloat && partial.dim() == 2 &&
+                  partial.size(1) == x.size(1) && partial.stride(1) == 1 &&
+                  partial.size(0) >= 1 && partial.size(0) <= 65535,
+              "partial must be fp32 [nblocks, w] with unit column stride");
+  c10::DeviceGuard gd(x.device());
+  DG_HIP_CHECK(row_scale_colsum(x.data_ptr(), x.stride(0), s.data_ptr<float>(), out.data_ptr(),
+                                out.stride(0), x.size(0), static_cast<int>(x.size(1)),
+                                partial.data_ptr<float>(), partial.stride(0),
+                                static_cast<int>(partial.size(0)), cur_stream(x)));
+}
+
 // mode 0 (agg): out[r] = sum_c relu(rowterm[r] + gat[c]); mode 1 (cnt): out[r] = rowmul[r] *
 // #{c : rowterm[r] + gat[c] > 0}; mode 2 (tgrad): out[r] = sum_c gat2[c] * [rowterm[r]+gat[c]>0]
 void pair_relu_op(const at::Tensor& rowptr, const at::Tensor& col, int64_t mode,
@@ -676,6 +707,7 @@ TORCH_LIBRARY(dgraph_amd, m) {
   m.def("relu_mask_bwd(Tensor(a!) g, Tensor bits) -> ()");
   m.def("col_sum(Tensor g) -> Tensor");
   m.def("row_scale_cols(Tensor x, Tensor s, Tensor(a!) out) -> ()");
+  m.def("row_scale_colsum(Tensor x, Tensor s, Tensor(a!) out, Tensor(b!) partial) -> ()");
   m.def("pair_relu(Tensor rowptr, Tensor col, int mode, Tensor rowterm, Tensor gat, Tensor? gat2, "
         "Tensor? rowmul, Tensor(a!) out) -> ()");
   m.def("layer_norm_fwd(Tensor x, Tensor? gamma, Tensor? beta, Tensor? res, float eps) -> "
@@ -718,6 +750,7 @@ TORCH_LIBRARY_IMPL(dgraph_amd, CUDA, m) {
   m.impl("relu_mask_bwd", &dgraph::relu_mask_bwd_op);
   m.impl("col_sum", &dgraph::col_sum_op);
   m.impl("row_scale_cols", &dgraph::row_scale_cols_op);
+  m.impl("row_scale_colsum", &dgraph::row_scale_colsum_op);
   m.impl("pair_relu", &dgraph::pair_relu_op);
   m.impl("gather_add_act", &dgraph::gather_add_act_op);
   m.impl("layer_norm_fwd", &dgraph::layer_norm_fwd_op);

@@ -290,7 +290,79 @@ __global__ __launch_bounds__(256) void row_scale_cols_kernel(
   }
 }
 
+// Same pass, plus the fp32 column sums of the UNSCALED x (the SAGE bias gradient of the
+// layer whose output gradient is being pre-scaled for the transposed mean aggregation):
+// the bias gradient then costs no pass of its own over x. Block b owns rows
+// [b * rows_per_block, ...) (col_sum_partial's layout: fixed partition, fixed-order LDS
+// reduction, deterministic); each thread keeps UR rows' vectors in flight.
+template <int UR>
+__global__ __launch_bounds__(256) void row_scale_colsum_kernel(
+    const uint16_t* __restrict__ x, int64_t ldx, const float* __restrict__ s,
+    uint16_t* __restrict__ out, int64_t ldo, int64_t L, int w, int64_t rows_per_block,
+    float* __restrict__ partial, int64_t ldp) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int VEC = 8;
+  const int tpr = w / VEC;           // threads per row (w <= 256)
+  const int rpi = blockDim.x / tpr;  // rows per iteration
+  const int t = threadIdx.x;
+  const int rg = t / tpr;
+  const int cc = (t % tpr) * VEC;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
+  const int64_t r1 = r0 + rows_per_block < L ? r0 + rows_per_block : L;
+  float acc[VEC];
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) acc[i] = 0.f;
+  if (rg < rpi) {
+    for (int64_t rb = r0 + rg; rb < r1; rb += static_cast<int64_t>(rpi) * UR) {
+      float v[UR][VEC];
+      float sc[UR];
+#pragma unroll
+      for (int u = 0; u < UR; ++u) {
+        const int64_t r = rb + static_cast<int64_t>(u) * rpi;
+        if (r < r1) {
+          load_vec_f32<uint16_t, VEC>(x + r * ldx + cc, v[u]);
+          sc[u] = s[r];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < UR; ++u) {
+        const int64_t r = rb + static_cast<int64_t>(u) * rpi;
+        if (r < r1) {
+#pragma unroll
+          for (int i = 0; i < VEC; ++i) {
+            acc[i] += v[u][i];
+            v[u][i] *= sc[u];
+          }
+          store_vec_f32<uint16_t, VEC>(out + r * ldo + cc, v[u]);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) smem[rg * w + cc + i] = acc[i];
+  }
+  __syncthreads();
+  for (int c = t; c < w; c += blockDim.x) {
+    float sum = 0.f;
+    for (int k = 0; k < rpi; ++k) sum += smem[k * w + c];
+    partial[static_cast<int64_t>(blockIdx.x) * ldp + c] = sum;
+  }
+}
+
 }  // namespace
+
+hipError_t row_scale_colsum(const void* x, int64_t ldx, const float* s, void* out,
+                            int64_t ldo, int64_t L, int w, float* partial, int64_t ldp,
+                            int nblocks, hipStream_t st) {
+  if (L <= 0 || w <= 0) return hipSuccess;
+  if (w % 8 != 0 || w > 256 || ldx % 8 != 0 || ldo % 8 != 0) return hipErrorInvalidValue;
+  const int64_t rpb = (L + nblocks - 1) / nblocks;
+  const int rpi = 256 / (w / 8);
+  const size_t lds = static_cast<size_t>(rpi) * w * sizeof(float);
+  hipLaunchKernelGGL((row_scale_colsum_kernel<4>), dim3(nblocks), dim3(256), lds, st,
+                     static_cast<const uint16_t*>(x), ldx, s, static_cast<uint16_t*>(out),
+                     ldo, L, w, rpb, partial, ldp);
+  return hipGetLastError();
+}
 
 hipError_t row_scale_cols(DType dt, const void* x, int64_t ldx, const float* s, void* out,
                           int64_t ldo, int64_t L, int w, hipStream_t st) {

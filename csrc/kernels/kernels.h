@@ -93,6 +93,11 @@ hipError_t col_sum_partial(DType dt, const void* g, int64_t ld, int64_t L, int F
                            float* partial, int nblocks, hipStream_t stream);
 //   row_scale_cols: out[r, 0:w] = x[r, c0:c0+w] * s[r] (x already offset by c0; w % 8 == 0,
 //                   16-B aligned rows).
+//   row_scale_colsum: row_scale_cols (bf16) + partial[b, 0:w] (row stride ldp) = fp32
+//   column sums of the unscaled x over block b's rows (nblocks blocks, fixed partition)
+hipError_t row_scale_colsum(const void* x, int64_t ldx, const float* s, void* out,
+                            int64_t ldo, int64_t L, int w, float* partial, int64_t ldp,
+                            int nblocks, hipStream_t st);
 hipError_t row_scale_cols(DType dt, const void* x, int64_t ldx, const float* s, void* out,
                           int64_t ldo, int64_t L, int w, hipStream_t stream);
 

@@ -528,12 +528,16 @@ class SAGEStackFn(Function):
             ext1 = rc is not None and i == 1  # x has the L1 extended rows, g the owned L
             xs = x[:L] if ext1 else x
 
-            def self_grads(i=i, x=xs, g=g, ws=ws, b=b, r_in=r_in, r_out=r_out):
+            # bias gradient (column sums of g) formed by aggregate_T's pre-scale pass
+            gsum = [] if b is not None else None
+
+            def self_grads(i=i, x=xs, g=g, ws=ws, b=b, r_in=r_in, r_out=r_out, gsum=gsum):
                 # W_self / bias gradients need no aggregation: on a multi-GPU graph they
                 # run while the layer's reverse halo exchange is on the links
                 grads[3 * i] = wgrad(x, g)[:r_in, :r_out].to(ws.dtype)
                 if b is not None:
-                    grads[3 * i + 2] = col_sum_f32(g)[:r_out].to(b.dtype)
+                    cs = gsum[0] if gsum else col_sum_f32(g)
+                    grads[3 * i + 2] = cs[:r_out].to(b.dtype)
 
             dx = None
             if pf:
@@ -560,7 +564,7 @@ class SAGEStackFn(Function):
                     u[L:Lp].zero_()
                 scratch = ws_obj.slots["tmp_b"] if use_ws else None
                 graph.aggregate_T(g, mean=True, out=u[:L], scratch=scratch,
-                                  overlap=self_grads, halo_out=u[Lp:L1])
+                                  overlap=self_grads, halo_out=u[Lp:L1], colsum=gsum)
                 del scratch
                 grads[3 * i + 1] = wgrad(x, u)[:r_in, :r_out].to(wn.dtype)
                 if fuse_dx:
@@ -589,7 +593,7 @@ class SAGEStackFn(Function):
                 scratch = ws_obj.slots["tmp_b" if u_name == "tmp_a" else "tmp_a"] \
                     if use_ws and i < n - 1 else None
                 u = graph.aggregate_T(g, mean=True, out=V(u_name, dims[i + 1]),
-                                      scratch=scratch, overlap=self_grads)
+                                      scratch=scratch, overlap=self_grads, colsum=gsum)
                 del scratch
                 grads[3 * i + 1] = wgrad(x, u)[:r_in, :r_out].to(wn.dtype)
                 if fuse_dx:

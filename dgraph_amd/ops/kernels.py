@@ -164,6 +164,18 @@ def col_sum(g: torch.Tensor) -> torch.Tensor:
     return _ref.col_sum(g)
 
 
+def row_scale_colsum(x: torch.Tensor, s: torch.Tensor, out: torch.Tensor,
+                     partial: torch.Tensor) -> torch.Tensor:
+    """:func:`row_scale_cols` (bf16) that also writes fp32 column sums of the UNSCALED
+    ``x`` over a fixed row partition into ``partial [nblocks, w]`` (may be a column slice
+    of a wider partials tensor); ``partial.sum(0)`` are the column sums. Native: one
+    pass (elementwise.hip row_scale_colsum)."""
+    if _native_ok(x):
+        _native.ops().row_scale_colsum(x, _f32(s), out, partial)
+        return out
+    return _ref.row_scale_colsum(x, s, out, partial)
+
+
 def row_scale_cols(x: torch.Tensor, s: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
     """``out[r, :] = x[r, :] * s[r]`` for a row-strided ``x`` (e.g. a column slice);
     fp32 ``s``. Native: one streaming pass with 16-B lanes (elementwise.hip)."""

@@ -205,6 +205,17 @@ def row_scale_cols(x: torch.Tensor, s: torch.Tensor, out: torch.Tensor) -> torch
     return out
 
 
+def row_scale_colsum(x: torch.Tensor, s: torch.Tensor, out: torch.Tensor,
+                     partial: torch.Tensor) -> torch.Tensor:
+    nb = partial.shape[0]
+    rpb = (x.shape[0] + nb - 1) // nb
+    xf = x.float()
+    partial.zero_()
+    for b in range(nb):
+        partial[b] = xf[b * rpb:(b + 1) * rpb].sum(0)
+    return row_scale_cols(x, s, out)
+
+
 def col_sum(g: torch.Tensor) -> torch.Tensor:
     return g.float().sum(0)
 

@@ -196,8 +196,12 @@ class DistGraph:
         w = -(-w // 64) * 64
         return [(c, min(c + w, F)) for c in range(0, F, w)]
 
+    # row blocks of the fused pre-scale + bias-gradient column sums (row_scale_colsum)
+    COLSUM_BLOCKS = 1024
+
     @staticmethod
-    def _spmm_col_scaled(csr: CSR, g: torch.Tensor, cs: torch.Tensor, out, scratch):
+    def _spmm_col_scaled(csr: CSR, g: torch.Tensor, cs: torch.Tensor, out, scratch,
+                         colsum: Optional[list] = None):
         """``A g`` with a column scale. With a ``scratch`` buffer (a free workspace slot)
         the scale is applied to column slices of ``g`` first (one streaming pass) and the
         SpMM runs unweighted: a per-edge scale gather costs the gather-bound kernel a
@@ -206,31 +210,57 @@ class DistGraph:
         rows, F = g.shape
         S = 0 if scratch is None else min(F, (scratch.numel() // max(rows, 1)) // 64 * 64)
         if S < 64 or g.dtype != torch.bfloat16 or not g.is_cuda:
-            return K.spmm(csr.rowptr, csr.col, g, out, col_scale=cs, split=_hs(csr))
+            out = K.spmm(csr.rowptr, csr.col, g, out, col_scale=cs, split=_hs(csr))
+            if colsum is not None:
+                colsum.append(K.col_sum(g))
+            return out
         if out is None:
             out = torch.empty(csr.num_rows, F, dtype=g.dtype, device=g.device)
         aligned = g.data_ptr() % 16 == 0 and scratch.data_ptr() % 16 == 0 and F % 8 == 0
+        # ``colsum`` (a list): append the fp32 column sums of g, formed by the scale pass
+        partial = None
+        if colsum is not None and aligned and F <= 2048:
+            partial = torch.empty(min(DistGraph.COLSUM_BLOCKS, max(rows, 1)), F,
+                                  dtype=torch.float32, device=g.device)
         for c0 in range(0, F, S):
             w = min(S, F - c0)
             buf = scratch[: rows * w].view(rows, w)
-            if aligned and w % 8 == 0:
+            if partial is not None and w % 8 == 0 and w <= 256:
+                K.row_scale_colsum(g[:, c0:c0 + w], cs, buf, partial[:, c0:c0 + w])
+            elif aligned and w % 8 == 0:
+                if partial is not None:
+                    partial[:, c0:c0 + w].zero_()
+                    partial[0, c0:c0 + w] = K.col_sum(g[:, c0:c0 + w])
                 K.row_scale_cols(g[:, c0:c0 + w], cs, buf)
             else:
                 torch.mul(g[:, c0:c0 + w], cs.unsqueeze(1), out=buf)
             K.spmm(csr.rowptr, csr.col, buf, out[:, c0:c0 + w], split=_hs(csr))
+        if colsum is not None:
+            colsum.append(partial.sum(0) if partial is not None else K.col_sum(g))
+        return out
+
+    def _interior_T(self, it: CSR, g, cs, out, scratch, colsum):
+        if cs is not None and scratch is not None:
+            return self._spmm_col_scaled(it, g, cs, out, scratch.reshape(-1), colsum)
+        out = K.spmm(it.rowptr, it.col, g, out, col_scale=cs, split=_hs(it))
+        if colsum is not None:
+            colsum.append(K.col_sum(g))
         return out
 
     def aggregate_T(self, g: torch.Tensor, mean: bool = True,
                     out: Optional[torch.Tensor] = None,
                     scratch: Optional[torch.Tensor] = None, overlap=None,
-                    halo_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                    halo_out: Optional[torch.Tensor] = None,
+                    colsum: Optional[list] = None) -> torch.Tensor:
         """Transposed aggregation (the backward of :meth:`aggregate`). ``scratch``: an
         optional free buffer (any shape, same dtype as ``g``) for the pre-scaled path.
         ``overlap``: a callable of independent work, run after the reverse exchange and
         the interior SpMM are issued and before the exchange is waited for.
         ``halo_out``: ``[H, F]`` buffer that receives the halo rows' gradient, which then
         stays on this rank (halo recomputation: the rows were computed here) — no
-        exchange, no owner-side segment sum."""
+        exchange, no owner-side segment sum. ``colsum``: a list that receives the fp32
+        column sums of ``g`` (a bias gradient) before ``overlap`` runs — formed by the
+        pre-scale pass when there is one, else by a column-sum pass."""
         cs = self.inv_deg if mean else None
         self.edges_aggregated += self.nnz
         g = g.contiguous()
@@ -238,18 +268,12 @@ class DistGraph:
         if halo_out is not None and self.halo is not None:
             K.spmm(self.halo.transpose().rowptr, self.halo.transpose().col, g, halo_out,
                    col_scale=cs, split=_hs(self.halo.transpose()))
-            if cs is not None and scratch is not None:
-                out = self._spmm_col_scaled(it, g, cs, out, scratch.reshape(-1))
-            else:
-                out = K.spmm(it.rowptr, it.col, g, out, col_scale=cs, split=_hs(it))
+            out = self._interior_T(it, g, cs, out, scratch, colsum)
             if overlap is not None:
                 overlap()
             return out
         if self.halo is None:
-            if cs is not None and scratch is not None:
-                out = self._spmm_col_scaled(it, g, cs, out, scratch.reshape(-1))
-            else:
-                out = K.spmm(it.rowptr, it.col, g, out, col_scale=cs, split=_hs(it))
+            out = self._interior_T(it, g, cs, out, scratch, colsum)
             if overlap is not None:
                 overlap()
             return out
@@ -263,10 +287,7 @@ class DistGraph:
             if not self.overlap:
                 work.wait()
             pend.append((c0, c1, sg, work))
-        if cs is not None and scratch is not None:
-            out = self._spmm_col_scaled(it, g, cs, out, scratch.reshape(-1))
-        else:
-            out = K.spmm(it.rowptr, it.col, g, out, col_scale=cs, split=_hs(it))
+        out = self._interior_T(it, g, cs, out, scratch, colsum)
         if overlap is not None:
             overlap()  # independent work queued behind the exchange (e.g. a weight grad)
         st = self.send_map.transpose_csr().compact_rows()
