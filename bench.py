@@ -12,7 +12,9 @@ A step is the reference's full-graph epoch (experiments/OGB/main.py:129-184):
   accumulation, fp32 master weights) -> masked cross-entropy on the train split, and
   validation/test accuracy from the SAME forward -> backward -> gradient all-reduce ->
   Adam step.
-The output layer's backward uses only the train rows' nonzero gradient (A[train, :]^T):
+The output layer's backward uses only the train rows' nonzero gradient (A[train, :]^T),
+and the layer below it aggregates transposed only from the rows where its incoming
+gradient can be nonzero (the train rows and their neighbours, DistGraph.grad_support):
 exact (the dense backward multiplies zeros), counted as what it aggregates.
 
     value = edges_per_s = num_layers * E_msg / step_s      (BASELINE.md §2 definition)
@@ -175,6 +177,12 @@ class Job:
                                      _offsets(shape.num_nodes, p_world), dev, seed=args.seed,
                                      dtype=dtype, return_split=True)
         self.train_idx = torch.nonzero(split == SPLIT_TRAIN, as_tuple=True)[0]
+        # partitioned graphs: the gradient support of the layer below the output layer
+        # (DistGraph.prepare_grad_support), built now while device memory is free
+        # (collective: every rank builds it at this point). Not at W=1 on the papers100M
+        # shape: its ~5 GB costs the near-full step allocator stalls (PERFORMANCE.md).
+        if args.layers >= 2 and p_world > 1:
+            self.graph.prepare_grad_support(self.train_idx)
         self.y_train = y[self.train_idx]
         ev = split == SPLIT_VALID
         ev |= split == SPLIT_TEST

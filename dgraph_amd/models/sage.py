@@ -527,6 +527,10 @@ class SAGEStackFn(Function):
 
             ext1 = rc is not None and i == 1  # x has the L1 extended rows, g the owned L
             xs = x[:L] if ext1 else x
+            # below a loss-row-sparse output layer, g is zero off the loss rows and their
+            # neighbours: the transposed aggregation walks only those sources (exact)
+            sup = graph.grad_support(ctx.out_rows) if (sparse_last and i == n - 2) \
+                else None
 
             # bias gradient (column sums of g) formed by aggregate_T's pre-scale pass
             gsum = [] if b is not None else None
@@ -542,7 +546,7 @@ class SAGEStackFn(Function):
             dx = None
             if pf:
                 dz = graph.aggregate_T(g, mean=True, out=V("tmp_b", dims[i + 1]),
-                                       overlap=self_grads)
+                                       overlap=self_grads, support=sup)
                 grads[3 * i + 1] = wgrad(x, dz)[:r_in, :r_out].to(wn.dtype)
                 if need_dx:
                     if fuse_dx:
@@ -564,7 +568,8 @@ class SAGEStackFn(Function):
                     u[L:Lp].zero_()
                 scratch = ws_obj.slots["tmp_b"] if use_ws else None
                 graph.aggregate_T(g, mean=True, out=u[:L], scratch=scratch,
-                                  overlap=self_grads, halo_out=u[Lp:L1], colsum=gsum)
+                                  overlap=self_grads, halo_out=u[Lp:L1], colsum=gsum,
+                                  support=sup)
                 del scratch
                 grads[3 * i + 1] = wgrad(x, u)[:r_in, :r_out].to(wn.dtype)
                 if fuse_dx:
@@ -593,7 +598,8 @@ class SAGEStackFn(Function):
                 scratch = ws_obj.slots["tmp_b" if u_name == "tmp_a" else "tmp_a"] \
                     if use_ws and i < n - 1 else None
                 u = graph.aggregate_T(g, mean=True, out=V(u_name, dims[i + 1]),
-                                      scratch=scratch, overlap=self_grads, colsum=gsum)
+                                      scratch=scratch, overlap=self_grads, colsum=gsum,
+                                      support=sup)
                 del scratch
                 grads[3 * i + 1] = wgrad(x, u)[:r_in, :r_out].to(wn.dtype)
                 if fuse_dx:
@@ -625,7 +631,8 @@ class SAGEStackFn(Function):
                 grads[3 * i + 1] = wgrad(a, g)[:r_in, :r_out].to(wn.dtype)
                 if need_dx:
                     t = torch.mm(g, wn_.t(), out=a)
-                    dx = graph.aggregate_T(t, mean=True, out=x if recyclable else None)
+                    dx = graph.aggregate_T(t, mean=True, out=x if recyclable else None,
+                                           support=sup)
                     del t
                     dx.addmm_(g, ws_.t())
                 del a, a_buf

@@ -37,6 +37,43 @@ def _hs(csr: CSR):
     return csr.hub_split(SPMM_HUB_CAP) if SPMM_HUB_CAP > 0 else None
 
 
+def _select_columns(csr: CSR, cols: torch.Tensor, ncols: int) -> CSR:
+    """``csr`` restricted to the entries whose column is in ``cols`` (row order and the
+    order within a row kept). Two passes over row chunks of ~2^26 entries: count, then
+    copy into the exact-size column array (bounded temporaries at 10^9+ entries, no
+    concatenation copy)."""
+    dev = csr.device
+    keep = torch.zeros(ncols, dtype=torch.bool, device=dev)
+    keep[cols] = True
+    R = csr.num_rows
+    nnz = max(csr.col.numel(), 1)
+    step = max(1, int(R * (1 << 26) // nnz))
+    chunks = [(r0, min(R, r0 + step)) for r0 in range(0, R, step)]
+    deg = torch.zeros(R, dtype=torch.long, device=dev)
+    for r0, r1 in chunks:
+        a, b = int(csr.rowptr[r0]), int(csr.rowptr[r1])
+        if b == a:
+            continue
+        m = keep[csr.col[a:b].long()]
+        rows = torch.repeat_interleave(torch.arange(r0, r1, device=dev),
+                                       csr.rowptr[r0 + 1:r1 + 1] - csr.rowptr[r0:r1],
+                                       output_size=b - a)
+        deg[r0:r1] = torch.bincount(rows[m] - r0, minlength=r1 - r0)
+        del m, rows
+    rowptr = torch.zeros(R + 1, dtype=torch.long, device=dev)
+    torch.cumsum(deg, 0, out=rowptr[1:])
+    del deg
+    col = torch.empty(int(rowptr[-1]), dtype=csr.col.dtype, device=dev)
+    for r0, r1 in chunks:
+        a, b = int(csr.rowptr[r0]), int(csr.rowptr[r1])
+        if b == a:
+            continue
+        c = csr.col[a:b]
+        col[int(rowptr[r0]):int(rowptr[r1])] = c[keep[c.long()]]
+        del c
+    return CSR(rowptr, col, csr.num_cols, None, symmetric=False)
+
+
 def _cache_lookup(cache: dict, rows: torch.Tensor):
     """Plan-cache hit for the row-index tensor ``rows``: the SAME live tensor object (a
     weak reference, never the address, which a freed tensor's successor can reuse) at the
@@ -81,6 +118,7 @@ class DistGraph:
         self._restrict_cache = {}
         self._restrict_fwd_cache = {}
         self._static_cache = {}
+        self._support_cache = {}
         # edges (nonzeros) aggregated by every call so far, forward and transposed:
         # bench.py reports the per-step delta as ``edges_aggregated_per_step``
         self.edges_aggregated = 0
@@ -251,7 +289,7 @@ class DistGraph:
                     out: Optional[torch.Tensor] = None,
                     scratch: Optional[torch.Tensor] = None, overlap=None,
                     halo_out: Optional[torch.Tensor] = None,
-                    colsum: Optional[list] = None) -> torch.Tensor:
+                    colsum: Optional[list] = None, support=None) -> torch.Tensor:
         """Transposed aggregation (the backward of :meth:`aggregate`). ``scratch``: an
         optional free buffer (any shape, same dtype as ``g``) for the pre-scaled path.
         ``overlap``: a callable of independent work, run after the reverse exchange and
@@ -262,9 +300,13 @@ class DistGraph:
         column sums of ``g`` (a bias gradient) before ``overlap`` runs — formed by the
         pre-scale pass when there is one, else by a column-sum pass."""
         cs = self.inv_deg if mean else None
-        self.edges_aggregated += self.nnz
         g = g.contiguous()
         it = self.interior if self.interior.symmetric else self.interior.transpose()
+        if support is not None:
+            # ``support`` = grad_support(rows): g is zero outside S, so only the interior
+            # entries with a source in S contribute
+            it = support[1]
+        self.edges_aggregated += it.nnz + (self.halo.nnz if self.halo is not None else 0)
         if halo_out is not None and self.halo is not None:
             K.spmm(self.halo.transpose().rowptr, self.halo.transpose().col, g, halo_out,
                    col_scale=cs, split=_hs(self.halo.transpose()))
@@ -380,6 +422,54 @@ class DistGraph:
         work.wait()
         K.spmm(st.rowptr, st.col, sg, out, beta=1.0, split=_hs(st))
         return out
+
+    # gradient-support restriction of the transposed aggregation (see grad_support); off
+    # with DGRAPH_GRAD_SUPPORT=0. Built only with this much device memory left over.
+    GRAD_SUPPORT = os.environ.get("DGRAPH_GRAD_SUPPORT", "1") != "0"
+    SUPPORT_HEADROOM = 12 << 30
+
+    def grad_support(self, rows: torch.Tensor):
+        """The :meth:`prepare_grad_support` result for ``rows`` (``None`` when it was not
+        prepared for this row tensor: then the full transposed block is used)."""
+        return _cache_lookup(self._support_cache, rows)
+
+    def prepare_grad_support(self, rows: torch.Tensor):
+        """For a loss on ``rows`` with a project-first output layer: the local rows where
+        the gradient entering the layer below the output layer can be nonzero — the loss
+        rows and their in-neighbours (the rows :meth:`aggregate_T_rows` writes, plus the
+        rows the halo sub-plan adds to), and the interior transposed block restricted to
+        those columns, ``A^T[:, S]`` (cached per ``rows``, like the restricted plans).
+
+        The transposed aggregation of that gradient then walks only the edges whose
+        source lies in S (~30 % of them on the bench graph): exact, the other terms are
+        products with rows that are zero by construction. Returns ``None`` when disabled
+        or when the restricted block does not fit in device memory. Build it at setup,
+        before the training workspace exists (bench.py does so on partitioned graphs; on
+        one GPU at the papers100M shape the extra ~5 GB pushed the caching allocator into
+        per-step release/re-map stalls: 791 -> 853 ms although the kernels got 80 ms
+        faster). Collective on a partitioned graph (the restricted plan)."""
+        if not self.GRAD_SUPPORT:
+            return None
+        hit = _cache_lookup(self._support_cache, rows)
+        if hit is not None:
+            return hit
+        it, _, sub = self._restricted(rows)
+        parts = [rows.long(), it.compact_rows().row_map.long()]
+        if sub is not None:
+            parts.append(sub[4].long())  # local rows the halo sub-plan adds to
+        S = torch.unique(torch.cat(parts))
+        full = self.interior if self.interior.symmetric else self.interior.transpose()
+        res = None
+        dev = full.device
+        keep_frac = S.numel() / max(self.L, 1)
+        # the kept columns (~|S|/L of the entries) + row pointers + chunk temporaries
+        need = int(full.col.numel() * keep_frac * 1.1) * full.col.element_size() + \
+            2 * full.rowptr.numel() * 8 + (1 << 30)
+        free = torch.cuda.mem_get_info(dev)[0] if dev.type == "cuda" else need + (64 << 30)
+        if free - need >= self.SUPPORT_HEADROOM:
+            res = (S, _select_columns(full, S, self.L))
+        _cache_store(self._support_cache, rows, res)
+        return res
 
     def _restricted_fwd(self, rows: torch.Tensor):
         """Forward counterpart of :meth:`_restricted`: A[rows, :L] and A[rows, halo] with

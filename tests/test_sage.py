@@ -196,3 +196,32 @@ def test_eval_rows_and_restricted_last_layer(classes):
         torch.testing.assert_close(a, b, atol=1e-6, rtol=1e-4)
     with pytest.raises(ValueError):
         res[True][3](x, g, out_rows=rows, eval_rows=ev_rows, restrict_last=True)
+
+
+@pytest.mark.parametrize("hidden,classes", [(64, 40), (96, 47)])
+def test_grad_support_matches_dense(hidden, classes):
+    """With the gradient support prepared (DistGraph.prepare_grad_support), the layer
+    below the loss-row-sparse output layer aggregates transposed only from the loss rows
+    and their neighbours: same gradients as dense autograd, fewer edges aggregated."""
+    p, g, A = _graph()
+    x, _, tr = node_data(SHAPE, 0, p["offsets"], "cpu", dtype=torch.float32)
+    rows = torch.nonzero(tr).squeeze(1)[:8]  # a few loss rows: a small support
+    sup = g.prepare_grad_support(rows)
+    assert sup is not None and sup[1].nnz < g.nnz
+    torch.manual_seed(0)
+    m = GraphSAGE(SHAPE.num_features, hidden, classes, 3)
+    e0 = g.edges_aggregated
+    out = m(x, g, out_rows=rows)
+    out.square().mean().backward()
+    e_sup = g.edges_aggregated - e0
+    grads = [q.grad.clone() for q in m.parameters()]
+    m.zero_grad()
+    ref = _dense_forward(m, x, A)[rows]
+    ref.square().mean().backward()
+    for a, q in zip(grads, m.parameters()):
+        torch.testing.assert_close(a, q.grad, atol=1e-6, rtol=1e-4)
+    g.GRAD_SUPPORT = False
+    g._support_cache.clear()
+    e0 = g.edges_aggregated
+    m(x, g, out_rows=rows).square().mean().backward()
+    assert e_sup < g.edges_aggregated - e0
