@@ -181,7 +181,8 @@ class Job:
         # (DistGraph.prepare_grad_support), built now while device memory is free
         # (collective: every rank builds it at this point). Not at W=1 on the papers100M
         # shape: its ~5 GB costs the near-full step allocator stalls (PERFORMANCE.md).
-        if args.layers >= 2 and p_world > 1:
+        gs = os.environ.get("DGRAPH_BENCH_GRAD_SUPPORT", "auto")
+        if args.layers >= 2 and (gs == "on" or (gs == "auto" and p_world > 1)):
             self.graph.prepare_grad_support(self.train_idx)
         self.y_train = y[self.train_idx]
         ev = split == SPLIT_VALID

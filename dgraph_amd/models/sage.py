@@ -229,6 +229,18 @@ class SageWorkspace:
                 self.slots["agg0"] = torch.empty(rows0 * dims[0], dtype=dtype, device=device)
         self.key = key
 
+    def mask(self, i: int, words: int, device) -> torch.Tensor:
+        """Layer ``i``'s 1-bit ReLU mask words (persistent: a 3.5 GB-per-layer allocation
+        per step at the papers100M shape otherwise, which at ~271 GB makes the caching
+        allocator release and re-map blocks once anything else grows)."""
+        name = f"mask{i}"
+        buf = self.slots.get(name)
+        if buf is None or buf.numel() < words or buf.device != torch.device(device):
+            self.slots.pop(name, None)
+            buf = torch.empty(words, dtype=torch.int64, device=device)
+            self.slots[name] = buf
+        return buf[:words]
+
     def has(self, name: str) -> bool:
         return name in self.slots
 
@@ -328,8 +340,9 @@ class SAGEStackFn(Function):
                 not relu or (i + 1 < n and _bwd_fused(specs, dims_p, i + 1, True, h)))
             mask = None
             if fused and relu:
-                mask = torch.empty(tile32_mask_words(rows_i, Fo), dtype=torch.int64,
-                                   device=h.device)
+                words = tile32_mask_words(rows_i, Fo)
+                mask = ws_obj.mask(i, words, h.device) if use_ws else \
+                    torch.empty(words, dtype=torch.int64, device=h.device)
             if last and pf and not relu and out_rows is not None and restrict_last:
                 # only the loss rows leave the node: y[rows] = A[rows, :] (h Wn) +
                 # h[rows] Ws + b — the row-restricted SpMM reads ~|rows|/L of the edges
