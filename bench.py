@@ -177,12 +177,12 @@ class Job:
                                      _offsets(shape.num_nodes, p_world), dev, seed=args.seed,
                                      dtype=dtype, return_split=True)
         self.train_idx = torch.nonzero(split == SPLIT_TRAIN, as_tuple=True)[0]
-        # partitioned graphs: the gradient support of the layer below the output layer
+        # the gradient support of the layer below the output layer
         # (DistGraph.prepare_grad_support), built now while device memory is free
-        # (collective: every rank builds it at this point). Not at W=1 on the papers100M
-        # shape: its ~5 GB costs the near-full step allocator stalls (PERFORMANCE.md).
-        gs = os.environ.get("DGRAPH_BENCH_GRAD_SUPPORT", "auto")
-        if args.layers >= 2 and (gs == "on" or (gs == "auto" and p_world > 1)):
+        # (collective: every rank builds it at this point); DGRAPH_BENCH_GRAD_SUPPORT=off
+        # for the A/B
+        gs = os.environ.get("DGRAPH_BENCH_GRAD_SUPPORT", "on")
+        if args.layers >= 2 and gs != "off":
             self.graph.prepare_grad_support(self.train_idx)
         self.y_train = y[self.train_idx]
         ev = split == SPLIT_VALID
@@ -213,6 +213,12 @@ class Job:
             self.steppers = {r: GraphedStep(lambda r=r: self.step(r), warmup=1)
                              for r in (False, True)}
         self.sync = GradSync(self.model.parameters(), group=None) if self.world > 1 else None
+        if dev.type == "cuda":
+            # return the graph build's cached temporaries (blocks > 512 MB are never split:
+            # left cached they pin tens of GB the training workspace cannot reuse, and the
+            # libraries' own device allocations then find no free memory)
+            gc.collect()
+            torch.cuda.empty_cache()
         self.inv_n = 1.0 / max(self.n_train, 1)
         self.correct = torch.zeros(2, dtype=torch.long, device=dev)  # val, test
 
