@@ -326,16 +326,40 @@ def timed(job: Job, steps: int, warmup: int, restrict_last: bool, verbose: bool 
     return float(red.item()), float(tot[0].item()), float(tot[1].item())
 
 
+def _spawn_ranks(n: int) -> int:
+    """Run this script under ``torch.distributed.run`` with ``n`` local ranks (loopback
+    rendezvous on a free port) as a CHILD process and return its exit status. Called only
+    before anything initialised the GPU (no exec from a GPU-initialised process)."""
+    import socket
+    import subprocess
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1",
+           "--nproc-per-node", str(n), "--master-addr", "127.0.0.1", "--master-port",
+           str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"[bench] WORLD_SIZE unset: launching {n} ranks: {' '.join(cmd)}", file=sys.stderr,
+          flush=True)
+    return subprocess.call(cmd)
+
+
 def main():
     args = parse()
     from dgraph_amd import Communicator
     from dgraph_amd.utils.config import RunConfig
     from dgraph_amd.utils.metrics import ExperimentLogger
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # not launched by torchrun: start the N ranks ourselves (this process never touches
+        # the GPU) and exit with their status — never measure W=1 under an N-GPU label
+        sys.exit(_spawn_ranks(args.gpus))
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
-    if world_env != args.gpus:
-        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world_env}",
+    if world_env != args.gpus and not (args.rehearse_world > 1 and world_env == 1):
+        print(f"[bench] error: --gpus {args.gpus} but WORLD_SIZE={world_env} (launch one rank "
+              f"per GPU: torchrun --nproc-per-node {args.gpus} bench.py --gpus {args.gpus})",
               file=sys.stderr)
+        sys.exit(2)
     cfg = RunConfig.from_env()  # DGRAPH_<SECTION>_<FIELD> overrides (kernel knobs etc.)
     cfg.model.hidden, cfg.model.num_layers, cfg.model.dtype = args.hidden, args.layers, args.dtype
     cfg.data.dataset, cfg.data.global_frac = args.shape, args.global_frac

@@ -1,0 +1,290 @@
+// dgraph_amd — dispatcher registration of the fp32 (reference-precision) kernels:
+// row-group SpMM with input-row lists / column maps, MFMA f32 dual GEMM, split-M weight
+// gradient, and the 1-bit keep masks of selected rows. A TORCH_LIBRARY_FRAGMENT of the
+// dgraph_amd library (csrc/bindings.cpp); every launch goes to the current HIP stream and
+// every shape contract is checked here, before a kernel sees a pointer.
+#include <ATen/ATen.h>
+#include <c10/core/DeviceGuard.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/library.h>
+
+#include "check.h"
+#include "kernels/kernels.h"
+
+namespace dgraph {
+namespace {
+
+hipStream_t stream_of(const at::Tensor& t) {
+  return c10::hip::getCurrentHIPStream(t.device().index()).stream();
+}
+
+void same_dev(const at::Tensor& t, const at::Tensor& ref, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.device() == ref.device(), "dgraph_amd: ", name,
+              " must be a GPU tensor on ", ref.device());
+}
+
+const at::Tensor* opt(const c10::optional<at::Tensor>& t) {
+  return (t.has_value() && t->defined()) ? &*t : nullptr;
+}
+
+void f32_rows(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.scalar_type() == at::kFloat && t.dim() == 2 && t.stride(1) == 1,
+              "dgraph_amd: ", name, " must be a 2-D float32 tensor with unit column stride");
+}
+
+const int64_t* idx64(const c10::optional<at::Tensor>& t, const at::Tensor& ref, int64_t n,
+                     const char* name) {
+  const at::Tensor* p = opt(t);
+  if (!p) return nullptr;
+  same_dev(*p, ref, name);
+  TORCH_CHECK(p->scalar_type() == at::kLong && p->is_contiguous() && p->numel() == n,
+              "dgraph_amd: ", name, " must be contiguous int64 with ", n, " entries");
+  return p->data_ptr<int64_t>();
+}
+
+// ------------------------------------------------------------------------------------
+void spmm_f32_ex_op(const at::Tensor& rowptr, const at::Tensor& col,
+                    const c10::optional<at::Tensor>& ew, const c10::optional<at::Tensor>& cs,
+                    const c10::optional<at::Tensor>& rs, const c10::optional<at::Tensor>& cmap,
+                    const c10::optional<at::Tensor>& row_ids, const at::Tensor& x,
+                    const at::Tensor& out, double beta, int64_t cap,
+                    const c10::optional<at::Tensor>& row_map,
+                    const c10::optional<at::Tensor>& gate) {
+  same_dev(rowptr, x, "rowptr");
+  same_dev(col, x, "col");
+  same_dev(out, x, "out");
+  f32_rows(x, "x");
+  f32_rows(out, "out");
+  TORCH_CHECK(rowptr.scalar_type() == at::kLong && rowptr.is_contiguous(),
+              "rowptr must be contiguous int64");
+  TORCH_CHECK(col.is_contiguous() && (col.scalar_type() == at::kInt || col.scalar_type() == at::kLong),
+              "col must be contiguous int32/int64");
+  TORCH_CHECK(x.size(1) == out.size(1), "x/out feature mismatch");
+  const at::Tensor* ri = opt(row_ids);
+  const int64_t nrows = ri ? ri->numel() : rowptr.numel() - 1;
+  const int64_t* rid = idx64(row_ids, x, nrows, "row_ids");
+  const int64_t* rmap = idx64(row_map, x, nrows, "row_map");
+  if (!rmap) TORCH_CHECK(out.size(0) >= nrows, "out has fewer rows than the CSR rows");
+  auto f32opt = [&](const c10::optional<at::Tensor>& t, const char* name) -> const float* {
+    const at::Tensor* p = opt(t);
+    if (!p) return nullptr;
+    same_dev(*p, x, name);
+    TORCH_CHECK(p->scalar_type() == at::kFloat && p->is_contiguous(), name,
+                " must be contiguous float32");
+    return p->data_ptr<float>();
+  };
+  const float* ewp = f32opt(ew, "edge_weight");
+  if (ewp) TORCH_CHECK(ew->numel() == col.numel(), "edge_weight must be [E]");
+  const float* csp = f32opt(cs, "col_scale");
+  const float* rsp = f32opt(rs, "row_scale");
+  const int32_t* cm = nullptr;
+  if (const at::Tensor* p = opt(cmap)) {
+    same_dev(*p, x, "col_map");
+    TORCH_CHECK(p->scalar_type() == at::kInt && p->is_contiguous(),
+                "col_map must be contiguous int32");
+    cm = p->data_ptr<int32_t>();
+  }
+  TORCH_CHECK(spmm_f32_rowgroup_ok(static_cast<int>(x.size(1)), x.stride(0), out.stride(0),
+                                   x.data_ptr(), out.data_ptr()),
+              "spmm_f32_ex: F % 4 == 0 and 16-B aligned rows/strides required");
+  const float* gp = nullptr;
+  int64_t ldg = 0;
+  if (const at::Tensor* gt = opt(gate)) {
+    f32_rows(*gt, "gate");
+    same_dev(*gt, x, "gate");
+    TORCH_CHECK(gt->size(1) >= x.size(1) && gt->stride(0) % 4 == 0 &&
+                    reinterpret_cast<uintptr_t>(gt->data_ptr()) % 16 == 0,
+                "gate must be 16-B aligned with row stride % 4 == 0, width >= F");
+    if (!rmap) TORCH_CHECK(gt->size(0) >= nrows, "gate has fewer rows than the output");
+    gp = gt->data_ptr<float>();
+    ldg = gt->stride(0);
+  }
+  c10::DeviceGuard g(x.device());
+  DG_HIP_CHECK(spmm_f32_rowgroup(col.scalar_type() == at::kInt ? IType::I32 : IType::I64,
+                                 rowptr.data_ptr<int64_t>(), col.data_ptr(), ewp, csp, rsp, cm,
+                                 rid, x.data_ptr<float>(), x.stride(0), out.data_ptr<float>(),
+                                 out.stride(0), nrows, static_cast<int>(x.size(1)),
+                                 static_cast<float>(beta), cap, rmap, stream_of(x), gp, ldg));
+}
+
+void gemm_f32_op(const at::Tensor& A1, const at::Tensor& B1, const c10::optional<at::Tensor>& A2,
+                 const c10::optional<at::Tensor>& B2, const c10::optional<at::Tensor>& a_rows,
+                 const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& cin,
+                 double beta, const c10::optional<at::Tensor>& gate,
+                 const c10::optional<at::Tensor>& o_rows, bool relu, const at::Tensor& out,
+                 const c10::optional<at::Tensor>& row_scale) {
+  f32_rows(A1, "A1");
+  f32_rows(B1, "B1");
+  f32_rows(out, "out");
+  same_dev(B1, A1, "B1");
+  same_dev(out, A1, "out");
+  const at::Tensor* ar = opt(a_rows);
+  const int64_t M = ar ? ar->numel() : A1.size(0);
+  const int64_t N = B1.size(1), K1 = A1.size(1);
+  TORCH_CHECK(B1.size(0) == K1, "gemm_f32: A1/B1 inner dimension mismatch");
+  TORCH_CHECK(out.size(1) == N, "gemm_f32: out width != N");
+  const int64_t* arp = idx64(a_rows, A1, M, "a_rows");
+  const int64_t* orp = idx64(o_rows, A1, M, "o_rows");
+  if (!orp) TORCH_CHECK(out.size(0) >= M, "gemm_f32: out has fewer than M rows");
+  const at::Tensor *a2 = opt(A2), *b2 = opt(B2);
+  TORCH_CHECK((a2 == nullptr) == (b2 == nullptr), "gemm_f32: A2 and B2 go together");
+  int64_t K2 = 0;
+  if (a2) {
+    f32_rows(*a2, "A2");
+    f32_rows(*b2, "B2");
+    same_dev(*a2, A1, "A2");
+    same_dev(*b2, A1, "B2");
+    K2 = a2->size(1);
+    TORCH_CHECK(b2->size(0) == K2 && b2->size(1) == N, "gemm_f32: A2/B2 shape mismatch");
+    TORCH_CHECK(a2->size(0) >= M, "gemm_f32: A2 has fewer than M rows");
+  }
+  TORCH_CHECK(gemm_f32_supported(N, K1, K2),
+              "gemm_f32: unsupported shape N=", N, " K1=", K1, " K2=", K2);
+  const float* bp = nullptr;
+  if (const at::Tensor* b = opt(bias)) {
+    same_dev(*b, A1, "bias");
+    TORCH_CHECK(b->scalar_type() == at::kFloat && b->is_contiguous() && b->numel() == N,
+                "bias must be contiguous float32 [N]");
+    bp = b->data_ptr<float>();
+  }
+  const float* cp = nullptr;
+  int64_t ldc = 0;
+  if (const at::Tensor* c = opt(cin)) {
+    f32_rows(*c, "cin");
+    same_dev(*c, A1, "cin");
+    TORCH_CHECK(c->size(1) == N, "cin width != N");
+    if (!orp) TORCH_CHECK(c->size(0) >= M, "cin has fewer than M rows");
+    cp = c->data_ptr<float>();
+    ldc = c->stride(0);
+  }
+  const float* gp = nullptr;
+  int64_t ldg = 0;
+  if (const at::Tensor* gt = opt(gate)) {
+    f32_rows(*gt, "gate");
+    same_dev(*gt, A1, "gate");
+    TORCH_CHECK(gt->size(1) >= N, "gate narrower than N");
+    if (!orp) TORCH_CHECK(gt->size(0) >= M, "gate has fewer than M rows");
+    gp = gt->data_ptr<float>();
+    ldg = gt->stride(0);
+  }
+  const float* rsp = nullptr;
+  if (const at::Tensor* rs = opt(row_scale)) {
+    same_dev(*rs, A1, "row_scale");
+    TORCH_CHECK(rs->scalar_type() == at::kFloat && rs->is_contiguous() && rs->numel() == M,
+                "row_scale must be contiguous float32 [M]");
+    rsp = rs->data_ptr<float>();
+  }
+  c10::DeviceGuard g(A1.device());
+  DG_HIP_CHECK(gemm_f32(A1.data_ptr<float>(), A1.stride(0), K1, B1.data_ptr<float>(),
+                        B1.stride(0), a2 ? a2->data_ptr<float>() : nullptr,
+                        a2 ? a2->stride(0) : 0, K2, b2 ? b2->data_ptr<float>() : nullptr,
+                        b2 ? b2->stride(0) : 0, arp, bp, cp, ldc, static_cast<float>(beta), gp,
+                        ldg, orp, rsp, relu, out.data_ptr<float>(), out.stride(0), M, N,
+                        stream_of(A1)));
+}
+
+void wgrad_f32_op(const at::Tensor& A1, const c10::optional<at::Tensor>& A2,
+                  const c10::optional<at::Tensor>& a1_rows, const at::Tensor& G,
+                  const at::Tensor& partials, bool accumulate) {
+  f32_rows(A1, "A1");
+  f32_rows(G, "G");
+  same_dev(G, A1, "G");
+  same_dev(partials, A1, "partials");
+  const int64_t M = G.size(0), N = G.size(1);
+  const int64_t* arp = idx64(a1_rows, A1, M, "a1_rows");
+  if (!arp) TORCH_CHECK(A1.size(0) >= M, "wgrad_f32: A1 has fewer rows than G");
+  const at::Tensor* a2 = opt(A2);
+  int64_t K2 = 0;
+  if (a2) {
+    f32_rows(*a2, "A2");
+    same_dev(*a2, A1, "A2");
+    TORCH_CHECK(a2->size(0) >= M, "wgrad_f32: A2 has fewer rows than G");
+    K2 = a2->size(1);
+  }
+  const int64_t K = A1.size(1) + K2;
+  TORCH_CHECK(wgrad_f32_supported(K, N), "wgrad_f32: unsupported K=", K, " N=", N);
+  TORCH_CHECK(partials.scalar_type() == at::kFloat && partials.is_contiguous() &&
+                  partials.dim() == 3 && partials.size(1) == K && partials.size(2) == N,
+              "partials must be contiguous float32 [P, K, N]");
+  c10::DeviceGuard g(A1.device());
+  DG_HIP_CHECK(wgrad_f32(A1.data_ptr<float>(), A1.stride(0), A1.size(1),
+                         a2 ? a2->data_ptr<float>() : nullptr, a2 ? a2->stride(0) : 0, K2, arp,
+                         G.data_ptr<float>(), G.stride(0), M, N, partials.data_ptr<float>(),
+                         static_cast<int>(partials.size(0)), accumulate, stream_of(A1)));
+}
+
+void wgrad_f32_reduce_op(const at::Tensor& partials, const at::Tensor& out) {
+  same_dev(out, partials, "out");
+  TORCH_CHECK(partials.scalar_type() == at::kFloat && partials.is_contiguous() &&
+                  partials.dim() == 3,
+              "partials must be contiguous float32 [P, K, N]");
+  TORCH_CHECK(out.scalar_type() == at::kFloat && out.is_contiguous() &&
+                  out.numel() == partials.size(1) * partials.size(2),
+              "out must be contiguous float32 [K, N]");
+  c10::DeviceGuard g(out.device());
+  DG_HIP_CHECK(wgrad_f32_reduce(partials.data_ptr<float>(), static_cast<int>(partials.size(0)),
+                                out.numel(), out.data_ptr<float>(), stream_of(out)));
+}
+
+void row_keep_bits_op(const at::Tensor& h, const c10::optional<at::Tensor>& rows,
+                      const at::Tensor& bits) {
+  f32_rows(h, "h");
+  same_dev(bits, h, "bits");
+  const at::Tensor* r = opt(rows);
+  const int64_t n = r ? r->numel() : h.size(0);
+  const int64_t* rp = idx64(rows, h, n, "rows");
+  const int F = static_cast<int>(h.size(1));
+  TORCH_CHECK(F % 32 == 0, "row_keep_bits: F % 32 != 0");
+  TORCH_CHECK(bits.scalar_type() == at::kInt && bits.is_contiguous() &&
+                  bits.numel() >= n * (F / 32),
+              "bits must be contiguous int32 with >= rows * F/32 words");
+  c10::DeviceGuard g(h.device());
+  DG_HIP_CHECK(row_keep_bits(h.data_ptr<float>(), h.stride(0), rp, n, F,
+                             reinterpret_cast<uint32_t*>(bits.data_ptr<int32_t>()), stream_of(h)));
+}
+
+void apply_keep_bits_op(const at::Tensor& g, const at::Tensor& bits) {
+  f32_rows(g, "g");
+  same_dev(bits, g, "bits");
+  const int F = static_cast<int>(g.size(1));
+  TORCH_CHECK(F % 32 == 0, "apply_keep_bits: F % 32 != 0");
+  TORCH_CHECK(bits.scalar_type() == at::kInt && bits.is_contiguous() &&
+                  bits.numel() >= g.size(0) * (F / 32),
+              "bits must be contiguous int32 with >= rows * F/32 words");
+  c10::DeviceGuard dg(g.device());
+  DG_HIP_CHECK(apply_keep_bits(g.data_ptr<float>(), g.stride(0),
+                               reinterpret_cast<const uint32_t*>(bits.data_ptr<int32_t>()),
+                               g.size(0), F, stream_of(g)));
+}
+
+void set_spmm_f32_config_op(int64_t rowgroup, int64_t pass_cols) {
+  set_spmm_f32_config(static_cast<int>(rowgroup), static_cast<int>(pass_cols));
+}
+
+}  // namespace
+}  // namespace dgraph
+
+TORCH_LIBRARY_FRAGMENT(dgraph_amd, m) {
+  m.def("set_spmm_f32_config(int rowgroup, int pass_cols=-1) -> ()",
+        &dgraph::set_spmm_f32_config_op);
+  m.def("spmm_f32_ex(Tensor rowptr, Tensor col, Tensor? edge_weight, Tensor? col_scale, "
+        "Tensor? row_scale, Tensor? col_map, Tensor? row_ids, Tensor x, Tensor(a!) out, "
+        "float beta=0., int cap=0, Tensor? row_map=None, Tensor? gate=None) -> ()");
+  m.def("gemm_f32(Tensor A1, Tensor B1, Tensor? A2, Tensor? B2, Tensor? a_rows, Tensor? bias, "
+        "Tensor? cin, float beta, Tensor? gate, Tensor? o_rows, bool relu, Tensor(a!) out, "
+        "Tensor? row_scale=None) -> ()");
+  m.def("wgrad_f32(Tensor A1, Tensor? A2, Tensor? a1_rows, Tensor G, Tensor(a!) partials, "
+        "bool accumulate) -> ()");
+  m.def("wgrad_f32_reduce(Tensor partials, Tensor(a!) out) -> ()");
+  m.def("row_keep_bits(Tensor h, Tensor? rows, Tensor(a!) bits) -> ()");
+  m.def("apply_keep_bits(Tensor(a!) g, Tensor bits) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(dgraph_amd, CUDA, m) {
+  m.impl("spmm_f32_ex", &dgraph::spmm_f32_ex_op);
+  m.impl("gemm_f32", &dgraph::gemm_f32_op);
+  m.impl("wgrad_f32", &dgraph::wgrad_f32_op);
+  m.impl("wgrad_f32_reduce", &dgraph::wgrad_f32_reduce_op);
+  m.impl("row_keep_bits", &dgraph::row_keep_bits_op);
+  m.impl("apply_keep_bits", &dgraph::apply_keep_bits_op);
+}

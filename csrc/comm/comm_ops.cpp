@@ -142,13 +142,21 @@ void heap_wait_op(const at::Tensor& flags, int64_t me, int64_t world, int64_t ep
   TORCH_CHECK(flags.is_cuda() && flags.scalar_type() == at::kLong && flags.numel() >= world &&
                   flags.is_contiguous(),
               "flags must be a contiguous int64 GPU tensor of >= world words");
-  TORCH_CHECK(timed_out.is_cuda() && timed_out.scalar_type() == at::kInt,
-              "timed_out must be an int32 GPU tensor");
+  TORCH_CHECK(timed_out.scalar_type() == at::kInt && (timed_out.is_cuda() || timed_out.is_pinned()),
+              "timed_out must be an int32 GPU tensor or pinned host tensor");
   c10::DeviceGuard g(flags.device());
+  int* flag = timed_out.data_ptr<int>();
+  if (!timed_out.is_cuda()) {
+    // pinned host word: the wait kernel reports a timeout straight into host memory, so
+    // the host can poll it on every call without a device sync
+    void* dptr = nullptr;
+    DG_HIP_CHECK(hipHostGetDevicePointer(&dptr, flag, 0));
+    flag = static_cast<int*>(dptr);
+  }
   DG_HIP_CHECK(heap_wait(reinterpret_cast<const uint64_t*>(flags.data_ptr()),
                          static_cast<int>(me), static_cast<int>(world),
-                         static_cast<uint64_t>(epoch), max_spins, self_too,
-                         timed_out.data_ptr<int>(), cur_stream(flags)));
+                         static_cast<uint64_t>(epoch), max_spins, self_too, flag,
+                         cur_stream(flags)));
 }
 
 // ------------------------------------------------------------------ RCCL executor

@@ -99,7 +99,8 @@ __global__ __launch_bounds__(64) void heap_wait_kernel(const uint64_t* __restric
   int64_t spins = 0;
   while (__hip_atomic_load(flags + q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
     if (++spins >= max_spins) {
-      __hip_atomic_store(timed_out, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // system scope: the word may be pinned host memory polled by the host
+      __hip_atomic_store(timed_out, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       return;
     }
     __builtin_amdgcn_s_sleep(2);

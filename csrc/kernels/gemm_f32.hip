@@ -1,0 +1,299 @@
+// dgraph_amd — fp32 MFMA dual GEMM for the GraphSAGE combine at the reference's precision
+// (gfx950, v_mfma_f32_16x16x4_f32: exact f32, a k-ordered fmaf chain per output).
+//
+//   out[o(i), :] = epi( A1[a(i), 0:K1] @ B1[K1, N] (+ A2[a(i), 0:K2] @ B2[K2, N]) )
+//   epi(v) = relu?( gate?( rs[i] * v + bias[n] + beta * cin[o(i), n] ) )   (rs nullable)
+//   gate: v = gate[o(i), n] > 0 ? v : 0   (the ReLU derivative read from an activation)
+//   a(i) = a_rows ? a_rows[i] : i (A1 only; A2 is read densely), o(i) = o_rows ? o_rows[i] : i
+//
+// The reference runs these combines as two torch.mm calls plus adds (fp32 only,
+// DGraph/distributed/csrc/torch_local_kernels.cu:43-46 and the experiments' nn.Linear
+// layers). fp32 MFMA runs at the f32 vector rate (64 FLOP/clk/SIMD, 157 TF/s), so at
+// K=256..512 the combine is COMPUTE bound (~64 FLOP per byte moved): the design goal is
+// keeping the matrix pipe busy, and fusing the second GEMM, bias, ReLU and the gradient
+// gate so no extra pass over an [M, N] fp32 tensor is spent.
+//
+// Tiling: 512 threads (8 waves, 2 per SIMD); a block owns BM = 256 rows x all N columns
+// (A is read from HBM once); waves form a WM x WN grid, each with TM x TN 16x16 tiles
+// (TM*TN*4 accumulator registers). K runs in 32-deep stages through two LDS buffers:
+//   * A stage [256][32] fp32 (32 KB), B stage [32][N+4] fp32 (row pad: the 8-apart k rows
+//     one b32 fragment read touches fall in different banks);
+//   * global -> registers for stage s+1 is issued before the MFMAs of stage s and written
+//     to the other buffer after them (one barrier per stage);
+//   * k order inside a stage: lane group h = lane>>4 takes k = 8h + j in MFMA step j, so a
+//     lane's A fragments of the stage are ONE contiguous 32-B piece (2 x ds_read_b128) and
+//     its B fragment of step j is row 8h + j (the permutation is applied to A and B alike;
+//     the summation order stays fixed, so results are run-to-run identical).
+#include "../common.h"
+#include "kernels.h"
+
+namespace dgraph {
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kBM = 256;
+constexpr int kBK = 32;
+constexpr int kThreads = 512;
+
+template <int N>
+struct GCfg;
+// N: (TM, TN, WM, WN) with 16*TM*WM = 256 and 16*TN*WN = N
+template <> struct GCfg<256> { static constexpr int TM = 4, TN = 8, WM = 4, WN = 2; };
+template <> struct GCfg<192> { static constexpr int TM = 4, TN = 6, WM = 4, WN = 2; };
+template <> struct GCfg<176> { static constexpr int TM = 2, TN = 11, WM = 8, WN = 1; };
+template <> struct GCfg<128> { static constexpr int TM = 2, TN = 8, WM = 8, WN = 1; };
+template <> struct GCfg<64> { static constexpr int TM = 2, TN = 4, WM = 8, WN = 1; };
+
+template <int N>
+struct GLds {
+  static constexpr int BP = N + 4;                      // B stage row pitch (floats)
+  static constexpr int A_FL = kBM * kBK;                // A stage floats
+  static constexpr int B_FL = kBK * BP;                 // B stage floats
+  static constexpr int STAGE = A_FL + B_FL;
+  static constexpr size_t BYTES = 2 * STAGE * sizeof(float);
+  static constexpr int A_V4 = A_FL / 4 / kThreads;      // float4 per thread (A stage) = 4
+  static constexpr int B_V4 = (kBK * N / 4 + kThreads - 1) / kThreads;  // float4 (B stage)
+};
+
+template <int N, bool HAS_A2, bool RELU, bool HAS_BIAS, bool HAS_CIN, bool HAS_GATE>
+__global__ __launch_bounds__(kThreads, 1) void gemm_f32_kernel(
+    const float* __restrict__ A1, int64_t lda1, int K1, const float* __restrict__ B1,
+    int64_t ldb1, const float* __restrict__ A2, int64_t lda2, int K2,
+    const float* __restrict__ B2, int64_t ldb2, const int64_t* __restrict__ a_rows,
+    const float* __restrict__ bias, const float* cin, int64_t ldc, float beta,
+    const float* __restrict__ gate, int64_t ldg, const int64_t* __restrict__ o_rows,
+    const float* __restrict__ row_scale, float* out, int64_t ldo, int64_t M) {
+  using C = GCfg<N>;
+  using L = GLds<N>;
+  constexpr int TM = C::TM, TN = C::TN, WN = C::WN;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int li = lane & 15;  // fragment row (A) / column (B, C)
+  const int lh = lane >> 4;  // k slot group
+  const int64_t row0 = static_cast<int64_t>(blockIdx.x) * kBM;
+  const int K = K1 + K2;
+  const int nst = K / kBK;
+
+  // ---- per-thread global load slots of a stage
+  // A: float4 q = tid + kThreads*u -> row q / 8, 16-B chunk q % 8 of the stage's 32 k
+  int64_t a_src_row[L::A_V4];  // A1 rows (through a_rows)
+  int64_t a2_src_row[L::A_V4];  // A2 rows (dense)
+#pragma unroll
+  for (int u = 0; u < L::A_V4; ++u) {
+    const int q = tid + kThreads * u;
+    int64_t r = row0 + q / 8;
+    r = r < M ? r : M - 1;  // rows past M read a valid row (never stored)
+    a_src_row[u] = a_rows ? a_rows[r] : r;
+    a2_src_row[u] = r;
+  }
+  f32x4 ra[L::A_V4];
+  f32x4 rb[L::B_V4];
+  auto load_stage = [&](int s) {
+    const int k0 = s * kBK;
+    const bool first = !HAS_A2 || k0 < K1;
+    const float* Ab = first ? A1 : A2;
+    const int64_t lda = first ? lda1 : lda2;
+    const int ka = first ? k0 : k0 - K1;
+#pragma unroll
+    for (int u = 0; u < L::A_V4; ++u) {
+      const int q = tid + kThreads * u;
+      ra[u] = *reinterpret_cast<const f32x4*>(Ab + (first ? a_src_row[u] : a2_src_row[u]) * lda +
+                                              ka + (q % 8) * 4);
+    }
+    const float* Bb = first ? B1 : B2;
+    const int64_t ldb = first ? ldb1 : ldb2;
+#pragma unroll
+    for (int u = 0; u < L::B_V4; ++u) {
+      const int q = tid + kThreads * u;
+      if (q < kBK * N / 4) {
+        const int kr = q / (N / 4), c4 = q % (N / 4);
+        rb[u] = *reinterpret_cast<const f32x4*>(Bb + static_cast<int64_t>(ka + kr) * ldb + c4 * 4);
+      }
+    }
+  };
+  auto store_stage = [&](int buf) {
+    float* sa = lds + buf * L::STAGE;
+    float* sb = sa + L::A_FL;
+#pragma unroll
+    for (int u = 0; u < L::A_V4; ++u) {
+      const int q = tid + kThreads * u;
+      *reinterpret_cast<f32x4*>(sa + (q / 8) * kBK + (q % 8) * 4) = ra[u];
+    }
+#pragma unroll
+    for (int u = 0; u < L::B_V4; ++u) {
+      const int q = tid + kThreads * u;
+      if (q < kBK * N / 4) {
+        const int kr = q / (N / 4), c4 = q % (N / 4);
+        *reinterpret_cast<f32x4*>(sb + kr * L::BP + c4 * 4) = rb[u];
+      }
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  load_stage(0);
+  store_stage(0);
+  __syncthreads();
+  const int arow_w = wm * TM * 16;  // this wave's first row within the block tile
+  const int bcol_w = wn * TN * 16;  // this wave's first column
+  for (int s = 0; s < nst; ++s) {
+    const int buf = s & 1;
+    if (s + 1 < nst) load_stage(s + 1);  // in flight during this stage's MFMAs
+    const float* sa = lds + buf * L::STAGE;
+    const float* sb = sa + L::A_FL;
+    // A fragments of the whole stage: k = 8 lh .. 8 lh + 7 of row (tile a, li)
+    f32x4 af[TM][2];
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+      const float* p = sa + (arow_w + a * 16 + li) * kBK + 8 * lh;
+      af[a][0] = *reinterpret_cast<const f32x4*>(p);
+      af[a][1] = *reinterpret_cast<const f32x4*>(p + 4);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float bf[TN];
+#pragma unroll
+      for (int b = 0; b < TN; ++b) bf[b] = sb[(8 * lh + j) * L::BP + bcol_w + b * 16 + li];
+#pragma unroll
+      for (int a = 0; a < TM; ++a) {
+        const float av = af[a][j >> 2][j & 3];
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bf[b], acc[a][b], 0, 0, 0);
+      }
+    }
+    if (s + 1 < nst) store_stage(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: tile (a, b) register r of lane l is element
+  //      (row 4 (l >> 4) + r, column l & 15) of the 16x16 block
+#pragma unroll
+  for (int a = 0; a < TM; ++a) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t i = row0 + arow_w + a * 16 + 4 * lh + r;
+      if (i >= M) continue;
+      const int64_t orow = o_rows ? o_rows[i] : i;
+      const float rsc = row_scale ? row_scale[i] : 1.f;
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const int n = bcol_w + b * 16 + li;
+        float v = acc[a][b][r] * rsc;
+        if constexpr (HAS_BIAS) v += bias[n];
+        if constexpr (HAS_CIN) v = fmaf(beta, cin[orow * ldc + n], v);
+        if constexpr (HAS_GATE) v = gate[orow * ldg + n] > 0.f ? v : 0.f;
+        if constexpr (RELU) v = v > 0.f ? v : 0.f;
+        out[orow * ldo + n] = v;
+      }
+    }
+  }
+}
+
+template <int N, bool HAS_A2, bool RELU, bool HAS_BIAS, bool HAS_CIN, bool HAS_GATE>
+hipError_t launch_gemm_f32(const float* A1, int64_t lda1, int K1, const float* B1, int64_t ldb1,
+                           const float* A2, int64_t lda2, int K2, const float* B2,
+                           int64_t ldb2, const int64_t* a_rows, const float* bias,
+                           const float* cin, int64_t ldc, float beta, const float* gate,
+                           int64_t ldg, const int64_t* o_rows, const float* rsc, float* out,
+                           int64_t ldo, int64_t M, hipStream_t st) {
+  auto kern = &gemm_f32_kernel<N, HAS_A2, RELU, HAS_BIAS, HAS_CIN, HAS_GATE>;
+  constexpr size_t lds = GLds<N>::BYTES;
+  static_assert(lds <= 160 * 1024, "LDS budget");
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+    attr = true;
+  }
+  const int64_t blocks = (M + kBM - 1) / kBM;
+  if (blocks > 0x7fffffff) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(blocks)), dim3(kThreads), lds, st, A1,
+                     lda1, K1, B1, ldb1, A2, lda2, K2, B2, ldb2, a_rows, bias, cin, ldc, beta,
+                     gate, ldg, o_rows, rsc, out, ldo, M);
+  return hipGetLastError();
+}
+
+template <int N, bool HAS_A2, bool RELU>
+hipError_t gemm_f32_flags(const float* A1, int64_t lda1, int K1, const float* B1, int64_t ldb1,
+                          const float* A2, int64_t lda2, int K2, const float* B2, int64_t ldb2,
+                          const int64_t* a_rows, const float* bias, const float* cin,
+                          int64_t ldc, float beta, const float* gate, int64_t ldg,
+                          const int64_t* o_rows, const float* rsc, float* out, int64_t ldo,
+                          int64_t M, hipStream_t st) {
+#define DG_GF(HB_, HC_, HG_)                                                                  \
+  return launch_gemm_f32<N, HAS_A2, RELU, HB_, HC_, HG_>(A1, lda1, K1, B1, ldb1, A2, lda2, K2, \
+                                                         B2, ldb2, a_rows, bias, cin, ldc,   \
+                                                         beta, gate, ldg, o_rows, rsc, out,  \
+                                                         ldo, M, st);
+  const bool hb = bias != nullptr, hc = cin != nullptr, hg = gate != nullptr;
+  if (hb && !hc && !hg) { DG_GF(true, false, false) }
+  if (!hb && !hc && !hg) { DG_GF(false, false, false) }
+  if (!hb && hc && !hg) { DG_GF(false, true, false) }
+  if (!hb && hc && hg) { DG_GF(false, true, true) }
+  if (!hb && !hc && hg) { DG_GF(false, false, true) }
+  if (hb && hc && !hg) { DG_GF(true, true, false) }
+  if (hb && !hc && hg) { DG_GF(true, false, true) }
+  DG_GF(true, true, true)
+#undef DG_GF
+}
+
+template <int N>
+hipError_t gemm_f32_n(const float* A1, int64_t lda1, int K1, const float* B1, int64_t ldb1,
+                      const float* A2, int64_t lda2, int K2, const float* B2, int64_t ldb2,
+                      const int64_t* a_rows, const float* bias, const float* cin, int64_t ldc,
+                      float beta, const float* gate, int64_t ldg, const int64_t* o_rows,
+                      const float* rsc, bool relu, float* out, int64_t ldo, int64_t M,
+                      hipStream_t st) {
+#define DG_GN(A2_, R_)                                                                     \
+  return gemm_f32_flags<N, A2_, R_>(A1, lda1, K1, B1, ldb1, A2, lda2, K2, B2, ldb2, a_rows, \
+                                    bias, cin, ldc, beta, gate, ldg, o_rows, rsc, out, ldo, M, st);
+  const bool two = A2 != nullptr && K2 > 0;
+  if (two) {
+    if (relu) { DG_GN(true, true) }
+    DG_GN(true, false)
+  }
+  if (relu) { DG_GN(false, true) }
+  DG_GN(false, false)
+#undef DG_GN
+}
+
+inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+}  // namespace
+
+bool gemm_f32_supported(int64_t N, int64_t K1, int64_t K2) {
+  return (N == 64 || N == 128 || N == 176 || N == 192 || N == 256) && K1 > 0 &&
+         K1 % kBK == 0 && K2 >= 0 && K2 % kBK == 0;
+}
+
+hipError_t gemm_f32(const float* A1, int64_t lda1, int64_t K1, const float* B1, int64_t ldb1,
+                    const float* A2, int64_t lda2, int64_t K2, const float* B2, int64_t ldb2,
+                    const int64_t* a_rows, const float* bias, const float* cin, int64_t ldc,
+                    float beta, const float* gate, int64_t ldg, const int64_t* o_rows,
+                    const float* row_scale, bool relu, float* out, int64_t ldo, int64_t M,
+                    int64_t N, hipStream_t st) {
+  if (M <= 0) return hipSuccess;
+  if (!gemm_f32_supported(N, K1, A2 ? K2 : 0)) return hipErrorInvalidValue;
+  if (!al16(A1) || lda1 % 4 || !al16(B1) || ldb1 % 4) return hipErrorInvalidValue;
+  if (A2 && K2 > 0 && (!al16(A2) || lda2 % 4 || !al16(B2) || ldb2 % 4))
+    return hipErrorInvalidValue;
+  const int k1 = static_cast<int>(K1), k2 = A2 ? static_cast<int>(K2) : 0;
+  switch (N) {
+    case 256: return gemm_f32_n<256>(A1, lda1, k1, B1, ldb1, A2, lda2, k2, B2, ldb2, a_rows, bias, cin, ldc, beta, gate, ldg, o_rows, row_scale, relu, out, ldo, M, st);
+    case 192: return gemm_f32_n<192>(A1, lda1, k1, B1, ldb1, A2, lda2, k2, B2, ldb2, a_rows, bias, cin, ldc, beta, gate, ldg, o_rows, row_scale, relu, out, ldo, M, st);
+    case 176: return gemm_f32_n<176>(A1, lda1, k1, B1, ldb1, A2, lda2, k2, B2, ldb2, a_rows, bias, cin, ldc, beta, gate, ldg, o_rows, row_scale, relu, out, ldo, M, st);
+    case 128: return gemm_f32_n<128>(A1, lda1, k1, B1, ldb1, A2, lda2, k2, B2, ldb2, a_rows, bias, cin, ldc, beta, gate, ldg, o_rows, row_scale, relu, out, ldo, M, st);
+    default: return gemm_f32_n<64>(A1, lda1, k1, B1, ldb1, A2, lda2, k2, B2, ldb2, a_rows, bias, cin, ldc, beta, gate, ldg, o_rows, row_scale, relu, out, ldo, M, st);
+  }
+}
+
+}  // namespace dgraph

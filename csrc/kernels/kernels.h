@@ -36,6 +36,23 @@ hipError_t spmm_csr(DType dt, IType it, const int64_t* rowptr, const void* col,
 // row_map (optional, int64 [nrows]): CSR row r writes output row row_map[r] and reads
 // row_scale[row_map[r]] (a row-compacted CSR that skips empty rows).
 
+// fp32 row-group SpMM (spmm_f32.hip): F % 4 == 0, 16-B aligned rows and strides.
+// row_ids (nullable): group row i aggregates CSR row row_ids[i] (output row i, or
+// row_map[i]); col_map (nullable): column c reads x row col_map[c], < 0 skips the entry.
+// row_scale is indexed by the OUTPUT row, col_scale by the row of x read.
+bool spmm_f32_rowgroup_ok(int F, int64_t ldx, int64_t ldo, const void* x, const void* out);
+hipError_t spmm_f32_rowgroup(IType it, const int64_t* rowptr, const void* col,
+                             const float* ew, const float* col_scale, const float* row_scale,
+                             const int32_t* col_map, const int64_t* row_ids, const float* x,
+                             int64_t ldx, float* out, int64_t ldo, int64_t nrows, int F,
+                             float beta, int64_t cap, const int64_t* row_map,
+                             hipStream_t st, const float* gate = nullptr, int64_t ldgate = 0);
+// gate (nullable, indexed like out): the stored value is kept where gate > 0, else 0
+void set_spmm_f32_pass_cols(int cols);
+// rowgroup: 1 = fp32 row-group kernel (default), 0 = generic kernels; pass_cols: column
+// pass width (0 = default 128); negative arguments leave a setting unchanged
+void set_spmm_f32_config(int rowgroup, int pass_cols);
+
 // Hub-row splitting (rows whose degree exceeds `cap` are aggregated in three steps):
 //   1. spmm_csr(..., cap): every row sums at most its first `cap` entries;
 //   2. spmm_hub_partials: segment i = entries [seg_beg[i], seg_end[i]) of one hub row's tail
@@ -171,6 +188,36 @@ hipError_t dual_gemm_bs(const void* A1, int64_t lda1, const void* B1t, int64_t K
                         const float* bias, const void* cin, int64_t ldc, void* out, int64_t ldo,
                         int64_t M, int64_t N, uint64_t* mask_out, const uint64_t* mask_in,
                         bool relu, hipStream_t st);
+// ---------------------------------------------------------------------------
+// fp32 MFMA dual GEMM (gemm_f32.hip), exact f32 (v_mfma_f32_16x16x4_f32):
+//   out[o(i)] = relu?(gate?(A1[a(i)] @ B1 (+ A2[i] @ B2) + bias + beta * cin[o(i)]))
+// B row-major [K, N]; N in {64,128,176,192,256}; K1, K2 multiples of 32; 16-B aligned
+// operands with leading dimensions % 4 == 0. a_rows / o_rows nullable int64 [M].
+// gate (nullable, [*, N] with ldg): v = gate[o(i)][n] > 0 ? v : 0. cin may alias out.
+bool gemm_f32_supported(int64_t N, int64_t K1, int64_t K2);
+hipError_t gemm_f32(const float* A1, int64_t lda1, int64_t K1, const float* B1, int64_t ldb1,
+                    const float* A2, int64_t lda2, int64_t K2, const float* B2, int64_t ldb2,
+                    const int64_t* a_rows, const float* bias, const float* cin, int64_t ldc,
+                    float beta, const float* gate, int64_t ldg, const int64_t* o_rows,
+                    const float* row_scale, bool relu, float* out, int64_t ldo, int64_t M,
+                    int64_t N, hipStream_t st);
+// (row_scale nullable, [M]: the product of row i is scaled by row_scale[i] before bias)
+// fp32 weight gradient (wgrad_f32.hip): partials[b] (=|+=) block b's share of
+// [A1[a1(m)] | A2[m]]^T G over rows m < M (P blocks, K1 + K2 in {128, 256}, N in
+// {128, 176, 192, 256}); wgrad_f32_reduce: out[K*N] = sum_b partials[b] in block order.
+bool wgrad_f32_supported(int64_t K, int64_t N);
+hipError_t wgrad_f32(const float* A1, int64_t lda1, int64_t K1, const float* A2, int64_t lda2,
+                     int64_t K2, const int64_t* a1_rows, const float* G, int64_t ldg,
+                     int64_t M, int64_t N, float* partials, int P, bool accumulate,
+                     hipStream_t st);
+hipError_t wgrad_f32_reduce(const float* partials, int P, int64_t KN, float* out,
+                            hipStream_t st);
+// 1-bit ReLU keep masks of selected rows (bits.hip): F % 32 == 0, F/32 words per row.
+hipError_t row_keep_bits(const float* h, int64_t ldh, const int64_t* rows, int64_t n, int F,
+                         uint32_t* bits, hipStream_t st);
+hipError_t apply_keep_bits(float* g, int64_t ldg, const uint32_t* bits, int64_t n, int F,
+                           hipStream_t st);
+
 // 1 = column-half kernel (dual_gemm.hip), 2 = B-stationary (default); < 0 restores it
 void set_dual_gemm_variant(int variant);
 int get_dual_gemm_variant();

@@ -628,17 +628,35 @@ hipError_t spmm_hub_partials(DType dt, IType it, const int64_t* seg_beg,
   const int64_t blocks = (nseg + 3) / 4;
   if (blocks > 0x7fffffff) return hipErrorInvalidValue;
   dim3 grid(static_cast<unsigned>(blocks)), block(256);
+  // widest vector that divides the row width and the row stride and matches the base
+  // pointer's alignment (an output-width aggregate can be 47 or 153 columns wide: a
+  // fixed 4-wide bf16 vector would read past the row and write past the partial row)
+  const int esz = dt == DType::BF16 ? 2 : 4;
+  auto vec_ok = [&](int v) {
+    return F % v == 0 && ldx % v == 0 && aligned(x, v * esz);
+  };
+  const int vec = dt == DType::BF16 ? (vec_ok(4) ? 4 : vec_ok(2) ? 2 : 1)
+                                    : (vec_ok(2) ? 2 : 1);
 #define DG_HP(T_, I_, V_)                                                                   \
   hipLaunchKernelGGL((hub_partials_kernel<T_, I_, V_>), grid, block, 0, stream, seg_beg,  \
                      seg_end, static_cast<const I_*>(col), ew, col_scale,                  \
                      static_cast<const T_*>(x), ldx, partials, nseg, F);                   \
   return hipGetLastError();
+#define DG_HP_V(T_, I_)                      \
+  if (vec == 4) { DG_HP(T_, I_, 4) }         \
+  if (vec == 2) { DG_HP(T_, I_, 2) }         \
+  DG_HP(T_, I_, 1)
   if (dt == DType::BF16) {
-    if (it == IType::I32) { DG_HP(uint16_t, int32_t, 4) }
-    DG_HP(uint16_t, int64_t, 4)
+    if (it == IType::I32) { DG_HP_V(uint16_t, int32_t) }
+    DG_HP_V(uint16_t, int64_t)
   }
-  if (it == IType::I32) { DG_HP(float, int32_t, 2) }
-  DG_HP(float, int64_t, 2)
+  if (vec == 2) {
+    if (it == IType::I32) { DG_HP(float, int32_t, 2) }
+    DG_HP(float, int64_t, 2)
+  }
+  if (it == IType::I32) { DG_HP(float, int32_t, 1) }
+  DG_HP(float, int64_t, 1)
+#undef DG_HP_V
 #undef DG_HP
 }
 
@@ -657,6 +675,13 @@ hipError_t spmm_hub_reduce(DType dt, const float* partials, const int64_t* hub_s
                        hub_seg_ptr, hub_rows, row_scale, static_cast<float*>(out), ldo, nhub,
                        F);
   return hipGetLastError();
+}
+
+bool g_spmm_f32_rowgroup = true;
+
+void set_spmm_f32_config(int rowgroup, int pass_cols) {
+  if (rowgroup >= 0) g_spmm_f32_rowgroup = rowgroup != 0;
+  if (pass_cols >= 0) set_spmm_f32_pass_cols(pass_cols);
 }
 
 void set_spmm_config(int variant, int xcd, int pass_cols) {
@@ -683,6 +708,11 @@ hipError_t spmm_csr(DType dt, IType it, const int64_t* rowptr, const void* col,
   rowptr, static_cast<const I*>(col), ew, heads, head_dim, col_scale, row_scale,        \
       static_cast<const T*>(x), ldx, static_cast<T*>(out), ldo, nrows, F, beta, cap, row_map, stream
   if (dt == DType::F32) {
+    // fp32 row-group kernel (spmm_f32.hip) for one head and 16-B aligned rows
+    if (g_spmm_f32_rowgroup && heads <= 1 && spmm_f32_rowgroup_ok(F, ldx, ldo, x, out))
+      return spmm_f32_rowgroup(it, rowptr, col, ew, col_scale, row_scale, nullptr, nullptr,
+                               static_cast<const float*>(x), ldx, static_cast<float*>(out),
+                               ldo, nrows, F, beta, cap, row_map, stream);
     if (it == IType::I32) return launch_vec<float, int32_t>(DG_ARGS(float, int32_t));
     return launch_vec<float, int64_t>(DG_ARGS(float, int64_t));
   }

@@ -1,0 +1,241 @@
+// dgraph_amd — fp32 row-group CSR SpMM for gfx950 (K-new-2 at the reference's precision).
+//
+// The reference is fp32-only (DGraph/distributed/csrc/torch_local_kernels.cu:43-46); its
+// aggregation was scatter_add + float atomics. This is the fp32 instantiation of the
+// row-group design of spmm.hip (v4), not a widened bf16 kernel:
+//   * each LPR-lane group of a wave owns ONE output row (G = 64/LPR rows per wave): no
+//     cross-lane reduction, one 16-B store per lane per row;
+//   * lane l of a group covers columns [4l, 4l+4) (16-B fp32 vector); a pass covers
+//     4*LPR columns, wider rows run as column passes (the launcher slices them);
+//   * per chunk of LPR neighbours every lane loads ONE column id (coalesced), the ids are
+//     broadcast in-group with ds_bpermute and U neighbour rows are in flight per lane;
+//   * weights (edge weights / column scale, compile-time WMODE) are loaded one chunk ahead;
+//   * trip count = the largest degree of the G rows (wave-uniform); slots past a row's
+//     degree read a valid row with weight 0 (no branches around loads).
+// Two extensions used by the memory-lean full-graph executor (models/sage_fused.py):
+//   * row_ids (runtime, nullable): group row i aggregates CSR row row_ids[i] (an input row
+//     list, e.g. the gradient-support rows) and writes output row i (or row_map[i]);
+//   * col_map (compile-time CMAP): column c reads x row col_map[c]; entries with
+//     col_map[c] < 0 are skipped (x is a row-compacted operand, e.g. a gradient that is
+//     nonzero only on the support rows and is stored only there).
+// Accumulation fp32 with packed FMAs in a fixed order per row: bitwise deterministic.
+#include "../common.h"
+#include "kernels.h"
+
+namespace dgraph {
+namespace {
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+template <typename IdxT, int LPR, int WMODE, bool CMAP>
+__global__ __launch_bounds__(256) void spmm_f32_rowgroup_kernel(
+    const int64_t* __restrict__ rowptr, const IdxT* __restrict__ col,
+    const float* __restrict__ ew, const float* __restrict__ col_scale,
+    const float* __restrict__ row_scale, const int32_t* __restrict__ col_map,
+    const int64_t* __restrict__ row_ids, const float* __restrict__ x, int64_t ldx,
+    float* __restrict__ out, int64_t ldo, int64_t nrows, int F, float beta, int cap,
+    const int64_t* __restrict__ row_map, const float* __restrict__ gate, int64_t ldgate) {
+  constexpr int VEC = 4;
+  constexpr int G = kWave / LPR;
+  constexpr int U = LPR < 8 ? LPR : 8;  // neighbour rows in flight per lane per batch
+  constexpr bool HAS_EW = (WMODE & 1) != 0;
+  constexpr bool HAS_CS = (WMODE & 2) != 0;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int g = lane / LPR;
+  const int l = lane % LPR;
+  const int64_t ngroups = (nrows + G - 1) / G;
+  const int64_t q0 = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t qstep = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
+  const int f = l * VEC;  // launcher guarantees F <= LPR * VEC
+  const bool active = f < F;
+  const float* xf = x + (active ? f : 0);
+  for (int64_t q = q0; q < ngroups; q += qstep) {
+    const int64_t r = q * G + g;
+    const bool has_row = r < nrows;
+    const int64_t rr = has_row ? (row_ids ? row_ids[r] : r) : 0;
+    const int64_t s = has_row ? rowptr[rr] : 0;
+    const int64_t deg1 = has_row ? rowptr[rr + 1] - s : 0;
+    const int deg = static_cast<int>(deg1 > cap ? cap : deg1);
+    int maxdeg = deg;
+#pragma unroll
+    for (int off = LPR; off < kWave; off <<= 1) {
+      const int o = __shfl_xor(maxdeg, off, kWave);
+      maxdeg = o > maxdeg ? o : maxdeg;
+    }
+    f32x2 acc[VEC / 2];
+#pragma unroll
+    for (int i = 0; i < VEC / 2; ++i) acc[i] = f32x2{0.f, 0.f};
+    // slot k of this group's row -> (row of x to read, weight); padding slots read the
+    // row of entry 0 (valid whenever maxdeg > 0) with weight 0
+    auto load_c = [&](int k) -> int64_t {
+      const IdxT c = col[k < deg ? s + k : 0];
+      return static_cast<int64_t>(c);
+    };
+    auto load_w = [&](int64_t& c, int k) -> float {
+      float w = k < deg ? 1.f : 0.f;
+      if constexpr (CMAP) {
+        const int32_t m = col_map[c];
+        w = m >= 0 ? w : 0.f;
+        c = m >= 0 ? m : 0;
+      }
+      if constexpr (HAS_EW) w *= ew[k < deg ? s + k : 0];
+      if constexpr (HAS_CS) w *= col_scale[c];
+      return w;
+    };
+    int64_t my_c = 0;
+    float my_w = 0.f;
+    if (maxdeg > 0) {
+      my_c = load_c(l);
+      my_w = load_w(my_c, l);
+    }
+    for (int k0 = 0; k0 < maxdeg; k0 += LPR) {
+      const int kn = k0 + LPR + l;
+      int64_t nx_c = 0;
+#pragma unroll
+      for (int j0 = 0; j0 < LPR; j0 += U) {
+        if (j0 > 0 && k0 + j0 >= maxdeg) break;  // wave-uniform: no all-padding batch
+        uint4 v[U];
+        uint32_t c[U];
+        float w[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          c[u] = static_cast<uint32_t>(
+              __shfl(static_cast<int>(my_c), g * LPR + j0 + u, kWave));
+        // next chunk's ids in flight during this chunk (issued after this batch's
+        // shuffles, unconditionally: past the end it re-reads entry 0)
+        if (j0 == 0) nx_c = load_c(kn);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          v[u] = *reinterpret_cast<const uint4*>(xf + static_cast<uint64_t>(c[u]) *
+                                                          static_cast<uint64_t>(ldx));
+#pragma unroll
+        for (int u = 0; u < U; ++u) w[u] = __shfl(my_w, g * LPR + j0 + u, kWave);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const f32x2 ww{w[u], w[u]};
+          const f32x2 t0{__uint_as_float(v[u].x), __uint_as_float(v[u].y)};
+          const f32x2 t1{__uint_as_float(v[u].z), __uint_as_float(v[u].w)};
+          acc[0] = __builtin_elementwise_fma(t0, ww, acc[0]);
+          acc[1] = __builtin_elementwise_fma(t1, ww, acc[1]);
+        }
+      }
+      my_w = load_w(nx_c, kn);
+      my_c = nx_c;
+    }
+    if (has_row && active) {
+      const int64_t orow = row_map ? row_map[r] : r;
+      const float rs = row_scale ? row_scale[orow] : 1.f;
+      float* o = out + orow * ldo + f;
+      float4 res;
+      if (beta != 0.f) {
+        const float4 old = *reinterpret_cast<const float4*>(o);
+        res.x = fmaf(acc[0].x, rs, beta * old.x);
+        res.y = fmaf(acc[0].y, rs, beta * old.y);
+        res.z = fmaf(acc[1].x, rs, beta * old.z);
+        res.w = fmaf(acc[1].y, rs, beta * old.w);
+      } else {
+        res.x = acc[0].x * rs;
+        res.y = acc[0].y * rs;
+        res.z = acc[1].x * rs;
+        res.w = acc[1].y * rs;
+      }
+      if (gate) {  // ReLU derivative from a stored activation (row-uniform branch)
+        const float4 gv = *reinterpret_cast<const float4*>(gate + orow * ldgate + f);
+        res.x = gv.x > 0.f ? res.x : 0.f;
+        res.y = gv.y > 0.f ? res.y : 0.f;
+        res.z = gv.z > 0.f ? res.z : 0.f;
+        res.w = gv.w > 0.f ? res.w : 0.f;
+      }
+      *reinterpret_cast<float4*>(o) = res;
+    }
+  }
+}
+
+template <typename IdxT, bool CMAP>
+hipError_t launch_f32_rg(const int64_t* rowptr, const IdxT* col, const float* ew,
+                         const float* cs, const float* rs, const int32_t* cmap,
+                         const int64_t* rids, const float* x, int64_t ldx, float* out,
+                         int64_t ldo, int64_t nrows, int F, float beta, int icap,
+                         const int64_t* row_map, const float* gate, int64_t ldgate,
+                         hipStream_t st) {
+  const int lanes = (F + 3) / 4;
+  const int LPR = lanes <= 8 ? 8 : lanes <= 16 ? 16 : lanes <= 32 ? 32 : 64;
+  const int64_t G = kWave / LPR;
+  const int64_t ngroups = (nrows + G - 1) / G;
+  const int64_t blocks = (ngroups + 3) / 4;  // in order: one row group per wave
+  if (blocks > 0x7fffffff) return hipErrorInvalidValue;
+  const int wmode = (ew != nullptr ? 1 : 0) | (cs != nullptr ? 2 : 0);
+  dim3 grid(static_cast<unsigned>(blocks)), block(256);
+#define DG_F32_W(LPR_, W_)                                                                \
+  if (LPR == LPR_ && wmode == W_) {                                                       \
+    hipLaunchKernelGGL((spmm_f32_rowgroup_kernel<IdxT, LPR_, W_, CMAP>), grid, block, 0, \
+                       st, rowptr, col, ew, cs, rs, cmap, rids, x, ldx, out, ldo, nrows,  \
+                       F, beta, icap, row_map, gate, ldgate);                             \
+    return hipGetLastError();                                                             \
+  }
+#define DG_F32(LPR_) DG_F32_W(LPR_, 0) DG_F32_W(LPR_, 1) DG_F32_W(LPR_, 2) DG_F32_W(LPR_, 3)
+  DG_F32(8)
+  DG_F32(16)
+  DG_F32(32)
+  DG_F32(64)
+#undef DG_F32_W
+#undef DG_F32
+  return hipErrorInvalidValue;
+}
+
+// fp32 rows wider than this run as column passes (each pass gathers a narrower window,
+// which the per-XCD L2 / Infinity Cache holds longer). A/B: benchmarks/bench_spmm.py
+int g_f32_pass_cols = 128;
+
+}  // namespace
+
+void set_spmm_f32_pass_cols(int cols) { g_f32_pass_cols = cols > 0 ? cols : 128; }
+
+bool spmm_f32_rowgroup_ok(int F, int64_t ldx, int64_t ldo, const void* x, const void* out) {
+  auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) % 16) == 0; };
+  return F % 4 == 0 && ldx % 4 == 0 && ldo % 4 == 0 && al(x) && al(out) &&
+         ldx < (int64_t(1) << 40);
+}
+
+hipError_t spmm_f32_rowgroup(IType it, const int64_t* rowptr, const void* col,
+                             const float* ew, const float* col_scale, const float* row_scale,
+                             const int32_t* col_map, const int64_t* row_ids, const float* x,
+                             int64_t ldx, float* out, int64_t ldo, int64_t nrows, int F,
+                             float beta, int64_t cap, const int64_t* row_map,
+                             hipStream_t st, const float* gate, int64_t ldgate) {
+  if (nrows <= 0 || F <= 0) return hipSuccess;
+  if (gate && ((reinterpret_cast<uintptr_t>(gate) & 15) || ldgate % 4)) return hipErrorInvalidValue;
+  if (!spmm_f32_rowgroup_ok(F, ldx, ldo, x, out)) return hipErrorInvalidValue;
+  const int icap = (cap > 0 && cap < (int64_t(1) << 30)) ? static_cast<int>(cap) : (1 << 30);
+  int pc = g_f32_pass_cols;
+  pc = pc > 256 ? 256 : (pc < 16 ? 16 : pc - pc % 4);
+  for (int c0 = 0; c0 < F; c0 += pc) {
+    const int w = F - c0 < pc ? F - c0 : pc;
+    hipError_t err;
+    if (it == IType::I32) {
+      const auto* cp = static_cast<const int32_t*>(col);
+      err = col_map ? launch_f32_rg<int32_t, true>(rowptr, cp, ew, col_scale, row_scale,
+                                                   col_map, row_ids, x + c0, ldx, out + c0,
+                                                   ldo, nrows, w, beta, icap, row_map,
+                                                   gate ? gate + c0 : nullptr, ldgate, st)
+                    : launch_f32_rg<int32_t, false>(rowptr, cp, ew, col_scale, row_scale,
+                                                    nullptr, row_ids, x + c0, ldx, out + c0,
+                                                    ldo, nrows, w, beta, icap, row_map,
+                                                   gate ? gate + c0 : nullptr, ldgate, st);
+    } else {
+      const auto* cp = static_cast<const int64_t*>(col);
+      err = col_map ? launch_f32_rg<int64_t, true>(rowptr, cp, ew, col_scale, row_scale,
+                                                   col_map, row_ids, x + c0, ldx, out + c0,
+                                                   ldo, nrows, w, beta, icap, row_map,
+                                                   gate ? gate + c0 : nullptr, ldgate, st)
+                    : launch_f32_rg<int64_t, false>(rowptr, cp, ew, col_scale, row_scale,
+                                                    nullptr, row_ids, x + c0, ldx, out + c0,
+                                                    ldo, nrows, w, beta, icap, row_map,
+                                                   gate ? gate + c0 : nullptr, ldgate, st);
+    }
+    if (err != hipSuccess) return err;
+  }
+  return hipSuccess;
+}
+
+}  // namespace dgraph

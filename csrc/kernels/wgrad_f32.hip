@@ -1,0 +1,229 @@
+// dgraph_amd — fp32 MFMA weight gradient for tall operands (gfx950, v_mfma_f32_16x16x4_f32).
+//
+//   C[K1 + K2, N] = [A1[a1(m), 0:K1] | A2[m, 0:K2]]^T  @  G[m, 0:N]     summed over m < M
+//
+// The GraphSAGE weight gradients x^T g and agg^T g reduce over 10^7 - 10^8 vertex rows
+// into a 256 x 256 output: a library GEMM gets only (K/tile) x (N/tile) output tiles, i.e.
+// a handful of workgroups for 256 CUs. Here the REDUCTION is split: a persistent grid of
+// P blocks (one per CU), block b owns a contiguous range of rows and accumulates the whole
+// [K, N] product in MFMA accumulators (8 waves x TM x TN 16x16 tiles), then writes (or adds
+// to) its private fp32 partial slab partials[b]. wgrad_f32_reduce sums the P slabs in block
+// order — deterministic for a fixed M and P, and the slabs can accumulate over several
+// calls (row chunks of one step) before the single reduce.
+// Data flow per 32-row stage: A and G rows -> registers (issued one stage ahead) -> padded
+// LDS [32][K+4] / [32][N+4]; MFMA step j uses rows 8h + j (lane group h = lane >> 4) of both
+// (the k-slot permutation of gemm_f32.hip, here over the reduced row index).
+#include "../common.h"
+#include "kernels.h"
+
+namespace dgraph {
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kRows = 32;  // rows per stage
+constexpr int kThr = 512;
+
+template <int K, int N>
+struct WCfg {
+  static constexpr int NTK = K / 16, NTN = N / 16;
+  static constexpr bool TWO = (NTN % 2 == 0) && (NTK % 4 == 0);
+  static constexpr int WN = TWO ? 2 : 1;
+  static constexpr int WM = TWO ? 4 : 8;
+  static constexpr int TM = NTK / WM, TN = NTN / WN;
+  static constexpr int AP = K + 4, GP = N + 4;  // LDS row pitches (floats)
+  static constexpr int STAGE = kRows * (AP + GP);
+  static constexpr size_t BYTES = 2 * STAGE * sizeof(float);
+  static constexpr int A_V4 = (kRows * K / 4 + kThr - 1) / kThr;
+  static constexpr int G_V4 = (kRows * N / 4 + kThr - 1) / kThr;
+  static_assert(TM >= 1 && TM * WM == NTK && TN * WN == NTN, "wgrad tiling");
+};
+
+template <int K, int N>
+__global__ __launch_bounds__(kThr, 1) void wgrad_f32_kernel(
+    const float* __restrict__ A1, int64_t lda1, int K1, const float* __restrict__ A2,
+    int64_t lda2, const int64_t* __restrict__ a1_rows, const float* __restrict__ G,
+    int64_t ldg, int64_t M, int64_t rows_per_block, float* __restrict__ partials,
+    bool accumulate) {
+  using C = WCfg<K, N>;
+  constexpr int TM = C::TM, TN = C::TN, WN = C::WN;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int li = lane & 15;
+  const int lh = lane >> 4;
+  const int64_t m_begin = static_cast<int64_t>(blockIdx.x) * rows_per_block;
+  int64_t m_end = m_begin + rows_per_block;
+  m_end = m_end < M ? m_end : M;
+  const int64_t nst = m_end > m_begin ? (m_end - m_begin + kRows - 1) / kRows : 0;
+
+  f32x4 ra[C::A_V4];
+  f32x4 rg[C::G_V4];
+  auto load_stage = [&](int64_t s) {
+    const int64_t m0 = m_begin + s * kRows;
+#pragma unroll
+    for (int u = 0; u < C::A_V4; ++u) {
+      const int q = tid + kThr * u;
+      if (q < kRows * K / 4) {
+        const int rr = q / (K / 4), c = (q % (K / 4)) * 4;
+        const int64_t m = m0 + rr;
+        const bool ok = m < m_end;
+        const int64_t mm = ok ? m : m_begin;  // a valid row; zeroed below
+        const float* src = c < K1 ? A1 + (a1_rows ? a1_rows[mm] : mm) * lda1 + c
+                                  : A2 + mm * lda2 + (c - K1);
+        const f32x4 v = *reinterpret_cast<const f32x4*>(src);
+        ra[u] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < C::G_V4; ++u) {
+      const int q = tid + kThr * u;
+      if (q < kRows * N / 4) {
+        const int rr = q / (N / 4), c = (q % (N / 4)) * 4;
+        const int64_t m = m0 + rr;
+        const bool ok = m < m_end;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(G + (ok ? m : m_begin) * ldg + c);
+        rg[u] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  };
+  auto store_stage = [&](int buf) {
+    float* sa = lds + buf * C::STAGE;
+    float* sg = sa + kRows * C::AP;
+#pragma unroll
+    for (int u = 0; u < C::A_V4; ++u) {
+      const int q = tid + kThr * u;
+      if (q < kRows * K / 4) {
+        const int rr = q / (K / 4), c = (q % (K / 4)) * 4;
+        *reinterpret_cast<f32x4*>(sa + rr * C::AP + c) = ra[u];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < C::G_V4; ++u) {
+      const int q = tid + kThr * u;
+      if (q < kRows * N / 4) {
+        const int rr = q / (N / 4), c = (q % (N / 4)) * 4;
+        *reinterpret_cast<f32x4*>(sg + rr * C::GP + c) = rg[u];
+      }
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int kw = wm * TM * 16, nw = wn * TN * 16;
+  if (nst > 0) {
+    load_stage(0);
+    store_stage(0);
+    __syncthreads();
+    for (int64_t s = 0; s < nst; ++s) {
+      const int buf = static_cast<int>(s & 1);
+      if (s + 1 < nst) load_stage(s + 1);
+      const float* sa = lds + buf * C::STAGE;
+      const float* sg = sa + kRows * C::AP;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int row = 8 * lh + j;
+        float av[TM], gv[TN];
+#pragma unroll
+        for (int a = 0; a < TM; ++a) av[a] = sa[row * C::AP + kw + a * 16 + li];
+#pragma unroll
+        for (int b = 0; b < TN; ++b) gv[b] = sg[row * C::GP + nw + b * 16 + li];
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+          for (int b = 0; b < TN; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[a], gv[b], acc[a][b], 0, 0, 0);
+      }
+      if (s + 1 < nst) store_stage(buf ^ 1);
+      __syncthreads();
+    }
+  }
+  // register r of tile (a, b), lane l: C[kw + 16a + 4(l>>4) + r][nw + 16b + (l&15)]
+  float* slab = partials + static_cast<int64_t>(blockIdx.x) * K * N;
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int k = kw + a * 16 + 4 * lh + r;
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        float* p = slab + k * N + nw + b * 16 + li;
+        *p = accumulate ? *p + acc[a][b][r] : acc[a][b][r];
+      }
+    }
+}
+
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ partials,
+                                                           int P, int64_t KN,
+                                                           float* __restrict__ out) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= KN) return;
+  float s = 0.f;
+  for (int b = 0; b < P; ++b) s += partials[b * KN + i];  // fixed block order
+  out[i] = s;
+}
+
+template <int K, int N>
+hipError_t launch_wgrad(const float* A1, int64_t lda1, int K1, const float* A2, int64_t lda2,
+                        const int64_t* a1_rows, const float* G, int64_t ldg, int64_t M,
+                        float* partials, int P, bool accumulate, hipStream_t st) {
+  using C = WCfg<K, N>;
+  auto kern = &wgrad_f32_kernel<K, N>;
+  static_assert(C::BYTES <= 160 * 1024, "LDS budget");
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              static_cast<int>(C::BYTES));
+    attr = true;
+  }
+  int64_t rpb = (M + P - 1) / P;
+  rpb = (rpb + kRows - 1) / kRows * kRows;
+  hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(P)), dim3(kThr), C::BYTES, st, A1, lda1,
+                     K1, A2, lda2, a1_rows, G, ldg, M, rpb, partials, accumulate);
+  return hipGetLastError();
+}
+
+inline bool al16w(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+}  // namespace
+
+bool wgrad_f32_supported(int64_t K, int64_t N) {
+  return (K == 128 || K == 256) && (N == 128 || N == 176 || N == 192 || N == 256);
+}
+
+hipError_t wgrad_f32(const float* A1, int64_t lda1, int64_t K1, const float* A2, int64_t lda2,
+                     int64_t K2, const int64_t* a1_rows, const float* G, int64_t ldg,
+                     int64_t M, int64_t N, float* partials, int P, bool accumulate,
+                     hipStream_t st) {
+  const int64_t K = K1 + (A2 ? K2 : 0);
+  if (!wgrad_f32_supported(K, N) || P <= 0) return hipErrorInvalidValue;
+  if (K1 % 4 || !al16w(A1) || lda1 % 4 || !al16w(G) || ldg % 4) return hipErrorInvalidValue;
+  if (A2 && K2 > 0 && (!al16w(A2) || lda2 % 4)) return hipErrorInvalidValue;
+  if (M < 0) return hipErrorInvalidValue;
+  const int k1 = static_cast<int>(K1);
+#define DG_WG(K_, N_)                                                                      \
+  if (K == K_ && N == N_)                                                                  \
+    return launch_wgrad<K_, N_>(A1, lda1, k1, A2, lda2, a1_rows, G, ldg, M, partials, P,  \
+                                accumulate, st);
+  DG_WG(256, 256) DG_WG(256, 176) DG_WG(256, 192) DG_WG(256, 128)
+  DG_WG(128, 256) DG_WG(128, 176) DG_WG(128, 192) DG_WG(128, 128)
+#undef DG_WG
+  return hipErrorInvalidValue;
+}
+
+hipError_t wgrad_f32_reduce(const float* partials, int P, int64_t KN, float* out,
+                            hipStream_t st) {
+  if (KN <= 0) return hipSuccess;
+  const int64_t blocks = (KN + 255) / 256;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, st,
+                     partials, P, KN, out);
+  return hipGetLastError();
+}
+
+}  // namespace dgraph

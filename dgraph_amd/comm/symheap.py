@@ -61,6 +61,18 @@ def _allgather_obj(obj, group):
     return out
 
 
+def _base_of(t: torch.Tensor) -> torch.Tensor:
+    return t._base if t._base is not None else t
+
+
+def _view_key(t: torch.Tensor) -> tuple:
+    """Identity of the data a tensor (or any view object of it) denotes: its base tensor,
+    storage offset, shape, strides and dtype. Two view objects of the same data share the
+    key, so per-call ``x[0]`` / ``reshape`` views hit the cache; the base identity is
+    verified through a weak reference at lookup (a freed base's id can be reused)."""
+    return (id(_base_of(t)), t.storage_offset(), tuple(t.shape), tuple(t.stride()), t.dtype)
+
+
 class SymmetricHeap:
     """One IPC-mapped heap per rank; see the module docstring."""
 
@@ -96,11 +108,17 @@ class SymmetricHeap:
         self.flags = self.local[:_FLAG_BYTES].view(torch.int64).view(_NKINDS, _MAX_W)
         self.flags.zero_()
         self._epoch = [0] * _NKINDS
-        self._timed_out = torch.zeros(1, dtype=torch.int32, device=dev)
+        # timeout word of the device-side waits: pinned host memory, so check() is a plain
+        # host load that every data-path call can afford (a device word would need a sync)
+        try:
+            self._timed_out = torch.zeros(1, dtype=torch.int32).pin_memory() \
+                if dev.type == "cuda" else torch.zeros(1, dtype=torch.int32)
+        except RuntimeError:
+            self._timed_out = torch.zeros(1, dtype=torch.int32, device=dev)
         self._cursor = _FLAG_BYTES
         self._allocs: Dict[int, Tuple[int, int]] = {}  # data_ptr -> (offset, nbytes)
         self._put_cache: Dict[tuple, Tuple[torch.Tensor, torch.Tensor]] = {}
-        self._registered: Dict[int, dict] = {}  # id(tensor) -> registration
+        self._registered: Dict[tuple, dict] = {}  # view key -> registration
         self._scatter_plans: Dict[tuple, "_ScatterPlan"] = {}
         # Device-side completion needs every rank's kernels to run concurrently (one GPU
         # per rank). Ranks sharing one GPU (the 2-process-on-one-GPU test harness) are
@@ -175,8 +193,15 @@ class SymmetricHeap:
         self.wait(_BAR, e)
 
     def check(self) -> None:
-        """Raise if a device-side wait gave up (a peer never signalled). Host sync."""
-        if self._timed_out is not None and int(self._timed_out.item()) != 0:
+        """Raise if a device-side wait gave up (a peer never signalled). The flag is a
+        pinned host word written by the wait kernel: reading it does not sync the device,
+        so every data-path call checks it on entry (a timeout in call k is reported by call
+        k + 1 at the latest, or by the next :meth:`barrier`)."""
+        t = self._timed_out
+        if t is None:
+            return
+        v = int(t[0]) if not t.is_cuda else int(t.item())
+        if v != 0:
             raise RuntimeError("symmetric heap: a device-side wait timed out (a peer did not "
                                "reach the matching signal; see DGRAPH_SHMEM_MAX_SPINS)")
 
@@ -221,22 +246,42 @@ class SymmetricHeap:
     def register(self, x: torch.Tensor) -> torch.Tensor:
         """Collective (first call for a tensor): a persistent symmetric copy of ``x``
         ([N_r, F], per-rank N may differ; the slot is sized for the largest). Later
-        :meth:`remote_gather` calls on the same tensor reuse it; an in-place update of
-        ``x`` (version change) is re-copied into the same slot without renegotiation."""
+        :meth:`remote_gather` calls on the same data — the same tensor or any view object
+        of it with the same offset, shape and strides (callers pass fresh ``x[0]`` /
+        ``reshape`` views every call) — reuse it; an in-place update (version change) is
+        re-copied into the same slot without renegotiation. Slots of registrations whose
+        tensor has been freed ON EVERY RANK are reused (agreed collectively, so a slot
+        sits at the same heap offset everywhere)."""
         F = x.shape[-1]
         x2 = x.reshape(-1, F)
-        n_max = max(_allgather_obj(int(x2.shape[0]), self.group))
-        slot = self.alloc_tensor((max(n_max, 1), F), x2.dtype)
+        es = x2.element_size()
+        dead = sorted((e["slot"].data_ptr() - self.local.data_ptr(), e["slot"].numel() * es, k)
+                      for k, e in self._registered.items() if e["ref"]() is None)
+        infos = _allgather_obj((int(x2.shape[0]), [(o, n) for o, n, _ in dead]), self.group)
+        n_max = max(i[0] for i in infos)
+        need = max(n_max, 1) * F * es
+        common = set.intersection(*[set(map(tuple, i[1])) for i in infos])
+        slot = None
+        for off, nb, k in dead:
+            if (off, nb) in common and nb >= need:
+                del self._registered[k]
+                slot = self.local[off:off + need].view(x2.dtype).view(max(n_max, 1), F)
+                break
+        if slot is None:
+            slot = self.alloc_tensor((max(n_max, 1), F), x2.dtype)
         slot[: x2.shape[0]].copy_(x2)
-        ent = {"ref": weakref.ref(x), "version": x._version, "slot": slot, "rows": x2.shape[0]}
-        self._registered[id(x)] = ent
+        base = x._base if x._base is not None else x
+        ent = {"ref": weakref.ref(base), "version": x._version, "slot": slot,
+               "rows": x2.shape[0]}
+        self._registered[_view_key(x)] = ent
         return slot
 
     def _slot_for(self, x: torch.Tensor) -> torch.Tensor:
         if self.owns(x):
             return x.reshape(-1, x.shape[-1])
-        ent = self._registered.get(id(x))
-        if ent is None or ent["ref"]() is not x:
+        ent = self._registered.get(_view_key(x))
+        base = x._base if x._base is not None else x
+        if ent is None or ent["ref"]() is not base:
             return self.register(x)
         if ent["version"] != x._version:
             # readers of the previous epoch must be done with the slot before it changes
@@ -256,6 +301,7 @@ class SymmetricHeap:
         synchronisation after the first (registering) call for a tensor.
         """
         F = x.shape[-1]
+        self.check()
         slot = self._slot_for(x)
         if self.device_completion:
             e = self.next_epoch(_READY)
@@ -272,6 +318,11 @@ class SymmetricHeap:
         if self.device_completion:
             d = self.next_epoch(_DONE)
             self.signal(_DONE, d)
+            if self.owns(x):
+                # peers read a heap-resident x in place (no private slot): later kernels on
+                # this stream — which may overwrite x, e.g. with the next layer's output —
+                # start only once every peer has finished reading it (write-after-read)
+                self.wait(_DONE, d)
         else:
             self.barrier()  # nobody rewrites a slot while peers still read it
         return out
@@ -284,6 +335,7 @@ class SymmetricHeap:
         ``recv``; a peer's rows of the previous call are not overwritten before that peer
         has entered this call (its reads of them were issued before)."""
         F = send.shape[-1]
+        self.check()
         s2 = send.reshape(-1, F).contiguous()
         key = (tuple(int(v) for v in send_splits), tuple(int(v) for v in remote_offsets))
         idx = self._put_cache.get(key)
@@ -343,10 +395,15 @@ class SymmetricHeap:
         return out
 
     def _scatter_plan(self, indices, owners, n_out: int, F: int, dtype) -> "_ScatterPlan":
-        key = (id(indices), id(owners), n_out, F, dtype)
+        # keyed by the index DATA (base tensor, offset, shape, strides), not the Python view
+        # object: engines pass a fresh ``indices.reshape(-1)`` every call
+        key = (_view_key(indices), _view_key(owners), n_out, F, dtype)
         plan = self._scatter_plans.get(key)
         if plan is not None and plan.matches(indices, owners):
             return plan
+        # drop plans whose index tensors are gone (their slots stay allocated: bump heap)
+        for k in [k for k, p in self._scatter_plans.items() if p.dead()]:
+            del self._scatter_plans[k]
         plan = _ScatterPlan(self, indices, owners, n_out, F, dtype)
         self._scatter_plans[key] = plan
         return plan
@@ -364,7 +421,7 @@ class _ScatterPlan:
         from ..ops.csr import CSR
         from ..plan.pattern import _alltoall_counts, _alltoallv_ids
 
-        self.refs = (weakref.ref(indices), weakref.ref(owners))
+        self.refs = (weakref.ref(_base_of(indices)), weakref.ref(_base_of(owners)))
         self.versions = (indices._version, owners._version)
         dev = heap.device
         W = heap.world
@@ -406,8 +463,11 @@ class _ScatterPlan:
                                  max(r_max, 1)).compact_rows()
 
     def matches(self, indices, owners) -> bool:
-        return (self.refs[0]() is indices and self.refs[1]() is owners
+        return (self.refs[0]() is _base_of(indices) and self.refs[1]() is _base_of(owners)
                 and self.versions == (indices._version, owners._version))
+
+    def dead(self) -> bool:
+        return self.refs[0]() is None or self.refs[1]() is None
 
 
 class NVSHMEMP2P:

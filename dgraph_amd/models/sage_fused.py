@@ -1,0 +1,413 @@
+"""Memory-lean fp32 full-graph GraphSAGE step (the headline config at the reference's
+precision).
+
+The reference trains in fp32 only (DGraph/distributed/csrc/torch_local_kernels.cu:43-46;
+experiments/OGB/main.py:129-184 run the full-graph epoch: forward of every vertex, masked
+loss, backward, optimizer step). At the ogbn-papers100M shape a plain fp32 layer-by-layer
+autograd step needs ~420 GB on one GPU (features 57 GB, two hidden activations 114 GB each,
+their aggregates and gradients as large). This executor is a hand-scheduled forward and
+backward over ROW CHUNKS that never materialises an aggregate, a logit matrix or a dense
+hidden gradient:
+
+forward (per row chunk c, interior + halo parts, every vertex of every layer):
+  F0  a_c = mean_N(x)_c            -> h1[c] = relu([x_c | a_c] [Ws0; Wn0] + b0)
+  F1  a_c = mean_N(h1)_c           -> h2[c] = relu([h1_c | a_c] [Ws1; Wn1] + b1)
+  F2  a_c = mean_N(h2)_c           -> z_c = [h2_c | a_c] [Ws2; Wn2] + b2 (all rows' logits)
+      loss rows of c: cross-entropy, dz (kept, |T| rows), dW2 += [h2 | a]_T^T dz;
+      validation/test rows of c: argmax hits.          (aggregate-first everywhere)
+backward, with S = T + N(T) (+ rows remote loss rows reach: the gradient support):
+  B2  dZ1[S] = keep(h2 > 0) * (A_T^T (dz Wn2^T / deg_T) + scatter_T(dz Ws2^T))
+  B1a over S chunks: dW1 += [h1 | mean_N(h1)]_S^T dZ1      (aggregate of S rows only)
+      u1 = (dZ1 Wn1^T) / deg_S
+  B1b over row chunks c: dZ0_c = keep(h1_c > 0) * (A^T u1 (column-mapped onto S) +
+      scatter_S(dZ1 Ws1^T))_c ;  dW0 += [x_c | mean_N(x)_c]^T dZ0_c
+Exact: every term the dense backward has is computed (the omitted products are with rows
+that are zero by construction). Live device memory at the papers100M shape, W=1: x 57 GB +
+CSR 14 GB + h1 114 GB + h2 114 GB + ~4 GB of chunk buffers; dZ1 and u1 live in h2's
+storage after its last use. Kernels: fp32 row-group SpMM with row lists / column maps /
+gates (csrc/kernels/spmm_f32.hip), MFMA f32 dual GEMM with bias/ReLU/gate/row-scatter
+epilogues (gemm_f32.hip), split-M MFMA weight gradients (wgrad_f32.hip), keep bits
+(bits.hip). Deterministic: fixed chunking, fixed reduction orders, no atomics.
+
+Vertex-partitioned graphs (W > 1): halo rows of x are exchanged once (static input), of
+h1/h2 once per forward; B2 sends the loss rows' contributions to remote support rows
+(restricted sub-plan of :class:`~dgraph_amd.parallel.dist_graph.DistGraph`), B1b sends the
+support rows' contributions to remote vertices (reverse halo exchange, issued before the
+B1a work so it overlaps it).
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Optional, Tuple
+
+import torch
+
+from ..ops import f32 as F32
+from ..ops import kernels as K
+from ..parallel.dist_graph import DistGraph
+
+# rows per chunk of the row-chunked passes (0 = auto from free memory)
+CHUNK_ROWS = int(os.environ.get("DGRAPH_FUSED_CHUNK_ROWS", "0"))
+
+
+def _ranges(n: int, step: int) -> List[Tuple[int, int]]:
+    return [(a, min(n, a + step)) for a in range(0, n, step)] or [(0, 0)]
+
+
+def _pad_to(n: int, m: int) -> int:
+    return (n + m - 1) // m * m
+
+
+def supported(model, x: torch.Tensor) -> bool:
+    """Shapes the fused executor runs (the GraphSAGE of bench.py / the OGB shapes)."""
+    layers = list(model.layers)
+    if len(layers) not in (2, 3) or getattr(model, "dropout", 0.0) != 0.0:
+        return False
+    hid = layers[0].out_dim
+    d0 = x.shape[1]
+    return (x.dtype == torch.float32 and d0 % 32 == 0 and d0 in (128, 256)
+            and hid == 256 and all(l.out_dim == hid for l in layers[:-1])
+            and layers[-1].out_dim <= 176)
+
+
+class FusedSAGE:
+    """The fp32 training step of a 2- or 3-layer :class:`~dgraph_amd.models.sage.GraphSAGE`
+    (mean aggregator, ReLU between layers, no dropout) over a :class:`DistGraph`.
+
+    ``step()`` runs forward + backward, leaves the weight gradients in ``p.grad`` of the
+    model's parameters and returns the loss (device scalar, this rank's share of the global
+    mean: the sum over this rank's loss rows divided by the GLOBAL train-row count
+    ``n_train``, so an all-reduce of the gradients gives the full-batch gradient).
+    ``self.correct`` holds (validation hits, test hits) of the same forward."""
+
+    def __init__(self, model, graph: DistGraph, x: torch.Tensor, train_idx: torch.Tensor,
+                 y_train: torch.Tensor, eval_idx: torch.Tensor, y_eval: torch.Tensor,
+                 eval_is_val: torch.Tensor, n_train: int, chunk_rows: int = 0):
+        if not supported(model, x):
+            raise ValueError("FusedSAGE: unsupported model/feature shape")
+        self.model, self.g, self.x = model, graph, x.contiguous()
+        dev = x.device
+        self.dev = dev
+        L, H = graph.L, graph.H
+        self.L, self.H = L, H
+        self.nl = len(model.layers)
+        self.d0 = x.shape[1]
+        self.hid = model.layers[0].out_dim
+        self.C = model.layers[-1].out_dim
+        self.Cp = 176 if self.C > 128 else (128 if self.C > 64 else 64)  # logit GEMM width
+        self.Cg = _pad_to(self.C, 32) if self.C > 128 else self.Cp      # dz width (a K dim)
+        if self.Cg not in (128, 176, 192, 256):
+            self.Cg = 192
+        self.inv_n = 1.0 / max(int(n_train), 1)
+        # ---- loss / eval rows, sorted (chunk ranges are searchsorted)
+        t, tp = torch.sort(train_idx.long())
+        self.T, self.yT = t.contiguous(), y_train[tp].contiguous()
+        e, ep = torch.sort(eval_idx.long())
+        self.E, self.yE = e.contiguous(), y_eval[ep].contiguous()
+        self.E_val = eval_is_val[ep].contiguous()
+        self.inv_deg = graph.inv_deg
+        self.invdegT = self.inv_deg[self.T].contiguous()
+        # ---- gradient support S (rows where dZ of the last hidden layer can be nonzero)
+        it_t, _, sub = graph._restricted(self.T)  # A[T, :L]^T (rows L, cols |T|), sub-plan
+        parts = [self.T, it_t.compact_rows().row_map.long()]
+        if sub is not None:
+            parts.append(sub[4].long())
+        S = torch.unique(torch.cat(parts))
+        self.S = S.contiguous()
+        self.nS = S.numel()
+        smap = torch.full((L,), -1, dtype=torch.int32, device=dev)
+        smap[S] = torch.arange(self.nS, dtype=torch.int32, device=dev)
+        self.smap = smap
+        self.posT = smap[self.T].long().contiguous()
+        self.invdegS = self.inv_deg[S].contiguous()
+        self.AT_S = it_t.select_rows(S)            # rows S (compact), cols T (compact)
+        self.sub = None
+        if sub is not None:
+            ht_nz, a2a_sub, st = sub[0], sub[1], sub[2]
+            stc = st.compact_rows()
+            self.sub = (ht_nz, a2a_sub, stc, smap[stc.row_map].long().contiguous())
+        # ---- interior / halo structures
+        self.it = graph.interior
+        self.halo = graph.halo
+        self.hcomp = graph.halo.compact_rows() if graph.halo is not None else None
+        self.haloT = graph.halo.transpose() if graph.halo is not None else None
+        self.send_st = graph.send_map.transpose_csr().compact_rows() \
+            if graph.halo is not None else None
+        # ---- chunking
+        free = torch.cuda.mem_get_info(dev)[0] if dev.type == "cuda" else (64 << 30)
+        need_h = (self.nl - 1) * L * self.hid * 4
+        self.store_sep = 2 * self.nS > L   # dZ and u do not fit in the last hidden buffer
+        if self.store_sep:
+            need_h += 2 * self.nS * self.hid * 4
+        spare = max(free - need_h - (6 << 30), 1 << 30)
+        cr = chunk_rows or CHUNK_ROWS
+        if cr <= 0:
+            per_row = 4 * (self.hid + max(self.Cp, self.d0) + self.hid)
+            cr = int(min(max(spare // 3 // per_row, 1 << 16), 1 << 21))
+        self.cr = max(256, min(int(cr), max(L, 256)))
+        self.chunks = _ranges(L, self.cr)
+        self.s_chunks = _ranges(self.nS, self.cr)
+        ss = lambda v, a: int(torch.searchsorted(v, torch.tensor(a, device=v.device)))  # noqa
+        self.ch_T = [(ss(self.T, r0), ss(self.T, r1)) for r0, r1 in self.chunks]
+        self.ch_E = [(ss(self.E, r0), ss(self.E, r1)) for r0, r1 in self.chunks]
+        self.ch_S = [(ss(self.S, r0), ss(self.S, r1)) for r0, r1 in self.chunks]
+        self.ch_Tloc = [(self.T[a:b] - r0).contiguous()
+                        for (r0, _), (a, b) in zip(self.chunks, self.ch_T)]
+        self.ch_Eloc = [(self.E[a:b] - r0).contiguous()
+                        for (r0, _), (a, b) in zip(self.chunks, self.ch_E)]
+        self.ch_Sloc = [(self.S[a:b] - r0).contiguous()
+                        for (r0, _), (a, b) in zip(self.chunks, self.ch_S)]
+        self.ch_halo = [self._halo_range(self.hcomp, r0, r1) for r0, r1 in self.chunks]
+        self.ch_send = [self._halo_range(self.send_st, r0, r1) for r0, r1 in self.chunks]
+        # ---- persistent buffers (allocated once: no allocation in the steady state)
+        f = dict(dtype=torch.float32, device=dev)
+        self.h = [torch.empty(L, self.hid, **f) for _ in range(self.nl - 1)]
+        if self.store_sep:
+            self.dZ = torch.empty(self.nS, self.hid, **f)
+            self.u = torch.empty(self.nS, self.hid, **f) if self.nl == 3 else None
+        else:
+            hl = self.h[-1].view(-1)
+            n = self.nS * self.hid
+            self.dZ = hl[:n].view(self.nS, self.hid)
+            self.u = hl[n:2 * n].view(self.nS, self.hid) if self.nl == 3 else None
+        wA = max(self.hid, self.d0)
+        self.bufA = torch.empty(self.cr, wA, **f)           # chunk aggregate
+        self.bufB = torch.empty(self.cr, max(self.Cp, self.hid), **f)  # logits / dZ0 chunk
+        self.dz = torch.zeros(self.T.numel(), self.Cg, **f)  # output-layer gradient rows
+        self.bits = torch.empty(self.nS, self.hid // 32, dtype=torch.int32, device=dev)
+        self.u_out = torch.empty(self.T.numel(), self.hid, **f)
+        self.acc_out_s = F32.WgradAcc(self.hid, self.Cg, dev)
+        self.acc_out_n = F32.WgradAcc(self.hid, self.Cg, dev)
+        self.acc_hid_s = F32.WgradAcc(self.hid if self.nl == 3 else self.d0, self.hid, dev)
+        self.acc_hid_n = F32.WgradAcc(self.hid if self.nl == 3 else self.d0, self.hid, dev)
+        self.acc_in = F32.WgradAcc(2 * self.d0, self.hid, dev) if self.nl == 3 else None
+        # entries of the S-row aggregation (B1a), counted on the host once
+        self.nnz_S = int(self.it.degree()[S].sum())
+        if self.halo is not None:
+            self.nnz_S += int(self.halo.degree()[S].sum())
+        self.loss = torch.zeros((), **f)
+        self.correct = torch.zeros(2, dtype=torch.long, device=dev)
+        self.exchange_events = []
+
+    @property
+    def edges_aggregated(self) -> int:
+        return self.g.edges_aggregated
+
+    @edges_aggregated.setter
+    def edges_aggregated(self, v: int) -> None:
+        self.g.edges_aggregated = v
+
+    # ------------------------------------------------------------------ helpers
+    @staticmethod
+    def _halo_range(csr, r0: int, r1: int):
+        """Rows [k0, k1) of a row-compacted CSR whose output rows fall in [r0, r1), with
+        their chunk-local output rows."""
+        if csr is None:
+            return None
+        rm = csr.row_map
+        k0 = int(torch.searchsorted(rm, torch.tensor(r0, device=rm.device)))
+        k1 = int(torch.searchsorted(rm, torch.tensor(r1, device=rm.device)))
+        if k1 <= k0:
+            return None
+        return (csr.rowptr[k0:k1 + 1], (rm[k0:k1] - r0).contiguous(), k1 - k0)
+
+    def _agg_chunk(self, xin: torch.Tensor, xhalo: Optional[torch.Tensor], ci: int,
+                   out: torch.Tensor, gate=None) -> torch.Tensor:
+        """``out[:n] = mean over in-neighbours of rows chunk ci`` (interior + halo)."""
+        r0, r1 = self.chunks[ci]
+        n = r1 - r0
+        o = out[:n]
+        it = self.it
+        F32.spmm_f32(it.rowptr[r0:r1 + 1], it.col, xin, o, row_scale=self.inv_deg[r0:r1],
+                     gate=gate)
+        hr = self.ch_halo[ci]
+        if xhalo is not None and hr is not None:
+            rp, rmap, _ = hr
+            F32.spmm_f32(rp, self.hcomp.col, xhalo, o, row_scale=self.inv_deg[r0:r1], beta=1.0,
+                         row_map=rmap, gate=gate)
+        return o
+
+    def _exchange(self, h: torch.Tensor) -> Optional[torch.Tensor]:
+        """Halo rows of ``h`` from their owners (forward all-to-all-v), None at W=1."""
+        g = self.g
+        if g.halo is None:
+            return None
+        return g.a2a(K.gather_rows(h, g.send_map.idx))
+
+    def _params(self):
+        out = []
+        for l in self.model.layers:
+            out.append((l.w_self, l.w_neigh, l.bias))
+        return out
+
+    # ------------------------------------------------------------------ the step
+    def step(self) -> torch.Tensor:
+        g, x = self.g, self.x
+        nl, hid, C, Cp, Cg = self.nl, self.hid, self.C, self.Cp, self.Cg
+        P = self._params()
+        dev = self.dev
+        self.loss.zero_()
+        self.correct.zero_()
+        nnz_it = self.it.nnz
+        nnz_h = self.halo.nnz if self.halo is not None else 0
+        # ---------------- forward: hidden layers
+        hin, hin_halo = x, (g._static_halo(x) if g.halo is not None else None)
+        halos = [hin_halo]
+        for l in range(nl - 1):
+            ws, wn, b = P[l]
+            ws, wn = ws.detach().contiguous(), wn.detach().contiguous()
+            hout = self.h[l]
+            for ci, (r0, r1) in enumerate(self.chunks):
+                if r1 <= r0:
+                    continue
+                a = self._agg_chunk(hin, hin_halo, ci, self.bufA[:, :hin.shape[1]])
+                F32.gemm_f32(hin[r0:r1], ws, a, wn, bias=b.detach(), relu=True,
+                             out=hout[r0:r1])
+            self.edges_aggregated += nnz_it + nnz_h
+            hin = hout
+            hin_halo = self._exchange(hout)
+            halos.append(hin_halo)
+        # ---------------- forward: output layer (all rows), loss and eval on the fly
+        ws, wn, b = P[nl - 1]
+        wsp = torch.zeros(hid, Cp, device=dev)
+        wsp[:, :C] = ws.detach()
+        wnp = torch.zeros(hid, Cp, device=dev)
+        wnp[:, :C] = wn.detach()
+        bp = torch.zeros(Cp, device=dev)
+        bp[:C] = b.detach()
+        self.acc_out_s.reset()
+        self.acc_out_n.reset()
+        hl, hl_halo = hin, hin_halo
+        for ci, (r0, r1) in enumerate(self.chunks):
+            if r1 <= r0:
+                continue
+            n = r1 - r0
+            a = self._agg_chunk(hl, hl_halo, ci, self.bufA[:, :hid])
+            z = F32.gemm_f32(hl[r0:r1], wsp, a, wnp, bias=bp, out=self.bufB[:n, :Cp])
+            t0, t1 = self.ch_T[ci]
+            if t1 > t0:
+                tl = self.ch_Tloc[ci]
+                zt = z.index_select(0, tl)[:, :C]
+                lse = torch.logsumexp(zt, 1)
+                y = self.yT[t0:t1]
+                self.loss += (lse - zt.gather(1, y.unsqueeze(1)).squeeze(1)).sum()
+                p = torch.exp(zt - lse.unsqueeze(1))
+                p.scatter_add_(1, y.unsqueeze(1), torch.full_like(lse, -1.0).unsqueeze(1))
+                dzt = self.dz[t0:t1]
+                dzt[:, :C] = p * self.inv_n
+                self.acc_out_s.add(hl, dzt, a1_rows=self.T[t0:t1])
+                self.acc_out_n.add(a, dzt, a1_rows=tl)
+            e0, e1 = self.ch_E[ci]
+            if e1 > e0:
+                hit = z.index_select(0, self.ch_Eloc[ci])[:, :C].argmax(1) == self.yE[e0:e1]
+                iv = self.E_val[e0:e1]
+                self.correct[0] += (hit & iv).sum()
+                self.correct[1] += (hit & ~iv).sum()
+        self.edges_aggregated += nnz_it + nnz_h
+        loss = self.loss * self.inv_n
+        # ---------------- backward: output layer -> dZ of the last hidden layer on S
+        hlast = hl
+        F32.row_keep_bits(hlast, self.S, self.bits)  # the last hidden ReLU derivative on S
+        del hl_halo, halos[-1]
+        gw = {}
+        dws2 = self.acc_out_s.result()[:, :C]
+        dwn2 = self.acc_out_n.result()[:, :C]
+        gw[(nl - 1, 0)], gw[(nl - 1, 1)] = dws2, dwn2
+        gw[(nl - 1, 2)] = K.col_sum(self.dz)[:C]
+        wn_t = torch.zeros(Cg, hid, device=dev)
+        wn_t[:C] = wn.detach().t()
+        ws_t = torch.zeros(Cg, hid, device=dev)
+        ws_t[:C] = ws.detach().t()
+        u2 = F32.gemm_f32(self.dz, wn_t, row_scale=self.invdegT, out=self.u_out)
+        dZ = self.dZ
+        work = None
+        if self.sub is not None:
+            ht_nz, a2a_sub, stc, stc_rows = self.sub
+            hg = F32.spmm_f32(ht_nz.rowptr, ht_nz.col, u2)
+            sg, work = a2a_sub(hg, async_op=True)
+            self.edges_aggregated += ht_nz.nnz
+        F32.spmm_f32(self.AT_S.rowptr, self.AT_S.col, u2, dZ)
+        self.edges_aggregated += self.AT_S.nnz
+        if work is not None:
+            work.wait()
+            F32.spmm_f32(stc.rowptr, stc.col, sg, dZ, beta=1.0, row_map=stc_rows)
+            del sg, hg
+        F32.gemm_f32(self.dz, ws_t, cin=dZ, o_rows=self.posT, out=dZ)
+        F32.apply_keep_bits(dZ, self.bits)
+        # ---------------- backward: last hidden layer (index nl-2) weights over S rows
+        lh = nl - 2
+        ws1, wn1, _ = P[lh]
+        hin_l = x if lh == 0 else self.h[lh - 1]
+        hin_l_halo = halos[lh]
+        gw[(lh, 2)] = K.col_sum(dZ)
+        u = None
+        work = None
+        if nl == 3:
+            # u1 = (dZ1 Wn1^T) / deg_S: its transposed aggregation feeds layer 0; the halo
+            # part is computed and sent first so the exchange overlaps the S-row work below
+            u = F32.gemm_f32(dZ, wn1.detach().t().contiguous(), row_scale=self.invdegS,
+                             out=self.u)
+            if self.haloT is not None:
+                hg1 = F32.spmm_f32(self.haloT.rowptr, self.haloT.col, u, col_map=self.smap)
+                sg1, work = g.a2a_rev(hg1, async_op=True)
+                self.edges_aggregated += self.haloT.nnz
+        self.acc_hid_s.reset()
+        self.acc_hid_n.reset()
+        for s0, s1 in self.s_chunks:
+            if s1 <= s0:
+                continue
+            rows = self.S[s0:s1]
+            aS = self.bufA[:s1 - s0, :hin_l.shape[1]]
+            F32.spmm_f32(self.it.rowptr, self.it.col, hin_l, aS, row_ids=rows,
+                         row_scale=self.invdegS[s0:s1])
+            if hin_l_halo is not None:
+                F32.spmm_f32(self.halo.rowptr, self.halo.col, hin_l_halo, aS, row_ids=rows,
+                             row_scale=self.invdegS[s0:s1], beta=1.0)
+            self.acc_hid_s.add(hin_l, dZ[s0:s1], a1_rows=rows)
+            self.acc_hid_n.add(aS, dZ[s0:s1])
+        self.edges_aggregated += self.nnz_S
+        gw[(lh, 0)] = self.acc_hid_s.result()
+        gw[(lh, 1)] = self.acc_hid_n.result()
+        if nl == 3:
+            # ------------ layer 0: dZ0 by row chunks, consumed at once by its weight grads
+            ws1_t = ws1.detach().t().contiguous()
+            if work is not None:
+                work.wait()
+            self.acc_in.reset()
+            db0 = torch.zeros(hid, device=dev)
+            h1 = self.h[0]
+            x_halo = halos[0]
+            for ci, (r0, r1) in enumerate(self.chunks):
+                if r1 <= r0:
+                    continue
+                n = r1 - r0
+                gz = self.bufB[:n, :hid]
+                F32.spmm_f32(self.it.rowptr[r0:r1 + 1], self.it.col, u, gz, col_map=self.smap,
+                             gate=h1[r0:r1])
+                sr = self.ch_send[ci]
+                if work is not None and sr is not None:
+                    rp, rmap, _ = sr
+                    F32.spmm_f32(rp, self.send_st.col, sg1, gz, beta=1.0, row_map=rmap,
+                                 gate=h1[r0:r1])
+                s0, s1 = self.ch_S[ci]
+                if s1 > s0:
+                    F32.gemm_f32(dZ[s0:s1], ws1_t, cin=gz, o_rows=self.ch_Sloc[ci],
+                                 gate=h1[r0:r1], out=gz)
+                a0 = self._agg_chunk(x, x_halo, ci, self.bufA[:, :self.d0])
+                self.acc_in.add(x[r0:r1], gz, A2=a0)
+                db0 += K.col_sum(gz)
+            self.edges_aggregated += 2 * nnz_it + nnz_h + \
+                (self.send_st.nnz if self.send_st is not None else 0)
+            w0 = self.acc_in.result()
+            gw[(0, 0)], gw[(0, 1)], gw[(0, 2)] = w0[:self.d0], w0[self.d0:], db0
+        # ---------------- gradients into the parameters
+        for l, (ws_, wn_, b_) in enumerate(P):
+            for k, p in enumerate((ws_, wn_, b_)):
+                if p is None:
+                    continue
+                gk = gw[(l, k)].to(p.dtype).reshape(p.shape)
+                if p.grad is None:
+                    p.grad = gk.clone()
+                else:
+                    p.grad.copy_(gk)
+        return loss

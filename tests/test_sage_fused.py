@@ -1,0 +1,87 @@
+"""The memory-lean fp32 executor (models/sage_fused.py) against the layer-stack autograd
+path of the same GraphSAGE: loss, every weight gradient and the validation/test hits, on
+one rank (CPU reference kernels) and vertex-partitioned over W = 2 / 4 gloo ranks
+(all-reduced gradients equal the W=1 gradients)."""
+import pytest
+import torch
+import torch.distributed as dist
+
+from dgraph_amd.data.synthetic import (SHAPES, SPLIT_TEST, SPLIT_TRAIN, SPLIT_VALID,
+                                       build_partition, contiguous_offsets, node_data)
+from dgraph_amd.models.sage import GraphSAGE
+from dgraph_amd.models.sage_fused import FusedSAGE
+from dgraph_amd.parallel.dist_graph import DistGraph
+
+SCALE = 2e-5  # ~2.2K vertices, ~65K messages
+
+
+def _setup(rank, world, dev="cpu", layers=3, chunk_rows=300, gf=0.3):
+    shape = SHAPES["ogbn-papers100M"].scaled(SCALE)
+    part = build_partition(shape, rank, world, dev, global_frac=gf, window=64)
+    csr = part["csr"]
+    if world == 1:
+        csr.num_cols = part["L"]
+    group = dist.group.WORLD if world > 1 else None
+    g = DistGraph(csr, part["L"], part["H"], part["send_local_idx"], part["send_splits"],
+                  part["recv_splits"], group, symmetric=True)
+    offs = contiguous_offsets(shape.num_nodes, world)
+    x, y, split = node_data(shape, rank, offs, dev, dtype=torch.float32, return_split=True)
+    tr = torch.nonzero(split == SPLIT_TRAIN).reshape(-1)
+    ev = torch.nonzero((split == SPLIT_VALID) | (split == SPLIT_TEST)).reshape(-1)
+    n_tr = torch.tensor([tr.numel()])
+    if world > 1:
+        dist.all_reduce(n_tr)
+    torch.manual_seed(0)
+    model = GraphSAGE(shape.num_features, 256, shape.num_classes, layers)
+    return shape, g, x, y, split, tr, ev, int(n_tr), model
+
+
+def _fused_grads(rank, world, layers=3, chunk_rows=300):
+    shape, g, x, y, split, tr, ev, n_tr, model = _setup(rank, world, layers=layers)
+    ex = FusedSAGE(model, g, x, tr, y[tr], ev, y[ev], split[ev] == SPLIT_VALID, n_tr,
+                   chunk_rows=chunk_rows)
+    loss = ex.step()
+    grads = [p.grad.clone() for p in model.parameters()]
+    return loss, grads, ex.correct.clone()
+
+
+def _stack_grads(layers=3):
+    shape, g, x, y, split, tr, ev, n_tr, model = _setup(0, 1, layers=layers)
+    logits, evl = model(x, g, out_rows=tr, eval_rows=ev)
+    loss = torch.nn.functional.cross_entropy(logits.float(), y[tr], reduction="sum") / n_tr
+    loss.backward()
+    hit = evl.argmax(1) == y[ev]
+    iv = split[ev] == SPLIT_VALID
+    corr = torch.tensor([(hit & iv).sum(), (hit & ~iv).sum()])
+    return loss.detach(), [p.grad.clone() for p in model.parameters()], corr
+
+
+@pytest.mark.parametrize("layers", [2, 3])
+def test_fused_matches_stack_w1(layers):
+    l0, g0, c0 = _stack_grads(layers)
+    l1, g1, c1 = _fused_grads(0, 1, layers)
+    torch.testing.assert_close(l1, l0, atol=1e-5, rtol=1e-5)
+    for a, b in zip(g1, g0):
+        torch.testing.assert_close(a, b, atol=2e-5, rtol=1e-4)
+    assert torch.equal(c1, c0)
+
+
+def _dist_body(rank, world, ref_path):
+    loss, grads, corr = _fused_grads(rank, world)
+    for t in grads:
+        dist.all_reduce(t)
+    dist.all_reduce(loss)
+    dist.all_reduce(corr)
+    ref = torch.load(ref_path)
+    torch.testing.assert_close(loss, ref["loss"], atol=1e-5, rtol=1e-5)
+    for a, b in zip(grads, ref["grads"]):
+        torch.testing.assert_close(a, b, atol=2e-5, rtol=1e-4)
+    assert torch.equal(corr, ref["corr"])
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_fused_partitioned_matches_w1(ranks, world, tmp_path):
+    loss, grads, corr = _fused_grads(0, 1)
+    p = tmp_path / "ref.pt"
+    torch.save({"loss": loss, "grads": grads, "corr": corr}, p)
+    ranks(_dist_body, world, str(p))
