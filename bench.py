@@ -8,10 +8,10 @@ partition of a synthetic graph with the papers100M shape: 111,059,956 nodes,
 172 classes), RCCL all-to-all-v halo exchange overlapped with interior aggregation.
 
 A step is the reference's full-graph epoch (experiments/OGB/main.py:129-184):
-  forward of ALL 3 SAGE-mean layers over ALL vertices (hidden 256, bf16 compute with fp32
-  accumulation, fp32 master weights) -> masked cross-entropy on the train split, and
-  validation/test accuracy from the SAME forward -> backward -> gradient all-reduce ->
-  Adam step.
+  forward of ALL 3 SAGE-mean layers over ALL vertices (hidden 256, fp32 — the reference's
+  precision — on the memory-lean row-chunked executor models/sage_fused.py) -> masked
+  cross-entropy on the train split, and validation/test accuracy from the SAME forward ->
+  backward -> gradient all-reduce -> Adam step.
 The output layer's backward uses only the train rows' nonzero gradient (A[train, :]^T),
 and the layer below it aggregates transposed only from the rows where its incoming
 gradient can be nonzero (the train rows and their neighbours, DistGraph.grad_support):
@@ -23,8 +23,12 @@ exact (the dense backward multiplies zeros), counted as what it aggregates.
 Secondary measurements in the same JSON line (unless --no-extra):
   * "structureless": the same step on a --global-frac 1.0 graph (uniformly random
     endpoints: no locality for any cache to exploit);
-  * "train_rows_only": the step with the output layer aggregated only at the train rows
-    (not a full-graph forward; labelled, never the headline).
+  * "bf16_stack": the headline graph at bf16 storage/compute on the layer-stack path
+    (below the reference's precision; labelled, never the headline);
+  * "train_rows_only" (layer-stack executor only): the step with the output layer
+    aggregated only at the train rows (not a full-graph forward; never the headline).
+  * "regions": per-region device ms of one extra step (max/min over ranks), exposed
+    exchange vs compute, bytes per peer (the reference's TimingReport regions).
 The whole graph is fixed as N grows (strong scaling). Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
@@ -57,9 +61,16 @@ def parse():
     ap.add_argument("--hidden", type=int, default=256)
     ap.add_argument("--layers", type=int, default=3)
     ap.add_argument("--lr", type=float, default=1e-3)
-    ap.add_argument("--dtype", choices=("bf16", "fp32"), default="bf16",
-                    help="compute/storage dtype of features and activations (weights are "
-                         "fp32 masters either way)")
+    ap.add_argument("--dtype", choices=("bf16", "fp32"), default="fp32",
+                    help="compute/storage dtype of features and activations; fp32 (default) "
+                         "is the reference's precision (weights are fp32 masters either way)")
+    ap.add_argument("--executor", choices=("auto", "fused", "stack"), default="auto",
+                    help="fused: the memory-lean fp32 row-chunked executor "
+                         "(models/sage_fused.py; fits papers100M fp32 on one GPU); stack: the "
+                         "layer-stack autograd node (models/sage.py SAGEStackFn); auto = fused "
+                         "for fp32 shapes it supports")
+    ap.add_argument("--no-bf16-extra", action="store_true",
+                    help="skip the secondary bf16 (layer-stack) measurement of the headline graph")
     ap.add_argument("--global-frac", type=float, default=0.05,
                     help="fraction of uniformly random (non-local) edges of the headline "
                          "graph; the rest join ids within +-window")
@@ -153,10 +164,14 @@ class Job:
                                overlap=not args.no_overlap)
         halo_gids = part["halo_gids"]
         del part, csr
-        self.graph.prepare_backward()
+        ex = getattr(args, "executor", "auto")
+        self.use_fused = ex == "fused" or (ex == "auto" and dtype == torch.float32 and
+                                           args.layers in (2, 3) and args.hidden == 256)
+        if not self.use_fused:
+            self.graph.prepare_backward()
         self.recompute = False
         mode = getattr(args, "halo_recompute", "off")
-        if p_world > 1 and mode != "off" and args.layers >= 3:
+        if p_world > 1 and mode != "off" and args.layers >= 3 and not self.use_fused:
             want = torch.tensor([1 if (mode == "on" or self.H < self.L) else 0],
                                 dtype=torch.long, device=dev)
             if self.world > 1:
@@ -182,7 +197,7 @@ class Job:
         # (collective: every rank builds it at this point); DGRAPH_BENCH_GRAD_SUPPORT=off
         # for the A/B
         gs = os.environ.get("DGRAPH_BENCH_GRAD_SUPPORT", "on")
-        if args.layers >= 2 and gs != "off":
+        if args.layers >= 2 and gs != "off" and not self.use_fused:
             self.graph.prepare_grad_support(self.train_idx)
         self.y_train = y[self.train_idx]
         ev = split == SPLIT_VALID
@@ -205,6 +220,18 @@ class Job:
                                args.layers).to(dev)
         self.opt = torch.optim.Adam(self.model.parameters(), lr=args.lr,
                                     fused=dev.type == "cuda")
+        self.fused = None
+        if self.use_fused:
+            from dgraph_amd.models.sage_fused import FusedSAGE, supported
+
+            if dev.type == "cuda":
+                gc.collect()  # the build's cached blocks back before the workspace is sized
+                torch.cuda.empty_cache()
+
+            if not supported(self.model, self.x):
+                raise SystemExit("[bench] --executor fused does not support this shape/dtype")
+            self.fused = FusedSAGE(self.model, self.graph, self.x, self.train_idx, self.y_train,
+                                   self.eval_idx, self.y_eval, self.eval_is_val, self.n_train)
         self.steppers = {}
         if getattr(args, "cuda_graph", False) and dev.type == "cuda":
             from dgraph_amd.utils.graphed import GraphedStep, make_capturable
@@ -226,6 +253,14 @@ class Job:
         import torch.nn.functional as Fn
 
         g = self.graph
+        if self.fused is not None:
+            # fp32 row-chunked executor: loss, p.grad and val/test hits of one full-graph step
+            loss = self.fused.step()
+            self.correct.copy_(self.fused.correct)
+            if self.sync is not None:
+                self.sync.all_reduce()
+            self.opt.step()
+            return loss
         if restrict_last:
             logits = self.model(self.x, g, out_rows=self.train_idx, restrict_last=True)
         else:
@@ -262,9 +297,15 @@ class Job:
         from dgraph_amd.models.sage import _pad_width
 
         c_out = _pad_width(self.shape.num_classes)
-        widths = [c_out] if self.recompute else \
-            [self.args.hidden] * (self.args.layers - 2) + [c_out] + \
-            [self.args.hidden] * (self.args.layers - 2)
+        if self.fused is not None:
+            # hidden activations forward (layers - 1) + layer 0's reverse exchange
+            widths = [self.args.hidden] * (self.args.layers - 1) + \
+                ([self.args.hidden] if self.args.layers == 3 else [])
+        elif self.recompute:
+            widths = [c_out]
+        else:
+            widths = [self.args.hidden] * (self.args.layers - 2) + [c_out] + \
+                [self.args.hidden] * (self.args.layers - 2)
         out["exchange_widths_per_step"] = widths
         if "max_pairwise_bytes" in out:
             rows = out["max_pairwise_bytes"] / fb
@@ -272,8 +313,8 @@ class Job:
         return out
 
     def free(self):
-        for k in ("graph", "x", "model", "opt", "sync", "train_idx", "y_train", "eval_idx",
-                  "y_eval", "eval_is_val"):
+        for k in ("fused", "graph", "x", "model", "opt", "sync", "train_idx", "y_train",
+                  "eval_idx", "y_eval", "eval_is_val"):
             setattr(self, k, None)
 
 
@@ -324,6 +365,59 @@ def timed(job: Job, steps: int, warmup: int, restrict_last: bool, verbose: bool 
         dist.all_reduce(red, op=dist.ReduceOp.MAX)
         dist.all_reduce(tot)  # each rank holds its share of the global mean loss
     return float(red.item()), float(tot[0].item()), float(tot[1].item())
+
+
+def region_breakdown(job: "Job") -> dict:
+    """One extra (untimed) step with stream events at the executor's region boundaries:
+    per-region device ms on every rank (no barrier or host sync inside the step), reduced
+    to max / min over ranks, plus the halo bytes each rank sent per peer during that step
+    and the achieved bytes per second over its exposed exchange time."""
+    ex = job.fused
+    if ex is None or job.dev.type != "cuda":
+        return {}
+    from dgraph_amd.comm.alltoallv import CommStats
+
+    CommStats.reset()
+    ex.record = True
+    job.step()
+    ex.record = False
+    reg = ex.region_ms()
+    sent = dict(CommStats.peer_bytes_sent)
+    names = sorted(reg)
+    exch = sum(v for k, v in reg.items() if k.startswith("exchange"))
+    comp = sum(v for k, v in reg.items() if not k.startswith("exchange"))
+    vals = [reg[k] for k in names] + [comp, exch]
+    world = job.world
+    if world > 1:
+        names_all = [None] * world
+        dist.all_gather_object(names_all, names)
+        if any(n != names for n in names_all):
+            return {"error": "ranks recorded different regions"}
+        t = torch.tensor(vals, dtype=torch.float64, device=job.dev)
+        tmax, tmin = t.clone(), t.clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tmin, op=dist.ReduceOp.MIN)
+        sent_all = [None] * world
+        dist.all_gather_object(sent_all, sent)
+        tmax, tmin = tmax.tolist(), tmin.tolist()
+    else:
+        tmax = tmin = vals
+        sent_all = [sent]
+    out = {
+        "ms_max_over_ranks": {k: round(v, 3) for k, v in zip(names, tmax)},
+        "ms_min_over_ranks": {k: round(v, 3) for k, v in zip(names, tmin)},
+        "compute_ms_max": round(tmax[-2], 3), "compute_ms_min": round(tmin[-2], 3),
+        "exposed_exchange_ms_max": round(tmax[-1], 3),
+        "exposed_exchange_ms_min": round(tmin[-1], 3),
+    }
+    if world > 1:
+        per_peer = [max(d.values()) if d else 0 for d in sent_all]
+        out["max_bytes_per_peer_per_step"] = max(per_peer)
+        out["bytes_sent_per_rank"] = [int(sum(d.values())) for d in sent_all]
+        if tmax[-1] > 0:
+            out["achieved_peer_GBps_over_exposed_exchange"] = round(
+                max(per_peer) / (tmax[-1] / 1e3) / 1e9, 2)
+    return out
 
 
 def _spawn_ranks(n: int) -> int:
@@ -388,6 +482,8 @@ def main():
     val_acc = float(corr[0]) / max(job.n_val, 1)
     test_acc = float(corr[1]) / max(job.n_test, 1)
     halo = job.halo_stats()
+    regions = region_breakdown(job)
+    use_fused = job.use_fused
     if args.profile_ops:
         _profile_one_step(lambda: job.step(head_restrict), args.profile_ops, rank)
     E_msg, n_train, halo_total = job.E_msg, job.n_train, job.halo_total
@@ -402,7 +498,7 @@ def main():
     extra = {}
     if not args.no_extra and not job.rehearse:
         ks = max(args.extra_steps, 1)
-        if not head_restrict:
+        if not head_restrict and not use_fused:
             t_ms, _, t_e = timed(job, ks, 1, True)
             extra["train_rows_only"] = {
                 "ms_per_step": t_ms, "edges_aggregated_per_step": t_e,
@@ -425,6 +521,24 @@ def main():
             mlog.metrics(phase="structureless", **extra["structureless"])
         sjob.free()
         del sjob
+        if dtype == torch.float32 and dev.type == "cuda" and not args.no_bf16_extra:
+            # secondary: the same headline graph at bf16 storage/compute (fp32 accumulate,
+            # fp32 master weights) on the layer-stack path — NOT the reference's precision
+            gc.collect()
+            torch.cuda.empty_cache()
+            import copy
+
+            bargs = copy.copy(args)
+            bargs.dtype, bargs.executor = "bf16", "stack"
+            bjob = Job(bargs, comm, dev, args.global_frac, torch.bfloat16)
+            b_ms, b_loss, b_e = timed(bjob, ks, 1, False)
+            extra["bf16_stack"] = {
+                "ms_per_step": b_ms, "edges_per_s": args.layers * bjob.E_msg / (b_ms / 1000.0),
+                "edges_aggregated_per_step": b_e, "steps": ks, "warmup": 1,
+                "final_loss": b_loss,
+                "note": "bf16 storage/compute, fp32 accumulate (below the reference's fp32)"}
+            bjob.free()
+            del bjob
     else:
         job.free()
 
@@ -452,6 +566,7 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": args.dtype if dev.type == "cuda" else "fp32",
+            "executor": "fused (models/sage_fused.py)" if use_fused else "stack (SAGEStackFn)",
             "data": (f"synthetic {shape.name}-shaped graph (V={shape.num_nodes}, "
                      f"directed={shape.num_directed_edges}, symmetrised E_msg={E_msg}, "
                      f"global_frac={args.global_frac}, window={args.window}), random "
@@ -460,9 +575,12 @@ def main():
                 "model": f"GraphSAGE-mean {args.layers}-layer hidden {args.hidden}",
                 "global_batch": shape.num_nodes,
                 "seq_len": None,
-                "parallelism": f"graph-partition{world} (RCCL all-to-all-v halo"
-                               + (", layer-1 halo recomputed" if job_recompute else "")
-                               + ") + dp-allreduce",
+                "parallelism": ("single GPU (whole graph, no exchange)" if world == 1 else
+                                f"graph-partition{world} (RCCL all-to-all-v halo"
+                                + (", layer-1 halo recomputed" if job_recompute else "")
+                                + ") + dp-allreduce"),
+                "rccl_world_size": (dist.get_world_size() if dist.is_initialized() else 1),
+                "process_group_backend": (dist.get_backend() if dist.is_initialized() else None),
                 "dataset_shape": shape.name,
                 "num_layers": args.layers,
                 "hidden": args.hidden,
@@ -475,7 +593,9 @@ def main():
                 "launch": "HIP graph replay" if args.cuda_graph else "eager",
                 "halo_recompute": job_recompute,
                 "precision": ("bf16 storage/compute, fp32 accumulate, fp32 master weights"
-                              if dtype == torch.bfloat16 else "fp32"),
+                              if dtype == torch.bfloat16 else
+                              "fp32 storage and compute (exact-f32 MFMA GEMMs, fp32 SpMM "
+                              "accumulation), fp32 weights: the reference's precision"),
             },
             "edges_aggregated_per_step": e_step,
             "edges_aggregated_per_s": e_step / (ms / 1000.0),
@@ -484,6 +604,7 @@ def main():
             "test_acc": test_acc,
             "peak_mem_gb_rank0": round(peak_gb, 2),
             **({"halo": halo} if halo else {}),
+            **({"regions": regions} if regions else {}),
             **extra,
         }
         print(json.dumps(rec), flush=True)

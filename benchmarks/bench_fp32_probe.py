@@ -124,7 +124,7 @@ def main():
             out = torch.empty_like(x)
             nbytes = csr.nnz * (F * 4 + 4) + p["L"] * F * 4
             for name, rg, pc in (("generic", 0, -1), ("rowgroup64", 1, 64),
-                                 ("rowgroup128", 1, 128), ("rowgroup256", 1, 256)):
+                                 ("rowgroup128", 1, 128), ("rowgroup32", 1, 32)):
                 if pc > F:
                     continue
                 ops.set_spmm_f32_config(rg, pc)
@@ -133,7 +133,7 @@ def main():
                                                 "TBps_eff": round(nbytes / ms / 1e9, 2)}
                 print(f"[spmm] fp32 F={F} {name}: {ms:.2f} ms {nbytes / ms / 1e9:.2f} TB/s eff",
                       flush=True)
-            ops.set_spmm_f32_config(1, 128)
+            ops.set_spmm_f32_config(1, 64)
             del x, out
             torch.cuda.empty_cache()
     print(json.dumps(res))

@@ -157,17 +157,25 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_f32_kernel(
       af[a][0] = *reinterpret_cast<const f32x4*>(p);
       af[a][1] = *reinterpret_cast<const f32x4*>(p + 4);
     }
+    // B fragments double-buffered across MFMA steps: step j+1's LDS reads are issued
+    // before step j's TM*TN MFMAs, so their latency hides behind a whole step instead of
+    // the few MFMAs that follow the read in a single-buffered schedule
+    float bf[2][TN];
+    const float* sbw = sb + (8 * lh) * L::BP + bcol_w + li;
+#pragma unroll
+    for (int b = 0; b < TN; ++b) bf[0][b] = sbw[b * 16];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      float bf[TN];
+      if (j + 1 < 8) {
 #pragma unroll
-      for (int b = 0; b < TN; ++b) bf[b] = sb[(8 * lh + j) * L::BP + bcol_w + b * 16 + li];
+        for (int b = 0; b < TN; ++b) bf[(j + 1) & 1][b] = sbw[(j + 1) * L::BP + b * 16];
+      }
 #pragma unroll
       for (int a = 0; a < TM; ++a) {
         const float av = af[a][j >> 2][j & 3];
 #pragma unroll
         for (int b = 0; b < TN; ++b)
-          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bf[b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bf[j & 1][b], acc[a][b], 0, 0, 0);
       }
     }
     if (s + 1 < nst) store_stage(buf ^ 1);

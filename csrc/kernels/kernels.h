@@ -50,7 +50,7 @@ hipError_t spmm_f32_rowgroup(IType it, const int64_t* rowptr, const void* col,
 // gate (nullable, indexed like out): the stored value is kept where gate > 0, else 0
 void set_spmm_f32_pass_cols(int cols);
 // rowgroup: 1 = fp32 row-group kernel (default), 0 = generic kernels; pass_cols: column
-// pass width (0 = default 128); negative arguments leave a setting unchanged
+// pass width (0 = default 64); negative arguments leave a setting unchanged
 void set_spmm_f32_config(int rowgroup, int pass_cols);
 
 // Hub-row splitting (rows whose degree exceeds `cap` are aggregated in three steps):

@@ -185,11 +185,11 @@ hipError_t launch_f32_rg(const int64_t* rowptr, const IdxT* col, const float* ew
 
 // fp32 rows wider than this run as column passes (each pass gathers a narrower window,
 // which the per-XCD L2 / Infinity Cache holds longer). A/B: benchmarks/bench_spmm.py
-int g_f32_pass_cols = 128;
+int g_f32_pass_cols = 64;
 
 }  // namespace
 
-void set_spmm_f32_pass_cols(int cols) { g_f32_pass_cols = cols > 0 ? cols : 128; }
+void set_spmm_f32_pass_cols(int cols) { g_f32_pass_cols = cols > 0 ? cols : 64; }
 
 bool spmm_f32_rowgroup_ok(int F, int64_t ldx, int64_t ldo, const void* x, const void* out) {
   auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) % 16) == 0; };

@@ -125,19 +125,29 @@ __global__ __launch_bounds__(kThr, 1) void wgrad_f32_kernel(
       if (s + 1 < nst) load_stage(s + 1);
       const float* sa = lds + buf * C::STAGE;
       const float* sg = sa + kRows * C::AP;
+      // operand fragments double-buffered across MFMA steps (reads of step j+1 are in
+      // flight during step j's MFMAs)
+      const float* saw = sa + (8 * lh) * C::AP + kw + li;
+      const float* sgw = sg + (8 * lh) * C::GP + nw + li;
+      float av[2][TM], gv[2][TN];
+#pragma unroll
+      for (int a = 0; a < TM; ++a) av[0][a] = saw[a * 16];
+#pragma unroll
+      for (int b = 0; b < TN; ++b) gv[0][b] = sgw[b * 16];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int row = 8 * lh + j;
-        float av[TM], gv[TN];
+        if (j + 1 < 8) {
 #pragma unroll
-        for (int a = 0; a < TM; ++a) av[a] = sa[row * C::AP + kw + a * 16 + li];
+          for (int a = 0; a < TM; ++a) av[(j + 1) & 1][a] = saw[(j + 1) * C::AP + a * 16];
 #pragma unroll
-        for (int b = 0; b < TN; ++b) gv[b] = sg[row * C::GP + nw + b * 16 + li];
+          for (int b = 0; b < TN; ++b) gv[(j + 1) & 1][b] = sgw[(j + 1) * C::GP + b * 16];
+        }
 #pragma unroll
         for (int a = 0; a < TM; ++a)
 #pragma unroll
           for (int b = 0; b < TN; ++b)
-            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[a], gv[b], acc[a][b], 0, 0, 0);
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j & 1][a], gv[j & 1][b],
+                                                             acc[a][b], 0, 0, 0);
       }
       if (s + 1 < nst) store_stage(buf ^ 1);
       __syncthreads();

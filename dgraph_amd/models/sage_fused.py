@@ -187,7 +187,30 @@ class FusedSAGE:
             self.nnz_S += int(self.halo.degree()[S].sum())
         self.loss = torch.zeros((), **f)
         self.correct = torch.zeros(2, dtype=torch.long, device=dev)
-        self.exchange_events = []
+        self.record = False
+        self._events: list = []
+
+    # ------------------------------------------------------------------ regions
+    def _mark(self, name: str):
+        """Record a stream event opening region ``name`` (closes the previous one) when
+        ``self.record`` is set: per-region device time of one step without barriers or
+        host syncs inside it (the reference's TimingReport regions, experiments/OGB/
+        GCN.py:101-116, barriered and synced every region)."""
+        if not self.record or self.dev.type != "cuda":
+            return
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        self._events.append((name, ev))
+
+    def region_ms(self) -> dict:
+        """Device milliseconds per region of the last recorded step (host sync)."""
+        if not self._events:
+            return {}
+        torch.cuda.synchronize(self.dev)
+        out: dict = {}
+        for (name, a), (_, b) in zip(self._events[:-1], self._events[1:]):
+            out[name] = out.get(name, 0.0) + a.elapsed_time(b)
+        return out
 
     @property
     def edges_aggregated(self) -> int:
@@ -246,6 +269,8 @@ class FusedSAGE:
         nl, hid, C, Cp, Cg = self.nl, self.hid, self.C, self.Cp, self.Cg
         P = self._params()
         dev = self.dev
+        self._events = []
+        self._mark("fwd_l0")
         self.loss.zero_()
         self.correct.zero_()
         nnz_it = self.it.nnz
@@ -265,8 +290,11 @@ class FusedSAGE:
                              out=hout[r0:r1])
             self.edges_aggregated += nnz_it + nnz_h
             hin = hout
+            if g.halo is not None:
+                self._mark(f"exchange_fwd_h{l + 1}")
             hin_halo = self._exchange(hout)
             halos.append(hin_halo)
+            self._mark(f"fwd_l{l + 1}" if l + 1 < nl - 1 else "fwd_out")
         # ---------------- forward: output layer (all rows), loss and eval on the fly
         ws, wn, b = P[nl - 1]
         wsp = torch.zeros(hid, Cp, device=dev)
@@ -305,6 +333,7 @@ class FusedSAGE:
                 self.correct[1] += (hit & ~iv).sum()
         self.edges_aggregated += nnz_it + nnz_h
         loss = self.loss * self.inv_n
+        self._mark("bwd_out")
         # ---------------- backward: output layer -> dZ of the last hidden layer on S
         hlast = hl
         F32.row_keep_bits(hlast, self.S, self.bits)  # the last hidden ReLU derivative on S
@@ -329,13 +358,16 @@ class FusedSAGE:
         F32.spmm_f32(self.AT_S.rowptr, self.AT_S.col, u2, dZ)
         self.edges_aggregated += self.AT_S.nnz
         if work is not None:
+            self._mark("exchange_bwd_out")
             work.wait()
+            self._mark("bwd_out")
             F32.spmm_f32(stc.rowptr, stc.col, sg, dZ, beta=1.0, row_map=stc_rows)
             del sg, hg
         F32.gemm_f32(self.dz, ws_t, cin=dZ, o_rows=self.posT, out=dZ)
         F32.apply_keep_bits(dZ, self.bits)
         # ---------------- backward: last hidden layer (index nl-2) weights over S rows
         lh = nl - 2
+        self._mark(f"bwd_l{lh}")
         ws1, wn1, _ = P[lh]
         hin_l = x if lh == 0 else self.h[lh - 1]
         hin_l_halo = halos[lh]
@@ -372,7 +404,9 @@ class FusedSAGE:
             # ------------ layer 0: dZ0 by row chunks, consumed at once by its weight grads
             ws1_t = ws1.detach().t().contiguous()
             if work is not None:
+                self._mark("exchange_bwd_l0")
                 work.wait()
+            self._mark("bwd_l0")
             self.acc_in.reset()
             db0 = torch.zeros(hid, device=dev)
             h1 = self.h[0]
@@ -400,6 +434,7 @@ class FusedSAGE:
                 (self.send_st.nnz if self.send_st is not None else 0)
             w0 = self.acc_in.result()
             gw[(0, 0)], gw[(0, 1)], gw[(0, 2)] = w0[:self.d0], w0[self.d0:], db0
+        self._mark("grads")
         # ---------------- gradients into the parameters
         for l, (ws_, wn_, b_) in enumerate(P):
             for k, p in enumerate((ws_, wn_, b_)):
@@ -410,4 +445,5 @@ class FusedSAGE:
                     p.grad = gk.clone()
                 else:
                     p.grad.copy_(gk)
+        self._mark("end")
         return loss
