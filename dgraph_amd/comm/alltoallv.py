@@ -25,7 +25,34 @@ import torch.distributed as dist
 # the W = 2..8 equivalence tests. "native" (comm/rccl_exec.py: a private communicator,
 # several tensors per group call, completion as a HIP event) stays selectable with
 # DGRAPH_A2A_IMPL=native for A/B runs on a multi-GPU node (benchmarks/bench_comm.py).
+#
+# "shmem": one-sided puts into the receivers' symmetric-heap slots over xGMI
+# (comm/symheap.py; the reference's put contract with remote offsets,
+# DGraph/distributed/Engine.py:67-86, commInfo.py:205-206). Needs no RCCL communicator, so it
+# also runs ranks that share one GPU (RCCL refuses two ranks per device): the
+# 2-process-on-one-GPU equivalence test of the bench step uses it.
 A2A_IMPL = os.environ.get("DGRAPH_A2A_IMPL", "torch")
+
+_HEAPS: dict = {}
+
+
+def shmem_heap(group, device):
+    """The process-wide symmetric heap of ``group`` on ``device`` (created collectively on
+    first use; size DGRAPH_SYMHEAP_BYTES)."""
+    key = (id(group), str(device))
+    h = _HEAPS.get(key)
+    if h is None:
+        from .symheap import SymmetricHeap
+
+        h = SymmetricHeap(SymmetricHeap.DEFAULT_BYTES, group, device)
+        _HEAPS[key] = h
+    return h
+
+
+def close_shmem_heaps() -> None:
+    for h in _HEAPS.values():
+        h.close()
+    _HEAPS.clear()
 
 
 def offsets_to_splits(offsets) -> List[int]:
@@ -70,6 +97,8 @@ class AllToAllV:
         self.total_send = sum(self.send_splits)
         self.total_recv = sum(self.recv_splits)
         self._world = len(self.send_splits)
+        self._shm_offsets = None  # peers' receive offsets of my rows (shmem transport)
+        self._shm_slots: dict = {}  # (row shape, dtype) -> symmetric receive slot
 
     def reversed(self) -> "AllToAllV":
         return AllToAllV(self.recv_splits, self.send_splits, self.group)
@@ -99,6 +128,9 @@ class AllToAllV:
                 out.copy_(send)
             return (out, _Done()) if async_op else out
         send_c = send.contiguous()
+        if A2A_IMPL == "shmem" and send_c.is_cuda:
+            self._shmem(send_c, out)
+            return (out, _Done()) if async_op else out
         if A2A_IMPL == "native" and send_c.is_cuda:
             from .rccl_exec import RCCLExecutor
 
@@ -115,6 +147,35 @@ class AllToAllV:
         if async_op:
             return out, work
         return out
+
+
+    def _shmem(self, send: torch.Tensor, out: torch.Tensor) -> None:
+        """One-sided exchange: every rank puts its segment for peer p straight into p's
+        symmetric receive slot at the offset where p expects rows from this rank (the
+        prefix of p's receive splits), then copies its own slot out. Completion is
+        stream-ordered on separate GPUs and host-ordered for ranks sharing one
+        (SymmetricHeap.put_rows). The first call per (plan, row shape, dtype) is collective:
+        the slot is sized for the largest receiver and the offsets are exchanged once."""
+        heap = shmem_heap(self.group, send.device)
+        if self._shm_offsets is None:
+            from ..plan.pattern import _alltoall_counts
+
+            pre = [0]
+            for n in self.recv_splits[:-1]:
+                pre.append(pre[-1] + n)
+            mine = torch.tensor(pre, dtype=torch.long)
+            self._shm_offsets = [int(v) for v in _alltoall_counts(mine, self.group).tolist()]
+        key = (tuple(send.shape[1:]), send.dtype)
+        slot = self._shm_slots.get(key)
+        if slot is None:
+            from .symheap import _allgather_obj
+
+            rmax = max(_allgather_obj(int(self.total_recv), self.group))
+            slot = heap.alloc_tensor((max(rmax, 1),) + tuple(send.shape[1:]), send.dtype)
+            self._shm_slots[key] = slot
+        heap.put_rows(send, slot, self.send_splits, self._shm_offsets)
+        if self.total_recv:
+            out.copy_(slot[: self.total_recv])
 
 
 def torch_alltoallv_with_comm_map(contiguous_send_tensor: torch.Tensor,

@@ -194,3 +194,45 @@ def test_device_signal_wait_two_streams():
     for r in range(2):
         exp = torch.stack([torch.full((R, F), float(100 * it + (1 - r))) for it in range(rounds)])
         assert torch.equal(got[r].cpu(), exp)
+
+
+def _engine_no_leak_body(rank, world):
+    """the engine passes fresh view objects (x3[0], indices.reshape(-1)) every
+    call; registrations and scatter plans must hit by data identity, so repeated calls
+    allocate nothing more on the symmetric heap after the first."""
+    import torch.distributed as dist
+
+    from dgraph_amd.comm.shmem_engine import ROCSHMEMBackendEngine
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    eng = ROCSHMEMBackendEngine()
+    h = eng.heap()
+    assert h is not None
+    F, n = 24, 200
+    x = (torch.arange(n * F, dtype=torch.float32).reshape(1, n, F) + 1e4 * rank).to(dev)
+    g = torch.Generator().manual_seed(3 + rank)
+    E = 300
+    owners = torch.randint(0, world, (1, E), generator=g).to(dev)
+    idx = torch.randint(0, n, (1, E), generator=g).to(dev)
+    cursors = []
+    for it in range(4):
+        y = eng.gather(x, idx, owners)
+        s = eng.scatter(y, idx, owners, n)
+        torch.cuda.synchronize()
+        cursors.append(h._cursor)
+    assert len(set(cursors)) == 1, f"heap grew across identical calls: {cursors}"
+    assert len(h._registered) == 1 and len(h._scatter_plans) == 1
+    # an in-place update of x is re-copied into the same slot (no new allocation)
+    x.add_(1.0)
+    y2 = eng.gather(x, idx, owners)
+    torch.cuda.synchronize()
+    assert h._cursor == cursors[0]
+    torch.testing.assert_close(y2, y + 1.0)
+    h.check()
+    h.close()
+    dist.barrier()
+
+
+def test_shmem_engine_repeated_calls_do_not_grow_heap():
+    run_ranks(_engine_no_leak_body, 2)

@@ -1,0 +1,164 @@
+"""The exact bench.py training step as TWO PROCESSES on ONE GPU (W=2 across a real process
+boundary, through the HIP kernels) against W=1 on the same GPU.
+
+RCCL refuses two ranks per device, so the halo all-to-all-v runs on the one-sided
+symmetric-heap transport (DGRAPH_A2A_IMPL=shmem: IPC-mapped peer heaps, puts at the
+receivers' remote offsets — the reference's put contract, DGraph/distributed/Engine.py:
+67-86); the small collectives (counts, gradient all-reduce) ride gloo. Rank 0 first runs the
+W=1 job alone, then both ranks run the W=2 job; rank 0 compares losses, the first step's
+all-reduced gradients, every parameter after 3 Adam steps and the validation/test hit
+counts (reference: tests/test_NCCLCommPlan.py:85-124,242-359, replicated ground truth).
+
+Covered: fp32 on the fused row-chunked executor (the headline path) in both graph
+localities; bf16 on the layer-stack path with halo recomputation off and on and the
+gradient support prepared (the round-2 fused bf16 path).
+"""
+import argparse
+import os
+import types
+
+import pytest
+import torch
+import torch.distributed as dist
+
+from conftest import run_ranks
+
+pytestmark = pytest.mark.gpu
+
+
+def _args(**kw):
+    a = argparse.Namespace(shape="ogbn-papers100M", scale=2e-4, hidden=256, layers=3, lr=1e-2,
+                           dtype="fp32", global_frac=0.05, window=256, seed=0,
+                           no_overlap=False, rehearse_world=0, rehearse_rank=0,
+                           halo_recompute="off", executor="auto", cuda_graph=False)
+    for k, v in kw.items():
+        setattr(a, k, v)
+    return a
+
+
+def _run(rank, world, args, dtype, steps=3):
+    import bench
+
+    comm = types.SimpleNamespace(get_rank=lambda: rank, get_world_size=lambda: world,
+                                 group=None)
+    dev = torch.device("cuda", 0)
+    job = bench.Job(args, comm, dev, args.global_frac, dtype)
+    if args.halo_recompute == "on" and world > 1:
+        assert job.recompute, "halo recomputation was not enabled"
+    if dtype == torch.float32:
+        assert job.fused is not None, "fp32 must run on the fused executor"
+    elif world > 1 and not job.recompute:
+        assert job.graph.grad_support(job.train_idx) is not None, "grad support not prepared"
+    grads = []
+    orig = job.opt.step
+
+    def capture(*a, **k):  # the gradients Adam consumes (all-reduced at W > 1)
+        if not grads:
+            grads.append([p.grad.detach().float().clone() for p in job.model.parameters()])
+        return orig(*a, **k)
+
+    job.opt.step = capture
+    losses = []
+    for _ in range(steps):
+        loss = job.step(False).detach().float().clone()
+        if world > 1:
+            dist.all_reduce(loss)
+        losses.append(float(loss))
+    corr = job.correct.clone()
+    if world > 1:
+        dist.all_reduce(corr)
+    out = {"losses": torch.tensor(losses, dtype=torch.float64), "grads": grads[0],
+           "params": [p.detach().float().clone() for p in job.model.parameters()],
+           "correct": corr.cpu(), "E_msg": job.E_msg, "halo": job.halo_total}
+    job.free()
+    torch.cuda.synchronize()
+    return out
+
+
+def _body(rank, world, kw, dt):
+    torch.cuda.set_device(0)
+    dtype = torch.float32 if dt == "fp32" else torch.bfloat16
+    args = _args(dtype=dt, **kw)
+    ref = _run(0, 1, args, dtype) if rank == 0 else None
+    dist.barrier()
+    got = _run(rank, world, args, dtype)
+    from dgraph_amd.comm.alltoallv import close_shmem_heaps
+
+    close_shmem_heaps()
+    if rank != 0:
+        return
+    assert got["halo"] > 0, "the W=2 partition has no halo: nothing crossed the boundary"
+    assert ref["E_msg"] == got["E_msg"]
+    if dt == "fp32":
+        torch.testing.assert_close(got["losses"], ref["losses"], atol=1e-5, rtol=1e-5)
+        for a, b in zip(got["grads"], ref["grads"]):
+            torch.testing.assert_close(a, b, atol=1e-6, rtol=1e-4)
+        for a, b in zip(got["params"], ref["params"]):
+            torch.testing.assert_close(a, b, atol=1e-5, rtol=1e-4)
+        assert torch.equal(got["correct"], ref["correct"])
+    else:
+        # bf16 storage: W=2 sums interior and halo parts in another order and rounds the
+        # partial aggregate once more; compare at bf16 resolution
+        torch.testing.assert_close(got["losses"], ref["losses"], atol=2e-3, rtol=2e-3)
+        for a, b in zip(got["grads"], ref["grads"]):
+            rel = float((a - b).norm() / b.norm().clamp_min(1e-12))
+            assert rel < 3e-2, f"bf16 W=2 gradient differs from W=1 by {rel:.3e} (relative)"
+        d = (got["correct"] - ref["correct"]).abs()
+        assert int(d.max()) <= max(2, int(0.02 * int(ref["correct"].max()))), \
+            (got["correct"], ref["correct"])
+
+
+@pytest.mark.parametrize("dt,kw", [
+    ("fp32", dict(global_frac=0.05)),
+    ("fp32", dict(global_frac=1.0)),
+    ("bf16", dict(global_frac=0.05, halo_recompute="off")),
+    ("bf16", dict(global_frac=0.05, halo_recompute="on")),
+    ("bf16", dict(global_frac=1.0, halo_recompute="on")),
+], ids=["fp32-local", "fp32-structureless", "bf16-local", "bf16-local-recompute",
+        "bf16-structureless-recompute"])
+def test_bench_step_two_processes_one_gpu(monkeypatch, dt, kw):
+    monkeypatch.setenv("DGRAPH_A2A_IMPL", "shmem")
+    monkeypatch.setenv("DGRAPH_SYMHEAP_BYTES", str(1 << 30))
+    run_ranks(_body, 2, kw, dt, timeout=240)
+
+
+def test_alltoallv_shmem_two_processes(monkeypatch):
+    """The shmem transport alone: random splits, two widths, two dtypes, repeated calls
+    (slot reuse across calls must not leak into the next exchange)."""
+    monkeypatch.setenv("DGRAPH_A2A_IMPL", "shmem")
+    monkeypatch.setenv("DGRAPH_SYMHEAP_BYTES", str(64 << 20))
+    run_ranks(_a2a_body, 2, timeout=120)
+
+
+def _a2a_body(rank, world):
+    torch.cuda.set_device(0)
+    from dgraph_amd.comm.alltoallv import AllToAllV, close_shmem_heaps, shmem_heap
+
+    g = torch.Generator().manual_seed(7)
+    splits = torch.randint(0, 500, (world, world), generator=g)  # splits[src][dst]
+    send_s = [int(v) for v in splits[rank]]
+    recv_s = [int(splits[q][rank]) for q in range(world)]
+    a2a = AllToAllV(send_s, recv_s)
+    for it in range(3):
+        for F, dt in ((64, torch.float32), (256, torch.bfloat16)):
+            # row j of the block for peer p carries (src rank, dst rank, j, it)
+            rows = []
+            for p in range(world):
+                j = torch.arange(send_s[p], dtype=torch.float32)
+                v = (rank * 1000 + p * 100 + it) + j.unsqueeze(1) * 0.0 + \
+                    torch.arange(F, dtype=torch.float32) * 0
+                v[:, 0] = j
+                rows.append(v)
+            send = torch.cat(rows).to(dt).cuda()
+            out = a2a(send)
+            torch.cuda.synchronize()
+            off = 0
+            for q in range(world):
+                blk = out[off:off + recv_s[q]].float().cpu()
+                exp = torch.full((recv_s[q], F), float(q * 1000 + rank * 100 + it))
+                exp[:, 0] = torch.arange(recv_s[q], dtype=torch.float32)
+                assert torch.equal(blk, exp.to(dt).float()), (rank, q, it, F)
+                off += recv_s[q]
+    used = shmem_heap(None, torch.device("cuda", 0))._cursor
+    close_shmem_heaps()
+    assert used < (64 << 20)
