@@ -58,6 +58,44 @@ def _pad_to(n: int, m: int) -> int:
     return (n + m - 1) // m * m
 
 
+class _Pipe:
+    """Two-stage chunk pipeline over two streams (GPU; plain sequence on CPU): stage 1
+    (the memory-bound aggregation of chunk c into buffer c % 2) runs on the current stream,
+    stage 2 (MFMA GEMMs and weight gradients reading that buffer) on a side stream, so
+    chunk c+1's aggregation overlaps chunk c's matrix work — the two use different pipes
+    (HBM / vector memory vs matrix cores) and the kernels co-reside on the CUs. Events
+    order buffer reuse (stage 1 of chunk c+2 waits for stage 2 of chunk c); ``run`` ends
+    with the current stream waiting for the side stream."""
+
+    def __init__(self, dev):
+        self.cuda = dev.type == "cuda"
+        if self.cuda:
+            self.side = torch.cuda.Stream(dev)
+            self.ready = [torch.cuda.Event() for _ in range(2)]
+            self.free = [torch.cuda.Event() for _ in range(2)]
+
+    def run(self, items, produce, consume):
+        if not self.cuda:
+            for k, it in enumerate(items):
+                consume(it, produce(it, k % 2), k % 2)
+            return
+        main = torch.cuda.current_stream()
+        self.side.wait_stream(main)
+        used = [False, False]
+        for k, it in enumerate(items):
+            b = k % 2
+            if used[b]:
+                main.wait_event(self.free[b])
+            res = produce(it, b)
+            self.ready[b].record(main)
+            with torch.cuda.stream(self.side):
+                self.side.wait_event(self.ready[b])
+                consume(it, res, b)
+                self.free[b].record(self.side)
+            used[b] = True
+        main.wait_stream(self.side)
+
+
 def supported(model, x: torch.Tensor) -> bool:
     """Shapes the fused executor runs (the GraphSAGE of bench.py / the OGB shapes)."""
     layers = list(model.layers)
@@ -142,8 +180,9 @@ class FusedSAGE:
         spare = max(free - need_h - (6 << 30), 1 << 30)
         cr = chunk_rows or CHUNK_ROWS
         if cr <= 0:
-            per_row = 4 * (self.hid + max(self.Cp, self.d0) + self.hid)
-            cr = int(min(max(spare // 3 // per_row, 1 << 16), 1 << 21))
+            # two aggregate + two logit/gradient chunk buffers, and the GEMM's own slack
+            per_row = 4 * 2 * (max(self.hid, self.d0) + max(self.Cp, self.hid))
+            cr = int(min(max(spare * 2 // 3 // per_row, 1 << 16), 1 << 21))
         self.cr = max(256, min(int(cr), max(L, 256)))
         self.chunks = _ranges(L, self.cr)
         self.s_chunks = _ranges(self.nS, self.cr)
@@ -171,8 +210,12 @@ class FusedSAGE:
             self.dZ = hl[:n].view(self.nS, self.hid)
             self.u = hl[n:2 * n].view(self.nS, self.hid) if self.nl == 3 else None
         wA = max(self.hid, self.d0)
-        self.bufA = torch.empty(self.cr, wA, **f)           # chunk aggregate
-        self.bufB = torch.empty(self.cr, max(self.Cp, self.hid), **f)  # logits / dZ0 chunk
+        # two of each chunk buffer: chunk c+1's aggregation (memory-bound SpMM, producer
+        # stream) runs while chunk c's MFMA GEMMs (consumer stream) read the other one
+        self.bufA2 = [torch.empty(self.cr, wA, **f) for _ in range(2)]   # chunk aggregates
+        self.bufB2 = [torch.empty(self.cr, max(self.Cp, self.hid), **f) for _ in range(2)]
+        self.bufA, self.bufB = self.bufA2[0], self.bufB2[0]
+        self.pipe = _Pipe(dev)
         self.dz = torch.zeros(self.T.numel(), self.Cg, **f)  # output-layer gradient rows
         self.bits = torch.empty(self.nS, self.hid // 32, dtype=torch.int32, device=dev)
         self.u_out = torch.empty(self.T.numel(), self.hid, **f)
@@ -282,12 +325,17 @@ class FusedSAGE:
             ws, wn, b = P[l]
             ws, wn = ws.detach().contiguous(), wn.detach().contiguous()
             hout = self.h[l]
-            for ci, (r0, r1) in enumerate(self.chunks):
-                if r1 <= r0:
-                    continue
-                a = self._agg_chunk(hin, hin_halo, ci, self.bufA[:, :hin.shape[1]])
-                F32.gemm_f32(hin[r0:r1], ws, a, wn, bias=b.detach(), relu=True,
-                             out=hout[r0:r1])
+            bias = b.detach()
+            items = [ci for ci, (r0, r1) in enumerate(self.chunks) if r1 > r0]
+
+            def produce(ci, k, hin=hin, hin_halo=hin_halo):
+                return self._agg_chunk(hin, hin_halo, ci, self.bufA2[k][:, :hin.shape[1]])
+
+            def consume(ci, a, k, hin=hin, hout=hout, ws=ws, wn=wn, bias=bias):
+                r0, r1 = self.chunks[ci]
+                F32.gemm_f32(hin[r0:r1], ws, a, wn, bias=bias, relu=True, out=hout[r0:r1])
+
+            self.pipe.run(items, produce, consume)
             self.edges_aggregated += nnz_it + nnz_h
             hin = hout
             if g.halo is not None:
@@ -306,34 +354,49 @@ class FusedSAGE:
         self.acc_out_s.reset()
         self.acc_out_n.reset()
         hl, hl_halo = hin, hin_halo
-        for ci, (r0, r1) in enumerate(self.chunks):
-            if r1 <= r0:
-                continue
-            n = r1 - r0
-            a = self._agg_chunk(hl, hl_halo, ci, self.bufA[:, :hid])
-            z = F32.gemm_f32(hl[r0:r1], wsp, a, wnp, bias=bp, out=self.bufB[:n, :Cp])
-            t0, t1 = self.ch_T[ci]
-            if t1 > t0:
-                tl = self.ch_Tloc[ci]
-                zt = z.index_select(0, tl)[:, :C]
-                lse = torch.logsumexp(zt, 1)
-                y = self.yT[t0:t1]
-                self.loss += (lse - zt.gather(1, y.unsqueeze(1)).squeeze(1)).sum()
-                p = torch.exp(zt - lse.unsqueeze(1))
-                p.scatter_add_(1, y.unsqueeze(1), torch.full_like(lse, -1.0).unsqueeze(1))
-                dzt = self.dz[t0:t1]
-                dzt[:, :C] = p * self.inv_n
-                self.acc_out_s.add(hl, dzt, a1_rows=self.T[t0:t1])
-                self.acc_out_n.add(a, dzt, a1_rows=tl)
-            e0, e1 = self.ch_E[ci]
-            if e1 > e0:
-                hit = z.index_select(0, self.ch_Eloc[ci])[:, :C].argmax(1) == self.yE[e0:e1]
-                iv = self.E_val[e0:e1]
-                self.correct[0] += (hit & iv).sum()
-                self.correct[1] += (hit & ~iv).sum()
+        items = [ci for ci, (r0, r1) in enumerate(self.chunks) if r1 > r0]
+
+        def produce_out(ci, k):
+            return self._agg_chunk(hl, hl_halo, ci, self.bufA2[k][:, :hid])
+
+        self.pipe.run(items, produce_out,
+                      lambda ci, a, k: self._out_chunk(ci, a, k, hl, wsp, wnp, bp))
         self.edges_aggregated += nnz_it + nnz_h
         loss = self.loss * self.inv_n
         self._mark("bwd_out")
+        return self._backward(P, halos, hl, hl_halo, loss, nnz_it, nnz_h)
+
+    def _out_chunk(self, ci, a, k, hl, wsp, wnp, bp):
+        """Output layer of row chunk ci (consumer stream): logits of every row, the loss
+        rows' cross-entropy gradient and output-layer weight gradients, eval hits."""
+        C, Cp = self.C, self.Cp
+        r0, r1 = self.chunks[ci]
+        n = r1 - r0
+        z = F32.gemm_f32(hl[r0:r1], wsp, a, wnp, bias=bp, out=self.bufB2[k][:n, :Cp])
+        t0, t1 = self.ch_T[ci]
+        if t1 > t0:
+            tl = self.ch_Tloc[ci]
+            zt = z.index_select(0, tl)[:, :C]
+            lse = torch.logsumexp(zt, 1)
+            y = self.yT[t0:t1]
+            self.loss += (lse - zt.gather(1, y.unsqueeze(1)).squeeze(1)).sum()
+            p = torch.exp(zt - lse.unsqueeze(1))
+            p.scatter_add_(1, y.unsqueeze(1), torch.full_like(lse, -1.0).unsqueeze(1))
+            dzt = self.dz[t0:t1]
+            dzt[:, :C] = p * self.inv_n
+            self.acc_out_s.add(hl, dzt, a1_rows=self.T[t0:t1])
+            self.acc_out_n.add(a, dzt, a1_rows=tl)
+        e0, e1 = self.ch_E[ci]
+        if e1 > e0:
+            hit = z.index_select(0, self.ch_Eloc[ci])[:, :C].argmax(1) == self.yE[e0:e1]
+            iv = self.E_val[e0:e1]
+            self.correct[0] += (hit & iv).sum()
+            self.correct[1] += (hit & ~iv).sum()
+
+    def _backward(self, P, halos, hl, hl_halo, loss, nnz_it, nnz_h):
+        g, x, dev = self.g, self.x, self.dev
+        nl, hid, C, Cg = self.nl, self.hid, self.C, self.Cg
+        ws, wn, _ = P[nl - 1]
         # ---------------- backward: output layer -> dZ of the last hidden layer on S
         hlast = hl
         F32.row_keep_bits(hlast, self.S, self.bits)  # the last hidden ReLU derivative on S
@@ -385,18 +448,23 @@ class FusedSAGE:
                 self.edges_aggregated += self.haloT.nnz
         self.acc_hid_s.reset()
         self.acc_hid_n.reset()
-        for s0, s1 in self.s_chunks:
-            if s1 <= s0:
-                continue
+        def produce_s(sr, k):
+            s0, s1 = sr
             rows = self.S[s0:s1]
-            aS = self.bufA[:s1 - s0, :hin_l.shape[1]]
+            aS = self.bufA2[k][:s1 - s0, :hin_l.shape[1]]
             F32.spmm_f32(self.it.rowptr, self.it.col, hin_l, aS, row_ids=rows,
                          row_scale=self.invdegS[s0:s1])
             if hin_l_halo is not None:
                 F32.spmm_f32(self.halo.rowptr, self.halo.col, hin_l_halo, aS, row_ids=rows,
                              row_scale=self.invdegS[s0:s1], beta=1.0)
-            self.acc_hid_s.add(hin_l, dZ[s0:s1], a1_rows=rows)
+            return aS
+
+        def consume_s(sr, aS, k):
+            s0, s1 = sr
+            self.acc_hid_s.add(hin_l, dZ[s0:s1], a1_rows=self.S[s0:s1])
             self.acc_hid_n.add(aS, dZ[s0:s1])
+
+        self.pipe.run([sr for sr in self.s_chunks if sr[1] > sr[0]], produce_s, consume_s)
         self.edges_aggregated += self.nnz_S
         gw[(lh, 0)] = self.acc_hid_s.result()
         gw[(lh, 1)] = self.acc_hid_n.result()
@@ -408,14 +476,16 @@ class FusedSAGE:
                 work.wait()
             self._mark("bwd_l0")
             self.acc_in.reset()
-            db0 = torch.zeros(hid, device=dev)
+            db0s = []
             h1 = self.h[0]
             x_halo = halos[0]
-            for ci, (r0, r1) in enumerate(self.chunks):
-                if r1 <= r0:
-                    continue
+
+            def produce_0(ci, k):
+                # memory-bound: the column-mapped transposed aggregation of u1 (gated by
+                # layer 0's ReLU) and the recomputed layer-0 input aggregate
+                r0, r1 = self.chunks[ci]
                 n = r1 - r0
-                gz = self.bufB[:n, :hid]
+                gz = self.bufB2[k][:n, :hid]
                 F32.spmm_f32(self.it.rowptr[r0:r1 + 1], self.it.col, u, gz, col_map=self.smap,
                              gate=h1[r0:r1])
                 sr = self.ch_send[ci]
@@ -423,13 +493,22 @@ class FusedSAGE:
                     rp, rmap, _ = sr
                     F32.spmm_f32(rp, self.send_st.col, sg1, gz, beta=1.0, row_map=rmap,
                                  gate=h1[r0:r1])
+                a0 = self._agg_chunk(x, x_halo, ci, self.bufA2[k][:, :self.d0])
+                return gz, a0
+
+            def consume_0(ci, ga, k):
+                gz, a0 = ga
+                r0, r1 = self.chunks[ci]
                 s0, s1 = self.ch_S[ci]
                 if s1 > s0:
                     F32.gemm_f32(dZ[s0:s1], ws1_t, cin=gz, o_rows=self.ch_Sloc[ci],
                                  gate=h1[r0:r1], out=gz)
-                a0 = self._agg_chunk(x, x_halo, ci, self.bufA[:, :self.d0])
                 self.acc_in.add(x[r0:r1], gz, A2=a0)
-                db0 += K.col_sum(gz)
+                db0s.append(K.col_sum(gz))
+
+            self.pipe.run([ci for ci, (r0, r1) in enumerate(self.chunks) if r1 > r0],
+                          produce_0, consume_0)
+            db0 = torch.stack(db0s).sum(0) if db0s else torch.zeros(hid, device=dev)
             self.edges_aggregated += 2 * nnz_it + nnz_h + \
                 (self.send_st.nnz if self.send_st is not None else 0)
             w0 = self.acc_in.result()
