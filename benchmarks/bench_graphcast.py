@@ -46,6 +46,9 @@ def main():
     ap.add_argument("--cuda-graph", action="store_true",
                     help="--mode step: capture the whole step into a HIP graph after one "
                          "eager step and replay it (dgraph_amd.utils.graphed)")
+    ap.add_argument("--mesh-vertex-placement", default=None,
+                    help="mesh_vertex_rank_placement.pt (int [V_mesh] ranks, loaded "
+                         "weights_only); default: latitude bands")
     ap.add_argument("--dedup-mesh-edges", action="store_true",
                     help="one processor edge per multimesh edge pair (327 660 at level 6); "
                          "default: the reference's graph, every multimesh edge carried twice "
@@ -69,7 +72,12 @@ def main():
     t0 = time.perf_counter()
     g = build_global_graph(a.mesh_level, tuple(int(v) for v in a.grid.split("x")),
                            duplicate_mesh_edges=not a.dedup_mesh_edges)
-    pg = partition_graphcast_graph(g, rank, W, group=comm.group).to(dev)
+    mesh_part = None
+    if a.mesh_vertex_placement:
+        from dgraph_amd.data.graphcast_graph import load_mesh_placement
+
+        mesh_part = load_mesh_placement(a.mesh_vertex_placement, g.mesh_xyz.shape[0], W)
+    pg = partition_graphcast_graph(g, rank, W, mesh_part=mesh_part, group=comm.group).to(dev)
     build_s = time.perf_counter() - t0
     cfg = Config()
     cfg.model.hidden_dim = a.hidden

@@ -204,6 +204,40 @@ def latitude_partition(g: GlobalGraphCastGraph, world_size: int
     return grid_part, mesh_part
 
 
+def grid_placement_from_mesh(g: GlobalGraphCastGraph, mesh_part: torch.Tensor) -> torch.Tensor:
+    """Grid placement that follows a given mesh placement: every grid vertex goes to the
+    owner of the first mesh vertex it is decoded from (its mesh2grid source triangle), so
+    the mesh-to-grid edges of a grid vertex stay with one rank and grid halos follow the
+    mesh partition boundary."""
+    src, dst = g.m2g
+    n_grid = g.grid_shape[0] * g.grid_shape[1]
+    first = np.full(n_grid, -1, dtype=np.int64)
+    # first edge per grid vertex (edges in any order: take the smallest edge index)
+    order = np.argsort(dst, kind="stable")
+    d_sorted = dst[order]
+    starts = np.ones(d_sorted.shape[0], dtype=bool)
+    starts[1:] = d_sorted[1:] != d_sorted[:-1]
+    first[d_sorted[starts]] = src[order[starts]]
+    if (first < 0).any():
+        raise ValueError("grid vertex without a mesh2grid edge")
+    return mesh_part.long()[torch.from_numpy(first)]
+
+
+def load_mesh_placement(path: str, num_mesh: int, world_size: int) -> torch.Tensor:
+    """``mesh_vertex_rank_placement.pt`` of the reference (experiments/GraphCast/dataset.py:
+    244, microbenchmark_graphcast.py:35): an int tensor [V_mesh] of ranks. Loaded with
+    ``weights_only=True`` (no code from the file runs) and validated."""
+    t = torch.load(path, map_location="cpu", weights_only=True)
+    if not isinstance(t, torch.Tensor):
+        raise ValueError(f"{path}: expected a tensor, got {type(t).__name__}")
+    t = t.reshape(-1).long()
+    if t.numel() != num_mesh:
+        raise ValueError(f"{path}: {t.numel()} entries for a {num_mesh}-vertex mesh")
+    if t.numel() and (int(t.min()) < 0 or int(t.max()) >= world_size):
+        raise ValueError(f"{path}: ranks outside [0, {world_size})")
+    return t
+
+
 # ----------------------------------------------------------------------------- per rank
 @dataclass
 class EdgeSet:
@@ -294,6 +328,8 @@ def partition_graphcast_graph(g: GlobalGraphCastGraph, rank: int, world_size: in
                               group=None) -> DistributedGraphCastGraph:
     """Per-rank view (collective when ``world_size > 1``). Local vertices keep increasing
     global-id order."""
+    if mesh_part is not None and grid_part is None:
+        grid_part = grid_placement_from_mesh(g, mesh_part)
     if grid_part is None or mesh_part is None:
         grid_part, mesh_part = latitude_partition(g, world_size)
     m_src, m_dst = g.m2m

@@ -26,7 +26,8 @@ import torch
 import torch.distributed as dist
 
 from .. import Communicator
-from ..data.graphcast_graph import build_global_graph, partition_graphcast_graph
+from ..data.graphcast_graph import (build_global_graph, load_mesh_placement,
+                                   partition_graphcast_graph)
 from ..data.weather import SyntheticWeatherDataset
 from ..models.graphcast import Config, DGraphCast
 from ..parallel.grad_sync import GradSync
@@ -57,7 +58,8 @@ def _device() -> torch.device:
 
 class GraphCastTrainer:
     def __init__(self, comm, cfg: Optional[Config] = None, dtype: torch.dtype = torch.float32,
-                 checkpoint_dir: Optional[str] = None, global_graph=None, support=None):
+                 checkpoint_dir: Optional[str] = None, global_graph=None, support=None,
+                 mesh_vertex_placement: Optional[str] = None):
         self.comm = comm
         self.cfg = cfg or Config()
         self.device = _device()
@@ -69,7 +71,13 @@ class GraphCastTrainer:
         part = comm.partition
         self.replica, self.num_replicas = ((part.partition_id, comm.get_world_size() // part.ranks_per_graph)
                                            if part is not None else (0, 1))
-        self.graph = partition_graphcast_graph(g, self.prank, self.psize,
+        mesh_part = None
+        if mesh_vertex_placement:
+            # the reference's mesh_vertex_rank_placement.pt (GraphCast/dataset.py:244); the
+            # grid placement follows it (data/graphcast_graph.grid_placement_from_mesh)
+            mesh_part = load_mesh_placement(mesh_vertex_placement, g.mesh_xyz.shape[0],
+                                            self.psize)
+        self.graph = partition_graphcast_graph(g, self.prank, self.psize, mesh_part=mesh_part,
                                                group=comm.group).to(self.device)
         self.dataset = SyntheticWeatherDataset(self.graph, self.cfg.data.num_channels_climate,
                                                self.cfg.data.num_samples_per_year_train)
@@ -159,7 +167,7 @@ def main(backend: str = "nccl", procs_per_graph: int = -1, iters: int = 10,
          mesh_level: int = 6, grid: str = "721x1440", hidden_dim: int = 128,
          processor_layers: int = 4, channels: int = 73, dtype: str = "fp32",
          checkpoint_dir: Optional[str] = None, test_run: bool = False, run_args=None,
-         log_dir: str = "logs"):
+         log_dir: str = "logs", mesh_vertex_placement: Optional[str] = None):
     rcfg = build_config(getattr(run_args, "config", ()), comm__backend=backend,
                         comm__ranks_per_graph=procs_per_graph, model__name="graphcast",
                         model__hidden=hidden_dim, model__num_layers=processor_layers,
@@ -180,7 +188,8 @@ def main(backend: str = "nccl", procs_per_graph: int = -1, iters: int = 10,
         support = RunSupport(run_args, rcfg, rcfg.data.dataset, comm.get_world_size(),
                              log_dir, _device())
     tr = GraphCastTrainer(comm, cfg, torch.bfloat16 if dtype == "bf16" else torch.float32,
-                          checkpoint_dir, support=support)
+                          checkpoint_dir, support=support,
+                          mesh_vertex_placement=mesh_vertex_placement)
     last = tr.train(1 if test_run else iters)
     return tr, last
 
@@ -198,6 +207,9 @@ def cli(argv=None):
     p.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
     p.add_argument("--test_run", action="store_true")
     p.add_argument("--log_dir", default="logs")
+    p.add_argument("--mesh_vertex_placement", default=None,
+                   help="mesh_vertex_rank_placement.pt: int tensor [V_mesh] of ranks (the "
+                        "reference's placement file; grid vertices follow their mesh source)")
     add_run_args(p)  # --checkpoint_dir: model_{iter}.pth (reference layout) + resumable state
     a = p.parse_args(argv)
     run_keys = ("config", "resume", "checkpoint_every", "metrics_jsonl", "checkpoint_dir")

@@ -101,7 +101,7 @@ def _small_cfg():
     return cfg
 
 
-def _gc_dist(rank, world, out_dir):
+def _gc_dist(rank, world, out_dir, placement=None):
     import torch.distributed as dist
 
     from dgraph_amd import Communicator
@@ -111,7 +111,15 @@ def _gc_dist(rank, world, out_dir):
     comm = Communicator.init_process_group("nccl")
     try:
         g = build_global_graph(2, (19, 36))
-        pg = partition_graphcast_graph(g, rank, world, group=comm.group)
+        mesh_part = None
+        if placement is not None:
+            from dgraph_amd.data.graphcast_graph import load_mesh_placement
+
+            mesh_part = load_mesh_placement(placement, g.mesh_xyz.shape[0], world)
+        pg = partition_graphcast_graph(g, rank, world, mesh_part=mesh_part, group=comm.group)
+        if mesh_part is not None:
+            assert torch.equal(pg.mesh_global_ids.sort().values,
+                               torch.nonzero(mesh_part == rank).reshape(-1))
         ds = SyntheticWeatherDataset(pg, num_channels=5, num_samples_per_year=3)
         x, y = ds[0]
         torch.manual_seed(0)
@@ -130,7 +138,8 @@ def _gc_dist(rank, world, out_dir):
         gn = torch.stack([p.grad.norm() if p.grad is not None else torch.zeros((), dtype=torch.float64)
                           for p in model.parameters()])
         if rank == 0:
-            torch.save({"out": full, "loss": gl, "gn": gn}, f"{out_dir}/gc_w{world}.pt")
+            tag = "p" if placement is not None else ""
+            torch.save({"out": full, "loss": gl, "gn": gn}, f"{out_dir}/gc_w{world}{tag}.pt")
     finally:
         comm.destroy()
 
@@ -152,3 +161,31 @@ def test_mlp_reference_layout():
     names = [k for k, _ in m.named_parameters()]
     assert names == ["_model.0.weight", "_model.0.bias", "_model.2.weight", "_model.2.bias",
                      "_model.4.weight", "_model.4.bias", "_model.5.weight", "_model.5.bias"]
+
+
+def test_graphcast_mesh_placement_file(ranks, tmp_path):
+    """A reference-style ``mesh_vertex_rank_placement.pt`` (random, non-contiguous ranks)
+    drives the partition (grid vertices follow their mesh2grid source) and reproduces W=1."""
+    from dgraph_amd.data.graphcast_graph import grid_placement_from_mesh
+
+    d = str(tmp_path)
+    g = build_global_graph(2, (19, 36))
+    world = 3
+    place = torch.randint(0, world, (g.mesh_xyz.shape[0],), generator=torch.Generator().manual_seed(1))
+    path = f"{d}/mesh_vertex_rank_placement.pt"
+    torch.save(place.int(), path)
+    gp = grid_placement_from_mesh(g, place)
+    assert gp.numel() == 19 * 36 and int(gp.max()) < world
+    ranks(_gc_dist, 1, d)
+    ranks(_gc_dist, world, d, path)
+    r1 = torch.load(f"{d}/gc_w1.pt", weights_only=True)
+    rp = torch.load(f"{d}/gc_w{world}p.pt", weights_only=True)
+    torch.testing.assert_close(rp["out"], r1["out"])
+    torch.testing.assert_close(rp["loss"], r1["loss"])
+    torch.testing.assert_close(rp["gn"], r1["gn"])
+    bad = f"{d}/bad.pt"
+    torch.save(torch.full((g.mesh_xyz.shape[0],), world), bad)
+    from dgraph_amd.data.graphcast_graph import load_mesh_placement
+
+    with pytest.raises(ValueError):
+        load_mesh_placement(bad, g.mesh_xyz.shape[0], world)
