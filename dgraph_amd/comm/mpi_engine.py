@@ -53,7 +53,8 @@ class MPIBackendEngine(BackendEngine):
         if mw is not None and "RANK" not in os.environ:
             os.environ["RANK"], os.environ["WORLD_SIZE"] = str(mw[0]), str(mw[1])
             os.environ.setdefault("LOCAL_RANK", str(mw[0]))
-        self._owns_pg = ensure_process_group(kwargs.pop("backend", None), **kwargs)
+        pgb = kwargs.pop("pg_backend", None)
+        self._owns_pg = ensure_process_group(pgb or kwargs.pop("backend", None), **kwargs)
         if dist.get_backend() != "gloo" and dist.get_world_size() > 1:
             self._cpu_group = dist.new_group(backend="gloo")
         MPIBackendEngine._is_initialized = True

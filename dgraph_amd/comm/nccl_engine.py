@@ -38,7 +38,7 @@ class NCCLBackendEngine(BackendEngine):
 
     # ------------------------------------------------------------------ setup
     def init_process_group(self, ranks_per_graph: int = -1, *args, **kwargs):
-        backend = kwargs.pop("backend", None)
+        backend = kwargs.pop("pg_backend", None) or kwargs.pop("backend", None)
         NCCLBackendEngine._owns_pg = ensure_process_group(backend or "nccl", **kwargs)
         NCCLBackendEngine._groups = make_partition_groups(ranks_per_graph)
         NCCLBackendEngine._is_initialized = True

@@ -40,7 +40,8 @@ class ROCSHMEMBackendEngine(BackendEngine):
         self.init_process_group(ranks_per_graph, **kwargs)
 
     def init_process_group(self, ranks_per_graph: int = -1, **kwargs):
-        self._owns_pg = ensure_process_group(kwargs.pop("backend", None), **kwargs)
+        pgb = kwargs.pop("pg_backend", None)
+        self._owns_pg = ensure_process_group(pgb or kwargs.pop("backend", None), **kwargs)
         self._groups = make_partition_groups(ranks_per_graph)
         ROCSHMEMBackendEngine._ranks_per_graph = self._groups.ranks_per_graph
         ROCSHMEMBackendEngine._partition_num = self._groups.partition_id
