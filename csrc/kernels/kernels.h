@@ -208,8 +208,9 @@ hipError_t gemm_f32(const float* A1, int64_t lda1, int64_t K1, const float* B1, 
 bool wgrad_f32_supported(int64_t K, int64_t N);
 hipError_t wgrad_f32(const float* A1, int64_t lda1, int64_t K1, const float* A2, int64_t lda2,
                      int64_t K2, const int64_t* a1_rows, const float* G, int64_t ldg,
-                     int64_t M, int64_t N, float* partials, int P, bool accumulate,
+                     int64_t M, int64_t N, float* partials, int P, int fresh_from,
                      hipStream_t st);
+// (P blocks run; block b adds into slab b when b < fresh_from, else overwrites it)
 hipError_t wgrad_f32_reduce(const float* partials, int P, int64_t KN, float* out,
                             hipStream_t st);
 // 1-bit ReLU keep masks of selected rows (bits.hip): F % 32 == 0, F/32 words per row.

@@ -5,11 +5,11 @@
 // The GraphSAGE weight gradients x^T g and agg^T g reduce over 10^7 - 10^8 vertex rows
 // into a 256 x 256 output: a library GEMM gets only (K/tile) x (N/tile) output tiles, i.e.
 // a handful of workgroups for 256 CUs. Here the REDUCTION is split: a persistent grid of
-// P blocks (one per CU), block b owns a contiguous range of rows and accumulates the whole
-// [K, N] product in MFMA accumulators (8 waves x TM x TN 16x16 tiles), then writes (or adds
-// to) its private fp32 partial slab partials[b]. wgrad_f32_reduce sums the P slabs in block
-// order — deterministic for a fixed M and P, and the slabs can accumulate over several
-// calls (row chunks of one step) before the single reduce.
+// P blocks (at most one per CU, fewer for short inputs: >= 2048 rows each), block b owns a
+// contiguous range of rows and accumulates the whole [K, N] product in MFMA accumulators
+// (8 waves x TM x TN 16x16 tiles), then writes (or adds to) its private fp32 partial slab
+// partials[b]. wgrad_f32_reduce sums the slabs in block order — deterministic for a fixed
+// sequence of calls, which can accumulate over row chunks of one step before the reduce.
 // Data flow per 32-row stage: A and G rows -> registers (issued one stage ahead) -> padded
 // LDS [32][K+4] / [32][N+4]; MFMA step j uses rows 8h + j (lane group h = lane >> 4) of both
 // (the k-slot permutation of gemm_f32.hip, here over the reduced row index).
@@ -44,7 +44,7 @@ __global__ __launch_bounds__(kThr, 1) void wgrad_f32_kernel(
     const float* __restrict__ A1, int64_t lda1, int K1, const float* __restrict__ A2,
     int64_t lda2, const int64_t* __restrict__ a1_rows, const float* __restrict__ G,
     int64_t ldg, int64_t M, int64_t rows_per_block, float* __restrict__ partials,
-    bool accumulate) {
+    int fresh_from) {
   using C = WCfg<K, N>;
   constexpr int TM = C::TM, TN = C::TN, WN = C::WN;
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -163,7 +163,9 @@ __global__ __launch_bounds__(kThr, 1) void wgrad_f32_kernel(
 #pragma unroll
       for (int b = 0; b < TN; ++b) {
         float* p = slab + k * N + nw + b * 16 + li;
-        *p = accumulate ? *p + acc[a][b][r] : acc[a][b][r];
+        // slabs below fresh_from hold this step's earlier calls: accumulate; the rest are
+        // written fresh (a call may use fewer blocks than an earlier one)
+        *p = static_cast<int>(blockIdx.x) < fresh_from ? *p + acc[a][b][r] : acc[a][b][r];
       }
     }
 }
@@ -181,7 +183,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
 template <int K, int N>
 hipError_t launch_wgrad(const float* A1, int64_t lda1, int K1, const float* A2, int64_t lda2,
                         const int64_t* a1_rows, const float* G, int64_t ldg, int64_t M,
-                        float* partials, int P, bool accumulate, hipStream_t st) {
+                        float* partials, int P, int fresh_from, hipStream_t st) {
   using C = WCfg<K, N>;
   auto kern = &wgrad_f32_kernel<K, N>;
   static_assert(C::BYTES <= 160 * 1024, "LDS budget");
@@ -195,7 +197,7 @@ hipError_t launch_wgrad(const float* A1, int64_t lda1, int K1, const float* A2, 
   int64_t rpb = (M + P - 1) / P;
   rpb = (rpb + kRows - 1) / kRows * kRows;
   hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(P)), dim3(kThr), C::BYTES, st, A1, lda1,
-                     K1, A2, lda2, a1_rows, G, ldg, M, rpb, partials, accumulate);
+                     K1, A2, lda2, a1_rows, G, ldg, M, rpb, partials, fresh_from);
   return hipGetLastError();
 }
 
@@ -209,7 +211,7 @@ bool wgrad_f32_supported(int64_t K, int64_t N) {
 
 hipError_t wgrad_f32(const float* A1, int64_t lda1, int64_t K1, const float* A2, int64_t lda2,
                      int64_t K2, const int64_t* a1_rows, const float* G, int64_t ldg,
-                     int64_t M, int64_t N, float* partials, int P, bool accumulate,
+                     int64_t M, int64_t N, float* partials, int P, int fresh_from,
                      hipStream_t st) {
   const int64_t K = K1 + (A2 ? K2 : 0);
   if (!wgrad_f32_supported(K, N) || P <= 0) return hipErrorInvalidValue;
@@ -220,7 +222,7 @@ hipError_t wgrad_f32(const float* A1, int64_t lda1, int64_t K1, const float* A2,
 #define DG_WG(K_, N_)                                                                      \
   if (K == K_ && N == N_)                                                                  \
     return launch_wgrad<K_, N_>(A1, lda1, k1, A2, lda2, a1_rows, G, ldg, M, partials, P,  \
-                                accumulate, st);
+                                fresh_from, st);
   DG_WG(256, 256) DG_WG(256, 176) DG_WG(256, 192) DG_WG(256, 128)
   DG_WG(128, 256) DG_WG(128, 176) DG_WG(128, 192) DG_WG(128, 128)
 #undef DG_WG

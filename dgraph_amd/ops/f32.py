@@ -133,16 +133,24 @@ class WgradAcc:
         else:
             self.partials = torch.zeros(1, self.K, self.N, dtype=torch.float64)
         self.fresh = True
+        self.used = 0  # slabs written since reset
+
+    # rows per block of a short call (fewer blocks -> fewer partial slabs read/written)
+    MIN_ROWS_PER_BLOCK = 2048
 
     def reset(self):
         self.fresh = True
+        self.used = 0
 
     def add(self, A1: torch.Tensor, G: torch.Tensor, A2: Optional[torch.Tensor] = None,
             a1_rows: Optional[torch.Tensor] = None) -> None:
         if G.shape[0] == 0:
             return
         if self.device.type == "cuda":
-            _native.ops().wgrad_f32(A1, A2, a1_rows, G, self.partials, not self.fresh)
+            P = self.partials.shape[0]
+            nb = max(1, min(P, -(-G.shape[0] // self.MIN_ROWS_PER_BLOCK)))
+            _native.ops().wgrad_f32(A1, A2, a1_rows, G, self.partials, nb, self.used)
+            self.used = max(self.used, nb)
         else:
             M = G.shape[0]
             a = A1.double()[a1_rows.long()] if a1_rows is not None else A1[:M].double()
@@ -161,7 +169,7 @@ class WgradAcc:
         if self.fresh:
             return out.zero_()
         if self.device.type == "cuda":
-            _native.ops().wgrad_f32_reduce(self.partials, out)
+            _native.ops().wgrad_f32_reduce(self.partials[: self.used], out)
         else:
             out.copy_(self.partials[0].to(out.dtype))
         return out
