@@ -68,7 +68,7 @@ class _Pipe:
     with the current stream waiting for the side stream."""
 
     def __init__(self, dev):
-        self.cuda = dev.type == "cuda"
+        self.cuda = dev.type == "cuda" and os.environ.get("DGRAPH_FUSED_PIPELINE", "1") != "0"
         if self.cuda:
             self.side = torch.cuda.Stream(dev)
             self.ready = [torch.cuda.Event() for _ in range(2)]
@@ -171,18 +171,25 @@ class FusedSAGE:
         self.haloT = graph.halo.transpose() if graph.halo is not None else None
         self.send_st = graph.send_map.transpose_csr().compact_rows() \
             if graph.halo is not None else None
+        # entries of the S-row aggregation (B1a), counted on the host once
+        self.nnz_S = int((self.it.rowptr[S + 1] - self.it.rowptr[S]).sum())
+        if self.halo is not None:
+            self.nnz_S += int((self.halo.rowptr[S + 1] - self.halo.rowptr[S]).sum())
         # ---- chunking
         free = torch.cuda.mem_get_info(dev)[0] if dev.type == "cuda" else (64 << 30)
         need_h = (self.nl - 1) * L * self.hid * 4
         self.store_sep = 2 * self.nS > L   # dZ and u do not fit in the last hidden buffer
         if self.store_sep:
             need_h += 2 * self.nS * self.hid * 4
-        spare = max(free - need_h - (6 << 30), 1 << 30)
+        nT = self.T.numel()
+        other = 4 * nT * (self.Cg + self.hid) + 4 * self.nS * (self.hid // 32) + \
+            5 * 4 * 256 * 256 * 256 + (2 << 30)  # dz, u_out, bits, wgrad slabs, slack
+        spare = max(free - need_h - other, 1 << 29)
         cr = chunk_rows or CHUNK_ROWS
         if cr <= 0:
-            # two aggregate + two logit/gradient chunk buffers, and the GEMM's own slack
+            # two aggregate + two logit/gradient chunk buffers (pipelined)
             per_row = 4 * 2 * (max(self.hid, self.d0) + max(self.Cp, self.hid))
-            cr = int(min(max(spare * 2 // 3 // per_row, 1 << 16), 1 << 21))
+            cr = int(min(max(spare // per_row, 1 << 16), 1 << 21))
         self.cr = max(256, min(int(cr), max(L, 256)))
         self.chunks = _ranges(L, self.cr)
         self.s_chunks = _ranges(self.nS, self.cr)
@@ -224,10 +231,6 @@ class FusedSAGE:
         self.acc_hid_s = F32.WgradAcc(self.hid if self.nl == 3 else self.d0, self.hid, dev)
         self.acc_hid_n = F32.WgradAcc(self.hid if self.nl == 3 else self.d0, self.hid, dev)
         self.acc_in = F32.WgradAcc(2 * self.d0, self.hid, dev) if self.nl == 3 else None
-        # entries of the S-row aggregation (B1a), counted on the host once
-        self.nnz_S = int(self.it.degree()[S].sum())
-        if self.halo is not None:
-            self.nnz_S += int(self.halo.degree()[S].sum())
         self.loss = torch.zeros((), **f)
         self.correct = torch.zeros(2, dtype=torch.long, device=dev)
         self.record = False
