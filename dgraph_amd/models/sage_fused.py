@@ -182,13 +182,16 @@ class FusedSAGE:
         if self.store_sep:
             need_h += 2 * self.nS * self.hid * 4
         nT = self.T.numel()
-        other = 4 * nT * (self.Cg + self.hid) + 4 * self.nS * (self.hid // 32) + \
-            5 * 4 * 256 * 256 * 256 + (2 << 30)  # dz, u_out, bits, wgrad slabs, slack
-        spare = max(free - need_h - other, 1 << 29)
+        # dz rows, wgrad slabs, (u_out when it cannot live in the last hidden buffer) and
+        # allocator / temporary slack; the chunk arena gets the rest
+        self.u_sep = 2 * self.nS + nT > L
+        other = 4 * nT * self.Cg + 5 * 4 * 256 * 256 * 256 + (3 << 29) + \
+            (4 * nT * self.hid if self.u_sep else 0)
+        spare = max(free - need_h - other, 1 << 28)
+        wA, wB = max(self.hid, self.d0), max(self.Cp, self.hid)
+        per_row = 4 * 2 * (wA + wB)  # two aggregate + two logit/gradient chunk buffers
         cr = chunk_rows or CHUNK_ROWS
         if cr <= 0:
-            # two aggregate + two logit/gradient chunk buffers (pipelined)
-            per_row = 4 * 2 * (max(self.hid, self.d0) + max(self.Cp, self.hid))
             cr = int(min(max(spare // per_row, 1 << 16), 1 << 21))
         self.cr = max(256, min(int(cr), max(L, 256)))
         self.chunks = _ranges(L, self.cr)
@@ -216,16 +219,29 @@ class FusedSAGE:
             n = self.nS * self.hid
             self.dZ = hl[:n].view(self.nS, self.hid)
             self.u = hl[n:2 * n].view(self.nS, self.hid) if self.nl == 3 else None
-        wA = max(self.hid, self.d0)
-        # two of each chunk buffer: chunk c+1's aggregation (memory-bound SpMM, producer
-        # stream) runs while chunk c's MFMA GEMMs (consumer stream) read the other one
-        self.bufA2 = [torch.empty(self.cr, wA, **f) for _ in range(2)]   # chunk aggregates
-        self.bufB2 = [torch.empty(self.cr, max(self.Cp, self.hid), **f) for _ in range(2)]
+        # ONE chunk arena: two of each chunk buffer (chunk c+1's aggregation, a memory-bound
+        # SpMM on the producer stream, runs while chunk c's MFMA GEMMs on the consumer
+        # stream read the other one) during the row-chunked passes, and the last hidden
+        # layer's keep bits (output-layer backward only, when no chunk buffer is live)
+        bits_words = self.nS * (self.hid // 32)
+        arena_fl = max(2 * self.cr * (wA + wB), bits_words)
+        self.arena = torch.empty(arena_fl, **f)
+        o = 0
+        self.bufA2, self.bufB2 = [], []
+        for w, lst in ((wA, self.bufA2), (wA, self.bufA2), (wB, self.bufB2), (wB, self.bufB2)):
+            lst.append(self.arena[o:o + self.cr * w].view(self.cr, w))
+            o += self.cr * w
         self.bufA, self.bufB = self.bufA2[0], self.bufB2[0]
+        self.bits = self.arena[:bits_words].view(torch.int32).view(self.nS, self.hid // 32)
         self.pipe = _Pipe(dev)
         self.dz = torch.zeros(self.T.numel(), self.Cg, **f)  # output-layer gradient rows
-        self.bits = torch.empty(self.nS, self.hid // 32, dtype=torch.int32, device=dev)
-        self.u_out = torch.empty(self.T.numel(), self.hid, **f)
+        # the output layer's projected gradient rows (B2 only): the last hidden buffer's tail,
+        # past dZ and u, is free by then
+        if self.u_sep:
+            self.u_out = torch.empty(nT, self.hid, **f)
+        else:
+            tail = self.h[-1].view(-1)[2 * self.nS * self.hid:]
+            self.u_out = tail[:nT * self.hid].view(nT, self.hid)
         self.acc_out_s = F32.WgradAcc(self.hid, self.Cg, dev)
         self.acc_out_n = F32.WgradAcc(self.hid, self.Cg, dev)
         self.acc_hid_s = F32.WgradAcc(self.hid if self.nl == 3 else self.d0, self.hid, dev)

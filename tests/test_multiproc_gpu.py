@@ -104,8 +104,8 @@ def _body(rank, world, kw, dt):
         lr = args.lr
         for a, b in zip(got["params"], ref["params"]):
             d = (a - b).abs()
-            assert float(d.max()) <= 3 * lr, float(d.max())
-            assert float((d > 1e-5).float().mean()) < 0.05, float((d > 1e-5).float().mean())
+            assert float(d.max()) <= 3 * lr, float(d.max())   # never more than the 3 steps
+            assert float(d.mean()) < 1e-3 * lr, float(d.mean())  # on average: rounding
         assert torch.equal(got["correct"], ref["correct"])
     else:
         # bf16 storage: W=2 sums interior and halo parts in another order and rounds the
