@@ -49,7 +49,9 @@ void spmm_f32_ex_op(const at::Tensor& rowptr, const at::Tensor& col,
                     const c10::optional<at::Tensor>& row_ids, const at::Tensor& x,
                     const at::Tensor& out, double beta, int64_t cap,
                     const c10::optional<at::Tensor>& row_map,
-                    const c10::optional<at::Tensor>& gate) {
+                    const c10::optional<at::Tensor>& gate,
+                    const c10::optional<at::Tensor>& self_add,
+                    const c10::optional<at::Tensor>& self_map, int64_t self_row0) {
   same_dev(rowptr, x, "rowptr");
   same_dev(col, x, "col");
   same_dev(out, x, "out");
@@ -99,12 +101,34 @@ void spmm_f32_ex_op(const at::Tensor& rowptr, const at::Tensor& col,
     gp = gt->data_ptr<float>();
     ldg = gt->stride(0);
   }
+  const float* sap = nullptr;
+  const int32_t* smp = nullptr;
+  int64_t lds = 0;
+  if (const at::Tensor* sa = opt(self_add)) {
+    f32_rows(*sa, "self_add");
+    same_dev(*sa, x, "self_add");
+    const at::Tensor* sm = opt(self_map);
+    TORCH_CHECK(sm != nullptr, "self_add needs self_map");
+    same_dev(*sm, x, "self_map");
+    TORCH_CHECK(sm->scalar_type() == at::kInt && sm->is_contiguous(),
+                "self_map must be contiguous int32");
+    TORCH_CHECK(sa->size(1) >= x.size(1) && sa->stride(0) % 4 == 0 &&
+                    reinterpret_cast<uintptr_t>(sa->data_ptr()) % 16 == 0,
+                "self_add must be 16-B aligned with row stride % 4 == 0, width >= F");
+    const int64_t max_out = rmap ? out.size(0) : nrows;
+    TORCH_CHECK(self_row0 >= 0 && self_row0 + max_out <= sm->numel(),
+                "self_map too short for self_row0 + output rows");
+    sap = sa->data_ptr<float>();
+    smp = sm->data_ptr<int32_t>();
+    lds = sa->stride(0);
+  }
   c10::DeviceGuard g(x.device());
   DG_HIP_CHECK(spmm_f32_rowgroup(col.scalar_type() == at::kInt ? IType::I32 : IType::I64,
                                  rowptr.data_ptr<int64_t>(), col.data_ptr(), ewp, csp, rsp, cm,
                                  rid, x.data_ptr<float>(), x.stride(0), out.data_ptr<float>(),
                                  out.stride(0), nrows, static_cast<int>(x.size(1)),
-                                 static_cast<float>(beta), cap, rmap, stream_of(x), gp, ldg));
+                                 static_cast<float>(beta), cap, rmap, stream_of(x), gp, ldg, sap,
+                                 lds, smp, self_row0));
 }
 
 void gemm_f32_op(const at::Tensor& A1, const at::Tensor& B1, const c10::optional<at::Tensor>& A2,
@@ -261,6 +285,50 @@ void apply_keep_bits_op(const at::Tensor& g, const at::Tensor& bits) {
                                g.size(0), F, stream_of(g)));
 }
 
+void xent_rows_op(const at::Tensor& z, const at::Tensor& rows, const at::Tensor& y,
+                  double scale, const at::Tensor& dz, const at::Tensor& row_loss, int64_t C) {
+  f32_rows(z, "z");
+  f32_rows(dz, "dz");
+  same_dev(rows, z, "rows");
+  same_dev(y, z, "y");
+  same_dev(dz, z, "dz");
+  same_dev(row_loss, z, "row_loss");
+  const int64_t n = rows.numel();
+  TORCH_CHECK(rows.scalar_type() == at::kLong && rows.is_contiguous() &&
+                  y.scalar_type() == at::kLong && y.is_contiguous() && y.numel() == n,
+              "rows / y must be contiguous int64 of equal length");
+  TORCH_CHECK(C > 0 && C <= 256 && C <= z.size(1) && dz.size(1) >= C && dz.size(1) <= 256 &&
+                  dz.size(0) >= n,
+              "xent_rows: C <= 256, z and dz at least C wide, dz >= n rows");
+  TORCH_CHECK(row_loss.scalar_type() == at::kFloat && row_loss.is_contiguous() &&
+                  row_loss.numel() >= n,
+              "row_loss must be contiguous float32 with >= n entries");
+  c10::DeviceGuard g(z.device());
+  DG_HIP_CHECK(xent_rows(z.data_ptr<float>(), z.stride(0), static_cast<int>(C),
+                         rows.data_ptr<int64_t>(), y.data_ptr<int64_t>(), n,
+                         static_cast<float>(scale), dz.data_ptr<float>(), dz.stride(0),
+                         static_cast<int>(dz.size(1)), row_loss.data_ptr<float>(), stream_of(z)));
+}
+
+void argmax_hits_op(const at::Tensor& z, const at::Tensor& rows, const at::Tensor& y,
+                    const at::Tensor& hit, int64_t C) {
+  f32_rows(z, "z");
+  same_dev(rows, z, "rows");
+  same_dev(y, z, "y");
+  same_dev(hit, z, "hit");
+  const int64_t n = rows.numel();
+  TORCH_CHECK(rows.scalar_type() == at::kLong && rows.is_contiguous() &&
+                  y.scalar_type() == at::kLong && y.is_contiguous() && y.numel() == n,
+              "rows / y must be contiguous int64 of equal length");
+  TORCH_CHECK(hit.scalar_type() == at::kByte && hit.is_contiguous() && hit.numel() >= n,
+              "hit must be contiguous uint8 with >= n entries");
+  TORCH_CHECK(C > 0 && C <= 256 && C <= z.size(1), "argmax_hits: 0 < C <= 256, C <= width");
+  c10::DeviceGuard g(z.device());
+  DG_HIP_CHECK(argmax_hits(z.data_ptr<float>(), z.stride(0), static_cast<int>(C),
+                           rows.data_ptr<int64_t>(), y.data_ptr<int64_t>(), n,
+                           hit.data_ptr<uint8_t>(), stream_of(z)));
+}
+
 void set_spmm_f32_config_op(int64_t rowgroup, int64_t pass_cols) {
   set_spmm_f32_config(static_cast<int>(rowgroup), static_cast<int>(pass_cols));
 }
@@ -273,7 +341,8 @@ TORCH_LIBRARY_FRAGMENT(dgraph_amd, m) {
         &dgraph::set_spmm_f32_config_op);
   m.def("spmm_f32_ex(Tensor rowptr, Tensor col, Tensor? edge_weight, Tensor? col_scale, "
         "Tensor? row_scale, Tensor? col_map, Tensor? row_ids, Tensor x, Tensor(a!) out, "
-        "float beta=0., int cap=0, Tensor? row_map=None, Tensor? gate=None) -> ()");
+        "float beta=0., int cap=0, Tensor? row_map=None, Tensor? gate=None, "
+        "Tensor? self_add=None, Tensor? self_map=None, int self_row0=0) -> ()");
   m.def("gemm_f32(Tensor A1, Tensor B1, Tensor? A2, Tensor? B2, Tensor? a_rows, Tensor? bias, "
         "Tensor? cin, float beta, Tensor? gate, Tensor? o_rows, bool relu, Tensor(a!) out, "
         "Tensor? row_scale=None) -> ()");
@@ -282,6 +351,9 @@ TORCH_LIBRARY_FRAGMENT(dgraph_amd, m) {
   m.def("wgrad_f32_reduce(Tensor partials, Tensor(a!) out) -> ()");
   m.def("row_keep_bits(Tensor h, Tensor? rows, Tensor(a!) bits) -> ()");
   m.def("apply_keep_bits(Tensor(a!) g, Tensor bits) -> ()");
+  m.def("xent_rows(Tensor z, Tensor rows, Tensor y, float scale, Tensor(a!) dz, "
+        "Tensor(b!) row_loss, int C) -> ()");
+  m.def("argmax_hits(Tensor z, Tensor rows, Tensor y, Tensor(a!) hit, int C) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(dgraph_amd, CUDA, m) {
@@ -291,4 +363,6 @@ TORCH_LIBRARY_IMPL(dgraph_amd, CUDA, m) {
   m.impl("wgrad_f32_reduce", &dgraph::wgrad_f32_reduce_op);
   m.impl("row_keep_bits", &dgraph::row_keep_bits_op);
   m.impl("apply_keep_bits", &dgraph::apply_keep_bits_op);
+  m.impl("xent_rows", &dgraph::xent_rows_op);
+  m.impl("argmax_hits", &dgraph::argmax_hits_op);
 }

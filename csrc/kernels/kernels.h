@@ -46,8 +46,12 @@ hipError_t spmm_f32_rowgroup(IType it, const int64_t* rowptr, const void* col,
                              const int32_t* col_map, const int64_t* row_ids, const float* x,
                              int64_t ldx, float* out, int64_t ldo, int64_t nrows, int F,
                              float beta, int64_t cap, const int64_t* row_map,
-                             hipStream_t st, const float* gate = nullptr, int64_t ldgate = 0);
-// gate (nullable, indexed like out): the stored value is kept where gate > 0, else 0
+                             hipStream_t st, const float* gate = nullptr, int64_t ldgate = 0,
+                             const float* self_add = nullptr, int64_t ld_self = 0,
+                             const int32_t* self_map = nullptr, int64_t self_row0 = 0);
+// self_add (nullable): output row o also gets self_add[self_map[self_row0 + o]] (skipped
+// when < 0) after the row scale / beta and before the gate; gate (nullable, indexed like
+// out): the stored value is kept where gate > 0, else 0
 void set_spmm_f32_pass_cols(int cols);
 // rowgroup: 1 = fp32 row-group kernel (default), 0 = generic kernels; pass_cols: column
 // pass width (0 = default 64); negative arguments leave a setting unchanged
@@ -218,6 +222,15 @@ hipError_t row_keep_bits(const float* h, int64_t ldh, const int64_t* rows, int64
                          uint32_t* bits, hipStream_t st);
 hipError_t apply_keep_bits(float* g, int64_t ldg, const uint32_t* bits, int64_t n, int F,
                            hipStream_t st);
+
+// Softmax cross-entropy / argmax of selected logit rows (loss.hip), C <= 256:
+//   row_loss[i] = lse(z[rows[i]]) - z[rows[i]][y[i]];  dz[i][c] = (p_c - [c == y]) * scale
+//   for c < C and 0 for C <= c < dz_width;  hit[i] = (argmax z[rows[i]] == y[i])
+hipError_t xent_rows(const float* z, int64_t ldz, int C, const int64_t* rows, const int64_t* y,
+                     int64_t n, float scale, float* dz, int64_t ldd, int dz_width,
+                     float* row_loss, hipStream_t st);
+hipError_t argmax_hits(const float* z, int64_t ldz, int C, const int64_t* rows,
+                       const int64_t* y, int64_t n, uint8_t* hit, hipStream_t st);
 
 // 1 = column-half kernel (dual_gemm.hip), 2 = B-stationary (default); < 0 restores it
 void set_dual_gemm_variant(int variant);

@@ -34,7 +34,9 @@ __global__ __launch_bounds__(256) void spmm_f32_rowgroup_kernel(
     const float* __restrict__ row_scale, const int32_t* __restrict__ col_map,
     const int64_t* __restrict__ row_ids, const float* __restrict__ x, int64_t ldx,
     float* __restrict__ out, int64_t ldo, int64_t nrows, int F, float beta, int cap,
-    const int64_t* __restrict__ row_map, const float* __restrict__ gate, int64_t ldgate) {
+    const int64_t* __restrict__ row_map, const float* __restrict__ gate, int64_t ldgate,
+    const float* __restrict__ self_add, int64_t ld_self, const int32_t* __restrict__ self_map,
+    int64_t self_row0) {
   constexpr int VEC = 4;
   constexpr int G = kWave / LPR;
   constexpr int U = LPR < 8 ? LPR : 8;  // neighbour rows in flight per lane per batch
@@ -139,6 +141,16 @@ __global__ __launch_bounds__(256) void spmm_f32_rowgroup_kernel(
         res.z = acc[1].x * rs;
         res.w = acc[1].y * rs;
       }
+      if (self_add) {  // + the row's own term, stored row-compacted (row-uniform branch)
+        const int32_t m = self_map[self_row0 + orow];
+        if (m >= 0) {
+          const float4 sv = *reinterpret_cast<const float4*>(self_add + m * ld_self + f);
+          res.x += sv.x;
+          res.y += sv.y;
+          res.z += sv.z;
+          res.w += sv.w;
+        }
+      }
       if (gate) {  // ReLU derivative from a stored activation (row-uniform branch)
         const float4 gv = *reinterpret_cast<const float4*>(gate + orow * ldgate + f);
         res.x = gv.x > 0.f ? res.x : 0.f;
@@ -157,7 +169,8 @@ hipError_t launch_f32_rg(const int64_t* rowptr, const IdxT* col, const float* ew
                          const int64_t* rids, const float* x, int64_t ldx, float* out,
                          int64_t ldo, int64_t nrows, int F, float beta, int icap,
                          const int64_t* row_map, const float* gate, int64_t ldgate,
-                         hipStream_t st) {
+                         const float* sadd, int64_t ld_self, const int32_t* smap,
+                         int64_t srow0, hipStream_t st) {
   const int lanes = (F + 3) / 4;
   const int LPR = lanes <= 8 ? 8 : lanes <= 16 ? 16 : lanes <= 32 ? 32 : 64;
   const int64_t G = kWave / LPR;
@@ -170,7 +183,7 @@ hipError_t launch_f32_rg(const int64_t* rowptr, const IdxT* col, const float* ew
   if (LPR == LPR_ && wmode == W_) {                                                       \
     hipLaunchKernelGGL((spmm_f32_rowgroup_kernel<IdxT, LPR_, W_, CMAP>), grid, block, 0, \
                        st, rowptr, col, ew, cs, rs, cmap, rids, x, ldx, out, ldo, nrows,  \
-                       F, beta, icap, row_map, gate, ldgate);                             \
+                       F, beta, icap, row_map, gate, ldgate, sadd, ld_self, smap, srow0);  \
     return hipGetLastError();                                                             \
   }
 #define DG_F32(LPR_) DG_F32_W(LPR_, 0) DG_F32_W(LPR_, 1) DG_F32_W(LPR_, 2) DG_F32_W(LPR_, 3)
@@ -202,8 +215,12 @@ hipError_t spmm_f32_rowgroup(IType it, const int64_t* rowptr, const void* col,
                              const int32_t* col_map, const int64_t* row_ids, const float* x,
                              int64_t ldx, float* out, int64_t ldo, int64_t nrows, int F,
                              float beta, int64_t cap, const int64_t* row_map,
-                             hipStream_t st, const float* gate, int64_t ldgate) {
+                             hipStream_t st, const float* gate, int64_t ldgate,
+                             const float* self_add, int64_t ld_self, const int32_t* self_map,
+                             int64_t self_row0) {
   if (nrows <= 0 || F <= 0) return hipSuccess;
+  if (self_add && (!self_map || (reinterpret_cast<uintptr_t>(self_add) & 15) || ld_self % 4))
+    return hipErrorInvalidValue;
   if (gate && ((reinterpret_cast<uintptr_t>(gate) & 15) || ldgate % 4)) return hipErrorInvalidValue;
   if (!spmm_f32_rowgroup_ok(F, ldx, ldo, x, out)) return hipErrorInvalidValue;
   const int icap = (cap > 0 && cap < (int64_t(1) << 30)) ? static_cast<int>(cap) : (1 << 30);
@@ -217,21 +234,29 @@ hipError_t spmm_f32_rowgroup(IType it, const int64_t* rowptr, const void* col,
       err = col_map ? launch_f32_rg<int32_t, true>(rowptr, cp, ew, col_scale, row_scale,
                                                    col_map, row_ids, x + c0, ldx, out + c0,
                                                    ldo, nrows, w, beta, icap, row_map,
-                                                   gate ? gate + c0 : nullptr, ldgate, st)
+                                                   gate ? gate + c0 : nullptr, ldgate,
+                                                   self_add ? self_add + c0 : nullptr, ld_self,
+                                                   self_map, self_row0, st)
                     : launch_f32_rg<int32_t, false>(rowptr, cp, ew, col_scale, row_scale,
                                                     nullptr, row_ids, x + c0, ldx, out + c0,
                                                     ldo, nrows, w, beta, icap, row_map,
-                                                   gate ? gate + c0 : nullptr, ldgate, st);
+                                                   gate ? gate + c0 : nullptr, ldgate,
+                                                   self_add ? self_add + c0 : nullptr, ld_self,
+                                                   self_map, self_row0, st);
     } else {
       const auto* cp = static_cast<const int64_t*>(col);
       err = col_map ? launch_f32_rg<int64_t, true>(rowptr, cp, ew, col_scale, row_scale,
                                                    col_map, row_ids, x + c0, ldx, out + c0,
                                                    ldo, nrows, w, beta, icap, row_map,
-                                                   gate ? gate + c0 : nullptr, ldgate, st)
+                                                   gate ? gate + c0 : nullptr, ldgate,
+                                                   self_add ? self_add + c0 : nullptr, ld_self,
+                                                   self_map, self_row0, st)
                     : launch_f32_rg<int64_t, false>(rowptr, cp, ew, col_scale, row_scale,
                                                     nullptr, row_ids, x + c0, ldx, out + c0,
                                                     ldo, nrows, w, beta, icap, row_map,
-                                                   gate ? gate + c0 : nullptr, ldgate, st);
+                                                   gate ? gate + c0 : nullptr, ldgate,
+                                                   self_add ? self_add + c0 : nullptr, ld_self,
+                                                   self_map, self_row0, st);
     }
     if (err != hipSuccess) return err;
   }

@@ -175,8 +175,14 @@ class FusedSAGE:
         self.nnz_S = int((self.it.rowptr[S + 1] - self.it.rowptr[S]).sum())
         if self.halo is not None:
             self.nnz_S += int((self.halo.rowptr[S + 1] - self.halo.rowptr[S]).sum())
-        # ---- chunking
-        free = torch.cuda.mem_get_info(dev)[0] if dev.type == "cuda" else (64 << 30)
+        # ---- chunking (the planning above left cached temporaries: return them first, and
+        # count what the caching allocator still holds unused as free)
+        if dev.type == "cuda":
+            torch.cuda.empty_cache()
+            free = torch.cuda.mem_get_info(dev)[0] + \
+                torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
+        else:
+            free = 64 << 30
         need_h = (self.nl - 1) * L * self.hid * 4
         self.store_sep = 2 * self.nS > L   # dZ and u do not fit in the last hidden buffer
         if self.store_sep:
@@ -242,12 +248,23 @@ class FusedSAGE:
         else:
             tail = self.h[-1].view(-1)[2 * self.nS * self.hid:]
             self.u_out = tail[:nT * self.hid].view(nT, self.hid)
+        self.v_self = None
+        if self.nl == 3:
+            n_used = (2 * self.nS + (0 if self.u_sep else nT)) * self.hid
+            if not self.store_sep and n_used + self.nS * self.hid <= L * self.hid:
+                self.v_self = self.h[-1].view(-1)[n_used:n_used + self.nS * self.hid].view(
+                    self.nS, self.hid)
+            elif dev.type != "cuda" or free - need_h > (4 * self.nS * self.hid + (8 << 30)):
+                self.v_self = torch.empty(self.nS, self.hid, **f)
+            # else: no room — the self term runs as a row-scattered GEMM per chunk
         self.acc_out_s = F32.WgradAcc(self.hid, self.Cg, dev)
         self.acc_out_n = F32.WgradAcc(self.hid, self.Cg, dev)
         self.acc_hid_s = F32.WgradAcc(self.hid if self.nl == 3 else self.d0, self.hid, dev)
         self.acc_hid_n = F32.WgradAcc(self.hid if self.nl == 3 else self.d0, self.hid, dev)
         self.acc_in = F32.WgradAcc(2 * self.d0, self.hid, dev) if self.nl == 3 else None
-        self.loss = torch.zeros((), **f)
+        self.row_loss = torch.zeros(nT, **f)
+        self.hit = torch.zeros(self.E.numel(), dtype=torch.uint8, device=dev)
+        self.E_val_l = self.E_val.long()
         self.correct = torch.zeros(2, dtype=torch.long, device=dev)
         self.record = False
         self._events: list = []
@@ -333,8 +350,6 @@ class FusedSAGE:
         dev = self.dev
         self._events = []
         self._mark("fwd_l0")
-        self.loss.zero_()
-        self.correct.zero_()
         nnz_it = self.it.nnz
         nnz_h = self.halo.nnz if self.halo is not None else 0
         # ---------------- forward: hidden layers
@@ -381,7 +396,11 @@ class FusedSAGE:
         self.pipe.run(items, produce_out,
                       lambda ci, a, k: self._out_chunk(ci, a, k, hl, wsp, wnp, bp))
         self.edges_aggregated += nnz_it + nnz_h
-        loss = self.loss * self.inv_n
+        # per-row losses / hits summed once, in a fixed order
+        loss = self.row_loss.sum() * self.inv_n
+        hv = self.hit.long()
+        self.correct[0] = (hv * self.E_val_l).sum()
+        self.correct[1] = (hv * (1 - self.E_val_l)).sum()
         self._mark("bwd_out")
         return self._backward(P, halos, hl, hl_halo, loss, nnz_it, nnz_h)
 
@@ -394,23 +413,15 @@ class FusedSAGE:
         z = F32.gemm_f32(hl[r0:r1], wsp, a, wnp, bias=bp, out=self.bufB2[k][:n, :Cp])
         t0, t1 = self.ch_T[ci]
         if t1 > t0:
+            # one fused kernel: per-row loss and the scaled softmax gradient rows
             tl = self.ch_Tloc[ci]
-            zt = z.index_select(0, tl)[:, :C]
-            lse = torch.logsumexp(zt, 1)
-            y = self.yT[t0:t1]
-            self.loss += (lse - zt.gather(1, y.unsqueeze(1)).squeeze(1)).sum()
-            p = torch.exp(zt - lse.unsqueeze(1))
-            p.scatter_add_(1, y.unsqueeze(1), torch.full_like(lse, -1.0).unsqueeze(1))
             dzt = self.dz[t0:t1]
-            dzt[:, :C] = p * self.inv_n
+            F32.xent_rows(z, tl, self.yT[t0:t1], self.inv_n, dzt, self.row_loss[t0:t1], C)
             self.acc_out_s.add(hl, dzt, a1_rows=self.T[t0:t1])
             self.acc_out_n.add(a, dzt, a1_rows=tl)
         e0, e1 = self.ch_E[ci]
         if e1 > e0:
-            hit = z.index_select(0, self.ch_Eloc[ci])[:, :C].argmax(1) == self.yE[e0:e1]
-            iv = self.E_val[e0:e1]
-            self.correct[0] += (hit & iv).sum()
-            self.correct[1] += (hit & ~iv).sum()
+            F32.argmax_hits(z, self.ch_Eloc[ci], self.yE[e0:e1], self.hit[e0:e1], C)
 
     def _backward(self, P, halos, hl, hl_halo, loss, nnz_it, nnz_h):
         g, x, dev = self.g, self.x, self.dev
@@ -498,6 +509,9 @@ class FusedSAGE:
             db0s = []
             h1 = self.h[0]
             x_halo = halos[0]
+            # the support rows' own term dZ1 Ws1^T, once over S (one full-size GEMM instead
+            # of a row-scattered one per chunk); added by the aggregation's epilogue
+            v = F32.gemm_f32(dZ, ws1_t, out=self.v_self) if self.v_self is not None else None
 
             def produce_0(ci, k):
                 # memory-bound: the column-mapped transposed aggregation of u1 (gated by
@@ -506,7 +520,8 @@ class FusedSAGE:
                 n = r1 - r0
                 gz = self.bufB2[k][:n, :hid]
                 F32.spmm_f32(self.it.rowptr[r0:r1 + 1], self.it.col, u, gz, col_map=self.smap,
-                             gate=h1[r0:r1])
+                             gate=h1[r0:r1], self_add=v,
+                             self_map=self.smap if v is not None else None, self_row0=r0)
                 sr = self.ch_send[ci]
                 if work is not None and sr is not None:
                     rp, rmap, _ = sr
@@ -519,7 +534,7 @@ class FusedSAGE:
                 gz, a0 = ga
                 r0, r1 = self.chunks[ci]
                 s0, s1 = self.ch_S[ci]
-                if s1 > s0:
+                if v is None and s1 > s0:  # no room for v_self: scattered self term
                     F32.gemm_f32(dZ[s0:s1], ws1_t, cin=gz, o_rows=self.ch_Sloc[ci],
                                  gate=h1[r0:r1], out=gz)
                 self.acc_in.add(x[r0:r1], gz, A2=a0)

@@ -23,11 +23,14 @@ def spmm_f32(rowptr: torch.Tensor, col: torch.Tensor, x: torch.Tensor,
              edge_weight=None, col_map: Optional[torch.Tensor] = None,
              row_ids: Optional[torch.Tensor] = None, beta: float = 0.0,
              row_map: Optional[torch.Tensor] = None,
-             gate: Optional[torch.Tensor] = None) -> torch.Tensor:
+             gate: Optional[torch.Tensor] = None, self_add: Optional[torch.Tensor] = None,
+             self_map: Optional[torch.Tensor] = None, self_row0: int = 0) -> torch.Tensor:
     """``out[o(i)] = row_scale[o(i)] * sum_j w_j x[m(col_j)] + beta * out[o(i)]`` over the
     entries of CSR row ``row_ids[i]`` (all rows when None); ``m = col_map`` (entries with
     ``col_map < 0`` skipped) or identity; ``o = row_map`` or identity. ``gate`` (indexed
-    like ``out``): the stored value is kept where ``gate > 0`` (a ReLU derivative)."""
+    like ``out``): the stored value is kept where ``gate > 0`` (a ReLU derivative).
+    ``self_add``: output row o also gets ``self_add[self_map[self_row0 + o]]`` (when >= 0),
+    before the gate."""
     n = row_ids.numel() if row_ids is not None else rowptr.numel() - 1
     if out is None:
         if row_map is not None:
@@ -36,7 +39,8 @@ def spmm_f32(rowptr: torch.Tensor, col: torch.Tensor, x: torch.Tensor,
         beta = 0.0
     if x.is_cuda:
         _native.ops().spmm_f32_ex(rowptr, col, edge_weight, col_scale, row_scale, col_map,
-                                  row_ids, x, out, float(beta), 0, row_map, gate)
+                                  row_ids, x, out, float(beta), 0, row_map, gate, self_add,
+                                  self_map, int(self_row0))
         return out
     # CPU reference (fp64 accumulation)
     rp = rowptr.long()
@@ -66,6 +70,10 @@ def spmm_f32(rowptr: torch.Tensor, col: torch.Tensor, x: torch.Tensor,
         acc = acc * row_scale.double()[o].unsqueeze(1)
     if beta != 0.0:
         acc = acc + beta * out[o].double()
+    if self_add is not None:
+        m = self_map.long()[self_row0 + o]
+        add = self_add.double()[m.clamp_min(0)][:, :acc.shape[1]]
+        acc = acc + torch.where((m >= 0).unsqueeze(1), add, torch.zeros_like(add))
     if gate is not None:
         acc = torch.where(gate[o][:, :acc.shape[1]] > 0, acc, torch.zeros_like(acc))
     out[o] = acc.to(out.dtype)
@@ -206,3 +214,36 @@ def apply_keep_bits(g: torch.Tensor, bits: torch.Tensor) -> torch.Tensor:
     keep = ((w.unsqueeze(-1) >> torch.arange(32, dtype=torch.long)) & 1).view(n, F).bool()
     g.mul_(keep.to(g.dtype))
     return g
+
+
+# ------------------------------------------------------------------------------ loss
+def xent_rows(z: torch.Tensor, rows: torch.Tensor, y: torch.Tensor, scale: float,
+              dz: torch.Tensor, row_loss: torch.Tensor, C: int) -> None:
+    """Softmax cross-entropy of logit rows ``z[rows[i], :C]`` with labels ``y``:
+    ``row_loss[i] = lse - z_y``, ``dz[i, :C] = (softmax - onehot) * scale`` and
+    ``dz[i, C:] = 0`` (csrc/kernels/loss.hip)."""
+    n = rows.numel()
+    if n == 0:
+        return
+    if z.is_cuda:
+        _native.ops().xent_rows(z, rows, y, float(scale), dz, row_loss, int(C))
+        return
+    zt = z[rows.long()][:, :C].double()
+    lse = torch.logsumexp(zt, 1)
+    row_loss[:n] = (lse - zt.gather(1, y.long().unsqueeze(1)).squeeze(1)).to(row_loss.dtype)
+    p = torch.exp(zt - lse.unsqueeze(1))
+    p[torch.arange(n), y.long()] -= 1.0
+    dz[:n].zero_()
+    dz[:n, :C] = (p * scale).to(dz.dtype)
+
+
+def argmax_hits(z: torch.Tensor, rows: torch.Tensor, y: torch.Tensor, hit: torch.Tensor,
+                C: int) -> None:
+    """``hit[i] = (argmax z[rows[i], :C] == y[i])`` (first maximum), uint8."""
+    n = rows.numel()
+    if n == 0:
+        return
+    if z.is_cuda:
+        _native.ops().argmax_hits(z, rows, y, hit, int(C))
+        return
+    hit[:n] = (z[rows.long()][:, :C].argmax(1) == y.long()).to(hit.dtype)

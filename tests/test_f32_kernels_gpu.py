@@ -180,3 +180,52 @@ def test_hub_split_odd_width(F, dtype):
                  None, None, rs.cpu())
     tol = dict(atol=3e-2, rtol=2e-2) if dtype == torch.bfloat16 else dict(atol=1e-3, rtol=1e-4)
     torch.testing.assert_close(out.double().cpu(), ref, **tol)
+
+
+def test_spmm_f32_self_add_gate():
+    rp, col = _csr(300, 300, 7, 11)
+    g = torch.Generator().manual_seed(2)
+    F = 256
+    u = torch.randn(90, F, generator=g)
+    keep = torch.randperm(300, generator=g)[:90].sort().values
+    smap = torch.full((300,), -1, dtype=torch.int32)
+    smap[keep] = torch.arange(90, dtype=torch.int32)
+    v = torch.randn(90, F, generator=g)
+    gate = torch.randn(120, F, generator=g)
+    r0, r1 = 100, 220
+    ref = torch.empty(r1 - r0, F)
+    F32.spmm_f32(rp.cpu()[r0:r1 + 1], col.cpu(), u, ref, col_map=smap, gate=gate,
+                 self_add=v, self_map=smap, self_row0=r0)
+    out = torch.empty(r1 - r0, F, device=DEV)
+    F32.spmm_f32(rp[r0:r1 + 1], col, u.to(DEV), out, col_map=smap.to(DEV), gate=gate.to(DEV),
+                 self_add=v.to(DEV), self_map=smap.to(DEV), self_row0=r0)
+    torch.testing.assert_close(out.cpu(), ref, atol=2e-5, rtol=1e-5)
+    # the self term appears exactly on the rows that are in the support
+    rows = torch.arange(r0, r1)
+    m = smap[rows]
+    assert bool(((m >= 0) | (ref.abs().sum(1) >= 0)).all())
+
+
+@pytest.mark.parametrize("C,W", [(172, 192), (47, 64), (256, 256)])
+def test_xent_argmax_rows_vs_cpu(C, W):
+    g = torch.Generator().manual_seed(C)
+    z = torch.randn(500, 256, generator=g) * 3
+    rows = torch.randperm(500, generator=g)[:150]
+    y = torch.randint(0, C, (150,), generator=g)
+    dz = torch.full((150, W), 7.0)
+    rl = torch.zeros(150)
+    F32.xent_rows(z, rows, y, 0.5, dz, rl, C)
+    dzg = torch.full((150, W), 7.0, device=DEV)
+    rlg = torch.zeros(150, device=DEV)
+    F32.xent_rows(z.to(DEV), rows.to(DEV), y.to(DEV), 0.5, dzg, rlg, C)
+    torch.testing.assert_close(dzg.cpu(), dz, atol=1e-6, rtol=1e-5)
+    torch.testing.assert_close(rlg.cpu(), rl, atol=1e-5, rtol=1e-5)
+    ref_loss = torch.nn.functional.cross_entropy(z[rows][:, :C].double(), y, reduction="none")
+    torch.testing.assert_close(rlg.double().cpu(), ref_loss, atol=1e-5, rtol=1e-5)
+    z[rows[0], 3] = z[rows[0], 5] = 1e3  # a tie: the first maximum wins (torch semantics)
+    hit = torch.zeros(150, dtype=torch.uint8)
+    F32.argmax_hits(z, rows, y, hit, C)
+    hitg = torch.zeros(150, dtype=torch.uint8, device=DEV)
+    F32.argmax_hits(z.to(DEV), rows.to(DEV), y.to(DEV), hitg, C)
+    assert torch.equal(hitg.cpu(), hit)
+    assert torch.equal(hit.bool(), z[rows][:, :C].argmax(1) == y)
