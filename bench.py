@@ -331,6 +331,15 @@ def barrier_sync(world, dev):
         torch.cuda.synchronize()
 
 
+def _alloc_counters(dev) -> dict:
+    """Caching-allocator counters: hipMalloc/hipFree calls and allocation retries."""
+    if dev.type != "cuda":
+        return {"num_device_alloc": 0, "num_device_free": 0, "num_alloc_retries": 0}
+    s = torch.cuda.memory_stats(dev)
+    return {k: int(s.get(k, 0)) for k in ("num_device_alloc", "num_device_free",
+                                          "num_alloc_retries")}
+
+
 def timed(job: Job, steps: int, warmup: int, restrict_last: bool, verbose: bool = False):
     """W untimed warmup steps, then K steps bracketed by barrier + synchronize; returns
     (ms_per_step as the MAX over ranks, mean loss of the last step summed over ranks,
@@ -346,6 +355,7 @@ def timed(job: Job, steps: int, warmup: int, restrict_last: bool, verbose: bool 
         if verbose:
             log(job.rank, f"warmup {i} loss {float(l.detach()):.4f}")
     barrier_sync(world, dev)
+    a0 = _alloc_counters(dev)
     e0 = job.graph.edges_aggregated
     t_start = time.perf_counter()
     l = None
@@ -353,6 +363,11 @@ def timed(job: Job, steps: int, warmup: int, restrict_last: bool, verbose: bool 
         l = stepf()
     barrier_sync(world, dev)
     elapsed = time.perf_counter() - t_start
+    a1 = _alloc_counters(dev)
+    job.alloc_timed = {k: a1[k] - a0[k] for k in a0 if k.startswith("num_")}
+    if dev.type == "cuda":
+        job.alloc_timed["reserved_minus_allocated_gb"] = round(
+            (torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)) / 1e9, 3)
     e1 = job.graph.edges_aggregated
     if job.steppers and e_eager is not None:
         # graph replays run no Python, so the host counter did not move: every replay
@@ -482,6 +497,7 @@ def main():
     val_acc = float(corr[0]) / max(job.n_val, 1)
     test_acc = float(corr[1]) / max(job.n_test, 1)
     halo = job.halo_stats()
+    alloc_timed = dict(getattr(job, "alloc_timed", {}))
     regions = region_breakdown(job)
     use_fused = job.use_fused
     if args.profile_ops:
@@ -551,7 +567,9 @@ def main():
                           "dtype": args.dtype, "global_frac": args.global_frac,
                           "halo_recompute": job_recompute,
                           "restrict_last": head_restrict,
-                          "final_loss_local": final_loss}), flush=True)
+                          "final_loss_local": final_loss,
+                          "executor": "fused" if use_fused else "stack",
+                          **({"regions": regions} if regions else {})}), flush=True)
     elif rank == 0:
         rec = {
             "metric": "edges_per_s",
@@ -603,6 +621,9 @@ def main():
             "val_acc": val_acc,
             "test_acc": test_acc,
             "peak_mem_gb_rank0": round(peak_gb, 2),
+            # hipMalloc/hipFree calls and allocation retries inside the timed steps (0 =
+            # steady state served from preplanned buffers and the allocator cache)
+            "allocator_in_timed_steps": alloc_timed,
             **({"halo": halo} if halo else {}),
             **({"regions": regions} if regions else {}),
             **extra,

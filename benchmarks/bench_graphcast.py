@@ -144,6 +144,15 @@ def main():
                 f.write(prof.key_averages(group_by_input_shape=True).table(
                     sort_by="self_cuda_time_total", row_limit=40, max_name_column_width=60,
                     max_shapes_column_width=80))
+                # the same step attributed to aten ops (which op launched each elementwise
+                # kernel), heaviest first
+                rows = [e for e in prof.key_averages(group_by_input_shape=True)
+                        if e.key.startswith("aten::") or e.key.startswith("dgraph_amd::")]
+                rows.sort(key=lambda e: -e.self_device_time_total)
+                f.write("\n\nop-level (self device us, calls, shapes):\n")
+                for e in rows[:80]:
+                    f.write(f"{e.self_device_time_total:10.0f} {e.count:5d}  {e.key:36s} "
+                            f"{str(e.input_shapes)[:110]}\n")
         result = {"metric": "graphcast_step_ms", "ms_per_step": ms,
                   "channels": a.channels, "channel_config": a.channel_config,
                   "mesh_edges": int(g.m2m[0].size), "duplicate_mesh_edges":
