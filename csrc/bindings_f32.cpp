@@ -147,6 +147,8 @@ void gemm_f32_op(const at::Tensor& A1, const at::Tensor& B1, const c10::optional
   const int64_t N = B1.size(1), K1 = A1.size(1);
   TORCH_CHECK(B1.size(0) == K1, "gemm_f32: A1/B1 inner dimension mismatch");
   TORCH_CHECK(out.size(1) == N, "gemm_f32: out width != N");
+  // the kernel keeps operand row indices in 32 bits
+  TORCH_CHECK(A1.size(0) <= INT32_MAX && M <= INT32_MAX, "gemm_f32: more than 2^31 rows");
   const int64_t* arp = idx64(a_rows, A1, M, "a_rows");
   const int64_t* orp = idx64(o_rows, A1, M, "o_rows");
   if (!orp) TORCH_CHECK(out.size(0) >= M, "gemm_f32: out has fewer than M rows");

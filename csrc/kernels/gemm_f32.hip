@@ -21,9 +21,17 @@
 //   * global -> registers for stage s+1 is issued before the MFMAs of stage s and written
 //     to the other buffer after them (one barrier per stage);
 //   * k order inside a stage: lane group h = lane>>4 takes k = 8h + j in MFMA step j, so a
-//     lane's A fragments of the stage are ONE contiguous 32-B piece (2 x ds_read_b128) and
-//     its B fragment of step j is row 8h + j (the permutation is applied to A and B alike;
-//     the summation order stays fixed, so results are run-to-run identical).
+//     lane's A fragments of the stage are two 16-B pieces (2 x ds_read_b128) and its B
+//     fragment of step j is row 8h + j (the permutation is applied to A and B alike; the
+//     summation order stays fixed, so results are run-to-run identical);
+//   * LDS bank conflicts removed: the A stage's 16-B chunks are XOR-swizzled per row pair
+//     (a_chunk: every ds_read_b128 lane group touches 16 distinct 4-bank slots; the naive
+//     layout was 4-way conflicted), B rows 8..15 and 24..31 of a stage sit 16 floats further
+//     inside an (N+16)-float pitch
+//     (the two 16-lane halves of a ds_read_b32 fall in opposite bank halves: was 2-way);
+//   * persistent grid (one 512-thread block per CU) walking 256-row tiles: the next tile's
+//     first stage is loaded during the current tile's last stage, so the prologue's global
+//     latency and the epilogue's stores overlap MFMAs instead of idling the CU.
 #include "../common.h"
 #include "kernels.h"
 
@@ -45,9 +53,16 @@ template <> struct GCfg<176> { static constexpr int TM = 2, TN = 11, WM = 8, WN 
 template <> struct GCfg<128> { static constexpr int TM = 2, TN = 8, WM = 8, WN = 1; };
 template <> struct GCfg<64> { static constexpr int TM = 2, TN = 4, WM = 8, WN = 1; };
 
+// A stage: 16-B chunk c of row r lives at chunk a_chunk(r, c) of the row (XOR swizzle by
+// row pair; table found by exhaustive search over the ds_read_b128 lane groups)
+constexpr uint32_t kASwz = 0x32765410u;
+__device__ __forceinline__ int a_chunk(int r, int c) {
+  return c ^ static_cast<int>((kASwz >> (4 * ((r >> 1) & 7))) & 7u);
+}
+
 template <int N>
 struct GLds {
-  static constexpr int BP = N + 4;                      // B stage row pitch (floats)
+  static constexpr int BP = N + 16;  // B stage row pitch (floats): room for b_row's shift
   static constexpr int A_FL = kBM * kBK;                // A stage floats
   static constexpr int B_FL = kBK * BP;                 // B stage floats
   static constexpr int STAGE = A_FL + B_FL;
@@ -55,6 +70,10 @@ struct GLds {
   static constexpr int A_V4 = A_FL / 4 / kThreads;      // float4 per thread (A stage) = 4
   static constexpr int B_V4 = (kBK * N / 4 + kThreads - 1) / kThreads;  // float4 (B stage)
 };
+
+// B stage row k starts at b_row(k): rows with bit 3 set are shifted by 16 floats
+template <int BP>
+__device__ __forceinline__ int b_row(int k) { return k * BP + ((k >> 3) & 1) * 16; }
 
 template <int N, bool HAS_A2, bool RELU, bool HAS_BIAS, bool HAS_CIN, bool HAS_GATE>
 __global__ __launch_bounds__(kThreads, 1) void gemm_f32_kernel(
@@ -74,22 +93,28 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_f32_kernel(
   const int wm = wave / WN, wn = wave % WN;
   const int li = lane & 15;  // fragment row (A) / column (B, C)
   const int lh = lane >> 4;  // k slot group
-  const int64_t row0 = static_cast<int64_t>(blockIdx.x) * kBM;
   const int K = K1 + K2;
   const int nst = K / kBK;
+  const int64_t ntiles = (M + kBM - 1) / kBM;
+  int64_t tile = blockIdx.x;
+  if (tile >= ntiles) return;  // block-uniform
 
   // ---- per-thread global load slots of a stage
-  // A: float4 q = tid + kThreads*u -> row q / 8, 16-B chunk q % 8 of the stage's 32 k
-  int64_t a_src_row[L::A_V4];  // A1 rows (through a_rows)
-  int64_t a2_src_row[L::A_V4];  // A2 rows (dense)
+  // A: float4 q = tid + kThreads*u -> row q / 8, 16-B chunk q % 8 of the stage's 32 k.
+  // Row indices are kept as 32-bit (the launcher checks every operand has < 2^31 rows).
+  int32_t a_src_row[L::A_V4];   // A1 rows of the tile being loaded (through a_rows)
+  int32_t nx_src_row[L::A_V4];  // the next tile's A1 rows (index loads issued early)
+  int64_t ld_tile = tile;       // the tile whose stages load_stage reads (A2 rows dense)
+  auto rows_of = [&](int64_t t, int32_t* a1) {
 #pragma unroll
-  for (int u = 0; u < L::A_V4; ++u) {
-    const int q = tid + kThreads * u;
-    int64_t r = row0 + q / 8;
-    r = r < M ? r : M - 1;  // rows past M read a valid row (never stored)
-    a_src_row[u] = a_rows ? a_rows[r] : r;
-    a2_src_row[u] = r;
-  }
+    for (int u = 0; u < L::A_V4; ++u) {
+      const int q = tid + kThreads * u;
+      int64_t r = t * kBM + q / 8;
+      r = r < M ? r : M - 1;  // rows past M read a valid row (never stored)
+      a1[u] = static_cast<int32_t>(a_rows ? a_rows[r] : r);
+    }
+  };
+  rows_of(tile, a_src_row);
   f32x4 ra[L::A_V4];
   f32x4 rb[L::B_V4];
   auto load_stage = [&](int s) {
@@ -101,8 +126,10 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_f32_kernel(
 #pragma unroll
     for (int u = 0; u < L::A_V4; ++u) {
       const int q = tid + kThreads * u;
-      ra[u] = *reinterpret_cast<const f32x4*>(Ab + (first ? a_src_row[u] : a2_src_row[u]) * lda +
-                                              ka + (q % 8) * 4);
+      int64_t r2 = ld_tile * kBM + q / 8;
+      r2 = r2 < M ? r2 : M - 1;
+      const int64_t ar = first ? static_cast<int64_t>(a_src_row[u]) : r2;
+      ra[u] = *reinterpret_cast<const f32x4*>(Ab + ar * lda + ka + (q % 8) * 4);
     }
     const float* Bb = first ? B1 : B2;
     const int64_t ldb = first ? ldb1 : ldb2;
@@ -121,14 +148,15 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_f32_kernel(
 #pragma unroll
     for (int u = 0; u < L::A_V4; ++u) {
       const int q = tid + kThreads * u;
-      *reinterpret_cast<f32x4*>(sa + (q / 8) * kBK + (q % 8) * 4) = ra[u];
+      const int r = q / 8;
+      *reinterpret_cast<f32x4*>(sa + r * kBK + a_chunk(r, q % 8) * 4) = ra[u];
     }
 #pragma unroll
     for (int u = 0; u < L::B_V4; ++u) {
       const int q = tid + kThreads * u;
       if (q < kBK * N / 4) {
         const int kr = q / (N / 4), c4 = q % (N / 4);
-        *reinterpret_cast<f32x4*>(sb + kr * L::BP + c4 * 4) = rb[u];
+        *reinterpret_cast<f32x4*>(sb + b_row<L::BP>(kr) + c4 * 4) = rb[u];
       }
     }
   };
@@ -144,65 +172,85 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_f32_kernel(
   __syncthreads();
   const int arow_w = wm * TM * 16;  // this wave's first row within the block tile
   const int bcol_w = wn * TN * 16;  // this wave's first column
-  for (int s = 0; s < nst; ++s) {
-    const int buf = s & 1;
-    if (s + 1 < nst) load_stage(s + 1);  // in flight during this stage's MFMAs
-    const float* sa = lds + buf * L::STAGE;
-    const float* sb = sa + L::A_FL;
-    // A fragments of the whole stage: k = 8 lh .. 8 lh + 7 of row (tile a, li)
-    f32x4 af[TM][2];
+  int g = 0;                        // stages run by this block (LDS buffer parity)
+  while (true) {
+    const int64_t next = tile + gridDim.x;
+    const bool has_next = next < ntiles;  // block-uniform
+    if (has_next) rows_of(next, nx_src_row);  // consumed at the tile's last stage
+    for (int s = 0; s < nst; ++s, ++g) {
+      const int buf = g & 1;
+      if (s + 1 < nst) {
+        load_stage(s + 1);  // in flight during this stage's MFMAs
+      } else if (has_next) {
+        // the next tile's first stage, in flight during this tile's last MFMAs + epilogue
 #pragma unroll
-    for (int a = 0; a < TM; ++a) {
-      const float* p = sa + (arow_w + a * 16 + li) * kBK + 8 * lh;
-      af[a][0] = *reinterpret_cast<const f32x4*>(p);
-      af[a][1] = *reinterpret_cast<const f32x4*>(p + 4);
-    }
-    // B fragments double-buffered across MFMA steps: step j+1's LDS reads are issued
-    // before step j's TM*TN MFMAs, so their latency hides behind a whole step instead of
-    // the few MFMAs that follow the read in a single-buffered schedule
-    float bf[2][TN];
-    const float* sbw = sb + (8 * lh) * L::BP + bcol_w + li;
-#pragma unroll
-    for (int b = 0; b < TN; ++b) bf[0][b] = sbw[b * 16];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      if (j + 1 < 8) {
-#pragma unroll
-        for (int b = 0; b < TN; ++b) bf[(j + 1) & 1][b] = sbw[(j + 1) * L::BP + b * 16];
+        for (int u = 0; u < L::A_V4; ++u) a_src_row[u] = nx_src_row[u];
+        ld_tile = next;
+        load_stage(0);
       }
+      const float* sa = lds + buf * L::STAGE;
+      const float* sb = sa + L::A_FL;
+      // A fragments of the whole stage: k = 8 lh .. 8 lh + 7 of row (tile a, li)
+      f32x4 af[TM][2];
 #pragma unroll
       for (int a = 0; a < TM; ++a) {
-        const float av = af[a][j >> 2][j & 3];
-#pragma unroll
-        for (int b = 0; b < TN; ++b)
-          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bf[j & 1][b], acc[a][b], 0, 0, 0);
+        const int r = arow_w + a * 16 + li;
+        const float* p = sa + r * kBK;
+        af[a][0] = *reinterpret_cast<const f32x4*>(p + a_chunk(r, 2 * lh) * 4);
+        af[a][1] = *reinterpret_cast<const f32x4*>(p + a_chunk(r, 2 * lh + 1) * 4);
       }
+      // B fragments double-buffered across MFMA steps: step j+1's LDS reads are issued
+      // before step j's TM*TN MFMAs
+      float bf[2][TN];
+      const float* sbw = sb + b_row<L::BP>(8 * lh) + bcol_w + li;
+#pragma unroll
+      for (int b = 0; b < TN; ++b) bf[0][b] = sbw[b * 16];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (j + 1 < 8) {
+#pragma unroll
+          for (int b = 0; b < TN; ++b) bf[(j + 1) & 1][b] = sbw[(j + 1) * L::BP + b * 16];
+        }
+#pragma unroll
+        for (int a = 0; a < TM; ++a) {
+          const float av = af[a][j >> 2][j & 3];
+#pragma unroll
+          for (int b = 0; b < TN; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bf[j & 1][b], acc[a][b], 0, 0, 0);
+        }
+      }
+      if (s + 1 < nst || has_next) store_stage(buf ^ 1);
+      __syncthreads();
     }
-    if (s + 1 < nst) store_stage(buf ^ 1);
-    __syncthreads();
-  }
 
-  // ---- epilogue: tile (a, b) register r of lane l is element
-  //      (row 4 (l >> 4) + r, column l & 15) of the 16x16 block
+    // ---- epilogue: tile (a, b) register r of lane l is element
+    //      (row 4 (l >> 4) + r, column l & 15) of the 16x16 block
+    const int64_t row0 = tile * kBM;
 #pragma unroll
-  for (int a = 0; a < TM; ++a) {
+    for (int a = 0; a < TM; ++a) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t i = row0 + arow_w + a * 16 + 4 * lh + r;
-      if (i >= M) continue;
-      const int64_t orow = o_rows ? o_rows[i] : i;
-      const float rsc = row_scale ? row_scale[i] : 1.f;
+      for (int r = 0; r < 4; ++r) {
+        const int64_t i = row0 + arow_w + a * 16 + 4 * lh + r;
+        if (i < M) {
+          const int64_t orow = o_rows ? o_rows[i] : i;
+          const float rsc = row_scale ? row_scale[i] : 1.f;
 #pragma unroll
-      for (int b = 0; b < TN; ++b) {
-        const int n = bcol_w + b * 16 + li;
-        float v = acc[a][b][r] * rsc;
-        if constexpr (HAS_BIAS) v += bias[n];
-        if constexpr (HAS_CIN) v = fmaf(beta, cin[orow * ldc + n], v);
-        if constexpr (HAS_GATE) v = gate[orow * ldg + n] > 0.f ? v : 0.f;
-        if constexpr (RELU) v = v > 0.f ? v : 0.f;
-        out[orow * ldo + n] = v;
+          for (int b = 0; b < TN; ++b) {
+            const int n = bcol_w + b * 16 + li;
+            float v = acc[a][b][r] * rsc;
+            if constexpr (HAS_BIAS) v += bias[n];
+            if constexpr (HAS_CIN) v = fmaf(beta, cin[orow * ldc + n], v);
+            if constexpr (HAS_GATE) v = gate[orow * ldg + n] > 0.f ? v : 0.f;
+            if constexpr (RELU) v = v > 0.f ? v : 0.f;
+            out[orow * ldo + n] = v;
+          }
+        }
+#pragma unroll
+        for (int b = 0; b < TN; ++b) acc[a][b][r] = 0.f;
       }
     }
+    if (!has_next) break;
+    tile = next;
   }
 }
 
@@ -222,8 +270,17 @@ hipError_t launch_gemm_f32(const float* A1, int64_t lda1, int K1, const float* B
                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
     attr = true;
   }
-  const int64_t blocks = (M + kBM - 1) / kBM;
-  if (blocks > 0x7fffffff) return hipErrorInvalidValue;
+  static int num_cus = 0;
+  if (num_cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&num_cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+            hipSuccess || num_cus <= 0)
+      num_cus = 256;
+  }
+  // persistent: one block per CU (LDS-limited), each walking tiles blockIdx + k * grid
+  const int64_t ntiles = (M + kBM - 1) / kBM;
+  const int64_t blocks = ntiles < num_cus ? ntiles : num_cus;
   hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(blocks)), dim3(kThreads), lds, st, A1,
                      lda1, K1, B1, ldb1, A2, lda2, K2, B2, ldb2, a_rows, bias, cin, ldc, beta,
                      gate, ldg, o_rows, rsc, out, ldo, M);

@@ -12,7 +12,9 @@
 // sequence of calls, which can accumulate over row chunks of one step before the reduce.
 // Data flow per 32-row stage: A and G rows -> registers (issued one stage ahead) -> padded
 // LDS [32][K+4] / [32][N+4]; MFMA step j uses rows 8h + j (lane group h = lane >> 4) of both
-// (the k-slot permutation of gemm_f32.hip, here over the reduced row index).
+// (the k-slot permutation of gemm_f32.hip, here over the reduced row index). Stage rows with
+// bit 3 set sit 16 floats further (srow): the two 16-lane halves of every ds_read_b32 read
+// rows 8 apart, which a (K+4)-float pitch alone maps to the same banks (2-way conflict).
 #include "../common.h"
 #include "kernels.h"
 
@@ -31,13 +33,17 @@ struct WCfg {
   static constexpr int WN = TWO ? 2 : 1;
   static constexpr int WM = TWO ? 4 : 8;
   static constexpr int TM = NTK / WM, TN = NTN / WN;
-  static constexpr int AP = K + 4, GP = N + 4;  // LDS row pitches (floats)
-  static constexpr int STAGE = kRows * (AP + GP);
+  static constexpr int AP = K + 16, GP = N + 16;  // LDS row pitches (floats; srow shift)
+  static constexpr int A_FL = kRows * AP, G_FL = kRows * GP;
+  static constexpr int STAGE = A_FL + G_FL;
   static constexpr size_t BYTES = 2 * STAGE * sizeof(float);
   static constexpr int A_V4 = (kRows * K / 4 + kThr - 1) / kThr;
   static constexpr int G_V4 = (kRows * N / 4 + kThr - 1) / kThr;
   static_assert(TM >= 1 && TM * WM == NTK && TN * WN == NTN, "wgrad tiling");
 };
+
+template <int P>
+__device__ __forceinline__ int srow(int r) { return r * P + ((r >> 3) & 1) * 16; }
 
 template <int K, int N>
 __global__ __launch_bounds__(kThr, 1) void wgrad_f32_kernel(
@@ -91,13 +97,13 @@ __global__ __launch_bounds__(kThr, 1) void wgrad_f32_kernel(
   };
   auto store_stage = [&](int buf) {
     float* sa = lds + buf * C::STAGE;
-    float* sg = sa + kRows * C::AP;
+    float* sg = sa + C::A_FL;
 #pragma unroll
     for (int u = 0; u < C::A_V4; ++u) {
       const int q = tid + kThr * u;
       if (q < kRows * K / 4) {
         const int rr = q / (K / 4), c = (q % (K / 4)) * 4;
-        *reinterpret_cast<f32x4*>(sa + rr * C::AP + c) = ra[u];
+        *reinterpret_cast<f32x4*>(sa + srow<C::AP>(rr) + c) = ra[u];
       }
     }
 #pragma unroll
@@ -105,7 +111,7 @@ __global__ __launch_bounds__(kThr, 1) void wgrad_f32_kernel(
       const int q = tid + kThr * u;
       if (q < kRows * N / 4) {
         const int rr = q / (N / 4), c = (q % (N / 4)) * 4;
-        *reinterpret_cast<f32x4*>(sg + rr * C::GP + c) = rg[u];
+        *reinterpret_cast<f32x4*>(sg + srow<C::GP>(rr) + c) = rg[u];
       }
     }
   };
@@ -124,11 +130,11 @@ __global__ __launch_bounds__(kThr, 1) void wgrad_f32_kernel(
       const int buf = static_cast<int>(s & 1);
       if (s + 1 < nst) load_stage(s + 1);
       const float* sa = lds + buf * C::STAGE;
-      const float* sg = sa + kRows * C::AP;
+      const float* sg = sa + C::A_FL;
       // operand fragments double-buffered across MFMA steps (reads of step j+1 are in
-      // flight during step j's MFMAs)
-      const float* saw = sa + (8 * lh) * C::AP + kw + li;
-      const float* sgw = sg + (8 * lh) * C::GP + nw + li;
+      // flight during step j's MFMAs); rows 8 lh + j, j < 8, share srow's shift
+      const float* saw = sa + srow<C::AP>(8 * lh) + kw + li;
+      const float* sgw = sg + srow<C::GP>(8 * lh) + nw + li;
       float av[2][TM], gv[2][TN];
 #pragma unroll
       for (int a = 0; a < TM; ++a) av[0][a] = saw[a * 16];

@@ -103,9 +103,16 @@ def supported(model, x: torch.Tensor) -> bool:
         return False
     hid = layers[0].out_dim
     d0 = x.shape[1]
-    return (x.dtype == torch.float32 and d0 % 32 == 0 and d0 in (128, 256)
+    # input widths up to 128 (narrower features are zero-padded to 64 / 128 columns)
+    return (x.dtype == torch.float32 and 0 < d0 <= 128
             and hid == 256 and all(l.out_dim == hid for l in layers[:-1])
             and layers[-1].out_dim <= 176)
+
+
+def _in_width(d0: int) -> int:
+    """Input width the kernels run at: the layer-0 GEMM's K (a multiple of 32) and the
+    input weight gradient's K = 2 * width (128 or 256)."""
+    return 64 if d0 <= 64 else 128
 
 
 class FusedSAGE:
@@ -123,13 +130,20 @@ class FusedSAGE:
                  eval_is_val: torch.Tensor, n_train: int, chunk_rows: int = 0):
         if not supported(model, x):
             raise ValueError("FusedSAGE: unsupported model/feature shape")
-        self.model, self.g, self.x = model, graph, x.contiguous()
         dev = x.device
         self.dev = dev
+        self.d0_in = x.shape[1]
+        self.d0 = _in_width(self.d0_in)
+        if self.d0 != self.d0_in:
+            # zero feature columns: their aggregates are zero, their weight rows get
+            # gradients that are dropped (ogbn-products: 100 -> 128)
+            xp = torch.zeros(x.shape[0], self.d0, dtype=x.dtype, device=dev)
+            xp[:, :self.d0_in] = x
+            x = xp
+        self.model, self.g, self.x = model, graph, x.contiguous()
         L, H = graph.L, graph.H
         self.L, self.H = L, H
         self.nl = len(model.layers)
-        self.d0 = x.shape[1]
         self.hid = model.layers[0].out_dim
         self.C = model.layers[-1].out_dim
         self.Cp = 176 if self.C > 128 else (128 if self.C > 64 else 64)  # logit GEMM width
@@ -342,6 +356,15 @@ class FusedSAGE:
             out.append((l.w_self, l.w_neigh, l.bias))
         return out
 
+    def _pad_in(self, w: torch.Tensor) -> torch.Tensor:
+        """A layer-0 weight [d0_in, hid] as the [d0, hid] operand of the padded input."""
+        w = w.detach()
+        if self.d0 == self.d0_in:
+            return w.contiguous()
+        wp = torch.zeros(self.d0, w.shape[1], dtype=w.dtype, device=w.device)
+        wp[:self.d0_in] = w
+        return wp
+
     # ------------------------------------------------------------------ the step
     def step(self) -> torch.Tensor:
         g, x = self.g, self.x
@@ -357,7 +380,10 @@ class FusedSAGE:
         halos = [hin_halo]
         for l in range(nl - 1):
             ws, wn, b = P[l]
-            ws, wn = ws.detach().contiguous(), wn.detach().contiguous()
+            if l == 0:
+                ws, wn = self._pad_in(ws), self._pad_in(wn)
+            else:
+                ws, wn = ws.detach().contiguous(), wn.detach().contiguous()
             hout = self.h[l]
             bias = b.detach()
             items = [ci for ci, (r0, r1) in enumerate(self.chunks) if r1 > r0]
@@ -498,6 +524,8 @@ class FusedSAGE:
         self.edges_aggregated += self.nnz_S
         gw[(lh, 0)] = self.acc_hid_s.result()
         gw[(lh, 1)] = self.acc_hid_n.result()
+        if lh == 0:
+            gw[(0, 0)], gw[(0, 1)] = gw[(0, 0)][:self.d0_in], gw[(0, 1)][:self.d0_in]
         if nl == 3:
             # ------------ layer 0: dZ0 by row chunks, consumed at once by its weight grads
             ws1_t = ws1.detach().t().contiguous()
@@ -546,7 +574,8 @@ class FusedSAGE:
             self.edges_aggregated += 2 * nnz_it + nnz_h + \
                 (self.send_st.nnz if self.send_st is not None else 0)
             w0 = self.acc_in.result()
-            gw[(0, 0)], gw[(0, 1)], gw[(0, 2)] = w0[:self.d0], w0[self.d0:], db0
+            gw[(0, 0)], gw[(0, 1)], gw[(0, 2)] = (w0[:self.d0_in],
+                                                  w0[self.d0:self.d0 + self.d0_in], db0)
         self._mark("grads")
         # ---------------- gradients into the parameters
         for l, (ws_, wn_, b_) in enumerate(P):

@@ -94,6 +94,30 @@ def test_gemm_f32_dual_vs_fp64(N, K1, K2):
     torch.testing.assert_close(out.double().cpu(), ref, atol=1e-4, rtol=1e-5)
 
 
+@pytest.mark.parametrize("N", [176, 256])
+def test_gemm_f32_persistent_multi_tile(N):
+    """More 256-row tiles than CUs: every persistent block walks several tiles and loads the
+    next tile's first stage (gathered A1 rows, dense A2 rows) during the current one."""
+    g = torch.Generator().manual_seed(21 + N)
+    M = 256 * 256 * 2 + 777
+    src = torch.randn(M + 5000, 128, generator=g)
+    a_rows = torch.randperm(M + 5000, generator=g)[:M]
+    A2 = torch.randn(M, 128, generator=g)
+    B1 = torch.randn(128, N, generator=g) / 11
+    B2 = torch.randn(128, N, generator=g) / 11
+    bias = torch.randn(N, generator=g)
+    rs = torch.rand(M, generator=g) + 0.5
+    o_rows = torch.randperm(M + 100, generator=g)[:M]
+    out = torch.zeros(M + 100, N).to(DEV)
+    F32.gemm_f32(src.to(DEV), B1.to(DEV), A2.to(DEV), B2.to(DEV), a_rows=a_rows.to(DEV),
+                 bias=bias.to(DEV), relu=True, o_rows=o_rows.to(DEV), out=out,
+                 row_scale=rs.to(DEV))
+    v = (src[a_rows].double() @ B1.double() + A2.double() @ B2.double()) * rs.double()[:, None]
+    ref = torch.zeros(M + 100, N, dtype=torch.float64)
+    ref[o_rows] = (v + bias.double()).clamp_min(0)
+    torch.testing.assert_close(out.double().cpu(), ref, atol=1e-4, rtol=1e-5)
+
+
 def test_gemm_f32_cin_gate_rows():
     g = torch.Generator().manual_seed(9)
     M, K1, N = 700, 256, 256
