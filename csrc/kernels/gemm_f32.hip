@@ -135,11 +135,12 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_f32_kernel(
     const int64_t ldb = first ? ldb1 : ldb2;
 #pragma unroll
     for (int u = 0; u < L::B_V4; ++u) {
-      const int q = tid + kThreads * u;
-      if (q < kBK * N / 4) {
-        const int kr = q / (N / 4), c4 = q % (N / 4);
-        rb[u] = *reinterpret_cast<const f32x4*>(Bb + static_cast<int64_t>(ka + kr) * ldb + c4 * 4);
-      }
+      // unconditional (slots past the stage re-read its last float4; store_stage skips
+      // them): a load under a branch makes the compiler wait for it at the join
+      int q = tid + kThreads * u;
+      q = q < kBK * N / 4 ? q : kBK * N / 4 - 1;
+      const int kr = q / (N / 4), c4 = q % (N / 4);
+      rb[u] = *reinterpret_cast<const f32x4*>(Bb + static_cast<int64_t>(ka + kr) * ldb + c4 * 4);
     }
   };
   auto store_stage = [&](int buf) {
@@ -153,11 +154,12 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_f32_kernel(
     }
 #pragma unroll
     for (int u = 0; u < L::B_V4; ++u) {
-      const int q = tid + kThreads * u;
-      if (q < kBK * N / 4) {
-        const int kr = q / (N / 4), c4 = q % (N / 4);
-        *reinterpret_cast<f32x4*>(sb + b_row<L::BP>(kr) + c4 * 4) = rb[u];
-      }
+      // clamped like the load: surplus slots rewrite the last float4 with its own value
+      // (no branch, so the compiler cannot sink the load into one)
+      int q = tid + kThreads * u;
+      q = q < kBK * N / 4 ? q : kBK * N / 4 - 1;
+      const int kr = q / (N / 4), c4 = q % (N / 4);
+      *reinterpret_cast<f32x4*>(sb + b_row<L::BP>(kr) + c4 * 4) = rb[u];
     }
   };
 
@@ -176,18 +178,22 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_f32_kernel(
   while (true) {
     const int64_t next = tile + gridDim.x;
     const bool has_next = next < ntiles;  // block-uniform
-    if (has_next) rows_of(next, nx_src_row);  // consumed at the tile's last stage
+    rows_of(has_next ? next : tile, nx_src_row);  // consumed at the tile's last stage
     for (int s = 0; s < nst; ++s, ++g) {
       const int buf = g & 1;
-      if (s + 1 < nst) {
-        load_stage(s + 1);  // in flight during this stage's MFMAs
-      } else if (has_next) {
-        // the next tile's first stage, in flight during this tile's last MFMAs + epilogue
+      // the next stage, in flight during this stage's MFMAs; at the tile's last stage the
+      // next tile's first stage (or, for the block's last tile, a harmless re-read of this
+      // tile's first stage). Branch-free: every path issues the same loads into the same
+      // registers, so no wait is forced before the MFMAs below.
+      const bool last = s + 1 == nst;
+      const bool switch_tile = last && has_next;
 #pragma unroll
-        for (int u = 0; u < L::A_V4; ++u) a_src_row[u] = nx_src_row[u];
-        ld_tile = next;
-        load_stage(0);
-      }
+      for (int u = 0; u < L::A_V4; ++u) a_src_row[u] = switch_tile ? nx_src_row[u] : a_src_row[u];
+      ld_tile = switch_tile ? next : ld_tile;
+      load_stage(last ? 0 : s + 1);
+      // keep the loads HERE: without this fence the scheduler sinks them next to their use
+      // (store_stage after the MFMAs) and their latency is exposed every stage
+      __builtin_amdgcn_sched_barrier(0);
       const float* sa = lds + buf * L::STAGE;
       const float* sb = sa + L::A_FL;
       // A fragments of the whole stage: k = 8 lh .. 8 lh + 7 of row (tile a, li)
@@ -219,7 +225,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_f32_kernel(
             acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bf[j & 1][b], acc[a][b], 0, 0, 0);
         }
       }
-      if (s + 1 < nst || has_next) store_stage(buf ^ 1);
+      store_stage(buf ^ 1);  // (the block's very last store lands in a buffer never read)
       __syncthreads();
     }
 

@@ -67,52 +67,61 @@ __global__ __launch_bounds__(kThr, 1) void wgrad_f32_kernel(
 
   f32x4 ra[C::A_V4];
   f32x4 rg[C::G_V4];
-  auto load_stage = [&](int64_t s) {
-    const int64_t m0 = m_begin + s * kRows;
+  int64_t ix[C::A_V4];  // A rows (through a1_rows for A1 slots) of the next stage to load
+  // slot u of this thread: stage row rr(u), column c(u) (surplus slots clamped to the
+  // stage's last float4: every load and store is unconditional — a load under a branch
+  // gets sunk next to its use by the compiler, exposing its latency)
+  auto slot = [&](int u, int W) {
+    int q = tid + kThr * u;
+    return q < kRows * W / 4 ? q : kRows * W / 4 - 1;
+  };
+  auto row_of = [&](int64_t s, int rr) {
+    const int64_t m = m_begin + s * kRows + rr;
+    return m < m_end ? m : m_begin;  // a valid row (its G row is zeroed at the store)
+  };
+  // the indices of stage s's A1 rows: loaded one stage before their data
+  auto load_idx = [&](int64_t s) {
 #pragma unroll
     for (int u = 0; u < C::A_V4; ++u) {
-      const int q = tid + kThr * u;
-      if (q < kRows * K / 4) {
-        const int rr = q / (K / 4), c = (q % (K / 4)) * 4;
-        const int64_t m = m0 + rr;
-        const bool ok = m < m_end;
-        const int64_t mm = ok ? m : m_begin;  // a valid row; zeroed below
-        const float* src = c < K1 ? A1 + (a1_rows ? a1_rows[mm] : mm) * lda1 + c
-                                  : A2 + mm * lda2 + (c - K1);
-        const f32x4 v = *reinterpret_cast<const f32x4*>(src);
-        ra[u] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
-      }
+      const int q = slot(u, K);
+      const int64_t mm = row_of(s, q / (K / 4));
+      ix[u] = (a1_rows && (q % (K / 4)) * 4 < K1) ? a1_rows[mm] : mm;
+    }
+  };
+  auto load_data = [&](int64_t s) {
+#pragma unroll
+    for (int u = 0; u < C::A_V4; ++u) {
+      const int q = slot(u, K);
+      const int c = (q % (K / 4)) * 4;
+      const bool first = c < K1;
+      const float* base = first ? A1 : A2;
+      const int64_t ld = first ? lda1 : lda2;
+      ra[u] = *reinterpret_cast<const f32x4*>(base + ix[u] * ld + (first ? c : c - K1));
     }
 #pragma unroll
     for (int u = 0; u < C::G_V4; ++u) {
-      const int q = tid + kThr * u;
-      if (q < kRows * N / 4) {
-        const int rr = q / (N / 4), c = (q % (N / 4)) * 4;
-        const int64_t m = m0 + rr;
-        const bool ok = m < m_end;
-        const f32x4 v = *reinterpret_cast<const f32x4*>(G + (ok ? m : m_begin) * ldg + c);
-        rg[u] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
-      }
+      const int q = slot(u, N);
+      rg[u] = *reinterpret_cast<const f32x4*>(G + row_of(s, q / (N / 4)) * ldg +
+                                              (q % (N / 4)) * 4);
     }
   };
-  auto store_stage = [&](int buf) {
+  auto store_stage = [&](int buf, int64_t s) {
     float* sa = lds + buf * C::STAGE;
     float* sg = sa + C::A_FL;
 #pragma unroll
     for (int u = 0; u < C::A_V4; ++u) {
-      const int q = tid + kThr * u;
-      if (q < kRows * K / 4) {
-        const int rr = q / (K / 4), c = (q % (K / 4)) * 4;
-        *reinterpret_cast<f32x4*>(sa + srow<C::AP>(rr) + c) = ra[u];
-      }
+      const int q = slot(u, K);  // surplus: same value, same place
+      const int rr = q / (K / 4), c = (q % (K / 4)) * 4;
+      *reinterpret_cast<f32x4*>(sa + srow<C::AP>(rr) + c) = ra[u];
     }
 #pragma unroll
     for (int u = 0; u < C::G_V4; ++u) {
-      const int q = tid + kThr * u;
-      if (q < kRows * N / 4) {
-        const int rr = q / (N / 4), c = (q % (N / 4)) * 4;
-        *reinterpret_cast<f32x4*>(sg + srow<C::GP>(rr) + c) = rg[u];
-      }
+      const int q = slot(u, N);
+      const int rr = q / (N / 4), c = (q % (N / 4)) * 4;
+      // rows past the block's range contribute zero (zeroing one operand suffices)
+      const bool ok = m_begin + s * kRows + rr < m_end;
+      *reinterpret_cast<f32x4*>(sg + srow<C::GP>(rr) + c) =
+          ok ? rg[u] : f32x4{0.f, 0.f, 0.f, 0.f};
     }
   };
 
@@ -123,12 +132,19 @@ __global__ __launch_bounds__(kThr, 1) void wgrad_f32_kernel(
     for (int b = 0; b < TN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int kw = wm * TM * 16, nw = wn * TN * 16;
   if (nst > 0) {
-    load_stage(0);
-    store_stage(0);
+    load_idx(0);
+    load_data(0);
+    store_stage(0, 0);
+    load_idx(nst > 1 ? 1 : 0);
     __syncthreads();
     for (int64_t s = 0; s < nst; ++s) {
       const int buf = static_cast<int>(s & 1);
-      if (s + 1 < nst) load_stage(s + 1);
+      // unconditional (the last stage re-reads itself into a buffer never read again);
+      // then the indices of the stage after
+      const int64_t sn = s + 1 < nst ? s + 1 : s;
+      load_data(sn);
+      load_idx(s + 2 < nst ? s + 2 : sn);
+      __builtin_amdgcn_sched_barrier(0);  // keep the loads ahead of this stage's MFMAs
       const float* sa = lds + buf * C::STAGE;
       const float* sg = sa + C::A_FL;
       // operand fragments double-buffered across MFMA steps (reads of step j+1 are in
@@ -155,7 +171,7 @@ __global__ __launch_bounds__(kThr, 1) void wgrad_f32_kernel(
             acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j & 1][a], gv[j & 1][b],
                                                              acc[a][b], 0, 0, 0);
       }
-      if (s + 1 < nst) store_stage(buf ^ 1);
+      store_stage(buf ^ 1, sn);
       __syncthreads();
     }
   }
