@@ -335,10 +335,16 @@ void set_spmm_f32_config_op(int64_t rowgroup, int64_t pass_cols) {
   set_spmm_f32_config(static_cast<int>(rowgroup), static_cast<int>(pass_cols));
 }
 
+void set_f32_sched_op(int64_t spmm_grid, int64_t gemm_tile) {
+  set_spmm_f32_grid(static_cast<int>(spmm_grid));
+  set_gemm_f32_tile(static_cast<int>(gemm_tile));
+}
+
 }  // namespace
 }  // namespace dgraph
 
 TORCH_LIBRARY_FRAGMENT(dgraph_amd, m) {
+  m.def("set_f32_sched(int spmm_grid, int gemm_tile) -> ()", &dgraph::set_f32_sched_op);
   m.def("set_spmm_f32_config(int rowgroup, int pass_cols=-1) -> ()",
         &dgraph::set_spmm_f32_config_op);
   m.def("spmm_f32_ex(Tensor rowptr, Tensor col, Tensor? edge_weight, Tensor? col_scale, "

@@ -40,18 +40,30 @@ namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kBM = 256;
 constexpr int kBK = 32;
-constexpr int kThreads = 512;
 
-template <int N>
+// Two block shapes:
+//   * BM = 256 rows, 512 threads (8 waves, 2 per SIMD at ~240 VGPRs): the GEMM owns the
+//     whole register file of the CU — best when it runs alone;
+//   * "lean": BM = 128 rows, 256 threads (ONE wave per SIMD, 32 rows x N columns each),
+//     102 KB LDS: a memory-bound kernel on another stream (the next chunk's aggregation)
+//     keeps 2 waves per SIMD resident next to it, so the two overlap on every CU instead of
+//     taking turns (the matrix pipe and the vector-memory pipe are different units).
+template <int BM, int N>
 struct GCfg;
-// N: (TM, TN, WM, WN) with 16*TM*WM = 256 and 16*TN*WN = N
-template <> struct GCfg<256> { static constexpr int TM = 4, TN = 8, WM = 4, WN = 2; };
-template <> struct GCfg<192> { static constexpr int TM = 4, TN = 6, WM = 4, WN = 2; };
-template <> struct GCfg<176> { static constexpr int TM = 2, TN = 11, WM = 8, WN = 1; };
-template <> struct GCfg<128> { static constexpr int TM = 2, TN = 8, WM = 8, WN = 1; };
-template <> struct GCfg<64> { static constexpr int TM = 2, TN = 4, WM = 8, WN = 1; };
+// (BM, N): (TM, TN, WM, WN) with 16*TM*WM = BM and 16*TN*WN = N; threads = 64*WM*WN
+template <> struct GCfg<256, 256> { static constexpr int TM = 4, TN = 8, WM = 4, WN = 2; };
+template <> struct GCfg<256, 192> { static constexpr int TM = 4, TN = 6, WM = 4, WN = 2; };
+template <> struct GCfg<256, 176> { static constexpr int TM = 2, TN = 11, WM = 8, WN = 1; };
+template <> struct GCfg<256, 128> { static constexpr int TM = 2, TN = 8, WM = 8, WN = 1; };
+template <> struct GCfg<256, 64> { static constexpr int TM = 2, TN = 4, WM = 8, WN = 1; };
+template <> struct GCfg<128, 256> { static constexpr int TM = 2, TN = 16, WM = 4, WN = 1; };
+template <> struct GCfg<128, 192> { static constexpr int TM = 2, TN = 12, WM = 4, WN = 1; };
+template <> struct GCfg<128, 176> { static constexpr int TM = 2, TN = 11, WM = 4, WN = 1; };
+template <> struct GCfg<128, 128> { static constexpr int TM = 2, TN = 8, WM = 4, WN = 1; };
+template <> struct GCfg<128, 64> { static constexpr int TM = 2, TN = 4, WM = 4, WN = 1; };
+template <int BM>
+constexpr int threads_of() { return BM == 256 ? 512 : 256; }
 
 // A stage: 16-B chunk c of row r lives at chunk a_chunk(r, c) of the row (XOR swizzle by
 // row pair; table found by exhaustive search over the ds_read_b128 lane groups)
@@ -60,10 +72,11 @@ __device__ __forceinline__ int a_chunk(int r, int c) {
   return c ^ static_cast<int>((kASwz >> (4 * ((r >> 1) & 7))) & 7u);
 }
 
-template <int N>
+template <int BM, int N>
 struct GLds {
+  static constexpr int kThreads = threads_of<BM>();
   static constexpr int BP = N + 16;  // B stage row pitch (floats): room for b_row's shift
-  static constexpr int A_FL = kBM * kBK;                // A stage floats
+  static constexpr int A_FL = BM * kBK;                 // A stage floats
   static constexpr int B_FL = kBK * BP;                 // B stage floats
   static constexpr int STAGE = A_FL + B_FL;
   static constexpr size_t BYTES = 2 * STAGE * sizeof(float);
@@ -75,16 +88,19 @@ struct GLds {
 template <int BP>
 __device__ __forceinline__ int b_row(int k) { return k * BP + ((k >> 3) & 1) * 16; }
 
-template <int N, bool HAS_A2, bool RELU, bool HAS_BIAS, bool HAS_CIN, bool HAS_GATE>
-__global__ __launch_bounds__(kThreads, 1) void gemm_f32_kernel(
+template <int BM, int N, bool HAS_A2, bool RELU, bool HAS_BIAS, bool HAS_CIN, bool HAS_GATE>
+__device__ __forceinline__ void gemm_f32_body(
     const float* __restrict__ A1, int64_t lda1, int K1, const float* __restrict__ B1,
     int64_t ldb1, const float* __restrict__ A2, int64_t lda2, int K2,
     const float* __restrict__ B2, int64_t ldb2, const int64_t* __restrict__ a_rows,
     const float* __restrict__ bias, const float* cin, int64_t ldc, float beta,
     const float* __restrict__ gate, int64_t ldg, const int64_t* __restrict__ o_rows,
     const float* __restrict__ row_scale, float* out, int64_t ldo, int64_t M) {
-  using C = GCfg<N>;
-  using L = GLds<N>;
+  constexpr int kBM = BM;
+  using C = GCfg<BM, N>;
+  using L = GLds<BM, N>;
+  constexpr int kThreads = L::kThreads;
+  static_assert(64 * C::WM * C::WN == kThreads, "waves x 64 == threads");
   constexpr int TM = C::TM, TN = C::TN, WN = C::WN;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x;
@@ -205,24 +221,49 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_f32_kernel(
         af[a][0] = *reinterpret_cast<const f32x4*>(p + a_chunk(r, 2 * lh) * 4);
         af[a][1] = *reinterpret_cast<const f32x4*>(p + a_chunk(r, 2 * lh + 1) * 4);
       }
-      // B fragments double-buffered across MFMA steps: step j+1's LDS reads are issued
-      // before step j's TM*TN MFMAs
-      float bf[2][TN];
       const float* sbw = sb + b_row<L::BP>(8 * lh) + bcol_w + li;
+      if constexpr (BM == 256) {
+        // B fragments double-buffered across MFMA steps: step j+1's LDS reads are issued
+        // before step j's TM*TN MFMAs
+        float bf[2][TN];
 #pragma unroll
-      for (int b = 0; b < TN; ++b) bf[0][b] = sbw[b * 16];
+        for (int b = 0; b < TN; ++b) bf[0][b] = sbw[b * 16];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        if (j + 1 < 8) {
+        for (int j = 0; j < 8; ++j) {
+          if (j + 1 < 8) {
 #pragma unroll
-          for (int b = 0; b < TN; ++b) bf[(j + 1) & 1][b] = sbw[(j + 1) * L::BP + b * 16];
+            for (int b = 0; b < TN; ++b) bf[(j + 1) & 1][b] = sbw[(j + 1) * L::BP + b * 16];
+          }
+#pragma unroll
+          for (int a = 0; a < TM; ++a) {
+            const float av = af[a][j >> 2][j & 3];
+#pragma unroll
+            for (int b = 0; b < TN; ++b)
+              acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bf[j & 1][b], acc[a][b], 0, 0, 0);
+          }
         }
+      } else {
+        // lean: ONE rolling set of B fragments — fragment b of step j+1 is read right after
+        // its last use in step j (TN MFMAs ahead of its own use), half the registers of a
+        // double buffer
+        float bf[TN];
 #pragma unroll
-        for (int a = 0; a < TM; ++a) {
-          const float av = af[a][j >> 2][j & 3];
+        for (int b = 0; b < TN; ++b) bf[b] = sbw[b * 16];
 #pragma unroll
-          for (int b = 0; b < TN; ++b)
-            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bf[j & 1][b], acc[a][b], 0, 0, 0);
+        for (int j = 0; j < 8; ++j) {
+#pragma unroll
+          for (int a = 0; a + 1 < TM; ++a) {
+            const float av = af[a][j >> 2][j & 3];
+#pragma unroll
+            for (int b = 0; b < TN; ++b)
+              acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bf[b], acc[a][b], 0, 0, 0);
+          }
+          const float av = af[TM - 1][j >> 2][j & 3];
+#pragma unroll
+          for (int b = 0; b < TN; ++b) {
+            acc[TM - 1][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bf[b], acc[TM - 1][b], 0, 0, 0);
+            if (j + 1 < 8) bf[b] = sbw[(j + 1) * L::BP + b * 16];
+          }
         }
       }
       store_stage(buf ^ 1);  // (the block's very last store lands in a buffer never read)
@@ -260,6 +301,32 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_f32_kernel(
   }
 }
 
+#define DG_GEMM_F32_ARGS                                                                        \
+  const float *__restrict__ A1, int64_t lda1, int K1, const float *__restrict__ B1,          \
+      int64_t ldb1, const float *__restrict__ A2, int64_t lda2, int K2,                       \
+      const float *__restrict__ B2, int64_t ldb2, const int64_t *__restrict__ a_rows,         \
+      const float *__restrict__ bias, const float *cin, int64_t ldc, float beta,              \
+      const float *__restrict__ gate, int64_t ldg, const int64_t *__restrict__ o_rows,        \
+      const float *__restrict__ row_scale, float *out, int64_t ldo, int64_t M
+#define DG_GEMM_F32_PASS                                                                       \
+  A1, lda1, K1, B1, ldb1, A2, lda2, K2, B2, ldb2, a_rows, bias, cin, ldc, beta, gate, ldg,     \
+      o_rows, row_scale, out, ldo, M
+
+template <int N, bool HAS_A2, bool RELU, bool HAS_BIAS, bool HAS_CIN, bool HAS_GATE>
+__global__ __launch_bounds__(512, 1) void gemm_f32_kernel(DG_GEMM_F32_ARGS) {
+  gemm_f32_body<256, N, HAS_A2, RELU, HAS_BIAS, HAS_CIN, HAS_GATE>(DG_GEMM_F32_PASS);
+}
+
+// lean tile: one wave per SIMD; its registers (<= 256) leave the rest of the file to a
+// co-resident kernel
+template <int N, bool HAS_A2, bool RELU, bool HAS_BIAS, bool HAS_CIN, bool HAS_GATE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void gemm_f32_lean_kernel(DG_GEMM_F32_ARGS) {
+  gemm_f32_body<128, N, HAS_A2, RELU, HAS_BIAS, HAS_CIN, HAS_GATE>(DG_GEMM_F32_PASS);
+}
+
+// row tile of the next launches: 256 (default) or 128 (lean; set_gemm_f32_tile)
+int g_gemm_f32_bm = 256;
+
 template <int N, bool HAS_A2, bool RELU, bool HAS_BIAS, bool HAS_CIN, bool HAS_GATE>
 hipError_t launch_gemm_f32(const float* A1, int64_t lda1, int K1, const float* B1, int64_t ldb1,
                            const float* A2, int64_t lda2, int K2, const float* B2,
@@ -267,14 +334,17 @@ hipError_t launch_gemm_f32(const float* A1, int64_t lda1, int K1, const float* B
                            const float* cin, int64_t ldc, float beta, const float* gate,
                            int64_t ldg, const int64_t* o_rows, const float* rsc, float* out,
                            int64_t ldo, int64_t M, hipStream_t st) {
-  auto kern = &gemm_f32_kernel<N, HAS_A2, RELU, HAS_BIAS, HAS_CIN, HAS_GATE>;
-  constexpr size_t lds = GLds<N>::BYTES;
-  static_assert(lds <= 160 * 1024, "LDS budget");
-  static bool attr = false;
-  if (!attr) {
+  const bool lean = g_gemm_f32_bm == 128;
+  auto kern = lean ? &gemm_f32_lean_kernel<N, HAS_A2, RELU, HAS_BIAS, HAS_CIN, HAS_GATE>
+                   : &gemm_f32_kernel<N, HAS_A2, RELU, HAS_BIAS, HAS_CIN, HAS_GATE>;
+  const int kBM = lean ? 128 : 256;
+  const size_t lds = lean ? GLds<128, N>::BYTES : GLds<256, N>::BYTES;
+  static_assert(GLds<256, N>::BYTES <= 160 * 1024, "LDS budget");
+  static bool attr[2] = {false, false};
+  if (!attr[lean]) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
-    attr = true;
+    attr[lean] = true;
   }
   static int num_cus = 0;
   if (num_cus == 0) {
@@ -287,7 +357,7 @@ hipError_t launch_gemm_f32(const float* A1, int64_t lda1, int K1, const float* B
   // persistent: one block per CU (LDS-limited), each walking tiles blockIdx + k * grid
   const int64_t ntiles = (M + kBM - 1) / kBM;
   const int64_t blocks = ntiles < num_cus ? ntiles : num_cus;
-  hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(blocks)), dim3(kThreads), lds, st, A1,
+  hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(blocks)), dim3(lean ? 256 : 512), lds, st, A1,
                      lda1, K1, B1, ldb1, A2, lda2, K2, B2, ldb2, a_rows, bias, cin, ldc, beta,
                      gate, ldg, o_rows, rsc, out, ldo, M);
   return hipGetLastError();
@@ -340,6 +410,8 @@ hipError_t gemm_f32_n(const float* A1, int64_t lda1, int K1, const float* B1, in
 inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 }  // namespace
+
+void set_gemm_f32_tile(int bm) { g_gemm_f32_bm = bm == 128 ? 128 : 256; }
 
 bool gemm_f32_supported(int64_t N, int64_t K1, int64_t K2) {
   return (N == 64 || N == 128 || N == 176 || N == 192 || N == 256) && K1 > 0 &&

@@ -56,6 +56,8 @@ void set_spmm_f32_pass_cols(int cols);
 // rowgroup: 1 = fp32 row-group kernel (default), 0 = generic kernels; pass_cols: column
 // pass width (0 = default 64); negative arguments leave a setting unchanged
 void set_spmm_f32_config(int rowgroup, int pass_cols);
+void set_spmm_f32_grid(int blocks);   // 0 = uncapped
+void set_gemm_f32_tile(int bm);       // 256 (default) or 128 (lean, co-resident)
 
 // Hub-row splitting (rows whose degree exceeds `cap` are aggregated in three steps):
 //   1. spmm_csr(..., cap): every row sums at most its first `cap` entries;

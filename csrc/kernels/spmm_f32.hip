@@ -163,6 +163,11 @@ __global__ __launch_bounds__(256) void spmm_f32_rowgroup_kernel(
   }
 }
 
+// grid cap (0 = one row group per wave, the whole graph in one launch): the kernel is
+// grid-strided, so a capped grid is a persistent one that leaves room on every CU for a
+// kernel of another stream (set_spmm_f32_grid)
+int g_f32_grid_cap = 0;
+
 template <typename IdxT, bool CMAP>
 hipError_t launch_f32_rg(const int64_t* rowptr, const IdxT* col, const float* ew,
                          const float* cs, const float* rs, const int32_t* cmap,
@@ -175,7 +180,8 @@ hipError_t launch_f32_rg(const int64_t* rowptr, const IdxT* col, const float* ew
   const int LPR = lanes <= 8 ? 8 : lanes <= 16 ? 16 : lanes <= 32 ? 32 : 64;
   const int64_t G = kWave / LPR;
   const int64_t ngroups = (nrows + G - 1) / G;
-  const int64_t blocks = (ngroups + 3) / 4;  // in order: one row group per wave
+  int64_t blocks = (ngroups + 3) / 4;  // in order: one row group per wave
+  if (g_f32_grid_cap > 0 && blocks > g_f32_grid_cap) blocks = g_f32_grid_cap;
   if (blocks > 0x7fffffff) return hipErrorInvalidValue;
   const int wmode = (ew != nullptr ? 1 : 0) | (cs != nullptr ? 2 : 0);
   dim3 grid(static_cast<unsigned>(blocks)), block(256);
@@ -203,6 +209,8 @@ int g_f32_pass_cols = 64;
 }  // namespace
 
 void set_spmm_f32_pass_cols(int cols) { g_f32_pass_cols = cols > 0 ? cols : 64; }
+
+void set_spmm_f32_grid(int blocks) { g_f32_grid_cap = blocks > 0 ? blocks : 0; }
 
 bool spmm_f32_rowgroup_ok(int F, int64_t ldx, int64_t ldo, const void* x, const void* out) {
   auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) % 16) == 0; };

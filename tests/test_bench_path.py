@@ -22,17 +22,25 @@ def _args(**kw):
     return a
 
 
-def _run_job(rank, world, out, steps, global_frac, restrict, recompute="off"):
+def _run_job(rank, world, out, steps, global_frac, restrict, recompute="off",
+             grad_support=True):
     import torch.distributed as dist
 
     import bench
+    from dgraph_amd.parallel.dist_graph import DistGraph
 
+    DistGraph.GRAD_SUPPORT = grad_support
     comm = types.SimpleNamespace(get_rank=lambda: rank, get_world_size=lambda: world,
                                  group=None)
     job = bench.Job(_args(global_frac=global_frac, halo_recompute=recompute), comm,
                     torch.device("cpu"), global_frac, torch.float32)
     if recompute == "on" and world > 1:
         assert job.recompute and job.graph.recompute is not None
+    # the gradient support of the layer below the output layer is what the timed step
+    # runs (bench.Job prepares it on every rank); a silently skipped build would leave the
+    # dense transposed aggregation in its place and these tests would not see it
+    sup = job.graph.grad_support(job.train_idx)
+    assert (sup is not None) == grad_support, "grad support built / skipped unexpectedly"
     losses = []
     for _ in range(steps):
         loss = job.step(restrict).detach().clone()
@@ -44,6 +52,7 @@ def _run_job(rank, world, out, steps, global_frac, restrict, recompute="off"):
     corr = job.correct.clone()
     if world > 1:
         dist.all_reduce(corr)
+    DistGraph.GRAD_SUPPORT = True
     if rank == 0:
         torch.save({"losses": torch.tensor(losses, dtype=torch.float64),
                     "params": [p.detach().clone() for p in job.model.parameters()],
@@ -96,6 +105,26 @@ def test_bench_step_halo_recompute_matches_single_rank(tmp_path, world, global_f
         torch.testing.assert_close(p, q, atol=5e-5, rtol=1e-3)
     if not restrict:
         assert torch.equal(a["correct"], b["correct"])
+
+
+@pytest.mark.parametrize("world,recompute", [(2, "off"), (4, "on")])
+def test_bench_step_grad_support_on_off(tmp_path, world, recompute):
+    """The gradient support (DistGraph.prepare_grad_support: the layer below the output
+    layer aggregates transposed only from rows whose incoming gradient can be nonzero,
+    including the halo sub-plan rows and, with recomputation, the extended halo rows) is
+    exact: W ranks with the support built reproduce W ranks without it (the dense
+    transposed aggregation) and W=1."""
+    steps = 2
+    run_ranks(_run_job, world, str(tmp_path / "on.pt"), steps, 0.05, False, recompute, True,
+              timeout=600)
+    run_ranks(_run_job, world, str(tmp_path / "off.pt"), steps, 0.05, False, recompute,
+              False, timeout=600)
+    a = torch.load(tmp_path / "on.pt", weights_only=True)
+    b = torch.load(tmp_path / "off.pt", weights_only=True)
+    torch.testing.assert_close(a["losses"], b["losses"], atol=1e-6, rtol=1e-6)
+    for p, q in zip(a["params"], b["params"]):
+        torch.testing.assert_close(p, q, atol=1e-5, rtol=1e-4)
+    assert torch.equal(a["correct"], b["correct"])
 
 
 def _run_job_fused(rank, world, out, steps, global_frac):

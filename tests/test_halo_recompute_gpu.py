@@ -18,7 +18,7 @@ def _args(**kw):
     a = argparse.Namespace(shape="ogbn-papers100M", scale=2e-4, hidden=256, layers=3,
                            lr=3e-3, dtype="bf16", global_frac=0.05, window=256, seed=0,
                            no_overlap=False, rehearse_world=2, rehearse_rank=1,
-                           halo_recompute="on", cuda_graph=False)
+                           halo_recompute="on", cuda_graph=False, executor="stack")
     for k, v in kw.items():
         setattr(a, k, v)
     return a
@@ -30,6 +30,7 @@ def _run(dtype, recompute="on", steps=4):
     comm = types.SimpleNamespace(get_rank=lambda: 0, get_world_size=lambda: 1, group=None)
     dev = torch.device("cuda", 0)
     job = bench.Job(_args(halo_recompute=recompute), comm, dev, 0.05, dtype)
+    assert job.fused is None, "the layer-stack path (the one with halo recomputation)"
     assert job.recompute == (recompute == "on")
     losses = [float(job.step(False).detach()) for _ in range(steps)]
     torch.cuda.synchronize()
