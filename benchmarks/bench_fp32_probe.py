@@ -39,6 +39,13 @@ def main():
     ap.add_argument("--feats", default="128,256")
     ap.add_argument("--skip-gemm", action="store_true")
     ap.add_argument("--skip-spmm", action="store_true")
+    ap.add_argument("--gemm-modes", default="256",
+                    help="native GEMM variants (set_f32_sched tile): 256 = exact-f32 MFMA, "
+                         "128 = lean tile, 3 = bf16x3 split products")
+    ap.add_argument("--global-frac", type=float, default=0.05,
+                    help="SpMM graph: fraction of uniformly random edges (1.0 = structureless)")
+    ap.add_argument("--passes", default="64,128,256",
+                    help="row-group column-pass widths to time")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     res = {}
@@ -57,22 +64,35 @@ def main():
             print(f"[gemm] M={M} K={K_} N={N_}: {ms:.3f} ms {tf:.1f} TF/s; addmm+relu "
                   f"{ms_e:.3f} ms", flush=True)
             if N_ != 172:
+                from dgraph_amd import _native
                 from dgraph_amd.ops.f32 import gemm_f32
 
-                if K_ >= 256:  # dual form: two K/2 operands, one fused kernel
-                    h = K_ // 2
-                    x1, x2 = x[:, :h].contiguous(), x[:, h:].contiguous()
-                    ms_n = _time(lambda: gemm_f32(x1, w[:h], x2, w[h:], bias=b, relu=True,
-                                                  out=out))
-                else:
-                    ms_n = _time(lambda: gemm_f32(x, w, bias=b, relu=True, out=out))
-                ref = torch.relu(torch.addmm(b, x, w))
-                err = (out - ref).abs().max().item()
-                tfn = 2 * M * K_ * N_ / ms_n / 1e9
-                res[f"gemm_f32_K{K_}_N{N_}"] = {"ms": round(ms_n, 3), "TFps": round(tfn, 1),
-                                                "max_err": err}
-                print(f"[gemm_f32] native dual+bias+relu K={K_} N={N_}: {ms_n:.3f} ms "
-                      f"{tfn:.1f} TF/s (max err {err:.2e})", flush=True)
+                # error vs an fp64 reference, in units of sum_k |a_k b_k| (the scale an
+                # fp32 product chain's rounding error is proportional to)
+                ref64 = torch.relu(torch.addmm(b.double(), x.double(), w.double()))
+                scale = (x.abs().double() @ w.abs().double()).clamp_min(1e-30)
+                err_lib = ((out_lib := torch.relu(torch.addmm(b, x, w))).double() - ref64
+                           ).abs().div(scale).max().item()
+                del out_lib
+                for mode in [int(m) for m in a.gemm_modes.split(",")]:
+                    _native.ops().set_f32_sched(0, mode)
+                    if K_ >= 256:  # dual form: two K/2 operands, one fused kernel
+                        h = K_ // 2
+                        x1, x2 = x[:, :h].contiguous(), x[:, h:].contiguous()
+                        ms_n = _time(lambda: gemm_f32(x1, w[:h], x2, w[h:], bias=b, relu=True,
+                                                      out=out))
+                    else:
+                        ms_n = _time(lambda: gemm_f32(x, w, bias=b, relu=True, out=out))
+                    err = (out.double() - ref64).abs().div(scale).max().item()
+                    tfn = 2 * M * K_ * N_ / ms_n / 1e9
+                    res[f"gemm_f32_m{mode}_K{K_}_N{N_}"] = {
+                        "ms": round(ms_n, 3), "TFps": round(tfn, 1),
+                        "max_err_rel_sumabs": err, "torch_mm_err_rel_sumabs": err_lib}
+                    print(f"[gemm_f32] mode {mode} dual+bias+relu K={K_} N={N_}: {ms_n:.3f} ms "
+                          f"{tfn:.1f} TF/s (max err / sum|ab| {err:.2e}; torch.mm fp32 "
+                          f"{err_lib:.2e})", flush=True)
+                _native.ops().set_f32_sched(0, 256)
+                del ref64, scale
             del x, w, out
         # weight gradient x^T g over tall M
         x = torch.randn(M, 256, device=dev)
@@ -113,7 +133,7 @@ def main():
         shape = SHAPES["ogbn-papers100M"]
         if a.spmm_scale != 1.0:
             shape = shape.scaled(a.spmm_scale)
-        p = build_partition(shape, 0, 1, dev)
+        p = build_partition(shape, 0, 1, dev, global_frac=a.global_frac)
         csr = p["csr"]
         inv = csr.inv_degree()
         from dgraph_amd import _native
@@ -123,15 +143,16 @@ def main():
             x = torch.randn(p["L"], F, device=dev)
             out = torch.empty_like(x)
             nbytes = csr.nnz * (F * 4 + 4) + p["L"] * F * 4
-            for name, rg, pc in (("generic", 0, -1), ("rowgroup64", 1, 64),
-                                 ("rowgroup128", 1, 128), ("rowgroup32", 1, 32)):
+            variants = [("generic", 0, -1)] + [(f"rowgroup{w}", 1, int(w))
+                                               for w in a.passes.split(",")]
+            for name, rg, pc in variants:
                 if pc > F:
                     continue
                 ops.set_spmm_f32_config(rg, pc)
                 ms = _time(lambda: K.spmm(csr.rowptr, csr.col, x, out, row_scale=inv), reps=3)
                 res[f"spmm_f32_F{F}_{name}"] = {"ms": round(ms, 2),
                                                 "TBps_eff": round(nbytes / ms / 1e9, 2)}
-                print(f"[spmm] fp32 F={F} {name}: {ms:.2f} ms {nbytes / ms / 1e9:.2f} TB/s eff",
+                print(f"[spmm] fp32 gf={a.global_frac} F={F} {name}: {ms:.2f} ms {nbytes / ms / 1e9:.2f} TB/s eff",
                       flush=True)
             ops.set_spmm_f32_config(1, 64)
             del x, out

@@ -88,7 +88,38 @@ struct GLds {
 template <int BP>
 __device__ __forceinline__ int b_row(int k) { return k * BP + ((k >> 3) & 1) * 16; }
 
-template <int BM, int N, bool HAS_A2, bool RELU, bool HAS_BIAS, bool HAS_CIN, bool HAS_GATE>
+// ---- fp32 as three bf16 parts (x = hi + mid + lo EXACTLY for normal x: hi and mid are
+// round-to-nearest-even bf16 of x and of x - hi, lo = x - hi - mid has <= 8 significant bits).
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+__device__ __forceinline__ uint32_t rne_bf16_bits(float x) {
+  uint32_t u = __float_as_uint(x);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return u & 0xFFFF0000u;
+}
+// 8 fp32 (k order) -> packed bf16x8 hi / mid / lo (element k in half k&1 of word k>>1)
+__device__ __forceinline__ void split3(const f32x4& f0, const f32x4& f1, uint4& H, uint4& M,
+                                       uint4& Lo) {
+  uint32_t h[8], m[8], l[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const float x = k < 4 ? f0[k] : f1[k - 4];
+    h[k] = rne_bf16_bits(x);
+    const float r1 = x - __uint_as_float(h[k]);
+    m[k] = rne_bf16_bits(r1);
+    l[k] = __float_as_uint(r1 - __uint_as_float(m[k]));
+  }
+  auto pk = [](uint32_t lo_e, uint32_t hi_e) { return __builtin_amdgcn_perm(hi_e, lo_e, 0x07060302u); };
+  H = uint4{pk(h[0], h[1]), pk(h[2], h[3]), pk(h[4], h[5]), pk(h[6], h[7])};
+  M = uint4{pk(m[0], m[1]), pk(m[2], m[3]), pk(m[4], m[5]), pk(m[6], m[7])};
+  Lo = uint4{pk(l[0], l[1]), pk(l[2], l[3]), pk(l[4], l[5]), pk(l[6], l[7])};
+}
+__device__ __forceinline__ f32x4 mfma_bf(const uint4& a, const uint4& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                 __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+
+template <int BM, int N, bool HAS_A2, bool RELU, bool HAS_BIAS, bool HAS_CIN, bool HAS_GATE,
+          bool X3 = false>
 __device__ __forceinline__ void gemm_f32_body(
     const float* __restrict__ A1, int64_t lda1, int K1, const float* __restrict__ B1,
     int64_t ldb1, const float* __restrict__ A2, int64_t lda2, int K2,
@@ -222,7 +253,36 @@ __device__ __forceinline__ void gemm_f32_body(
         af[a][1] = *reinterpret_cast<const f32x4*>(p + a_chunk(r, 2 * lh + 1) * 4);
       }
       const float* sbw = sb + b_row<L::BP>(8 * lh) + bcol_w + li;
-      if constexpr (BM == 256) {
+      if constexpr (X3) {
+        // one 16x16x32 bf16 MFMA per (a, b, product) covers the whole 32-deep stage: the six
+        // products of the split operands whose magnitude reaches fp32 rounding, smallest
+        // first (a_lo b_hi, a_hi b_lo, a_mid b_mid, a_mid b_hi, a_hi b_mid, a_hi b_hi); the
+        // dropped terms (mid*lo, lo*mid, lo*lo) are <= 2^-24 |a b| together
+        uint4 ah[TM], am[TM], al[TM];
+#pragma unroll
+        for (int a = 0; a < TM; ++a) split3(af[a][0], af[a][1], ah[a], am[a], al[a]);
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+          f32x4 b0, b1;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            b0[j] = sbw[j * L::BP + b * 16];
+            b1[j] = sbw[(j + 4) * L::BP + b * 16];
+          }
+          uint4 bh, bm, bl;
+          split3(b0, b1, bh, bm, bl);
+#pragma unroll
+          for (int a = 0; a < TM; ++a) {
+            f32x4 c = acc[a][b];
+            c = mfma_bf(al[a], bh, c);
+            c = mfma_bf(ah[a], bl, c);
+            c = mfma_bf(am[a], bm, c);
+            c = mfma_bf(am[a], bh, c);
+            c = mfma_bf(ah[a], bm, c);
+            acc[a][b] = mfma_bf(ah[a], bh, c);
+          }
+        }
+      } else if constexpr (BM == 256) {
         // B fragments double-buffered across MFMA steps: step j+1's LDS reads are issued
         // before step j's TM*TN MFMAs
         float bf[2][TN];
@@ -317,6 +377,12 @@ __global__ __launch_bounds__(512, 1) void gemm_f32_kernel(DG_GEMM_F32_ARGS) {
   gemm_f32_body<256, N, HAS_A2, RELU, HAS_BIAS, HAS_CIN, HAS_GATE>(DG_GEMM_F32_PASS);
 }
 
+// fp32 products as bf16x3 split MFMAs (same tile as gemm_f32_kernel)
+template <int N, bool HAS_A2, bool RELU, bool HAS_BIAS, bool HAS_CIN, bool HAS_GATE>
+__global__ __launch_bounds__(512, 1) void gemm_f32_x3_kernel(DG_GEMM_F32_ARGS) {
+  gemm_f32_body<256, N, HAS_A2, RELU, HAS_BIAS, HAS_CIN, HAS_GATE, true>(DG_GEMM_F32_PASS);
+}
+
 // lean tile: one wave per SIMD; its registers (<= 256) leave the rest of the file to a
 // co-resident kernel
 template <int N, bool HAS_A2, bool RELU, bool HAS_BIAS, bool HAS_CIN, bool HAS_GATE>
@@ -324,7 +390,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void g
   gemm_f32_body<128, N, HAS_A2, RELU, HAS_BIAS, HAS_CIN, HAS_GATE>(DG_GEMM_F32_PASS);
 }
 
-// row tile of the next launches: 256 (default) or 128 (lean; set_gemm_f32_tile)
+// row tile of the next launches: 256 (default) or 128 (lean; set_gemm_f32_tile); 3 = the
+// 256-row tile with bf16x3 split products
 int g_gemm_f32_bm = 256;
 
 template <int N, bool HAS_A2, bool RELU, bool HAS_BIAS, bool HAS_CIN, bool HAS_GATE>
@@ -335,16 +402,19 @@ hipError_t launch_gemm_f32(const float* A1, int64_t lda1, int K1, const float* B
                            int64_t ldg, const int64_t* o_rows, const float* rsc, float* out,
                            int64_t ldo, int64_t M, hipStream_t st) {
   const bool lean = g_gemm_f32_bm == 128;
+  const bool x3 = g_gemm_f32_bm == 3;
   auto kern = lean ? &gemm_f32_lean_kernel<N, HAS_A2, RELU, HAS_BIAS, HAS_CIN, HAS_GATE>
+              : x3 ? &gemm_f32_x3_kernel<N, HAS_A2, RELU, HAS_BIAS, HAS_CIN, HAS_GATE>
                    : &gemm_f32_kernel<N, HAS_A2, RELU, HAS_BIAS, HAS_CIN, HAS_GATE>;
   const int kBM = lean ? 128 : 256;
   const size_t lds = lean ? GLds<128, N>::BYTES : GLds<256, N>::BYTES;
   static_assert(GLds<256, N>::BYTES <= 160 * 1024, "LDS budget");
-  static bool attr[2] = {false, false};
-  if (!attr[lean]) {
+  static bool attr[3] = {false, false, false};
+  const int ai = lean ? 1 : x3 ? 2 : 0;
+  if (!attr[ai]) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
-    attr[lean] = true;
+    attr[ai] = true;
   }
   static int num_cus = 0;
   if (num_cus == 0) {
@@ -411,7 +481,7 @@ inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) =
 
 }  // namespace
 
-void set_gemm_f32_tile(int bm) { g_gemm_f32_bm = bm == 128 ? 128 : 256; }
+void set_gemm_f32_tile(int bm) { g_gemm_f32_bm = (bm == 128 || bm == 3) ? bm : 256; }
 
 bool gemm_f32_supported(int64_t N, int64_t K1, int64_t K2) {
   return (N == 64 || N == 128 || N == 176 || N == 192 || N == 256) && K1 > 0 &&

@@ -48,6 +48,8 @@ from ..parallel.dist_graph import DistGraph
 
 # rows per chunk of the row-chunked passes (0 = auto from free memory)
 CHUNK_ROWS = int(os.environ.get("DGRAPH_FUSED_CHUNK_ROWS", "0"))
+# W > 1: overlap each forward halo exchange with the next layer's interior aggregation
+OVERLAP_FWD = os.environ.get("DGRAPH_FUSED_OVERLAP", "1") != "0"
 
 
 def _ranges(n: int, step: int) -> List[Tuple[int, int]]:
@@ -207,8 +209,17 @@ class FusedSAGE:
         self.u_sep = 2 * self.nS + nT > L
         other = 4 * nT * self.Cg + 5 * 4 * 256 * 256 * 256 + (3 << 29) + \
             (4 * nT * self.hid if self.u_sep else 0)
-        spare = max(free - need_h - other, 1 << 28)
         wA, wB = max(self.hid, self.d0), max(self.Cp, self.hid)
+        # W > 1: a whole-layer aggregate buffer lets the interior aggregation of EVERY row run
+        # while the previous layer's halo rows are in flight (the halo part and the GEMMs
+        # follow once they land); without room for it the exchange is waited for up front
+        self.agg_full = None
+        need_full = L * wA * 4
+        if graph.halo is not None and OVERLAP_FWD and free - need_h - other - need_full > (
+                16 << 30 if dev.type == "cuda" else 0):
+            self.agg_full = torch.empty(L, wA, dtype=torch.float32, device=dev)
+            other += need_full
+        spare = max(free - need_h - other, 1 << 28)
         per_row = 4 * 2 * (wA + wB)  # two aggregate + two logit/gradient chunk buffers
         cr = chunk_rows or CHUNK_ROWS
         if cr <= 0:
@@ -343,12 +354,57 @@ class FusedSAGE:
                          row_map=rmap, gate=gate)
         return o
 
-    def _exchange(self, h: torch.Tensor) -> Optional[torch.Tensor]:
-        """Halo rows of ``h`` from their owners (forward all-to-all-v), None at W=1."""
+    def _exchange(self, h: torch.Tensor):
+        """Start the halo rows of ``h`` on their way from their owners (forward all-to-all-v,
+        asynchronous): ``(recv, work)``, or None at W=1."""
         g = self.g
         if g.halo is None:
             return None
-        return g.a2a(K.gather_rows(h, g.send_map.idx))
+        return g.a2a(K.gather_rows(h, g.send_map.idx), async_op=True)
+
+    def _layer(self, hin: torch.Tensor, halo, consume, width: int, name: str):
+        """Aggregate every row chunk of ``hin`` (interior + halo part) and hand it to
+        ``consume(ci, agg, k)``. ``halo``: None (W=1), the received halo rows, or a pending
+        ``(recv, work)`` exchange. With a pending exchange and the whole-layer aggregate
+        buffer, the interior aggregation of all chunks runs first — while the halo rows are
+        on the links — then the exchange is waited for and the halo parts and the GEMMs
+        follow chunk by chunk. Returns the halo rows (for the backward)."""
+        items = [ci for ci, (r0, r1) in enumerate(self.chunks) if r1 > r0]
+        if isinstance(halo, tuple) and self.agg_full is not None:
+            recv, work = halo
+            af = self.agg_full[:, :width]
+            it = self.it
+            for ci in items:
+                r0, r1 = self.chunks[ci]
+                F32.spmm_f32(it.rowptr[r0:r1 + 1], it.col, hin, af[r0:r1],
+                             row_scale=self.inv_deg[r0:r1])
+            self._mark(f"exchange_{name}")
+            work.wait()
+            self._mark(name)
+
+            def produce(ci, k):
+                r0, r1 = self.chunks[ci]
+                hr = self.ch_halo[ci]
+                if hr is not None:
+                    rp, rmap, _ = hr
+                    F32.spmm_f32(rp, self.hcomp.col, recv, af[r0:r1], beta=1.0, row_map=rmap,
+                                 row_scale=self.inv_deg[r0:r1])
+                return af[r0:r1]
+
+            self.pipe.run(items, produce, consume)
+            return recv
+        if isinstance(halo, tuple):
+            recv, work = halo
+            self._mark(f"exchange_{name}")
+            work.wait()
+            self._mark(name)
+            halo = recv
+
+        def produce(ci, k):
+            return self._agg_chunk(hin, halo, ci, self.bufA2[k][:, :width])
+
+        self.pipe.run(items, produce, consume)
+        return halo
 
     def _params(self):
         out = []
@@ -377,7 +433,7 @@ class FusedSAGE:
         nnz_h = self.halo.nnz if self.halo is not None else 0
         # ---------------- forward: hidden layers
         hin, hin_halo = x, (g._static_halo(x) if g.halo is not None else None)
-        halos = [hin_halo]
+        halos = []
         for l in range(nl - 1):
             ws, wn, b = P[l]
             if l == 0:
@@ -386,22 +442,16 @@ class FusedSAGE:
                 ws, wn = ws.detach().contiguous(), wn.detach().contiguous()
             hout = self.h[l]
             bias = b.detach()
-            items = [ci for ci, (r0, r1) in enumerate(self.chunks) if r1 > r0]
-
-            def produce(ci, k, hin=hin, hin_halo=hin_halo):
-                return self._agg_chunk(hin, hin_halo, ci, self.bufA2[k][:, :hin.shape[1]])
 
             def consume(ci, a, k, hin=hin, hout=hout, ws=ws, wn=wn, bias=bias):
                 r0, r1 = self.chunks[ci]
                 F32.gemm_f32(hin[r0:r1], ws, a, wn, bias=bias, relu=True, out=hout[r0:r1])
 
-            self.pipe.run(items, produce, consume)
+            halos.append(self._layer(hin, hin_halo, consume, hin.shape[1], f"fwd_l{l}"))
             self.edges_aggregated += nnz_it + nnz_h
             hin = hout
-            if g.halo is not None:
-                self._mark(f"exchange_fwd_h{l + 1}")
+            # this layer's halo rows leave now and land while the next layer aggregates
             hin_halo = self._exchange(hout)
-            halos.append(hin_halo)
             self._mark(f"fwd_l{l + 1}" if l + 1 < nl - 1 else "fwd_out")
         # ---------------- forward: output layer (all rows), loss and eval on the fly
         ws, wn, b = P[nl - 1]
@@ -413,14 +463,11 @@ class FusedSAGE:
         bp[:C] = b.detach()
         self.acc_out_s.reset()
         self.acc_out_n.reset()
-        hl, hl_halo = hin, hin_halo
-        items = [ci for ci, (r0, r1) in enumerate(self.chunks) if r1 > r0]
-
-        def produce_out(ci, k):
-            return self._agg_chunk(hl, hl_halo, ci, self.bufA2[k][:, :hid])
-
-        self.pipe.run(items, produce_out,
-                      lambda ci, a, k: self._out_chunk(ci, a, k, hl, wsp, wnp, bp))
+        hl = hin
+        hl_halo = self._layer(hl, hin_halo, lambda ci, a, k: self._out_chunk(ci, a, k, hl, wsp,
+                                                                             wnp, bp),
+                              hid, "fwd_out")
+        halos.append(hl_halo)
         self.edges_aggregated += nnz_it + nnz_h
         # per-row losses / hits summed once, in a fixed order
         loss = self.row_loss.sum() * self.inv_n

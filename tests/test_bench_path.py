@@ -138,6 +138,8 @@ def _run_job_fused(rank, world, out, steps, global_frac):
                           executor="auto"), comm, torch.device("cpu"), global_frac,
                     torch.float32)
     assert job.fused is not None, "hidden 256 fp32 must take the fused executor"
+    if world > 1:  # the forward exchanges overlap the next layer's interior aggregation
+        assert job.fused.agg_full is not None
     grads = []
     orig = job.opt.step
 
