@@ -500,6 +500,8 @@ def main():
     alloc_timed = dict(getattr(job, "alloc_timed", {}))
     regions = region_breakdown(job)
     use_fused = job.use_fused
+    pass_for = {str(k): v for k, v in getattr(job.fused, "pass_for", {}).items()} \
+        if job.fused is not None else {}
     if args.profile_ops:
         _profile_one_step(lambda: job.step(head_restrict), args.profile_ops, rank)
     E_msg, n_train, halo_total = job.E_msg, job.n_train, job.halo_total
@@ -533,6 +535,9 @@ def main():
             "edges_aggregated_per_step": s_e, "E_msg": sjob.E_msg,
             "halo_rows_total": sjob.halo_total, "steps": ks, "warmup": 1,
             "final_loss": s_loss, **sjob.halo_stats()}
+        if sjob.fused is not None:
+            extra["structureless"]["spmm_pass_cols"] = {
+                str(k): v for k, v in sjob.fused.pass_for.items()}
         if mlog is not None:
             mlog.metrics(phase="structureless", **extra["structureless"])
         sjob.free()
@@ -610,6 +615,7 @@ def main():
                          "from the same forward + backward + allreduce + Adam"),
                 "launch": "HIP graph replay" if args.cuda_graph else "eager",
                 "halo_recompute": job_recompute,
+                **({"spmm_pass_cols": pass_for} if pass_for else {}),
                 "precision": ("bf16 storage/compute, fp32 accumulate, fp32 master weights"
                               if dtype == torch.bfloat16 else
                               "fp32 storage and compute (exact-f32 MFMA GEMMs, fp32 SpMM "

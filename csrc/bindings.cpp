@@ -283,6 +283,47 @@ at::Tensor col_sum_op(const at::Tensor& g) {
   return partial.sum(0);
 }
 
+// y = act(z + b) (act: 0 identity, 1 SiLU, 2 ReLU); z, y 2-D row-strided, b fp32 [F] or None
+void bias_act_op(const at::Tensor& z, const c10::optional<at::Tensor>& b, int64_t act,
+                 const at::Tensor& y) {
+  check_dev(z, z, "z");
+  check_dev(y, z, "y");
+  check_rows(z, "z");
+  check_rows(y, "y");
+  TORCH_CHECK(z.sizes() == y.sizes() && z.scalar_type() == y.scalar_type(), "z / y mismatch");
+  const float* bp = opt_f32(b, z, "b");
+  if (bp) TORCH_CHECK(b->numel() == z.size(1) && b->is_contiguous(), "b must be [F]");
+  c10::DeviceGuard gd(z.device());
+  DG_HIP_CHECK(bias_act_fwd(dtype_of(z), static_cast<int>(act), z.data_ptr(), z.stride(0), bp,
+                            y.data_ptr(), y.stride(0), z.size(0), static_cast<int>(z.size(1)),
+                            cur_stream(z)));
+}
+
+// dz = dy * act'(z + b); returns the bias gradient sum_rows dz (fp32, fixed order)
+at::Tensor bias_act_bwd_op(const at::Tensor& dy, const at::Tensor& z,
+                           const c10::optional<at::Tensor>& b, int64_t act,
+                           const at::Tensor& dz) {
+  check_dev(dy, z, "dy");
+  check_dev(dz, z, "dz");
+  check_rows(dy, "dy");
+  check_rows(z, "z");
+  check_rows(dz, "dz");
+  TORCH_CHECK(dy.sizes() == z.sizes() && dz.sizes() == z.sizes(), "shape mismatch");
+  TORCH_CHECK(dy.scalar_type() == z.scalar_type() && dz.scalar_type() == z.scalar_type(),
+              "dtype mismatch");
+  const float* bp = opt_f32(b, z, "b");
+  if (bp) TORCH_CHECK(b->numel() == z.size(1) && b->is_contiguous(), "b must be [F]");
+  const int64_t L = z.size(0), F = z.size(1);
+  const int64_t nb = std::max<int64_t>(1, std::min<int64_t>(1024, (L + 255) / 256));
+  auto partial = at::empty({nb, F}, z.options().dtype(at::kFloat));
+  c10::DeviceGuard gd(z.device());
+  DG_HIP_CHECK(bias_act_bwd(dtype_of(z), static_cast<int>(act), dy.data_ptr(), dy.stride(0),
+                            z.data_ptr(), z.stride(0), bp, dz.data_ptr(), dz.stride(0), L,
+                            static_cast<int>(F), partial.data_ptr<float>(),
+                            static_cast<int>(nb), cur_stream(z)));
+  return partial.sum(0);
+}
+
 // out[r, :] = x[r, :] * s[r] for a row-strided 2-D x (a column slice of a wider tensor)
 void row_scale_cols_op(const at::Tensor& x, const at::Tensor& s, const at::Tensor& out) {
   check_dev(x, x, "x");
@@ -706,6 +747,8 @@ TORCH_LIBRARY(dgraph_amd, m) {
   m.def("bias_relu_pack(Tensor(a!) y, Tensor? bias, Tensor(b!)? bits, bool relu) -> ()");
   m.def("relu_mask_bwd(Tensor(a!) g, Tensor bits) -> ()");
   m.def("col_sum(Tensor g) -> Tensor");
+  m.def("bias_act(Tensor z, Tensor? b, int act, Tensor(a!) y) -> ()");
+  m.def("bias_act_bwd(Tensor dy, Tensor z, Tensor? b, int act, Tensor(a!) dz) -> Tensor");
   m.def("row_scale_cols(Tensor x, Tensor s, Tensor(a!) out) -> ()");
   m.def("row_scale_colsum(Tensor x, Tensor s, Tensor(a!) out, Tensor(b!) partial) -> ()");
   m.def("pair_relu(Tensor rowptr, Tensor col, int mode, Tensor rowterm, Tensor gat, Tensor? gat2, "
@@ -749,6 +792,8 @@ TORCH_LIBRARY_IMPL(dgraph_amd, CUDA, m) {
   m.impl("bias_relu_pack", &dgraph::bias_relu_pack_op);
   m.impl("relu_mask_bwd", &dgraph::relu_mask_bwd_op);
   m.impl("col_sum", &dgraph::col_sum_op);
+  m.impl("bias_act", &dgraph::bias_act_op);
+  m.impl("bias_act_bwd", &dgraph::bias_act_bwd_op);
   m.impl("row_scale_cols", &dgraph::row_scale_cols_op);
   m.impl("row_scale_colsum", &dgraph::row_scale_colsum_op);
   m.impl("pair_relu", &dgraph::pair_relu_op);

@@ -124,6 +124,13 @@ hipError_t row_scale_colsum(const void* x, int64_t ldx, const float* s, void* ou
 hipError_t row_scale_cols(DType dt, const void* x, int64_t ldx, const float* s, void* out,
                           int64_t ldo, int64_t L, int w, hipStream_t stream);
 
+// fused bias + activation (act.hip): act 0 identity, 1 SiLU, 2 ReLU; F <= 256 (vector lanes)
+hipError_t bias_act_fwd(DType dt, int act, const void* z, int64_t ldz, const float* b, void* y,
+                        int64_t ldy, int64_t M, int F, hipStream_t st);
+hipError_t bias_act_bwd(DType dt, int act, const void* dy, int64_t lddy, const void* z,
+                        int64_t ldz, const float* b, void* dz, int64_t lddz, int64_t M, int F,
+                        float* partial, int nblocks, hipStream_t st);
+
 // ---------------------------------------------------------------------------
 // Fused edge-MLP kernels (edge_fused.hip, K-new-6). mode 0: out[r] = sum relu(R[r]+X[c]);
 // mode 1: out[r] = M[r] * #{c : R[r]+X[c] > 0}; mode 2: out[r] = sum X2[c]*[R[r]+X[c] > 0].

@@ -26,6 +26,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops.act import linear_act
 from ..ops.aggregate import scatter_sum
 from ..ops.dense import linear
 from ..ops.norm import layer_norm
@@ -82,6 +83,14 @@ class Config:
     model: ModelConfig = field(default_factory=ModelConfig)
 
 
+def _act_name(act: nn.Module) -> str:
+    if isinstance(act, nn.SiLU):
+        return "silu"
+    if isinstance(act, nn.ReLU):
+        return "relu"
+    raise NotImplementedError(f"fused layers support SiLU/ReLU, got {act}")
+
+
 class MeshGraphMLP(nn.Module):
     def __init__(self, input_dim: int, output_dim: int, hidden_dim: int = 512,
                  hidden_layers: int = 1, activation_fn: Optional[nn.Module] = None,
@@ -99,8 +108,17 @@ class MeshGraphMLP(nn.Module):
 
     def _run(self, h: torch.Tensor, start: int, residual=None) -> torch.Tensor:
         mods = list(self._model)[start:]
+        skip = False
         for i, m in enumerate(mods):
-            if isinstance(m, nn.Linear):
+            if skip:  # the activation already applied by linear_act
+                skip = False
+                continue
+            if isinstance(m, nn.Linear) and i + 1 < len(mods) and \
+                    isinstance(mods[i + 1], (nn.SiLU, nn.ReLU)):
+                # Linear + bias + activation: one product and one fused pass each way
+                h = linear_act([(h, m.weight)], m.bias, _act_name(mods[i + 1]))
+                skip = True
+            elif isinstance(m, nn.Linear):
                 h = linear(h, m.weight, m.bias)
             elif isinstance(m, nn.LayerNorm) and i == len(mods) - 1:
                 h = layer_norm(h, m.weight, m.bias, m.eps, residual)  # residual fused
@@ -117,12 +135,7 @@ class MeshGraphMLP(nn.Module):
         return self._run(h, 2, residual)
 
     def first_act_name(self) -> str:
-        act = self._model[1]
-        if isinstance(act, nn.SiLU):
-            return "silu"
-        if isinstance(act, nn.ReLU):
-            return "relu"
-        raise NotImplementedError(f"fused first layer supports SiLU/ReLU, got {act}")
+        return _act_name(self._model[1])
 
 
 class MeshEdgeBlock(nn.Module):
@@ -183,9 +196,11 @@ class MeshNodeBlock(nn.Module):
         agg = scatter_sum(edge_features, agg_map)
         lin = self.mesh_mlp._model[0]
         n = self.node_dim
-        h = linear(node_features, lin.weight[:, :n], lin.bias)
-        h = h + linear(agg.to(h.dtype), lin.weight[:, n:])
-        h = self.mesh_mlp._model[1](h)
+        # the first Linear over [x || agg] as two terms of one product, bias and activation
+        # fused (no concatenation, no separate add / activation passes)
+        h = linear_act([(node_features, lin.weight[:, :n]),
+                        (agg.to(node_features.dtype), lin.weight[:, n:])], lin.bias,
+                       self.mesh_mlp.first_act_name())
         return self.mesh_mlp.tail(h, residual=node_features)
 
     def forward(self, node_features, edge_features, src_indices, rank_mapping=None):

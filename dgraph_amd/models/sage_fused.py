@@ -293,6 +293,7 @@ class FusedSAGE:
         self.correct = torch.zeros(2, dtype=torch.long, device=dev)
         self.record = False
         self._events: list = []
+        self._tune_passes()
 
     # ------------------------------------------------------------------ regions
     def _mark(self, name: str):
@@ -325,6 +326,50 @@ class FusedSAGE:
         self.g.edges_aggregated = v
 
     # ------------------------------------------------------------------ helpers
+    def _spmm(self, rowptr, col, x, out=None, **kw):
+        """fp32 SpMM at the column-pass width tuned for ``x``'s width (``_tune_passes``)."""
+        kw.setdefault("pass_cols", self.pass_for.get(x.shape[1], 0))
+        return F32.spmm_f32(rowptr, col, x, out, **kw)
+
+    def _tune_passes(self) -> None:
+        """Column-pass width per operand width, measured once on this graph: on a graph with
+        locality, narrow (64-column) passes keep each pass's window of neighbour rows in the
+        L2 / Infinity Cache; on a structureless one every neighbour row is a random HBM
+        access and full-width passes read each row once, in one long burst, instead of once
+        per pass (and touch its page once). Times the first row chunk's aggregation at each
+        width (DGRAPH_FUSED_PASS_COLS forces one)."""
+        self.pass_for = {}
+        forced = int(os.environ.get("DGRAPH_FUSED_PASS_COLS", "0"))
+        if forced:
+            self.pass_for = {self.d0: min(forced, self.d0), self.hid: min(forced, self.hid)}
+            return
+        if self.dev.type != "cuda" or os.environ.get("DGRAPH_FUSED_PASS_TUNE", "1") == "0":
+            return
+        r0, r1 = self.chunks[0]
+        it = self.it
+        for w, src in ((self.d0, self.x), (self.hid, self.h[0])):
+            o = self.bufA2[0][:r1 - r0, :w]
+            best = None
+            for pc in (64, 128, 256):
+                if pc > w:
+                    continue
+
+                def call(pc=pc, src=src, o=o):
+                    F32.spmm_f32(it.rowptr[r0:r1 + 1], it.col, src, o,
+                                 row_scale=self.inv_deg[r0:r1], pass_cols=pc)
+
+                call()
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                call()
+                call()
+                b.record()
+                b.synchronize()
+                ms = a.elapsed_time(b)
+                if best is None or ms < 0.95 * best[0]:  # wider only when clearly faster
+                    best = (ms, pc)
+            self.pass_for[w] = best[1]
+
     @staticmethod
     def _halo_range(csr, r0: int, r1: int):
         """Rows [k0, k1) of a row-compacted CSR whose output rows fall in [r0, r1), with
@@ -345,12 +390,12 @@ class FusedSAGE:
         n = r1 - r0
         o = out[:n]
         it = self.it
-        F32.spmm_f32(it.rowptr[r0:r1 + 1], it.col, xin, o, row_scale=self.inv_deg[r0:r1],
+        self._spmm(it.rowptr[r0:r1 + 1], it.col, xin, o, row_scale=self.inv_deg[r0:r1],
                      gate=gate)
         hr = self.ch_halo[ci]
         if xhalo is not None and hr is not None:
             rp, rmap, _ = hr
-            F32.spmm_f32(rp, self.hcomp.col, xhalo, o, row_scale=self.inv_deg[r0:r1], beta=1.0,
+            self._spmm(rp, self.hcomp.col, xhalo, o, row_scale=self.inv_deg[r0:r1], beta=1.0,
                          row_map=rmap, gate=gate)
         return o
 
@@ -376,7 +421,7 @@ class FusedSAGE:
             it = self.it
             for ci in items:
                 r0, r1 = self.chunks[ci]
-                F32.spmm_f32(it.rowptr[r0:r1 + 1], it.col, hin, af[r0:r1],
+                self._spmm(it.rowptr[r0:r1 + 1], it.col, hin, af[r0:r1],
                              row_scale=self.inv_deg[r0:r1])
             self._mark(f"exchange_{name}")
             work.wait()
@@ -387,7 +432,7 @@ class FusedSAGE:
                 hr = self.ch_halo[ci]
                 if hr is not None:
                     rp, rmap, _ = hr
-                    F32.spmm_f32(rp, self.hcomp.col, recv, af[r0:r1], beta=1.0, row_map=rmap,
+                    self._spmm(rp, self.hcomp.col, recv, af[r0:r1], beta=1.0, row_map=rmap,
                                  row_scale=self.inv_deg[r0:r1])
                 return af[r0:r1]
 
@@ -518,16 +563,16 @@ class FusedSAGE:
         work = None
         if self.sub is not None:
             ht_nz, a2a_sub, stc, stc_rows = self.sub
-            hg = F32.spmm_f32(ht_nz.rowptr, ht_nz.col, u2)
+            hg = self._spmm(ht_nz.rowptr, ht_nz.col, u2)
             sg, work = a2a_sub(hg, async_op=True)
             self.edges_aggregated += ht_nz.nnz
-        F32.spmm_f32(self.AT_S.rowptr, self.AT_S.col, u2, dZ)
+        self._spmm(self.AT_S.rowptr, self.AT_S.col, u2, dZ)
         self.edges_aggregated += self.AT_S.nnz
         if work is not None:
             self._mark("exchange_bwd_out")
             work.wait()
             self._mark("bwd_out")
-            F32.spmm_f32(stc.rowptr, stc.col, sg, dZ, beta=1.0, row_map=stc_rows)
+            self._spmm(stc.rowptr, stc.col, sg, dZ, beta=1.0, row_map=stc_rows)
             del sg, hg
         F32.gemm_f32(self.dz, ws_t, cin=dZ, o_rows=self.posT, out=dZ)
         F32.apply_keep_bits(dZ, self.bits)
@@ -546,7 +591,7 @@ class FusedSAGE:
             u = F32.gemm_f32(dZ, wn1.detach().t().contiguous(), row_scale=self.invdegS,
                              out=self.u)
             if self.haloT is not None:
-                hg1 = F32.spmm_f32(self.haloT.rowptr, self.haloT.col, u, col_map=self.smap)
+                hg1 = self._spmm(self.haloT.rowptr, self.haloT.col, u, col_map=self.smap)
                 sg1, work = g.a2a_rev(hg1, async_op=True)
                 self.edges_aggregated += self.haloT.nnz
         self.acc_hid_s.reset()
@@ -555,10 +600,10 @@ class FusedSAGE:
             s0, s1 = sr
             rows = self.S[s0:s1]
             aS = self.bufA2[k][:s1 - s0, :hin_l.shape[1]]
-            F32.spmm_f32(self.it.rowptr, self.it.col, hin_l, aS, row_ids=rows,
+            self._spmm(self.it.rowptr, self.it.col, hin_l, aS, row_ids=rows,
                          row_scale=self.invdegS[s0:s1])
             if hin_l_halo is not None:
-                F32.spmm_f32(self.halo.rowptr, self.halo.col, hin_l_halo, aS, row_ids=rows,
+                self._spmm(self.halo.rowptr, self.halo.col, hin_l_halo, aS, row_ids=rows,
                              row_scale=self.invdegS[s0:s1], beta=1.0)
             return aS
 
@@ -594,13 +639,13 @@ class FusedSAGE:
                 r0, r1 = self.chunks[ci]
                 n = r1 - r0
                 gz = self.bufB2[k][:n, :hid]
-                F32.spmm_f32(self.it.rowptr[r0:r1 + 1], self.it.col, u, gz, col_map=self.smap,
+                self._spmm(self.it.rowptr[r0:r1 + 1], self.it.col, u, gz, col_map=self.smap,
                              gate=h1[r0:r1], self_add=v,
                              self_map=self.smap if v is not None else None, self_row0=r0)
                 sr = self.ch_send[ci]
                 if work is not None and sr is not None:
                     rp, rmap, _ = sr
-                    F32.spmm_f32(rp, self.send_st.col, sg1, gz, beta=1.0, row_map=rmap,
+                    self._spmm(rp, self.send_st.col, sg1, gz, beta=1.0, row_map=rmap,
                                  gate=h1[r0:r1])
                 a0 = self._agg_chunk(x, x_halo, ci, self.bufA2[k][:, :self.d0])
                 return gz, a0

@@ -18,19 +18,25 @@ from .. import _native
 
 
 # ------------------------------------------------------------------------------ SpMM
+DEFAULT_PASS_COLS = 64  # csrc/kernels/spmm_f32.hip g_f32_pass_cols
+
+
 def spmm_f32(rowptr: torch.Tensor, col: torch.Tensor, x: torch.Tensor,
              out: Optional[torch.Tensor] = None, *, row_scale=None, col_scale=None,
              edge_weight=None, col_map: Optional[torch.Tensor] = None,
              row_ids: Optional[torch.Tensor] = None, beta: float = 0.0,
              row_map: Optional[torch.Tensor] = None,
              gate: Optional[torch.Tensor] = None, self_add: Optional[torch.Tensor] = None,
-             self_map: Optional[torch.Tensor] = None, self_row0: int = 0) -> torch.Tensor:
+             self_map: Optional[torch.Tensor] = None, self_row0: int = 0,
+             pass_cols: int = 0) -> torch.Tensor:
     """``out[o(i)] = row_scale[o(i)] * sum_j w_j x[m(col_j)] + beta * out[o(i)]`` over the
     entries of CSR row ``row_ids[i]`` (all rows when None); ``m = col_map`` (entries with
     ``col_map < 0`` skipped) or identity; ``o = row_map`` or identity. ``gate`` (indexed
     like ``out``): the stored value is kept where ``gate > 0`` (a ReLU derivative).
     ``self_add``: output row o also gets ``self_add[self_map[self_row0 + o]]`` (when >= 0),
-    before the gate."""
+    before the gate. ``pass_cols`` (GPU): the column-pass width of this call (0 = the
+    current default, 64): narrow passes keep a locality window in the caches, full-width
+    passes make each random row access one long read (see FusedSAGE's autotune)."""
     n = row_ids.numel() if row_ids is not None else rowptr.numel() - 1
     if out is None:
         if row_map is not None:
@@ -38,9 +44,16 @@ def spmm_f32(rowptr: torch.Tensor, col: torch.Tensor, x: torch.Tensor,
         out = torch.empty(n, x.shape[1], dtype=x.dtype, device=x.device)
         beta = 0.0
     if x.is_cuda:
-        _native.ops().spmm_f32_ex(rowptr, col, edge_weight, col_scale, row_scale, col_map,
-                                  row_ids, x, out, float(beta), 0, row_map, gate, self_add,
-                                  self_map, int(self_row0))
+        ops = _native.ops()
+        if pass_cols:
+            ops.set_spmm_f32_config(-1, int(pass_cols))
+        try:
+            ops.spmm_f32_ex(rowptr, col, edge_weight, col_scale, row_scale, col_map, row_ids, x,
+                            out, float(beta), 0, row_map, gate, self_add, self_map,
+                            int(self_row0))
+        finally:
+            if pass_cols:
+                ops.set_spmm_f32_config(-1, DEFAULT_PASS_COLS)
         return out
     # CPU reference (fp64 accumulation)
     rp = rowptr.long()
