@@ -388,7 +388,7 @@ def region_breakdown(job: "Job") -> dict:
     to max / min over ranks, plus the halo bytes each rank sent per peer during that step
     and the achieved bytes per second over its exposed exchange time."""
     ex = job.fused
-    if ex is None or job.dev.type != "cuda":
+    if ex is None:
         return {}
     from dgraph_amd.comm.alltoallv import CommStats
 
@@ -527,24 +527,42 @@ def main():
         gc.collect()
         if dev.type == "cuda":
             torch.cuda.empty_cache()
-        sjob = Job(args, comm, dev, 1.0, dtype)
-        s_ms, s_loss, s_e = timed(sjob, ks, 1, head_restrict)
-        extra["structureless"] = {
-            "global_frac": 1.0, "ms_per_step": s_ms,
-            "edges_per_s": args.layers * sjob.E_msg / (s_ms / 1000.0),
-            "edges_aggregated_per_step": s_e, "E_msg": sjob.E_msg,
-            "halo_rows_total": sjob.halo_total, "steps": ks, "warmup": 1,
-            "final_loss": s_loss, **sjob.halo_stats()}
-        if sjob.fused is not None:
-            extra["structureless"]["spmm_pass_cols"] = {
-                str(k): v for k, v in sjob.fused.pass_for.items()}
-        if mlog is not None:
-            mlog.metrics(phase="structureless", **extra["structureless"])
-        sjob.free()
+        # structureless secondary: built on every rank; a configuration that does not fit
+        # (the fused executor plans its memory and raises before allocating, e.g. fp32 halo
+        # rows of a structureless graph at W > 1) is skipped on every rank alike
+        try:
+            sjob = Job(args, comm, dev, 1.0, dtype)
+            ok = 1
+        except MemoryError as e:
+            sjob, ok = None, 0
+            log(rank, f"structureless extra skipped: {e}")
+        okt = torch.tensor([ok], dtype=torch.long, device=dev)
+        if world > 1:
+            dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+        if int(okt) == 1:
+            s_ms, s_loss, s_e = timed(sjob, ks, 1, head_restrict)
+            extra["structureless"] = {
+                "global_frac": 1.0, "ms_per_step": s_ms,
+                "edges_per_s": args.layers * sjob.E_msg / (s_ms / 1000.0),
+                "edges_aggregated_per_step": s_e, "E_msg": sjob.E_msg,
+                "halo_rows_total": sjob.halo_total, "steps": ks, "warmup": 1,
+                "final_loss": s_loss, **sjob.halo_stats()}
+            if sjob.fused is not None:
+                extra["structureless"]["spmm_pass_cols"] = {
+                    str(k): v for k, v in sjob.fused.pass_for.items()}
+            if mlog is not None:
+                mlog.metrics(phase="structureless", **extra["structureless"])
+        else:
+            extra["structureless"] = {"global_frac": 1.0, "skipped": "does not fit in HBM at "
+                                      "this W (fp32 halo rows of a structureless graph)"}
+        if sjob is not None:
+            sjob.free()
         del sjob
-        if dtype == torch.float32 and dev.type == "cuda" and not args.no_bf16_extra:
-            # secondary: the same headline graph at bf16 storage/compute (fp32 accumulate,
-            # fp32 master weights) on the layer-stack path — NOT the reference's precision
+        if dtype == torch.float32 and dev.type == "cuda" and not args.no_bf16_extra and \
+                world == 1:
+            # secondary (1 GPU): the same headline graph at bf16 storage/compute (fp32
+            # accumulate, fp32 master weights) on the layer-stack path — NOT the reference's
+            # precision
             gc.collect()
             torch.cuda.empty_cache()
             import copy

@@ -210,6 +210,20 @@ class FusedSAGE:
         other = 4 * nT * self.Cg + 5 * 4 * 256 * 256 * 256 + (3 << 29) + \
             (4 * nT * self.hid if self.u_sep else 0)
         wA, wB = max(self.hid, self.d0), max(self.Cp, self.hid)
+        # W > 1: the received halo rows live through the step — the input's (exchanged once,
+        # kept), every hidden layer's (the backward reads them) — and each exchange's send
+        # rows while it is in flight: planned here, not discovered by the allocator
+        H = graph.H if graph.halo is not None else 0
+        n_send = graph.send_map.idx.numel() if graph.halo is not None else 0
+        self.halo_bytes = 4 * (H * self.d0 + (self.nl - 1) * H * self.hid + n_send * self.hid)
+        need_h += self.halo_bytes
+        if dev.type == "cuda" and need_h + other + (6 << 30) > free:
+            # fail here, before any allocation (and after every collective of the setup), so a
+            # caller can skip the configuration on every rank alike instead of dying mid-step
+            raise MemoryError(
+                f"FusedSAGE: activations {need_h / 2**30:.1f} GiB (halo rows "
+                f"{self.halo_bytes / 2**30:.1f}) + workspace {other / 2**30:.1f} GiB exceed the "
+                f"{free / 2**30:.1f} GiB free on {dev}")
         # W > 1: a whole-layer aggregate buffer lets the interior aggregation of EVERY row run
         # while the previous layer's halo rows are in flight (the halo part and the GEMMs
         # follow once they land); without room for it the exchange is waited for up front
@@ -300,21 +314,29 @@ class FusedSAGE:
         """Record a stream event opening region ``name`` (closes the previous one) when
         ``self.record`` is set: per-region device time of one step without barriers or
         host syncs inside it (the reference's TimingReport regions, experiments/OGB/
-        GCN.py:101-116, barriered and synced every region)."""
-        if not self.record or self.dev.type != "cuda":
+        GCN.py:101-116, barriered and synced every region). CPU: host clock (the ops
+        run synchronously)."""
+        if not self.record:
+            return
+        if self.dev.type != "cuda":
+            import time
+
+            self._events.append((name, time.perf_counter()))
             return
         ev = torch.cuda.Event(enable_timing=True)
         ev.record()
         self._events.append((name, ev))
 
     def region_ms(self) -> dict:
-        """Device milliseconds per region of the last recorded step (host sync)."""
+        """Milliseconds per region of the last recorded step (device time; host sync)."""
         if not self._events:
             return {}
-        torch.cuda.synchronize(self.dev)
+        if self.dev.type == "cuda":
+            torch.cuda.synchronize(self.dev)
         out: dict = {}
         for (name, a), (_, b) in zip(self._events[:-1], self._events[1:]):
-            out[name] = out.get(name, 0.0) + a.elapsed_time(b)
+            dt = a.elapsed_time(b) if self.dev.type == "cuda" else (b - a) * 1e3
+            out[name] = out.get(name, 0.0) + dt
         return out
 
     @property

@@ -1,0 +1,41 @@
+"""bench.py as the round driver runs it at N > 1: ``python bench.py --gpus 2`` without a
+launcher spawns the ranks itself (never measures W=1 under an N-GPU label) and rank 0
+prints ONE JSON line with the whole-job value, the rank count the process group really has,
+and the per-region breakdown (max/min over ranks, exposed exchange, bytes per peer). CPU /
+gloo here; the same code path runs RCCL on an 8-GPU node."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_bench_cli_w2_spawns_ranks_and_reports_regions(tmp_path):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--scale", "2e-5",
+           "--steps", "2", "--warmup", "1", "--window", "64", "--extra-steps", "1"]
+    p = subprocess.run(cmd, cwd=tmp_path, env=env, capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["rccl_world_size"] == 2
+    assert d["metric"] == "edges_per_s" and d["value"] > 0 and d["steps"] == 2
+    assert d["executor"].startswith("fused") and d["dtype"] == "fp32"
+    r = d["regions"]
+    for k in ("ms_max_over_ranks", "ms_min_over_ranks", "compute_ms_max", "compute_ms_min",
+              "exposed_exchange_ms_max", "max_bytes_per_peer_per_step", "bytes_sent_per_rank"):
+        assert k in r, k
+    assert len(r["bytes_sent_per_rank"]) == 2 and min(r["bytes_sent_per_rank"]) > 0
+    assert any(k.startswith("exchange") for k in r["ms_max_over_ranks"])
+    assert "structureless" in d  # measured or explicitly skipped, never a crash
+
+
+def test_bench_cli_refuses_mismatched_world(tmp_path):
+    env = dict(os.environ, WORLD_SIZE="1")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--scale", "2e-5",
+           "--steps", "1", "--warmup", "0"]
+    p = subprocess.run(cmd, cwd=tmp_path, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode != 0 and not any(l.startswith("{") for l in p.stdout.splitlines())
