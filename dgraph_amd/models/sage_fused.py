@@ -429,17 +429,24 @@ class FusedSAGE:
             return None
         return g.a2a(K.gather_rows(h, g.send_map.idx), async_op=True)
 
-    def _layer(self, hin: torch.Tensor, halo, consume, width: int, name: str):
+    def _layer(self, hin: torch.Tensor, halo, consume, width: int, name: str,
+               store: Optional[torch.Tensor] = None):
         """Aggregate every row chunk of ``hin`` (interior + halo part) and hand it to
         ``consume(ci, agg, k)``. ``halo``: None (W=1), the received halo rows, or a pending
         ``(recv, work)`` exchange. With a pending exchange and the whole-layer aggregate
         buffer, the interior aggregation of all chunks runs first — while the halo rows are
         on the links — then the exchange is waited for and the halo parts and the GEMMs
-        follow chunk by chunk. Returns the halo rows (for the backward)."""
+        follow chunk by chunk. ``store`` (an [L, >= width] buffer that is free until the
+        consumer writes row chunk c, e.g. the layer's own output: the GEMM of chunk c reads
+        its aggregate rows before it overwrites them, tile by tile) stands in for the
+        whole-layer buffer when there is no room for one. Returns the halo rows (for the
+        backward)."""
         items = [ci for ci, (r0, r1) in enumerate(self.chunks) if r1 > r0]
-        if isinstance(halo, tuple) and self.agg_full is not None:
+        if store is None and self.agg_full is not None:
+            store = self.agg_full
+        if isinstance(halo, tuple) and store is not None:
             recv, work = halo
-            af = self.agg_full[:, :width]
+            af = store[:, :width]
             it = self.it
             for ci in items:
                 r0, r1 = self.chunks[ci]
@@ -514,7 +521,10 @@ class FusedSAGE:
                 r0, r1 = self.chunks[ci]
                 F32.gemm_f32(hin[r0:r1], ws, a, wn, bias=bias, relu=True, out=hout[r0:r1])
 
-            halos.append(self._layer(hin, hin_halo, consume, hin.shape[1], f"fwd_l{l}"))
+            # layer l >= 1 can aggregate in place in its own output buffer (same width)
+            inplace = hout if (OVERLAP_FWD and l > 0 and hin.shape[1] == hout.shape[1]) else None
+            halos.append(self._layer(hin, hin_halo, consume, hin.shape[1], f"fwd_l{l}",
+                                     store=inplace))
             self.edges_aggregated += nnz_it + nnz_h
             hin = hout
             # this layer's halo rows leave now and land while the next layer aggregates

@@ -39,10 +39,25 @@ def _setup(rank, world, dev="cpu", layers=3, chunk_rows=300, gf=0.3, name="ogbn-
     return shape, g, x, y, split, tr, ev, int(n_tr), model
 
 
-def _fused_grads(rank, world, layers=3, chunk_rows=300, name="ogbn-papers100M"):
+def _fused_grads(rank, world, layers=3, chunk_rows=300, name="ogbn-papers100M",
+                 schedule="full"):
+    """schedule (W > 1): "full" = forward exchanges overlapped through the whole-layer
+    aggregate buffer (output layer) and in place (hidden layers); "inplace" = no whole-layer
+    buffer (hidden layers in place, the output layer's exchange waited for up front);
+    "off" = every exchange waited for up front."""
+    import dgraph_amd.models.sage_fused as sf
+
     shape, g, x, y, split, tr, ev, n_tr, model = _setup(rank, world, layers=layers, name=name)
-    ex = FusedSAGE(model, g, x, tr, y[tr], ev, y[ev], split[ev] == SPLIT_VALID, n_tr,
-                   chunk_rows=chunk_rows)
+    sf.OVERLAP_FWD = schedule != "off"
+    try:
+        ex = FusedSAGE(model, g, x, tr, y[tr], ev, y[ev], split[ev] == SPLIT_VALID, n_tr,
+                       chunk_rows=chunk_rows)
+        if schedule == "inplace":
+            ex.agg_full = None
+        if world > 1:
+            assert (ex.agg_full is not None) == (schedule == "full")
+    finally:
+        sf.OVERLAP_FWD = True
     loss = ex.step()
     grads = [p.grad.clone() for p in model.parameters()]
     return loss, grads, ex.correct.clone()
@@ -70,8 +85,11 @@ def test_fused_matches_stack_w1(layers, name):
     assert torch.equal(c1, c0)
 
 
-def _dist_body(rank, world, ref_path):
-    loss, grads, corr = _fused_grads(rank, world)
+def _dist_body(rank, world, ref_path, schedule="full"):
+    import dgraph_amd.models.sage_fused as sf
+
+    sf.OVERLAP_FWD = schedule != "off"
+    loss, grads, corr = _fused_grads(rank, world, schedule=schedule)
     for t in grads:
         dist.all_reduce(t)
     dist.all_reduce(loss)
@@ -83,9 +101,10 @@ def _dist_body(rank, world, ref_path):
     assert torch.equal(corr, ref["corr"])
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_fused_partitioned_matches_w1(ranks, world, tmp_path):
+@pytest.mark.parametrize("world,schedule", [(2, "full"), (4, "full"), (2, "inplace"),
+                                            (2, "off")])
+def test_fused_partitioned_matches_w1(ranks, world, schedule, tmp_path):
     loss, grads, corr = _fused_grads(0, 1)
     p = tmp_path / "ref.pt"
     torch.save({"loss": loss, "grads": grads, "corr": corr}, p)
-    ranks(_dist_body, world, str(p))
+    ranks(_dist_body, world, str(p), schedule)
