@@ -50,6 +50,7 @@ def main():
     ap.add_argument("--chunk", type=int, default=1 << 21)
     ap.add_argument("--tiles", default="256,128")
     ap.add_argument("--grids", default="0,1,2,3")
+    ap.add_argument("--prios", default="0,1", help="side-stream priority variants (1 = high)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     from dgraph_amd import _native
@@ -71,7 +72,10 @@ def main():
     out = torch.empty(L, N, device=dev)
     chunks = _ranges(L, a.chunk)
     bufs = [torch.empty(a.chunk, F, device=dev) for _ in range(2)]
-    pipe = _Pipe(dev)
+    pipes = {}
+    for pr in [int(v) for v in a.prios.split(",")]:
+        os.environ["DGRAPH_FUSED_SIDE_PRIO"] = str(pr)
+        pipes[pr] = _Pipe(dev)
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
     items = list(range(len(chunks)))
 
@@ -93,8 +97,8 @@ def main():
         for ci in items:
             consume(ci, bufs[ci % 2][:chunks[ci][1] - chunks[ci][0]], ci % 2)
 
-    def piped():
-        pipe.run(items, produce, consume)
+    def piped(pr):
+        pipes[pr].run(items, produce, consume)
 
     flops = 2.0 * L * (2 * F) * N
     res = {"L": L, "nnz": csr.nnz, "F": F, "N": N, "chunks": len(chunks), "cus": ncu}
@@ -105,20 +109,21 @@ def main():
             ops.set_f32_sched(grid, tile)
             t_s = _time(spmm_only)
             t_g = _time(gemm_only)
-            t_p = _time(piped)
-            if ref is None:
-                ref = out.clone()
-                err = 0.0
-            else:
-                err = (out - ref).abs().max().item()
-            key = f"tile{tile}_grid{gk}"
-            res[key] = {"spmm_ms": round(t_s, 2), "gemm_ms": round(t_g, 2),
-                        "pipe_ms": round(t_p, 2), "sum_ms": round(t_s + t_g, 2),
-                        "max_ms": round(max(t_s, t_g), 2),
-                        "gemm_TFps": round(flops / t_g / 1e9, 1), "max_abs_vs_first": err}
-            print(f"[overlap] {key}: spmm {t_s:.2f} ms  gemm {t_g:.2f} ms "
-                  f"({flops / t_g / 1e9:.1f} TF/s)  pipe {t_p:.2f} ms  (sum {t_s + t_g:.2f}, "
-                  f"max {max(t_s, t_g):.2f})  err {err:.1e}", flush=True)
+            for pr in pipes:
+                t_p = _time(lambda: piped(pr))
+                if ref is None:
+                    ref = out.clone()
+                    err = 0.0
+                else:
+                    err = (out - ref).abs().max().item()
+                key = f"tile{tile}_grid{gk}_prio{pr}"
+                res[key] = {"spmm_ms": round(t_s, 2), "gemm_ms": round(t_g, 2),
+                            "pipe_ms": round(t_p, 2), "sum_ms": round(t_s + t_g, 2),
+                            "max_ms": round(max(t_s, t_g), 2),
+                            "gemm_TFps": round(flops / t_g / 1e9, 1), "max_abs_vs_first": err}
+                print(f"[overlap] {key}: spmm {t_s:.2f} ms  gemm {t_g:.2f} ms "
+                      f"({flops / t_g / 1e9:.1f} TF/s)  pipe {t_p:.2f} ms  (sum "
+                      f"{t_s + t_g:.2f}, max {max(t_s, t_g):.2f})  err {err:.1e}", flush=True)
     ops.set_f32_sched(0, 256)
     print(json.dumps(res))
 

@@ -72,7 +72,12 @@ class _Pipe:
     def __init__(self, dev):
         self.cuda = dev.type == "cuda" and os.environ.get("DGRAPH_FUSED_PIPELINE", "1") != "0"
         if self.cuda:
-            self.side = torch.cuda.Stream(dev)
+            # DGRAPH_FUSED_SIDE_PRIO=1: the matrix stage's stream at high priority, so when a
+            # chunk's GEMM and the next chunk's aggregation become ready together the GEMM's
+            # (LDS-heavy, one-per-CU) blocks are placed first and the aggregation fills the
+            # registers left over, instead of the other way round
+            prio = -1 if os.environ.get("DGRAPH_FUSED_SIDE_PRIO", "0") == "1" else 0
+            self.side = torch.cuda.Stream(dev, priority=prio)
             self.ready = [torch.cuda.Event() for _ in range(2)]
             self.free = [torch.cuda.Event() for _ in range(2)]
 
