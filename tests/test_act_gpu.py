@@ -61,4 +61,4 @@ def test_linear_act_matches_torch(two):
     yr.backward(gy.double())
     want = [t.grad for t in ((x1, x2, W, b) if two else (x1, W, b))]
     for a_, w_ in zip(got, want):
-        torch.testing.assert_close(a_.double(), w_, atol=5e-3, rtol=1e-4)
+        torch.testing.assert_close(a_.double(), w_.double(), atol=5e-3, rtol=1e-4)
