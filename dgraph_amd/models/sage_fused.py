@@ -222,7 +222,7 @@ class FusedSAGE:
         n_send = graph.send_map.idx.numel() if graph.halo is not None else 0
         self.halo_bytes = 4 * (H * self.d0 + (self.nl - 1) * H * self.hid + n_send * self.hid)
         need_h += self.halo_bytes
-        if dev.type == "cuda" and need_h + other + (6 << 30) > free:
+        if dev.type == "cuda" and need_h + other + (1 << 28) > free:
             # fail here, before any allocation (and after every collective of the setup), so a
             # caller can skip the configuration on every rank alike instead of dying mid-step
             raise MemoryError(
