@@ -550,6 +550,10 @@ def main():
             if sjob.fused is not None:
                 extra["structureless"]["spmm_pass_cols"] = {
                     str(k): v for k, v in sjob.fused.pass_for.items()}
+                sreg = region_breakdown(sjob)
+                if sreg:
+                    extra["structureless"]["regions_ms_max_over_ranks"] = \
+                        sreg["ms_max_over_ranks"]
             if mlog is not None:
                 mlog.metrics(phase="structureless", **extra["structureless"])
         else:
