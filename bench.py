@@ -502,6 +502,8 @@ def main():
     use_fused = job.use_fused
     pass_for = {str(k): v for k, v in getattr(job.fused, "pass_for", {}).items()} \
         if job.fused is not None else {}
+    if job.fused is not None and job.fused.locality is not None:
+        pass_for["graph_locality"] = round(job.fused.locality, 4)
     if args.profile_ops:
         _profile_one_step(lambda: job.step(head_restrict), args.profile_ops, rank)
     E_msg, n_train, halo_total = job.E_msg, job.n_train, job.halo_total
@@ -550,6 +552,9 @@ def main():
             if sjob.fused is not None:
                 extra["structureless"]["spmm_pass_cols"] = {
                     str(k): v for k, v in sjob.fused.pass_for.items()}
+                if sjob.fused.locality is not None:
+                    extra["structureless"]["spmm_pass_cols"]["graph_locality"] = round(
+                        sjob.fused.locality, 4)
                 sreg = region_breakdown(sjob)
                 if sreg:
                     extra["structureless"]["regions_ms_max_over_ranks"] = \
