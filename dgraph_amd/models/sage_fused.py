@@ -61,16 +61,16 @@ def _pad_to(n: int, m: int) -> int:
 
 
 class _Pipe:
-    """Two-stage chunk pipeline over two streams (GPU; plain sequence on CPU): stage 1
-    (the memory-bound aggregation of chunk c into buffer c % 2) runs on the current stream,
-    stage 2 (MFMA GEMMs and weight gradients reading that buffer) on a side stream, so
-    chunk c+1's aggregation overlaps chunk c's matrix work — the two use different pipes
-    (HBM / vector memory vs matrix cores) and the kernels co-reside on the CUs. Events
-    order buffer reuse (stage 1 of chunk c+2 waits for stage 2 of chunk c); ``run`` ends
-    with the current stream waiting for the side stream."""
+    """Two-stage chunk pipeline: stage 1 (the memory-bound aggregation of chunk c into
+    buffer c % 2) on the current stream, stage 2 (MFMA GEMMs / weight gradients reading that
+    buffer) on a side stream, events ordering buffer reuse. OFF by default
+    (DGRAPH_FUSED_PIPELINE=1 turns it on): the fp32 GEMM block takes every SIMD's register
+    file, so the two kernels do not co-reside and the streams only add ordering overhead
+    (benchmarks/bench_overlap_f32.py: 127.9 ms piped vs 122.7 serial per layer at 1/4
+    scale; full step 2060 ms piped vs 2051 serial, profiles/r03/). Off = plain sequence."""
 
     def __init__(self, dev):
-        self.cuda = dev.type == "cuda" and os.environ.get("DGRAPH_FUSED_PIPELINE", "1") != "0"
+        self.cuda = dev.type == "cuda" and os.environ.get("DGRAPH_FUSED_PIPELINE", "0") == "1"
         if self.cuda:
             # DGRAPH_FUSED_SIDE_PRIO=1: the matrix stage's stream at high priority, so when a
             # chunk's GEMM and the next chunk's aggregation become ready together the GEMM's
