@@ -136,7 +136,8 @@ void gemm_f32_op(const at::Tensor& A1, const at::Tensor& B1, const c10::optional
                  const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& cin,
                  double beta, const c10::optional<at::Tensor>& gate,
                  const c10::optional<at::Tensor>& o_rows, bool relu, const at::Tensor& out,
-                 const c10::optional<at::Tensor>& row_scale) {
+                 const c10::optional<at::Tensor>& row_scale,
+                 const c10::optional<at::Tensor>& b1x3, const c10::optional<at::Tensor>& b2x3) {
   f32_rows(A1, "A1");
   f32_rows(B1, "B1");
   f32_rows(out, "out");
@@ -164,8 +165,23 @@ void gemm_f32_op(const at::Tensor& A1, const at::Tensor& B1, const c10::optional
     TORCH_CHECK(b2->size(0) == K2 && b2->size(1) == N, "gemm_f32: A2/B2 shape mismatch");
     TORCH_CHECK(a2->size(0) >= M, "gemm_f32: A2 has fewer than M rows");
   }
-  TORCH_CHECK(gemm_f32_supported(N, K1, K2),
-              "gemm_f32: unsupported shape N=", N, " K1=", K1, " K2=", K2);
+  const at::Tensor *p1 = opt(b1x3), *p2 = opt(b2x3);
+  if (p1) {
+    auto chk = [&](const at::Tensor& p, int64_t Kx, const char* nm) {
+      same_dev(p, A1, nm);
+      TORCH_CHECK(p.scalar_type() == at::kBFloat16 && p.is_contiguous() && p.dim() == 3 &&
+                      p.size(0) == 3 && p.size(1) == N && p.size(2) == Kx,
+                  "gemm_f32: ", nm, " must be contiguous bf16 [3, N, K] split parts");
+    };
+    chk(*p1, K1, "b1x3");
+    TORCH_CHECK((a2 == nullptr) == (p2 == nullptr), "gemm_f32: b2x3 goes with A2");
+    if (p2) chk(*p2, K2, "b2x3");
+    TORCH_CHECK(gemm_x3_supported(N, K1, K2),
+                "gemm_f32 (bf16x3): unsupported shape N=", N, " K1=", K1, " K2=", K2);
+  } else {
+    TORCH_CHECK(gemm_f32_supported(N, K1, K2),
+                "gemm_f32: unsupported shape N=", N, " K1=", K1, " K2=", K2);
+  }
   const float* bp = nullptr;
   if (const at::Tensor* b = opt(bias)) {
     same_dev(*b, A1, "bias");
@@ -201,6 +217,15 @@ void gemm_f32_op(const at::Tensor& A1, const at::Tensor& B1, const c10::optional
     rsp = rs->data_ptr<float>();
   }
   c10::DeviceGuard g(A1.device());
+  if (p1) {
+    DG_HIP_CHECK(gemm_x3(A1.data_ptr<float>(), A1.stride(0), K1,
+                         reinterpret_cast<const uint16_t*>(p1->data_ptr()),
+                         a2 ? a2->data_ptr<float>() : nullptr, a2 ? a2->stride(0) : 0, K2,
+                         p2 ? reinterpret_cast<const uint16_t*>(p2->data_ptr()) : nullptr, arp,
+                         bp, cp, ldc, static_cast<float>(beta), gp, ldg, orp, rsp, relu,
+                         out.data_ptr<float>(), out.stride(0), M, N, stream_of(A1)));
+    return;
+  }
   DG_HIP_CHECK(gemm_f32(A1.data_ptr<float>(), A1.stride(0), K1, B1.data_ptr<float>(),
                         B1.stride(0), a2 ? a2->data_ptr<float>() : nullptr,
                         a2 ? a2->stride(0) : 0, K2, b2 ? b2->data_ptr<float>() : nullptr,
@@ -353,7 +378,7 @@ TORCH_LIBRARY_FRAGMENT(dgraph_amd, m) {
         "Tensor? self_add=None, Tensor? self_map=None, int self_row0=0) -> ()");
   m.def("gemm_f32(Tensor A1, Tensor B1, Tensor? A2, Tensor? B2, Tensor? a_rows, Tensor? bias, "
         "Tensor? cin, float beta, Tensor? gate, Tensor? o_rows, bool relu, Tensor(a!) out, "
-        "Tensor? row_scale=None) -> ()");
+        "Tensor? row_scale=None, Tensor? b1x3=None, Tensor? b2x3=None) -> ()");
   m.def("wgrad_f32(Tensor A1, Tensor? A2, Tensor? a1_rows, Tensor G, Tensor(a!) partials, "
         "int blocks, int fresh_from) -> ()");
   m.def("wgrad_f32_reduce(Tensor partials, Tensor(a!) out) -> ()");

@@ -208,6 +208,15 @@ hipError_t dual_gemm_bs(const void* A1, int64_t lda1, const void* B1t, int64_t K
 // operands with leading dimensions % 4 == 0. a_rows / o_rows nullable int64 [M].
 // gate (nullable, [*, N] with ldg): v = gate[o(i)][n] > 0 ? v : 0. cin may alias out.
 bool gemm_f32_supported(int64_t N, int64_t K1, int64_t K2);
+// the same dual GEMM as bf16x3 split-product MFMAs (gemm_x3.hip): B1p / B2p are the weights
+// pre-split into bf16 parts stored [3][N][K] (k contiguous); N in {64, 128, 192, 256}
+bool gemm_x3_supported(int64_t N, int64_t K1, int64_t K2);
+hipError_t gemm_x3(const float* A1, int64_t lda1, int64_t K1, const uint16_t* B1p,
+                   const float* A2, int64_t lda2, int64_t K2, const uint16_t* B2p,
+                   const int64_t* a_rows, const float* bias, const float* cin, int64_t ldc,
+                   float beta, const float* gate, int64_t ldg, const int64_t* o_rows,
+                   const float* row_scale, bool relu, float* out, int64_t ldo, int64_t M,
+                   int64_t N, hipStream_t st);
 hipError_t gemm_f32(const float* A1, int64_t lda1, int64_t K1, const float* B1, int64_t ldb1,
                     const float* A2, int64_t lda2, int64_t K2, const float* B2, int64_t ldb2,
                     const int64_t* a_rows, const float* bias, const float* cin, int64_t ldc,

@@ -48,6 +48,9 @@ from ..parallel.dist_graph import DistGraph
 
 # rows per chunk of the row-chunked passes (0 = auto from free memory)
 CHUNK_ROWS = int(os.environ.get("DGRAPH_FUSED_CHUNK_ROWS", "0"))
+# fp32 GEMMs as bf16x3 split-product MFMAs (csrc/kernels/gemm_x3.hip: fp32-accurate, error vs
+# fp64 below the exact-f32 MFMA's); 0 = exact-f32 MFMAs (gemm_f32.hip)
+GEMM_X3 = os.environ.get("DGRAPH_GEMM_X3", "0") == "1"
 # W > 1: overlap each forward halo exchange with the next layer's interior aggregation
 OVERLAP_FWD = os.environ.get("DGRAPH_FUSED_OVERLAP", "1") != "0"
 
@@ -153,7 +156,10 @@ class FusedSAGE:
         self.nl = len(model.layers)
         self.hid = model.layers[0].out_dim
         self.C = model.layers[-1].out_dim
-        self.Cp = 176 if self.C > 128 else (128 if self.C > 64 else 64)  # logit GEMM width
+        self.x3 = GEMM_X3 and dev.type == "cuda"
+        self._x3_cache: dict = {}
+        # logit GEMM width (the bf16x3 tile needs a multiple of 64)
+        self.Cp = (192 if self.x3 else 176) if self.C > 128 else (128 if self.C > 64 else 64)
         self.Cg = _pad_to(self.C, 32) if self.C > 128 else self.Cp      # dz width (a K dim)
         if self.Cg not in (128, 176, 192, 256):
             self.Cg = 192
@@ -353,6 +359,25 @@ class FusedSAGE:
         self.g.edges_aggregated = v
 
     # ------------------------------------------------------------------ helpers
+    def _gemm(self, A1, B1, A2=None, B2=None, **kw):
+        """fp32 dual GEMM: exact-f32 MFMAs, or bf16x3 split products with the weights split
+        once per step (``GEMM_X3``)."""
+        if self.x3:
+            kw["b1x3"] = self._split(B1)
+            if B2 is not None:
+                kw["b2x3"] = self._split(B2)
+        return F32.gemm_f32(A1, B1, A2, B2, **kw)
+
+    def _split(self, B):
+        # keyed by address; the entry keeps B alive, so no other tensor can take its address
+        # while the cache (one step) lives
+        key = (B.data_ptr(), tuple(B.shape), B.stride())
+        v = self._x3_cache.get(key)
+        if v is None:
+            v = (B, F32.split_x3(B))
+            self._x3_cache[key] = v
+        return v[1]
+
     def _spmm(self, rowptr, col, x, out=None, **kw):
         """fp32 SpMM at the column-pass width tuned for ``x``'s width (``_tune_passes``)."""
         kw.setdefault("pass_cols", self.pass_for.get(x.shape[1], 0))
@@ -503,6 +528,7 @@ class FusedSAGE:
         P = self._params()
         dev = self.dev
         self._events = []
+        self._x3_cache = {}  # weights changed since the last step: split again
         self._mark("fwd_l0")
         nnz_it = self.it.nnz
         nnz_h = self.halo.nnz if self.halo is not None else 0
@@ -520,7 +546,7 @@ class FusedSAGE:
 
             def consume(ci, a, k, hin=hin, hout=hout, ws=ws, wn=wn, bias=bias):
                 r0, r1 = self.chunks[ci]
-                F32.gemm_f32(hin[r0:r1], ws, a, wn, bias=bias, relu=True, out=hout[r0:r1])
+                self._gemm(hin[r0:r1], ws, a, wn, bias=bias, relu=True, out=hout[r0:r1])
 
             # layer l >= 1 can aggregate in place in its own output buffer (same width)
             inplace = hout if (OVERLAP_FWD and l > 0 and hin.shape[1] == hout.shape[1]) else None
@@ -561,7 +587,7 @@ class FusedSAGE:
         C, Cp = self.C, self.Cp
         r0, r1 = self.chunks[ci]
         n = r1 - r0
-        z = F32.gemm_f32(hl[r0:r1], wsp, a, wnp, bias=bp, out=self.bufB2[k][:n, :Cp])
+        z = self._gemm(hl[r0:r1], wsp, a, wnp, bias=bp, out=self.bufB2[k][:n, :Cp])
         t0, t1 = self.ch_T[ci]
         if t1 > t0:
             # one fused kernel: per-row loss and the scaled softmax gradient rows
@@ -591,7 +617,7 @@ class FusedSAGE:
         wn_t[:C] = wn.detach().t()
         ws_t = torch.zeros(Cg, hid, device=dev)
         ws_t[:C] = ws.detach().t()
-        u2 = F32.gemm_f32(self.dz, wn_t, row_scale=self.invdegT, out=self.u_out)
+        u2 = self._gemm(self.dz, wn_t, row_scale=self.invdegT, out=self.u_out)
         dZ = self.dZ
         work = None
         if self.sub is not None:
@@ -607,7 +633,7 @@ class FusedSAGE:
             self._mark("bwd_out")
             self._spmm(stc.rowptr, stc.col, sg, dZ, beta=1.0, row_map=stc_rows)
             del sg, hg
-        F32.gemm_f32(self.dz, ws_t, cin=dZ, o_rows=self.posT, out=dZ)
+        self._gemm(self.dz, ws_t, cin=dZ, o_rows=self.posT, out=dZ)
         F32.apply_keep_bits(dZ, self.bits)
         # ---------------- backward: last hidden layer (index nl-2) weights over S rows
         lh = nl - 2
@@ -621,7 +647,7 @@ class FusedSAGE:
         if nl == 3:
             # u1 = (dZ1 Wn1^T) / deg_S: its transposed aggregation feeds layer 0; the halo
             # part is computed and sent first so the exchange overlaps the S-row work below
-            u = F32.gemm_f32(dZ, wn1.detach().t().contiguous(), row_scale=self.invdegS,
+            u = self._gemm(dZ, wn1.detach().t().contiguous(), row_scale=self.invdegS,
                              out=self.u)
             if self.haloT is not None:
                 hg1 = self._spmm(self.haloT.rowptr, self.haloT.col, u, col_map=self.smap)
@@ -664,7 +690,7 @@ class FusedSAGE:
             x_halo = halos[0]
             # the support rows' own term dZ1 Ws1^T, once over S (one full-size GEMM instead
             # of a row-scattered one per chunk); added by the aggregation's epilogue
-            v = F32.gemm_f32(dZ, ws1_t, out=self.v_self) if self.v_self is not None else None
+            v = self._gemm(dZ, ws1_t, out=self.v_self) if self.v_self is not None else None
 
             def produce_0(ci, k):
                 # memory-bound: the column-mapped transposed aggregation of u1 (gated by
@@ -688,7 +714,7 @@ class FusedSAGE:
                 r0, r1 = self.chunks[ci]
                 s0, s1 = self.ch_S[ci]
                 if v is None and s1 > s0:  # no room for v_self: scattered self term
-                    F32.gemm_f32(dZ[s0:s1], ws1_t, cin=gz, o_rows=self.ch_Sloc[ci],
+                    self._gemm(dZ[s0:s1], ws1_t, cin=gz, o_rows=self.ch_Sloc[ci],
                                  gate=h1[r0:r1], out=gz)
                 self.acc_in.add(x[r0:r1], gz, A2=a0)
                 db0s.append(K.col_sum(gz))

@@ -98,12 +98,35 @@ def gemm_f32_ok(N: int, K1: int, K2: int = 0) -> bool:
     return N in (64, 128, 176, 192, 256) and K1 % 32 == 0 and K1 > 0 and K2 % 32 == 0
 
 
+def split_x3(B: torch.Tensor, N: int = 0) -> torch.Tensor:
+    """fp32 ``B [K, N']`` -> its three bf16 parts ``[3, N, K]`` (hi, mid, lo; k contiguous;
+    columns past N' zero) with ``B == hi + mid + lo`` exactly for normal values: hi and mid
+    are round-to-nearest-even, lo carries the <= 8 remaining significant bits. The weight
+    operand of the bf16x3 GEMM (csrc/kernels/gemm_x3.hip), split once per call site."""
+    K, n0 = B.shape
+    N = N or n0
+    Bt = torch.zeros(N, K, dtype=torch.float32, device=B.device)
+    Bt[:n0] = B.t()
+    hi = Bt.to(torch.bfloat16)
+    r1 = Bt - hi.float()
+    mid = r1.to(torch.bfloat16)
+    lo = (r1 - mid.float()).to(torch.bfloat16)
+    return torch.stack([hi, mid, lo]).contiguous()
+
+
+def gemm_x3_ok(N: int, K1: int, K2: int = 0) -> bool:
+    return N in (64, 128, 192, 256) and K1 % 32 == 0 and K1 > 0 and K2 % 32 == 0
+
+
 def gemm_f32(A1: torch.Tensor, B1: torch.Tensor, A2=None, B2=None, *, a_rows=None, bias=None,
              cin=None, beta: float = 1.0, gate=None, o_rows=None, relu: bool = False,
-             out: Optional[torch.Tensor] = None, row_scale=None) -> torch.Tensor:
+             out: Optional[torch.Tensor] = None, row_scale=None, b1x3=None,
+             b2x3=None) -> torch.Tensor:
     """``out[o(i)] = relu?(gate?(rs[i] (A1[a(i)] @ B1 (+ A2[i] @ B2)) + bias +
     beta*cin[o(i)]))`` (csrc/kernels/gemm_f32.hip; B row-major [K, N]); ``gate``: keep
-    where gate > 0; ``row_scale`` (nullable [M]): per input row."""
+    where gate > 0; ``row_scale`` (nullable [M]): per input row. ``b1x3`` / ``b2x3``
+    (``split_x3`` of B1 / B2): run the products as bf16x3 split-product MFMAs
+    (gemm_x3.hip; fp32-accurate) instead of exact-f32 MFMAs."""
     M = a_rows.numel() if a_rows is not None else A1.shape[0]
     N = B1.shape[1]
     if out is None:
@@ -114,7 +137,8 @@ def gemm_f32(A1: torch.Tensor, B1: torch.Tensor, A2=None, B2=None, *, a_rows=Non
         _native.ops().gemm_f32(A1, B1.contiguous(), A2, None if B2 is None else B2.contiguous(),
                                a_rows, None if bias is None else bias.float().contiguous(),
                                cin, float(beta), gate, o_rows, bool(relu), out,
-                               None if row_scale is None else row_scale.float().contiguous())
+                               None if row_scale is None else row_scale.float().contiguous(),
+                               b1x3, b2x3)
         return out
     a = A1.double()[a_rows.long()] if a_rows is not None else A1[:M].double()
     v = a @ B1.double()

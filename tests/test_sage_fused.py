@@ -35,19 +35,20 @@ def _setup(rank, world, dev="cpu", layers=3, chunk_rows=300, gf=0.3, name="ogbn-
     # products, seed 0: a layer-2 pre-activation of 6e-8 (a ReLU tie that summation order
     # flips) — seed 1 keeps every |pre-activation| well above fp32 rounding
     torch.manual_seed(0 if name == "ogbn-papers100M" else 1)
-    model = GraphSAGE(shape.num_features, 256, shape.num_classes, layers)
+    model = GraphSAGE(shape.num_features, 256, shape.num_classes, layers).to(dev)
     return shape, g, x, y, split, tr, ev, int(n_tr), model
 
 
 def _fused_grads(rank, world, layers=3, chunk_rows=300, name="ogbn-papers100M",
-                 schedule="full"):
+                 schedule="full", dev="cpu"):
     """schedule (W > 1): "full" = forward exchanges overlapped through the whole-layer
     aggregate buffer (output layer) and in place (hidden layers); "inplace" = no whole-layer
     buffer (hidden layers in place, the output layer's exchange waited for up front);
     "off" = every exchange waited for up front."""
     import dgraph_amd.models.sage_fused as sf
 
-    shape, g, x, y, split, tr, ev, n_tr, model = _setup(rank, world, layers=layers, name=name)
+    shape, g, x, y, split, tr, ev, n_tr, model = _setup(rank, world, dev=dev, layers=layers,
+                                                        name=name)
     sf.OVERLAP_FWD = schedule != "off"
     try:
         ex = FusedSAGE(model, g, x, tr, y[tr], ev, y[ev], split[ev] == SPLIT_VALID, n_tr,
