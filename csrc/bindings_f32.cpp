@@ -236,7 +236,8 @@ void gemm_f32_op(const at::Tensor& A1, const at::Tensor& B1, const c10::optional
 
 void wgrad_f32_op(const at::Tensor& A1, const c10::optional<at::Tensor>& A2,
                   const c10::optional<at::Tensor>& a1_rows, const at::Tensor& G,
-                  const at::Tensor& partials, int64_t blocks, int64_t fresh_from) {
+                  const at::Tensor& partials, int64_t blocks, int64_t fresh_from,
+                  int64_t mode) {
   f32_rows(A1, "A1");
   f32_rows(G, "G");
   same_dev(G, A1, "G");
@@ -253,7 +254,8 @@ void wgrad_f32_op(const at::Tensor& A1, const c10::optional<at::Tensor>& A2,
     K2 = a2->size(1);
   }
   const int64_t K = A1.size(1) + K2;
-  TORCH_CHECK(wgrad_f32_supported(K, N), "wgrad_f32: unsupported K=", K, " N=", N);
+  TORCH_CHECK(mode == 1 ? wgrad_x3_supported(K, N) : wgrad_f32_supported(K, N),
+              "wgrad_f32: unsupported K=", K, " N=", N, " mode=", mode);
   TORCH_CHECK(partials.scalar_type() == at::kFloat && partials.is_contiguous() &&
                   partials.dim() == 3 && partials.size(1) == K && partials.size(2) == N,
               "partials must be contiguous float32 [P, K, N]");
@@ -261,6 +263,14 @@ void wgrad_f32_op(const at::Tensor& A1, const c10::optional<at::Tensor>& A2,
                   fresh_from <= partials.size(0),
               "wgrad_f32: 1 <= blocks <= P and 0 <= fresh_from <= P");
   c10::DeviceGuard g(A1.device());
+  if (mode == 1) {
+    DG_HIP_CHECK(wgrad_x3(A1.data_ptr<float>(), A1.stride(0), A1.size(1),
+                          a2 ? a2->data_ptr<float>() : nullptr, a2 ? a2->stride(0) : 0, K2, arp,
+                          G.data_ptr<float>(), G.stride(0), M, N, partials.data_ptr<float>(),
+                          static_cast<int>(blocks), static_cast<int>(fresh_from),
+                          stream_of(A1)));
+    return;
+  }
   DG_HIP_CHECK(wgrad_f32(A1.data_ptr<float>(), A1.stride(0), A1.size(1),
                          a2 ? a2->data_ptr<float>() : nullptr, a2 ? a2->stride(0) : 0, K2, arp,
                          G.data_ptr<float>(), G.stride(0), M, N, partials.data_ptr<float>(),
@@ -380,7 +390,7 @@ TORCH_LIBRARY_FRAGMENT(dgraph_amd, m) {
         "Tensor? cin, float beta, Tensor? gate, Tensor? o_rows, bool relu, Tensor(a!) out, "
         "Tensor? row_scale=None, Tensor? b1x3=None, Tensor? b2x3=None) -> ()");
   m.def("wgrad_f32(Tensor A1, Tensor? A2, Tensor? a1_rows, Tensor G, Tensor(a!) partials, "
-        "int blocks, int fresh_from) -> ()");
+        "int blocks, int fresh_from, int mode=0) -> ()");
   m.def("wgrad_f32_reduce(Tensor partials, Tensor(a!) out) -> ()");
   m.def("row_keep_bits(Tensor h, Tensor? rows, Tensor(a!) bits) -> ()");
   m.def("apply_keep_bits(Tensor(a!) g, Tensor bits) -> ()");

@@ -211,6 +211,11 @@ bool gemm_f32_supported(int64_t N, int64_t K1, int64_t K2);
 // the same dual GEMM as bf16x3 split-product MFMAs (gemm_x3.hip): B1p / B2p are the weights
 // pre-split into bf16 parts stored [3][N][K] (k contiguous); N in {64, 128, 192, 256}
 bool gemm_x3_supported(int64_t N, int64_t K1, int64_t K2);
+// weight gradient as bf16x3 split products (wgrad_x3.hip), same contract as wgrad_f32
+bool wgrad_x3_supported(int64_t K, int64_t N);
+hipError_t wgrad_x3(const float* A1, int64_t lda1, int64_t K1, const float* A2, int64_t lda2,
+                    int64_t K2, const int64_t* a1_rows, const float* G, int64_t ldg, int64_t M,
+                    int64_t N, float* partials, int P, int fresh_from, hipStream_t st);
 hipError_t gemm_x3(const float* A1, int64_t lda1, int64_t K1, const uint16_t* B1p,
                    const float* A2, int64_t lda2, int64_t K2, const uint16_t* B2p,
                    const int64_t* a_rows, const float* bias, const float* cin, int64_t ldc,

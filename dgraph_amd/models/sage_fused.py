@@ -307,11 +307,12 @@ class FusedSAGE:
             elif dev.type != "cuda" or free - need_h > (4 * self.nS * self.hid + (8 << 30)):
                 self.v_self = torch.empty(self.nS, self.hid, **f)
             # else: no room — the self term runs as a row-scattered GEMM per chunk
-        self.acc_out_s = F32.WgradAcc(self.hid, self.Cg, dev)
-        self.acc_out_n = F32.WgradAcc(self.hid, self.Cg, dev)
-        self.acc_hid_s = F32.WgradAcc(self.hid if self.nl == 3 else self.d0, self.hid, dev)
-        self.acc_hid_n = F32.WgradAcc(self.hid if self.nl == 3 else self.d0, self.hid, dev)
-        self.acc_in = F32.WgradAcc(2 * self.d0, self.hid, dev) if self.nl == 3 else None
+        self.acc_out_s = F32.WgradAcc(self.hid, self.Cg, dev, x3=self.x3)
+        self.acc_out_n = F32.WgradAcc(self.hid, self.Cg, dev, x3=self.x3)
+        kh = self.hid if self.nl == 3 else self.d0
+        self.acc_hid_s = F32.WgradAcc(kh, self.hid, dev, x3=self.x3)
+        self.acc_hid_n = F32.WgradAcc(kh, self.hid, dev, x3=self.x3)
+        self.acc_in = F32.WgradAcc(2 * self.d0, self.hid, dev, x3=self.x3) if self.nl == 3 else None
         self.row_loss = torch.zeros(nT, **f)
         self.hit = torch.zeros(self.E.numel(), dtype=torch.uint8, device=dev)
         self.E_val_l = self.E_val.long()

@@ -166,8 +166,10 @@ class WgradAcc:
 
     _P = 0
 
-    def __init__(self, K: int, N: int, device, blocks: int = 0):
+    def __init__(self, K: int, N: int, device, blocks: int = 0, x3: bool = False):
         self.K, self.N, self.device = int(K), int(N), torch.device(device)
+        # bf16x3 split-product MFMAs (wgrad_x3.hip) where the shape is supported
+        self.mode = 1 if (x3 and self.K in (128, 256) and self.N in (128, 192, 256)) else 0
         if self.device.type == "cuda":
             if blocks <= 0:
                 if WgradAcc._P == 0:
@@ -196,7 +198,7 @@ class WgradAcc:
         if self.device.type == "cuda":
             P = self.partials.shape[0]
             nb = max(1, min(P, -(-G.shape[0] // self.MIN_ROWS_PER_BLOCK)))
-            _native.ops().wgrad_f32(A1, A2, a1_rows, G, self.partials, nb, self.used)
+            _native.ops().wgrad_f32(A1, A2, a1_rows, G, self.partials, nb, self.used, self.mode)
             self.used = max(self.used, nb)
         else:
             M = G.shape[0]

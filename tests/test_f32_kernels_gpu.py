@@ -146,9 +146,12 @@ def test_gemm_f32_cin_gate_rows():
     torch.testing.assert_close(cpu_out.double(), ref, atol=1e-4, rtol=1e-5)
 
 
+@pytest.mark.parametrize("x3", [False, True])
 @pytest.mark.parametrize("K1,K2,N", [(128, 128, 256), (256, 0, 256), (128, 0, 176),
-                                     (256, 0, 128), (128, 0, 128)])
-def test_wgrad_f32_vs_fp64(K1, K2, N):
+                                     (256, 0, 128), (128, 0, 128), (128, 128, 192)])
+def test_wgrad_f32_vs_fp64(K1, K2, N, x3):
+    """exact-f32 (wgrad_f32.hip) and bf16x3 split-product (wgrad_x3.hip, where the shape is
+    supported) weight gradients against fp64, accumulated over two calls."""
     g = torch.Generator().manual_seed(K1 * 7 + N)
     M1, M2 = 5003, 777
     src = torch.randn(8000, K1, generator=g)
@@ -158,7 +161,9 @@ def test_wgrad_f32_vs_fp64(K1, K2, N):
     A1b = torch.randn(M2, K1, generator=g)
     A2b = torch.randn(M2, K2, generator=g) if K2 else None
     G2 = torch.randn(M2, N, generator=g)
-    acc = F32.WgradAcc(K1 + K2, N, DEV)
+    acc = F32.WgradAcc(K1 + K2, N, DEV, x3=x3)
+    if x3 and acc.mode != 1:
+        pytest.skip("shape not covered by the bf16x3 kernel (exact-f32 path)")
     acc.add(src.to(DEV), G1.to(DEV), None if A2a is None else A2a.to(DEV), rows1.to(DEV))
     acc.add(A1b.to(DEV), G2.to(DEV), None if A2b is None else A2b.to(DEV))
     out = acc.result()
