@@ -45,6 +45,8 @@ __global__ __launch_bounds__(256) void spmm_f32_rowgroup_kernel(
   const int lane = threadIdx.x & (kWave - 1);
   const int g = lane / LPR;
   const int l = lane % LPR;
+  const int wv = threadIdx.x >> 6;  // wave of the block (its row of the compaction table)
+  __shared__ uint8_t inv[CMAP ? 4 * 64 : 1];
   const int64_t ngroups = (nrows + G - 1) / G;
   const int64_t q0 = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
   const int64_t qstep = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
@@ -93,6 +95,54 @@ __global__ __launch_bounds__(256) void spmm_f32_rowgroup_kernel(
     for (int k0 = 0; k0 < maxdeg; k0 += LPR) {
       const int kn = k0 + LPR + l;
       int64_t nx_c = 0;
+      if constexpr (CMAP) {
+        // column-mapped operand (e.g. a gradient stored only on the support rows): most
+        // entries map to -1. Compact this chunk's mapped entries to the front of the group
+        // (ballot + rank, the inverse permutation through a 64-byte LDS table per wave) and
+        // gather only those: the trip count is the largest mapped count among the wave's
+        // groups, not LPR. Summation order = entry order (deterministic, same as uncompacted)
+        const bool valid = my_w != 0.f;
+        const uint64_t bal = __ballot(valid);
+        const uint64_t gm = LPR == 64 ? bal : (bal >> (g * LPR)) & ((1ull << (LPR & 63)) - 1);
+        const int cnt = __popcll(gm);
+        int mc = cnt;
+#pragma unroll
+        for (int off = LPR; off < kWave; off <<= 1) {
+          const int o = __shfl_xor(mc, off, kWave);
+          mc = o > mc ? o : mc;
+        }
+        const int rank = __popcll(gm & ((1ull << l) - 1));
+        if (valid) inv[wv * kWave + g * LPR + rank] = static_cast<uint8_t>(l);
+        nx_c = load_c(kn);
+        for (int j0 = 0; j0 < mc; j0 += U) {
+          uint4 v[U];
+          uint32_t c[U];
+          float w[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const int j = j0 + u;
+            const int src = j < cnt ? static_cast<int>(inv[wv * kWave + g * LPR + j]) : 0;
+            c[u] = static_cast<uint32_t>(__shfl(static_cast<int>(my_c), g * LPR + src, kWave));
+            const float ww = __shfl(my_w, g * LPR + src, kWave);
+            w[u] = j < cnt ? ww : 0.f;
+          }
+#pragma unroll
+          for (int u = 0; u < U; ++u)
+            v[u] = *reinterpret_cast<const uint4*>(xf + static_cast<uint64_t>(c[u]) *
+                                                            static_cast<uint64_t>(ldx));
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const f32x2 ww{w[u], w[u]};
+            const f32x2 t0{__uint_as_float(v[u].x), __uint_as_float(v[u].y)};
+            const f32x2 t1{__uint_as_float(v[u].z), __uint_as_float(v[u].w)};
+            acc[0] = __builtin_elementwise_fma(t0, ww, acc[0]);
+            acc[1] = __builtin_elementwise_fma(t1, ww, acc[1]);
+          }
+        }
+        my_w = load_w(nx_c, kn);
+        my_c = nx_c;
+        continue;
+      }
 #pragma unroll
       for (int j0 = 0; j0 < LPR; j0 += U) {
         if (j0 > 0 && k0 + j0 >= maxdeg) break;  // wave-uniform: no all-padding batch

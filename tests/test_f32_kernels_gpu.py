@@ -44,6 +44,32 @@ def test_spmm_f32_rowgroup_vs_fp64(F, idx):
     assert torch.equal(out, out2)
 
 
+@pytest.mark.parametrize("F,pc", [(32, 64), (128, 64), (256, 64), (256, 256), (256, 128)])
+@pytest.mark.parametrize("frac", [0.05, 0.2, 0.9])
+def test_spmm_f32_col_map_compaction(F, pc, frac):
+    """Column-mapped aggregation with most entries unmapped: the kernel compacts each
+    chunk's mapped entries (ballot + rank) before gathering; every lane-group width
+    (8/16/32/64 lanes per row) and rows longer than one chunk, vs the CPU reference."""
+    rp, col = _csr(3000, 2000, 70, 7)
+    g = torch.Generator().manual_seed(int(frac * 100) + F + pc)
+    nk = max(1, int(2000 * frac))
+    keep = torch.randperm(2000, generator=g)[:nk].sort().values
+    cmap = torch.full((2000,), -1, dtype=torch.int32)
+    cmap[keep] = torch.arange(nk, dtype=torch.int32)
+    xc = torch.randn(nk, F, generator=g)
+    rs = torch.rand(3000, generator=g)
+    ref = torch.zeros(3000, F)
+    F32.spmm_f32(rp.cpu(), col.cpu(), xc, ref, row_scale=rs, col_map=cmap)
+    out = torch.zeros(3000, F, device=DEV)
+    F32.spmm_f32(rp, col, xc.to(DEV), out, row_scale=rs.to(DEV), col_map=cmap.to(DEV),
+                 pass_cols=pc)
+    torch.testing.assert_close(out.cpu(), ref, atol=2e-5, rtol=1e-5)
+    out2 = torch.zeros_like(out)
+    F32.spmm_f32(rp, col, xc.to(DEV), out2, row_scale=rs.to(DEV), col_map=cmap.to(DEV),
+                 pass_cols=pc)
+    assert torch.equal(out, out2)
+
+
 def test_spmm_f32_ex_row_ids_col_map_row_map_beta():
     rp, col = _csr(400, 350, 11, 3)
     g = torch.Generator().manual_seed(5)
