@@ -370,6 +370,40 @@ void set_spmm_f32_config_op(int64_t rowgroup, int64_t pass_cols) {
   set_spmm_f32_config(static_cast<int>(rowgroup), static_cast<int>(pass_cols));
 }
 
+void sage_fwd_f32_op(const at::Tensor& X, const at::Tensor& rowptr, const at::Tensor& col,
+                     const at::Tensor& inv_deg, const at::Tensor& Ws, const at::Tensor& Wn,
+                     const at::Tensor& bias, const at::Tensor& out, const at::Tensor& ring,
+                     const at::Tensor& err) {
+  f32_rows(X, "X");
+  f32_rows(out, "out");
+  const int64_t M = out.size(0), F = X.size(1);
+  TORCH_CHECK(F == 128 || F == 256, "sage_fwd_f32: input width must be 128 or 256");
+  TORCH_CHECK(out.size(1) == 256, "sage_fwd_f32: output width must be 256");
+  TORCH_CHECK(X.size(0) >= M && X.size(0) <= INT32_MAX, "sage_fwd_f32: X rows");
+  TORCH_CHECK(rowptr.scalar_type() == at::kLong && rowptr.is_contiguous() &&
+                  rowptr.numel() == M + 1, "sage_fwd_f32: rowptr must be int64 [M + 1]");
+  TORCH_CHECK(col.scalar_type() == at::kInt && col.is_contiguous(),
+              "sage_fwd_f32: col must be contiguous int32");
+  TORCH_CHECK(inv_deg.scalar_type() == at::kFloat && inv_deg.is_contiguous() &&
+                  inv_deg.numel() >= M, "sage_fwd_f32: inv_deg");
+  for (const at::Tensor* w : {&Ws, &Wn})
+    TORCH_CHECK(w->scalar_type() == at::kFloat && w->is_contiguous() && w->dim() == 2 &&
+                    w->size(0) == F && w->size(1) == 256, "sage_fwd_f32: weights must be [F, 256]");
+  TORCH_CHECK(bias.scalar_type() == at::kFloat && bias.is_contiguous() && bias.numel() == 256,
+              "sage_fwd_f32: bias [256]");
+  TORCH_CHECK(ring.scalar_type() == at::kFloat && ring.is_contiguous(), "sage_fwd_f32: ring");
+  TORCH_CHECK(err.scalar_type() == at::kInt && err.numel() >= 1, "sage_fwd_f32: err");
+  for (const at::Tensor* t : {&X, &rowptr, &col, &inv_deg, &Ws, &Wn, &bias, &ring, &err})
+    same_dev(*t, out, "operand");
+  c10::DeviceGuard g(out.device());
+  DG_HIP_CHECK(sage_fwd_f32(X.data_ptr<float>(), X.stride(0), static_cast<int>(F),
+                            rowptr.data_ptr<int64_t>(), col.data_ptr<int32_t>(),
+                            inv_deg.data_ptr<float>(), Ws.data_ptr<float>(), Wn.data_ptr<float>(),
+                            bias.data_ptr<float>(), out.data_ptr<float>(), out.stride(0), M,
+                            ring.data_ptr<float>(), ring.numel(), err.data_ptr<int>(),
+                            stream_of(out)));
+}
+
 void set_f32_sched_op(int64_t spmm_grid, int64_t gemm_tile) {
   set_spmm_f32_grid(static_cast<int>(spmm_grid));
   set_gemm_f32_tile(static_cast<int>(gemm_tile));
@@ -380,6 +414,8 @@ void set_f32_sched_op(int64_t spmm_grid, int64_t gemm_tile) {
 
 TORCH_LIBRARY_FRAGMENT(dgraph_amd, m) {
   m.def("set_f32_sched(int spmm_grid, int gemm_tile) -> ()", &dgraph::set_f32_sched_op);
+  m.def("sage_fwd_f32(Tensor X, Tensor rowptr, Tensor col, Tensor inv_deg, Tensor Ws, "
+        "Tensor Wn, Tensor bias, Tensor(a!) out, Tensor(b!) ring, Tensor(c!) err) -> ()");
   m.def("set_spmm_f32_config(int rowgroup, int pass_cols=-1) -> ()",
         &dgraph::set_spmm_f32_config_op);
   m.def("spmm_f32_ex(Tensor rowptr, Tensor col, Tensor? edge_weight, Tensor? col_scale, "
@@ -402,6 +438,7 @@ TORCH_LIBRARY_FRAGMENT(dgraph_amd, m) {
 TORCH_LIBRARY_IMPL(dgraph_amd, CUDA, m) {
   m.impl("spmm_f32_ex", &dgraph::spmm_f32_ex_op);
   m.impl("gemm_f32", &dgraph::gemm_f32_op);
+  m.impl("sage_fwd_f32", &dgraph::sage_fwd_f32_op);
   m.impl("wgrad_f32", &dgraph::wgrad_f32_op);
   m.impl("wgrad_f32_reduce", &dgraph::wgrad_f32_reduce_op);
   m.impl("row_keep_bits", &dgraph::row_keep_bits_op);

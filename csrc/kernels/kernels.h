@@ -211,6 +211,12 @@ bool gemm_f32_supported(int64_t N, int64_t K1, int64_t K2);
 // the same dual GEMM as bf16x3 split-product MFMAs (gemm_x3.hip): B1p / B2p are the weights
 // pre-split into bf16 parts stored [3][N][K] (k contiguous); N in {64, 128, 192, 256}
 bool gemm_x3_supported(int64_t N, int64_t K1, int64_t K2);
+// fused fp32 SAGE hidden layer (sage_fwd_f32.hip): out = relu(X Ws + mean_N(X) Wn + b),
+// F in {128, 256}, 256 outputs; ring: >= min(tiles, CUs) * 2 * 128 * F floats; err: int flag
+hipError_t sage_fwd_f32(const float* X, int64_t ldx, int F, const int64_t* rowptr,
+                        const int32_t* col, const float* inv_deg, const float* Ws,
+                        const float* Wn, const float* bias, float* out, int64_t ldo, int64_t M,
+                        float* ring, int64_t ring_floats, int* err, hipStream_t st);
 // weight gradient as bf16x3 split products (wgrad_x3.hip), same contract as wgrad_f32
 bool wgrad_x3_supported(int64_t K, int64_t N);
 hipError_t wgrad_x3(const float* A1, int64_t lda1, int64_t K1, const float* A2, int64_t lda2,

@@ -42,6 +42,7 @@ from typing import List, Optional, Tuple
 
 import torch
 
+from .. import _native
 from ..ops import f32 as F32
 from ..ops import kernels as K
 from ..parallel.dist_graph import DistGraph
@@ -51,6 +52,9 @@ CHUNK_ROWS = int(os.environ.get("DGRAPH_FUSED_CHUNK_ROWS", "0"))
 # fp32 GEMMs as bf16x3 split-product MFMAs (csrc/kernels/gemm_x3.hip: fp32-accurate, error vs
 # fp64 below the exact-f32 MFMA's); 0 = exact-f32 MFMAs (gemm_f32.hip)
 GEMM_X3 = os.environ.get("DGRAPH_GEMM_X3", "0") == "1"
+# W = 1: each hidden layer as ONE fused kernel (csrc/kernels/sage_fwd_f32.hip: gather waves
+# and MFMA waves co-resident on every CU) instead of chunked aggregation + GEMM launches
+FUSED_FWD = os.environ.get("DGRAPH_FUSED_FWD", "0") == "1"
 # W > 1: overlap each forward halo exchange with the next layer's interior aggregation
 OVERLAP_FWD = os.environ.get("DGRAPH_FUSED_OVERLAP", "1") != "0"
 
@@ -244,6 +248,14 @@ class FusedSAGE:
                 16 << 30 if dev.type == "cuda" else 0):
             self.agg_full = torch.empty(L, wA, dtype=torch.float32, device=dev)
             other += need_full
+        # the fused hidden-layer kernel's per-block aggregate ring (W = 1, int32 columns)
+        self.fwd_ring = self.fwd_err = None
+        if (FUSED_FWD and dev.type == "cuda" and graph.halo is None
+                and self.it.col.dtype == torch.int32 and self.hid == 256):
+            ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+            self.fwd_ring = torch.empty(ncu * 2 * 128 * 256, dtype=torch.float32, device=dev)
+            self.fwd_err = torch.zeros(1, dtype=torch.int32, device=dev)
+            other += self.fwd_ring.numel() * 4
         spare = max(free - need_h - other, 1 << 28)
         per_row = 4 * 2 * (wA + wB)  # two aggregate + two logit/gradient chunk buffers
         cr = chunk_rows or CHUNK_ROWS
@@ -350,6 +362,11 @@ class FusedSAGE:
             dt = a.elapsed_time(b) if self.dev.type == "cuda" else (b - a) * 1e3
             out[name] = out.get(name, 0.0) + dt
         return out
+
+    def check_errors(self) -> None:
+        """Raise if a fused-kernel synchronisation wait timed out (host sync)."""
+        if self.fwd_err is not None and int(self.fwd_err.item()) != 0:
+            raise RuntimeError("FusedSAGE: sage_fwd_f32 role synchronisation timed out")
 
     @property
     def edges_aggregated(self) -> int:
@@ -549,10 +566,19 @@ class FusedSAGE:
                 r0, r1 = self.chunks[ci]
                 self._gemm(hin[r0:r1], ws, a, wn, bias=bias, relu=True, out=hout[r0:r1])
 
-            # layer l >= 1 can aggregate in place in its own output buffer (same width)
-            inplace = hout if (OVERLAP_FWD and l > 0 and hin.shape[1] == hout.shape[1]) else None
-            halos.append(self._layer(hin, hin_halo, consume, hin.shape[1], f"fwd_l{l}",
-                                     store=inplace))
+            if self.fwd_ring is not None and not self.x3 and hin.shape[1] in (128, 256):
+                # aggregation + combine of the whole layer in one kernel
+                it = self.it
+                _native.ops().sage_fwd_f32(hin, it.rowptr, it.col, self.inv_deg, ws, wn,
+                                           bias.float().contiguous(), hout, self.fwd_ring,
+                                           self.fwd_err)
+                halos.append(None)
+            else:
+                # layer l >= 1 can aggregate in place in its own output buffer (same width)
+                inplace = hout if (OVERLAP_FWD and l > 0 and hin.shape[1] == hout.shape[1]) \
+                    else None
+                halos.append(self._layer(hin, hin_halo, consume, hin.shape[1], f"fwd_l{l}",
+                                         store=inplace))
             self.edges_aggregated += nnz_it + nnz_h
             hin = hout
             # this layer's halo rows leave now and land while the next layer aggregates

@@ -367,3 +367,61 @@ def test_fused_step_x3_matches_exact():
     for a, b in zip(g1, g0):
         torch.testing.assert_close(a, b, atol=1e-5, rtol=1e-4)
     assert torch.equal(c1, c0)
+
+
+# ---------------------------------------------------------- fused hidden layer (one kernel)
+@pytest.mark.parametrize("F", [128, 256])
+def test_sage_fwd_fused_kernel_matches_chunked(F):
+    """sage_fwd_f32 (gather waves + MFMA waves in one persistent kernel) equals the chunked
+    path — fp32 row-group SpMM then the exact-f32 dual GEMM — BITWISE (same summation and
+    k orders), over more 128-row tiles than CUs with a partial last tile; and fp64."""
+    from dgraph_amd import _native
+
+    L = 128 * 256 * 3 + 77
+    rp, col = _csr(L, L, 20, 31 + F)
+    g = torch.Generator().manual_seed(F)
+    x = torch.randn(L, F, generator=g).to(DEV)
+    Ws = (torch.randn(F, 256, generator=g) / F ** 0.5).to(DEV)
+    Wn = (torch.randn(F, 256, generator=g) / F ** 0.5).to(DEV)
+    b = torch.randn(256, generator=g).to(DEV)
+    deg = (rp[1:] - rp[:-1]).float()
+    inv = torch.where(deg > 0, 1.0 / deg.clamp_min(1), torch.zeros_like(deg)).contiguous()
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    ring = torch.empty(ncu * 2 * 128 * 256, device=DEV)
+    err = torch.zeros(1, dtype=torch.int32, device=DEV)
+    out = torch.empty(L, 256, device=DEV)
+    _native.ops().sage_fwd_f32(x, rp, col, inv, Ws, Wn, b, out, ring, err)
+    torch.cuda.synchronize()
+    assert int(err.item()) == 0
+    agg = F32.spmm_f32(rp, col, x, torch.empty(L, F, device=DEV), row_scale=inv)
+    ref = F32.gemm_f32(x, Ws, agg, Wn, bias=b, relu=True)
+    assert torch.equal(out, ref)
+    # and against fp64 on a sample of rows
+    rows = torch.randperm(L, generator=g)[:500]
+    rpc, colc = rp.cpu(), col.cpu().long()
+    a64 = torch.zeros(500, F, dtype=torch.float64)
+    xc = x.cpu().double()
+    for i, r in enumerate(rows.tolist()):
+        nb = colc[rpc[r]:rpc[r + 1]]
+        if nb.numel():
+            a64[i] = xc[nb].sum(0) / nb.numel()
+    r64 = (xc[rows] @ Ws.cpu().double() + a64 @ Wn.cpu().double() + b.cpu().double()).clamp_min(0)
+    torch.testing.assert_close(out[rows.to(DEV)].cpu().double(), r64, atol=1e-4, rtol=1e-5)
+
+
+def test_fused_step_fused_fwd_bitwise():
+    """The fused executor with the one-kernel hidden layers reproduces the chunked step
+    bitwise: loss, every weight gradient and the hit counts."""
+    import dgraph_amd.models.sage_fused as sf
+    from test_sage_fused import _fused_grads
+
+    l0, g0, c0 = _fused_grads(0, 1, dev="cuda")
+    sf.FUSED_FWD = True
+    try:
+        l1, g1, c1 = _fused_grads(0, 1, dev="cuda")
+    finally:
+        sf.FUSED_FWD = False
+    assert torch.equal(l1, l0)
+    for a, b in zip(g1, g0):
+        assert torch.equal(a, b)
+    assert torch.equal(c1, c0)
