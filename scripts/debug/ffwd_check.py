@@ -29,7 +29,7 @@ def main():
     ex = job.fused
     state = {k: v.clone() for k, v in job.model.state_dict().items()}
     L = ex.L
-    rows = torch.randint(0, L, (1 << 20,), device=dev, generator=torch.Generator(device=dev).manual_seed(0))
+    rows = torch.randint(0, L, (1 << 14,), device=dev, generator=torch.Generator(device=dev).manual_seed(0))
     out = {}
     for mode in ("chunked", "fused"):
         job.model.load_state_dict(state)
