@@ -257,7 +257,11 @@ class FusedSAGE:
             self.fwd_err = torch.zeros(1, dtype=torch.int32, device=dev)
             other += self.fwd_ring.numel() * 4
         spare = max(free - need_h - other, 1 << 28)
-        per_row = 4 * 2 * (wA + wB)  # two aggregate + two logit/gradient chunk buffers
+        self.pipe = _Pipe(dev)
+        # chunk buffers: two of each when the two-stream pipeline runs (chunk c+1 is written
+        # while chunk c is read), one otherwise — the freed memory goes to larger chunks
+        self.nbuf = 2 if self.pipe.cuda else 1
+        per_row = 4 * self.nbuf * (wA + wB)  # aggregate + logit/gradient chunk buffers
         cr = chunk_rows or CHUNK_ROWS
         if cr <= 0:
             cr = int(min(max(spare // per_row, 1 << 16), 1 << 21))
@@ -292,16 +296,18 @@ class FusedSAGE:
         # stream read the other one) during the row-chunked passes, and the last hidden
         # layer's keep bits (output-layer backward only, when no chunk buffer is live)
         bits_words = self.nS * (self.hid // 32)
-        arena_fl = max(2 * self.cr * (wA + wB), bits_words)
+        arena_fl = max(self.nbuf * self.cr * (wA + wB), bits_words)
         self.arena = torch.empty(arena_fl, **f)
         o = 0
         self.bufA2, self.bufB2 = [], []
-        for w, lst in ((wA, self.bufA2), (wA, self.bufA2), (wB, self.bufB2), (wB, self.bufB2)):
-            lst.append(self.arena[o:o + self.cr * w].view(self.cr, w))
-            o += self.cr * w
+        for w, lst in ((wA, self.bufA2), (wB, self.bufB2)):
+            for _ in range(self.nbuf):
+                lst.append(self.arena[o:o + self.cr * w].view(self.cr, w))
+                o += self.cr * w
+            if self.nbuf == 1:  # index k % 2 reaches the single buffer either way
+                lst.append(lst[0])
         self.bufA, self.bufB = self.bufA2[0], self.bufB2[0]
         self.bits = self.arena[:bits_words].view(torch.int32).view(self.nS, self.hid // 32)
-        self.pipe = _Pipe(dev)
         self.dz = torch.zeros(self.T.numel(), self.Cg, **f)  # output-layer gradient rows
         # the output layer's projected gradient rows (B2 only): the last hidden buffer's tail,
         # past dZ and u, is free by then
