@@ -45,7 +45,11 @@ __device__ __forceinline__ int sb_row(int k) { return k * kSBP + ((k >> 3) & 1) 
 __device__ __forceinline__ int lds_load(int* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-// wait until *p >= target (bounded); every lane of the wave waits
+// wait until *p >= target (bounded); every lane of the wave waits. agent_acq: the data the
+// signal publishes is in GLOBAL memory (the aggregate ring), which this CU's vector L1 may
+// still hold from the slot's previous use: acquire at agent scope, which invalidates the L1
+// (a workgroup-scope acquire leaves it, and stale ring lines were read at full scale)
+template <bool AGENT_ACQ = false>
 __device__ __forceinline__ void wait_ge(int* p, int target, int* err) {
   int spins = 0;
   while (lds_load(p) < target) {
@@ -55,7 +59,10 @@ __device__ __forceinline__ void wait_ge(int* p, int target, int* err) {
       break;
     }
   }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  if constexpr (AGENT_ACQ)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  else
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 __device__ __forceinline__ void signal_add(int* p) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -133,7 +140,7 @@ __global__ __launch_bounds__(512, 1) void sage_fwd_f32_kernel(
         const float sc = has ? inv_deg[r] : 0.f;
         *reinterpret_cast<f32x4*>(slot + rr * F + 4 * l) = f32x4{a0 * sc, a1 * sc, a2 * sc, a3 * sc};
       }
-      signal_add(&ctr[0]);  // 4 gather waves per tile
+      signal_add(&ctr[0]);  // 4 gather waves per tile (the release waits for the ring stores)
     }
     return;
   }
@@ -208,7 +215,7 @@ __global__ __launch_bounds__(512, 1) void sage_fwd_f32_kernel(
     for (int s = 0; s < nst; ++s, ++gstage) {
       const int buf = gstage & 1;
       const bool last = s + 1 == nst;
-      if (s + 1 == nst1) wait_ge(&ctr[0], 4 * (i + 1), err);  // this tile's aggregate
+      if (s + 1 == nst1) wait_ge<true>(&ctr[0], 4 * (i + 1), err);  // this tile's aggregate
       if (last && has_next) {
         ld_tile = next;
         ld_i = i + 1;
