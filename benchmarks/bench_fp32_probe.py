@@ -51,7 +51,7 @@ def main():
     res = {}
     if not a.skip_gemm:
         M = a.M
-        for K_, N_ in ((128, 256), (256, 256), (512, 256), (256, 176), (256, 172)):
+        for K_, N_ in ((128, 256), (256, 256), (512, 256), (256, 176), (256, 192), (256, 172)):
             x = torch.randn(M, K_, device=dev)
             w = torch.randn(K_, N_, device=dev)
             b = torch.randn(N_, device=dev)
@@ -74,15 +74,24 @@ def main():
                 err_lib = ((out_lib := torch.relu(torch.addmm(b, x, w))).double() - ref64
                            ).abs().div(scale).max().item()
                 del out_lib
-                for mode in [int(m) for m in a.gemm_modes.split(",")]:
+                for mode_s in a.gemm_modes.split(","):
+                    # "x3k": the bf16x3 kernel (gemm_x3.hip) with weights pre-split once
+                    mode = 256 if mode_s == "x3k" else int(mode_s)
+                    if mode_s == "x3k" and N_ not in (64, 128, 192, 256):
+                        continue
                     _native.ops().set_f32_sched(0, mode)
+                    from dgraph_amd.ops.f32 import split_x3
+
                     if K_ >= 256:  # dual form: two K/2 operands, one fused kernel
                         h = K_ // 2
                         x1, x2 = x[:, :h].contiguous(), x[:, h:].contiguous()
+                        kx = dict(b1x3=split_x3(w[:h]), b2x3=split_x3(w[h:])) \
+                            if mode_s == "x3k" else {}
                         ms_n = _time(lambda: gemm_f32(x1, w[:h], x2, w[h:], bias=b, relu=True,
-                                                      out=out))
+                                                      out=out, **kx))
                     else:
-                        ms_n = _time(lambda: gemm_f32(x, w, bias=b, relu=True, out=out))
+                        kx = dict(b1x3=split_x3(w)) if mode_s == "x3k" else {}
+                        ms_n = _time(lambda: gemm_f32(x, w, bias=b, relu=True, out=out, **kx))
                     err = (out.double() - ref64).abs().div(scale).max().item()
                     tfn = 2 * M * K_ * N_ / ms_n / 1e9
                     res[f"gemm_f32_m{mode}_K{K_}_N{N_}"] = {
