@@ -77,12 +77,16 @@ __global__ __launch_bounds__(512, 1) void sage_fwd_f32_kernel(
     const float* __restrict__ Ws, const float* __restrict__ Wn, const float* __restrict__ bias,
     float* __restrict__ out, int64_t ldo, int64_t M, float* __restrict__ ring, int* err) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  int* ctr = reinterpret_cast<int*>(lds + 2 * kSStage);  // [0] ready [1] consumed [2] bar
+  // [1] consumed (tiles whose aggregate the MFMA role has read), [2] MFMA-wave barrier,
+  // [4 + w] tiles gathered by gather wave w: one counter PER gather wave — a single shared
+  // count is ambiguous when the waves drift apart (a wave one tile ahead makes the total
+  // look like a complete tile; the full-scale check caught exactly that)
+  int* ctr = reinterpret_cast<int*>(lds + 2 * kSStage);
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
   const int lane = tid & 63;
   const int64_t ntiles = (M + kSM - 1) / kSM;
-  if (tid < 4) ctr[tid] = 0;
+  if (tid < 8) ctr[tid] = 0;
   __syncthreads();  // the only block-wide barrier: before the roles split
   if (static_cast<int64_t>(blockIdx.x) >= ntiles) return;
   float* slot0 = ring + static_cast<int64_t>(blockIdx.x) * 2 * kSM * F;
@@ -140,7 +144,7 @@ __global__ __launch_bounds__(512, 1) void sage_fwd_f32_kernel(
         const float sc = has ? inv_deg[r] : 0.f;
         *reinterpret_cast<f32x4*>(slot + rr * F + 4 * l) = f32x4{a0 * sc, a1 * sc, a2 * sc, a3 * sc};
       }
-      signal_add(&ctr[0]);  // 4 gather waves per tile (the release waits for the ring stores)
+      signal_add(&ctr[4 + gw]);  // this wave's rows of tile i are in the ring
     }
     return;
   }
@@ -215,7 +219,10 @@ __global__ __launch_bounds__(512, 1) void sage_fwd_f32_kernel(
     for (int s = 0; s < nst; ++s, ++gstage) {
       const int buf = gstage & 1;
       const bool last = s + 1 == nst;
-      if (s + 1 == nst1) wait_ge<true>(&ctr[0], 4 * (i + 1), err);  // this tile's aggregate
+      if (s + 1 == nst1) {  // this tile's aggregate: every gather wave's rows
+#pragma unroll
+        for (int w = 0; w < 4; ++w) wait_ge<true>(&ctr[4 + w], i + 1, err);
+      }
       if (last && has_next) {
         ld_tile = next;
         ld_i = i + 1;
@@ -297,7 +304,7 @@ hipError_t sage_fwd_f32(const float* X, int64_t ldx, int F, const int64_t* rowpt
   const int64_t ntiles = (M + kSM - 1) / kSM;
   const int64_t blocks = ntiles < num_cus ? ntiles : num_cus;
   if (ring_floats < blocks * 2 * kSM * F) return hipErrorInvalidValue;
-  constexpr size_t lds = 2 * kSStage * sizeof(float) + 16;
+  constexpr size_t lds = 2 * kSStage * sizeof(float) + 64;
   static bool attr[2] = {false, false};
   const int fi = F == 256 ? 1 : 0;
   auto kern = F == 256 ? &sage_fwd_f32_kernel<256> : &sage_fwd_f32_kernel<128>;

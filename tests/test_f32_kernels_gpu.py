@@ -370,15 +370,26 @@ def test_fused_step_x3_matches_exact():
 
 
 # ---------------------------------------------------------- fused hidden layer (one kernel)
-@pytest.mark.parametrize("F", [128, 256])
-def test_sage_fwd_fused_kernel_matches_chunked(F):
+@pytest.mark.parametrize("F,skew", [(128, False), (256, False), (128, True), (256, True)])
+def test_sage_fwd_fused_kernel_matches_chunked(F, skew):
     """sage_fwd_f32 (gather waves + MFMA waves in one persistent kernel) equals the chunked
     path — fp32 row-group SpMM then the exact-f32 dual GEMM — BITWISE (same summation and
-    k orders), over more 128-row tiles than CUs with a partial last tile; and fp64."""
+    k orders), over more 128-row tiles than CUs with a partial last tile; and fp64.
+    ``skew``: many tiles per block and heavy-tailed degrees (every 13th row 150-400
+    neighbours), so the four gather waves drift apart by whole tiles — the case a shared
+    ready count got wrong."""
     from dgraph_amd import _native
 
-    L = 128 * 256 * 3 + 77
+    L = 128 * 256 * (12 if skew else 3) + 77
     rp, col = _csr(L, L, 20, 31 + F)
+    if skew:
+        g0 = torch.Generator().manual_seed(99)
+        deg = (rp[1:] - rp[:-1]).cpu()
+        deg[::13] = torch.randint(150, 400, (deg[::13].numel(),), generator=g0)
+        rpc = torch.zeros(L + 1, dtype=torch.long)
+        rpc[1:] = torch.cumsum(deg, 0)
+        rp = rpc.to(DEV)
+        col = torch.randint(0, L, (int(rpc[-1]),), generator=g0).to(torch.int32).to(DEV)
     g = torch.Generator().manual_seed(F)
     x = torch.randn(L, F, generator=g).to(DEV)
     Ws = (torch.randn(F, 256, generator=g) / F ** 0.5).to(DEV)
