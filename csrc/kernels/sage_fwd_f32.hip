@@ -103,12 +103,28 @@ __global__ __launch_bounds__(512, 1) void sage_fwd_f32_kernel(
       wait_ge(&ctr[1], i - 1, err);  // slot i%2 was last read by tile i-2
       float* slot = slot0 + (i & 1) * kSM * F;
       const int64_t r0 = t * kSM;
+      // software-pipelined over this wave's rows: the next row's bounds and its first chunk
+      // of column ids are loaded while the current row's neighbour rows are in flight (the
+      // index loads would otherwise add two dependent latencies per row)
+      const float* xf = X + 4 * l;
+      auto bounds = [&](int q0, int64_t& sb, int& db) {
+        const int64_t rq = r0 + q0 + g;
+        const bool h = q0 < kSM && rq < M;
+        sb = h ? rowptr[rq] : 0;
+        db = h ? static_cast<int>(rowptr[rq + 1] - sb) : 0;
+      };
+      int64_t s;
+      int deg;
+      bounds(gw * G, s, deg);
+      int c_first = col[l < deg ? s + l : (deg > 0 ? s : 0)];
       for (int rr0 = gw * G; rr0 < kSM; rr0 += 4 * G) {
         const int rr = rr0 + g;
         const int64_t r = r0 + rr;
         const bool has = r < M;
-        const int64_t s = has ? rowptr[r] : 0;
-        const int deg = has ? static_cast<int>(rowptr[r + 1] - s) : 0;
+        int64_t sn;
+        int degn;
+        bounds(rr0 + 4 * G, sn, degn);  // next row (in flight during this row's gathers)
+        const float sc = has ? inv_deg[r] : 0.f;
         int maxdeg = deg;
 #pragma unroll
         for (int off = LPR; off < 64; off <<= 1) {
@@ -116,10 +132,10 @@ __global__ __launch_bounds__(512, 1) void sage_fwd_f32_kernel(
           maxdeg = o > maxdeg ? o : maxdeg;
         }
         float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-        const float* xf = X + 4 * l;
-        for (int k0 = 0; k0 < maxdeg; k0 += LPR) {
+        int c_next_first = 0;
+        for (int k0 = 0; k0 < maxdeg || k0 == 0; k0 += LPR) {
           const int kk = k0 + l;
-          const int my_c = col[kk < deg ? s + kk : (deg > 0 ? s : 0)];
+          const int my_c = k0 == 0 ? c_first : col[kk < deg ? s + kk : (deg > 0 ? s : 0)];
           const float my_w = kk < deg ? 1.f : 0.f;
           const int cnt = maxdeg - k0 < LPR ? maxdeg - k0 : LPR;
           for (int j0 = 0; j0 < cnt; j0 += U) {
@@ -132,6 +148,8 @@ __global__ __launch_bounds__(512, 1) void sage_fwd_f32_kernel(
               w[u] = j0 + u < cnt ? __shfl(my_w, g * LPR + j, 64) : 0.f;
               v[u] = *reinterpret_cast<const f32x4*>(xf + static_cast<int64_t>(c) * ldx);
             }
+            if (k0 == 0 && j0 == 0)  // the next row's first ids, behind this batch's loads
+              c_next_first = col[l < degn ? sn + l : (degn > 0 ? sn : 0)];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
               a0 = fmaf(v[u][0], w[u], a0);
@@ -140,9 +158,14 @@ __global__ __launch_bounds__(512, 1) void sage_fwd_f32_kernel(
               a3 = fmaf(v[u][3], w[u], a3);
             }
           }
+          if (k0 == 0 && cnt <= 0)  // empty row pair: still fetch the next row's ids
+            c_next_first = col[l < degn ? sn + l : (degn > 0 ? sn : 0)];
+          if (maxdeg == 0) break;
         }
-        const float sc = has ? inv_deg[r] : 0.f;
         *reinterpret_cast<f32x4*>(slot + rr * F + 4 * l) = f32x4{a0 * sc, a1 * sc, a2 * sc, a3 * sc};
+        s = sn;
+        deg = degn;
+        c_first = c_next_first;
       }
       signal_add(&ctr[4 + gw]);  // this wave's rows of tile i are in the ring
     }
