@@ -33,8 +33,16 @@ def _act_ref(z: torch.Tensor, act: int) -> torch.Tensor:
 
 
 def _native_ok(z: torch.Tensor) -> bool:
-    return (z.is_cuda and z.dtype in (torch.float32, torch.bfloat16) and z.dim() == 2
-            and z.shape[1] <= 256 * (8 if z.dtype == torch.bfloat16 else 4))
+    """Shapes csrc/kernels/act.hip takes: a row of F elements is covered by at most 256
+    threads — vectors of 8 (bf16) / 4 (fp32) when F and the row stride allow, else one
+    element per thread (F <= 256)."""
+    if not (z.is_cuda and z.dtype in (torch.float32, torch.bfloat16) and z.dim() == 2):
+        return False
+    F = z.shape[1]
+    vec = 8 if z.dtype == torch.bfloat16 else 4
+    if F % vec == 0 and z.stride(0) % vec == 0:
+        return F // vec <= 256
+    return F <= 256
 
 
 class _LinearActFn(torch.autograd.Function):
