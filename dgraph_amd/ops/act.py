@@ -19,7 +19,8 @@ import torch
 import torch.nn.functional as Fn
 
 from .. import _native
-from .dense import _auto_rows_per_chunk, _native_linear_sum_ok, dual_gemm, dual_gemm_shape_ok, wgrad
+from .dense import (_auto_rows_per_chunk, _native_linear_sum_ok, dual_gemm, dual_gemm_shape_ok,
+                    wgrad)
 
 ACTS = {"identity": 0, "silu": 1, "relu": 2}
 
@@ -100,7 +101,8 @@ class _LinearActFn(torch.autograd.Function):
             if ctx.needs_input_grad[3 + 2 * i]:
                 if dz.is_cuda:
                     L = dz.shape[0]
-                    dW = wgrad(dz, x.contiguous(), 0 if L >= 1 << 23 else _auto_rows_per_chunk(L))
+                    dW = wgrad(dz, x.contiguous(),
+                               0 if L >= 1 << 23 else _auto_rows_per_chunk(L))
                 else:
                     adt = torch.float64 if dz.dtype == torch.float64 else torch.float32
                     dW = dz.t().to(adt) @ x.to(adt)
