@@ -30,10 +30,21 @@ epilogues (gemm_f32.hip), split-M MFMA weight gradients (wgrad_f32.hip), keep bi
 (bits.hip). Deterministic: fixed chunking, fixed reduction orders, no atomics.
 
 Vertex-partitioned graphs (W > 1): halo rows of x are exchanged once (static input), of
-h1/h2 once per forward; B2 sends the loss rows' contributions to remote support rows
-(restricted sub-plan of :class:`~dgraph_amd.parallel.dist_graph.DistGraph`), B1b sends the
-support rows' contributions to remote vertices (reverse halo exchange, issued before the
-B1a work so it overlaps it).
+h1/h2 once per forward — each issued asynchronously as soon as its layer is done and
+overlapped with the next layer's interior aggregation of every row (through a whole-layer
+aggregate buffer, or in place in the layer's own output buffer when there is no room for
+one); B2 sends the loss rows' contributions to remote support rows (restricted sub-plan of
+:class:`~dgraph_amd.parallel.dist_graph.DistGraph`), B1b sends the support rows'
+contributions to remote vertices (reverse halo exchange, issued before the B1a work so it
+overlaps it). The halo rows are part of the memory plan, which raises MemoryError before
+allocating when a configuration cannot fit.
+
+Measured choices (profiles/r03/, PERFORMANCE.md): the SpMM column-pass width follows the
+graph's locality (64 columns on a windowed graph, full rows on a structureless one); the
+column-mapped transposed aggregation compacts each chunk's mapped entries before gathering;
+the chunks run on one stream (the two-stream pipeline and the one-kernel fused layer,
+DGRAPH_FUSED_PIPELINE / DGRAPH_FUSED_FWD, are correct but not faster: the fp32 GEMM's
+register footprint keeps the memory-bound and the MFMA-bound work from co-residing).
 """
 from __future__ import annotations
 
