@@ -130,6 +130,8 @@ hipError_t bwd_vec(int act, const T* dy, int64_t lddy, const T* z, int64_t ldz, 
   return hipGetLastError();
 }
 
+inline bool a16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
 }  // namespace
 
 hipError_t bias_act_fwd(DType dt, int act, const void* z, int64_t ldz, const float* b, void* y,
@@ -139,14 +141,14 @@ hipError_t bias_act_fwd(DType dt, int act, const void* z, int64_t ldz, const flo
   if (dt == DType::F32) {
     auto zp = static_cast<const float*>(z);
     auto yp = static_cast<float*>(y);
-    if (F % 4 == 0 && ldz % 4 == 0 && ldy % 4 == 0 && F / 4 <= 256)
+    if (F % 4 == 0 && ldz % 4 == 0 && ldy % 4 == 0 && F / 4 <= 256 && a16(z) && a16(y))
       return fwd_vec<float, 4>(act, zp, ldz, b, yp, ldy, M, F, st);
     if (F > 256) return hipErrorInvalidValue;
     return fwd_vec<float, 1>(act, zp, ldz, b, yp, ldy, M, F, st);
   }
   auto zp = static_cast<const uint16_t*>(z);
   auto yp = static_cast<uint16_t*>(y);
-  if (F % 8 == 0 && ldz % 8 == 0 && ldy % 8 == 0 && F / 8 <= 256)
+  if (F % 8 == 0 && ldz % 8 == 0 && ldy % 8 == 0 && F / 8 <= 256 && a16(z) && a16(y))
     return fwd_vec<uint16_t, 8>(act, zp, ldz, b, yp, ldy, M, F, st);
   if (F > 256) return hipErrorInvalidValue;
   return fwd_vec<uint16_t, 1>(act, zp, ldz, b, yp, ldy, M, F, st);
@@ -161,7 +163,8 @@ hipError_t bias_act_bwd(DType dt, int act, const void* dy, int64_t lddy, const v
     auto g = static_cast<const float*>(dy);
     auto zp = static_cast<const float*>(z);
     auto o = static_cast<float*>(dz);
-    if (F % 4 == 0 && lddy % 4 == 0 && ldz % 4 == 0 && lddz % 4 == 0 && F / 4 <= 256)
+    if (F % 4 == 0 && lddy % 4 == 0 && ldz % 4 == 0 && lddz % 4 == 0 && F / 4 <= 256 &&
+        a16(dy) && a16(z) && a16(dz))
       return bwd_vec<float, 4>(act, g, lddy, zp, ldz, b, o, lddz, M, F, partial, nblocks, st);
     if (F > 256) return hipErrorInvalidValue;
     return bwd_vec<float, 1>(act, g, lddy, zp, ldz, b, o, lddz, M, F, partial, nblocks, st);
@@ -169,7 +172,8 @@ hipError_t bias_act_bwd(DType dt, int act, const void* dy, int64_t lddy, const v
   auto g = static_cast<const uint16_t*>(dy);
   auto zp = static_cast<const uint16_t*>(z);
   auto o = static_cast<uint16_t*>(dz);
-  if (F % 8 == 0 && lddy % 8 == 0 && ldz % 8 == 0 && lddz % 8 == 0 && F / 8 <= 256)
+  if (F % 8 == 0 && lddy % 8 == 0 && ldz % 8 == 0 && lddz % 8 == 0 && F / 8 <= 256 &&
+      a16(dy) && a16(z) && a16(dz))
     return bwd_vec<uint16_t, 8>(act, g, lddy, zp, ldz, b, o, lddz, M, F, partial, nblocks, st);
   if (F > 256) return hipErrorInvalidValue;
   return bwd_vec<uint16_t, 1>(act, g, lddy, zp, ldz, b, o, lddz, M, F, partial, nblocks, st);

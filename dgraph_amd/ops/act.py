@@ -81,6 +81,8 @@ class _LinearActFn(torch.autograd.Function):
         xs, Ws = flat[0::2], flat[1::2]
         bf = bf if ctx.has_b else None
         dy = dy.contiguous()
+        if dy.is_cuda and dy.data_ptr() % 16:
+            dy = dy.clone()  # the vector lanes need 16-B aligned rows
         if _native_ok(z):
             dz = torch.empty_like(z)
             db = _native.ops().bias_act_bwd(dy, z, bf, int(ctx.act), dz)
