@@ -88,6 +88,15 @@ def parse():
                     help="single process: run rank --rehearse-rank of a W-way partition with "
                          "a loopback halo exchange (per-rank compute + memory; no peers)")
     ap.add_argument("--rehearse-rank", type=int, default=0)
+    ap.add_argument("--link-gbps", type=float,
+                    default=float(os.environ.get("DGRAPH_LOOPBACK_LINK_GBPS", "0")),
+                    help="rehearsal: hold each loopback exchange for latency + largest "
+                         "per-peer message / GBPS (one xGMI link per peer pair) on a side "
+                         "stream, so the exposed-exchange regions measure the overlap "
+                         "schedule against link-length transfers (0 = instant loopback)")
+    ap.add_argument("--no-interior-first", dest="interior_first", action="store_false",
+                    help="W>1 fused executor: keep the original row order (no interior-first "
+                         "renumbering, parallel/reorder.py)")
     ap.add_argument("--profile-ops", default="",
                     help="after the timed steps, profile one extra step (every rank runs it) "
                          "with torch.profiler; rank 0 writes the per-op device-time table")
@@ -151,10 +160,23 @@ class Job:
         part = build_partition(shape, p_rank, p_world, dev, seed=args.seed,
                                global_frac=global_frac, window=args.window,
                                rehearse=self.rehearse)
+        ex = getattr(args, "executor", "auto")
+        self.use_fused = ex == "fused" or (ex == "auto" and dtype == torch.float32 and
+                                           args.layers in (2, 3) and args.hidden == 256)
         csr = part["csr"]
         if p_world == 1:
             csr.num_cols = part["L"]
         self.L, self.H = part["L"], part["H"]
+        # W > 1, fused executor: number this rank's rows interior-first (rows with no halo
+        # neighbour and sent to nobody first), so each layer's interior rows run while its
+        # halo exchange is in flight (parallel/reorder.py); per-vertex data follows perm
+        self.perm, locality = None, None
+        if p_world > 1 and self.use_fused and getattr(args, "interior_first", True):
+            from dgraph_amd.parallel.reorder import interior_first
+
+            csr, part["send_local_idx"], self.perm, self.L_int, locality = interior_first(
+                csr, part["L"], part["send_local_idx"])
+            part["csr"] = csr
         self.graph = DistGraph(csr, part["L"], part["H"], part["send_local_idx"],
                                part["send_splits"],
                                # the synthetic graph is symmetrised, so the interior
@@ -162,11 +184,10 @@ class Job:
                                # transpose is never materialised
                                part["recv_splits"], comm.group, symmetric=True,
                                overlap=not args.no_overlap)
+        if locality is not None:
+            self.graph.locality_hint = locality
         halo_gids = part["halo_gids"]
         del part, csr
-        ex = getattr(args, "executor", "auto")
-        self.use_fused = ex == "fused" or (ex == "auto" and dtype == torch.float32 and
-                                           args.layers in (2, 3) and args.hidden == 256)
         if not self.use_fused:
             self.graph.prepare_backward()
         self.recompute = False
@@ -191,6 +212,9 @@ class Job:
         self.x, y, split = node_data(shape, p_rank,
                                      _offsets(shape.num_nodes, p_world), dev, seed=args.seed,
                                      dtype=dtype, return_split=True)
+        if self.perm is not None:
+            self.x, y, split = self.x[self.perm], y[self.perm], split[self.perm]
+            self.perm = None
         self.train_idx = torch.nonzero(split == SPLIT_TRAIN, as_tuple=True)[0]
         # the gradient support of the layer below the output layer
         # (DistGraph.prepare_grad_support), built now while device memory is free
@@ -231,7 +255,8 @@ class Job:
             if not supported(self.model, self.x):
                 raise SystemExit("[bench] --executor fused does not support this shape/dtype")
             self.fused = FusedSAGE(self.model, self.graph, self.x, self.train_idx, self.y_train,
-                                   self.eval_idx, self.y_eval, self.eval_is_val, self.n_train)
+                                   self.eval_idx, self.y_eval, self.eval_is_val, self.n_train,
+                                   release_graph=True)
         self.steppers = {}
         if getattr(args, "cuda_graph", False) and dev.type == "cuda":
             from dgraph_amd.utils.graphed import GraphedStep, make_capturable
@@ -469,6 +494,10 @@ def main():
               f"per GPU: torchrun --nproc-per-node {args.gpus} bench.py --gpus {args.gpus})",
               file=sys.stderr)
         sys.exit(2)
+    if args.link_gbps > 0:
+        from dgraph_amd.comm import alltoallv as _a2a
+
+        _a2a.LOOPBACK_LINK_GBPS = args.link_gbps
     cfg = RunConfig.from_env()  # DGRAPH_<SECTION>_<FIELD> overrides (kernel knobs etc.)
     cfg.model.hidden, cfg.model.num_layers, cfg.model.dtype = args.hidden, args.layers, args.dtype
     cfg.data.dataset, cfg.data.global_frac = args.shape, args.global_frac
@@ -500,6 +529,7 @@ def main():
     alloc_timed = dict(getattr(job, "alloc_timed", {}))
     regions = region_breakdown(job)
     use_fused = job.use_fused
+    schedule = job.fused.schedule if job.fused is not None else {}
     pass_for = {str(k): v for k, v in getattr(job.fused, "pass_for", {}).items()} \
         if job.fused is not None else {}
     if job.fused is not None and job.fused.locality is not None:
@@ -601,6 +631,9 @@ def main():
                           "restrict_last": head_restrict,
                           "final_loss_local": final_loss,
                           "executor": "fused" if use_fused else "stack",
+                          "link_gbps": args.link_gbps,
+                          **({"schedule": schedule} if schedule else {}),
+                          **({"halo": halo} if halo else {}),
                           **({"regions": regions} if regions else {})}), flush=True)
     elif rank == 0:
         rec = {
@@ -642,6 +675,7 @@ def main():
                          "from the same forward + backward + allreduce + Adam"),
                 "launch": "HIP graph replay" if args.cuda_graph else "eager",
                 "halo_recompute": job_recompute,
+                **({"schedule": schedule} if schedule else {}),
                 **({"spmm_pass_cols": pass_for} if pass_for else {}),
                 "precision": ("bf16 storage/compute, fp32 accumulate, fp32 master weights"
                               if dtype == torch.bfloat16 else

@@ -39,9 +39,6 @@ def main():
     ap.add_argument("--feats", default="128,256")
     ap.add_argument("--skip-gemm", action="store_true")
     ap.add_argument("--skip-spmm", action="store_true")
-    ap.add_argument("--gemm-modes", default="256",
-                    help="native GEMM variants (set_f32_sched tile): 256 = exact-f32 MFMA, "
-                         "128 = lean tile, 3 = bf16x3 split products")
     ap.add_argument("--global-frac", type=float, default=0.05,
                     help="SpMM graph: fraction of uniformly random edges (1.0 = structureless)")
     ap.add_argument("--passes", default="64,128,256",
@@ -64,7 +61,6 @@ def main():
             print(f"[gemm] M={M} K={K_} N={N_}: {ms:.3f} ms {tf:.1f} TF/s; addmm+relu "
                   f"{ms_e:.3f} ms", flush=True)
             if N_ != 172:
-                from dgraph_amd import _native
                 from dgraph_amd.ops.f32 import gemm_f32
 
                 # error vs an fp64 reference, in units of sum_k |a_k b_k| (the scale an
@@ -74,33 +70,21 @@ def main():
                 err_lib = ((out_lib := torch.relu(torch.addmm(b, x, w))).double() - ref64
                            ).abs().div(scale).max().item()
                 del out_lib
-                for mode_s in a.gemm_modes.split(","):
-                    # "x3k": the bf16x3 kernel (gemm_x3.hip) with weights pre-split once
-                    mode = 256 if mode_s == "x3k" else int(mode_s)
-                    if mode_s == "x3k" and N_ not in (64, 128, 192, 256):
-                        continue
-                    _native.ops().set_f32_sched(0, mode)
-                    from dgraph_amd.ops.f32 import split_x3
-
-                    if K_ >= 256:  # dual form: two K/2 operands, one fused kernel
-                        h = K_ // 2
-                        x1, x2 = x[:, :h].contiguous(), x[:, h:].contiguous()
-                        kx = dict(b1x3=split_x3(w[:h]), b2x3=split_x3(w[h:])) \
-                            if mode_s == "x3k" else {}
-                        ms_n = _time(lambda: gemm_f32(x1, w[:h], x2, w[h:], bias=b, relu=True,
-                                                      out=out, **kx))
-                    else:
-                        kx = dict(b1x3=split_x3(w)) if mode_s == "x3k" else {}
-                        ms_n = _time(lambda: gemm_f32(x, w, bias=b, relu=True, out=out, **kx))
-                    err = (out.double() - ref64).abs().div(scale).max().item()
-                    tfn = 2 * M * K_ * N_ / ms_n / 1e9
-                    res[f"gemm_f32_m{mode}_K{K_}_N{N_}"] = {
-                        "ms": round(ms_n, 3), "TFps": round(tfn, 1),
-                        "max_err_rel_sumabs": err, "torch_mm_err_rel_sumabs": err_lib}
-                    print(f"[gemm_f32] mode {mode} dual+bias+relu K={K_} N={N_}: {ms_n:.3f} ms "
-                          f"{tfn:.1f} TF/s (max err / sum|ab| {err:.2e}; torch.mm fp32 "
-                          f"{err_lib:.2e})", flush=True)
-                _native.ops().set_f32_sched(0, 256)
+                if K_ >= 256:  # dual form: two K/2 operands, one fused kernel
+                    h = K_ // 2
+                    x1, x2 = x[:, :h].contiguous(), x[:, h:].contiguous()
+                    ms_n = _time(lambda: gemm_f32(x1, w[:h], x2, w[h:], bias=b, relu=True,
+                                                  out=out))
+                else:
+                    ms_n = _time(lambda: gemm_f32(x, w, bias=b, relu=True, out=out))
+                err = (out.double() - ref64).abs().div(scale).max().item()
+                tfn = 2 * M * K_ * N_ / ms_n / 1e9
+                res[f"gemm_f32_K{K_}_N{N_}"] = {
+                    "ms": round(ms_n, 3), "TFps": round(tfn, 1),
+                    "max_err_rel_sumabs": err, "torch_mm_err_rel_sumabs": err_lib}
+                print(f"[gemm_f32] dual+bias+relu K={K_} N={N_}: {ms_n:.3f} ms "
+                      f"{tfn:.1f} TF/s (max err / sum|ab| {err:.2e}; torch.mm fp32 "
+                      f"{err_lib:.2e})", flush=True)
                 del ref64, scale
             del x, w, out
         # weight gradient x^T g over tall M

@@ -51,7 +51,9 @@ void spmm_f32_ex_op(const at::Tensor& rowptr, const at::Tensor& col,
                     const c10::optional<at::Tensor>& row_map,
                     const c10::optional<at::Tensor>& gate,
                     const c10::optional<at::Tensor>& self_add,
-                    const c10::optional<at::Tensor>& self_map, int64_t self_row0) {
+                    const c10::optional<at::Tensor>& self_map, int64_t self_row0,
+                    const c10::optional<at::Tensor>& rowend,
+                    const c10::optional<at::Tensor>& x2, int64_t nsplit, int64_t pass_cols) {
   same_dev(rowptr, x, "rowptr");
   same_dev(col, x, "col");
   same_dev(out, x, "out");
@@ -63,7 +65,16 @@ void spmm_f32_ex_op(const at::Tensor& rowptr, const at::Tensor& col,
               "col must be contiguous int32/int64");
   TORCH_CHECK(x.size(1) == out.size(1), "x/out feature mismatch");
   const at::Tensor* ri = opt(row_ids);
-  const int64_t nrows = ri ? ri->numel() : rowptr.numel() - 1;
+  const at::Tensor* re = opt(rowend);
+  // rows of the CSR: rowptr holds one start per row (+ the end sentinel unless rowend is given)
+  const int64_t csr_rows = re ? re->numel() : rowptr.numel() - 1;
+  if (re) {
+    same_dev(*re, x, "rowend");
+    TORCH_CHECK(re->scalar_type() == at::kLong && re->is_contiguous() &&
+                    rowptr.numel() >= re->numel(),
+                "rowend must be contiguous int64 with at most rowptr's entries");
+  }
+  const int64_t nrows = ri ? ri->numel() : csr_rows;
   const int64_t* rid = idx64(row_ids, x, nrows, "row_ids");
   const int64_t* rmap = idx64(row_map, x, nrows, "row_map");
   if (!rmap) TORCH_CHECK(out.size(0) >= nrows, "out has fewer rows than the CSR rows");
@@ -75,22 +86,38 @@ void spmm_f32_ex_op(const at::Tensor& rowptr, const at::Tensor& col,
                 " must be contiguous float32");
     return p->data_ptr<float>();
   };
-  const float* ewp = f32opt(ew, "edge_weight");
-  if (ewp) TORCH_CHECK(ew->numel() == col.numel(), "edge_weight must be [E]");
-  const float* csp = f32opt(cs, "col_scale");
-  const float* rsp = f32opt(rs, "row_scale");
-  const int32_t* cm = nullptr;
+  SpmmF32Args a;
+  a.rowptr = rowptr.data_ptr<int64_t>();
+  a.rowend = re ? re->data_ptr<int64_t>() : nullptr;
+  a.col = col.data_ptr();
+  a.it = col.scalar_type() == at::kInt ? IType::I32 : IType::I64;
+  a.ew = f32opt(ew, "edge_weight");
+  if (a.ew) TORCH_CHECK(ew->numel() == col.numel(), "edge_weight must be [E]");
+  a.col_scale = f32opt(cs, "col_scale");
+  a.row_scale = f32opt(rs, "row_scale");
   if (const at::Tensor* p = opt(cmap)) {
     same_dev(*p, x, "col_map");
     TORCH_CHECK(p->scalar_type() == at::kInt && p->is_contiguous(),
                 "col_map must be contiguous int32");
-    cm = p->data_ptr<int32_t>();
+    a.col_map = p->data_ptr<int32_t>();
   }
   TORCH_CHECK(spmm_f32_rowgroup_ok(static_cast<int>(x.size(1)), x.stride(0), out.stride(0),
                                    x.data_ptr(), out.data_ptr()),
               "spmm_f32_ex: F % 4 == 0 and 16-B aligned rows/strides required");
-  const float* gp = nullptr;
-  int64_t ldg = 0;
+  if (const at::Tensor* p = opt(x2)) {
+    f32_rows(*p, "x2");
+    same_dev(*p, x, "x2");
+    TORCH_CHECK(p->size(1) == x.size(1) && p->stride(0) % 4 == 0 &&
+                    reinterpret_cast<uintptr_t>(p->data_ptr()) % 16 == 0,
+                "x2 must be 16-B aligned, as wide as x, row stride % 4 == 0");
+    TORCH_CHECK(nsplit >= 0 && nsplit <= x.size(0) && nsplit < (int64_t(1) << 32),
+                "nsplit must be in [0, rows of x]");
+    TORCH_CHECK(!a.col_map && !a.ew && !a.col_scale,
+                "x2 (two sources) is not combined with col_map / edge weights / col_scale");
+    a.x2 = p->data_ptr<float>();
+    a.ldx2 = p->stride(0);
+    a.nsplit = nsplit;
+  }
   if (const at::Tensor* gt = opt(gate)) {
     f32_rows(*gt, "gate");
     same_dev(*gt, x, "gate");
@@ -98,12 +125,9 @@ void spmm_f32_ex_op(const at::Tensor& rowptr, const at::Tensor& col,
                     reinterpret_cast<uintptr_t>(gt->data_ptr()) % 16 == 0,
                 "gate must be 16-B aligned with row stride % 4 == 0, width >= F");
     if (!rmap) TORCH_CHECK(gt->size(0) >= nrows, "gate has fewer rows than the output");
-    gp = gt->data_ptr<float>();
-    ldg = gt->stride(0);
+    a.gate = gt->data_ptr<float>();
+    a.ldgate = gt->stride(0);
   }
-  const float* sap = nullptr;
-  const int32_t* smp = nullptr;
-  int64_t lds = 0;
   if (const at::Tensor* sa = opt(self_add)) {
     f32_rows(*sa, "self_add");
     same_dev(*sa, x, "self_add");
@@ -118,17 +142,24 @@ void spmm_f32_ex_op(const at::Tensor& rowptr, const at::Tensor& col,
     const int64_t max_out = rmap ? out.size(0) : nrows;
     TORCH_CHECK(self_row0 >= 0 && self_row0 + max_out <= sm->numel(),
                 "self_map too short for self_row0 + output rows");
-    sap = sa->data_ptr<float>();
-    smp = sm->data_ptr<int32_t>();
-    lds = sa->stride(0);
+    a.self_add = sa->data_ptr<float>();
+    a.self_map = sm->data_ptr<int32_t>();
+    a.ld_self = sa->stride(0);
+    a.self_row0 = self_row0;
   }
+  a.row_ids = rid;
+  a.row_map = rmap;
+  a.x = x.data_ptr<float>();
+  a.ldx = x.stride(0);
+  a.out = out.data_ptr<float>();
+  a.ldo = out.stride(0);
+  a.nrows = nrows;
+  a.F = static_cast<int>(x.size(1));
+  a.beta = static_cast<float>(beta);
+  a.cap = cap;
+  a.pass_cols = static_cast<int>(pass_cols);
   c10::DeviceGuard g(x.device());
-  DG_HIP_CHECK(spmm_f32_rowgroup(col.scalar_type() == at::kInt ? IType::I32 : IType::I64,
-                                 rowptr.data_ptr<int64_t>(), col.data_ptr(), ewp, csp, rsp, cm,
-                                 rid, x.data_ptr<float>(), x.stride(0), out.data_ptr<float>(),
-                                 out.stride(0), nrows, static_cast<int>(x.size(1)),
-                                 static_cast<float>(beta), cap, rmap, stream_of(x), gp, ldg, sap,
-                                 lds, smp, self_row0));
+  DG_HIP_CHECK(spmm_f32_run(a, stream_of(x)));
 }
 
 void gemm_f32_op(const at::Tensor& A1, const at::Tensor& B1, const c10::optional<at::Tensor>& A2,
@@ -136,8 +167,7 @@ void gemm_f32_op(const at::Tensor& A1, const at::Tensor& B1, const c10::optional
                  const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& cin,
                  double beta, const c10::optional<at::Tensor>& gate,
                  const c10::optional<at::Tensor>& o_rows, bool relu, const at::Tensor& out,
-                 const c10::optional<at::Tensor>& row_scale,
-                 const c10::optional<at::Tensor>& b1x3, const c10::optional<at::Tensor>& b2x3) {
+                 const c10::optional<at::Tensor>& row_scale) {
   f32_rows(A1, "A1");
   f32_rows(B1, "B1");
   f32_rows(out, "out");
@@ -165,23 +195,8 @@ void gemm_f32_op(const at::Tensor& A1, const at::Tensor& B1, const c10::optional
     TORCH_CHECK(b2->size(0) == K2 && b2->size(1) == N, "gemm_f32: A2/B2 shape mismatch");
     TORCH_CHECK(a2->size(0) >= M, "gemm_f32: A2 has fewer than M rows");
   }
-  const at::Tensor *p1 = opt(b1x3), *p2 = opt(b2x3);
-  if (p1) {
-    auto chk = [&](const at::Tensor& p, int64_t Kx, const char* nm) {
-      same_dev(p, A1, nm);
-      TORCH_CHECK(p.scalar_type() == at::kBFloat16 && p.is_contiguous() && p.dim() == 3 &&
-                      p.size(0) == 3 && p.size(1) == N && p.size(2) == Kx,
-                  "gemm_f32: ", nm, " must be contiguous bf16 [3, N, K] split parts");
-    };
-    chk(*p1, K1, "b1x3");
-    TORCH_CHECK((a2 == nullptr) == (p2 == nullptr), "gemm_f32: b2x3 goes with A2");
-    if (p2) chk(*p2, K2, "b2x3");
-    TORCH_CHECK(gemm_x3_supported(N, K1, K2),
-                "gemm_f32 (bf16x3): unsupported shape N=", N, " K1=", K1, " K2=", K2);
-  } else {
-    TORCH_CHECK(gemm_f32_supported(N, K1, K2),
-                "gemm_f32: unsupported shape N=", N, " K1=", K1, " K2=", K2);
-  }
+  TORCH_CHECK(gemm_f32_supported(N, K1, K2),
+              "gemm_f32: unsupported shape N=", N, " K1=", K1, " K2=", K2);
   const float* bp = nullptr;
   if (const at::Tensor* b = opt(bias)) {
     same_dev(*b, A1, "bias");
@@ -217,15 +232,6 @@ void gemm_f32_op(const at::Tensor& A1, const at::Tensor& B1, const c10::optional
     rsp = rs->data_ptr<float>();
   }
   c10::DeviceGuard g(A1.device());
-  if (p1) {
-    DG_HIP_CHECK(gemm_x3(A1.data_ptr<float>(), A1.stride(0), K1,
-                         reinterpret_cast<const uint16_t*>(p1->data_ptr()),
-                         a2 ? a2->data_ptr<float>() : nullptr, a2 ? a2->stride(0) : 0, K2,
-                         p2 ? reinterpret_cast<const uint16_t*>(p2->data_ptr()) : nullptr, arp,
-                         bp, cp, ldc, static_cast<float>(beta), gp, ldg, orp, rsp, relu,
-                         out.data_ptr<float>(), out.stride(0), M, N, stream_of(A1)));
-    return;
-  }
   DG_HIP_CHECK(gemm_f32(A1.data_ptr<float>(), A1.stride(0), K1, B1.data_ptr<float>(),
                         B1.stride(0), a2 ? a2->data_ptr<float>() : nullptr,
                         a2 ? a2->stride(0) : 0, K2, b2 ? b2->data_ptr<float>() : nullptr,
@@ -236,8 +242,7 @@ void gemm_f32_op(const at::Tensor& A1, const at::Tensor& B1, const c10::optional
 
 void wgrad_f32_op(const at::Tensor& A1, const c10::optional<at::Tensor>& A2,
                   const c10::optional<at::Tensor>& a1_rows, const at::Tensor& G,
-                  const at::Tensor& partials, int64_t blocks, int64_t fresh_from,
-                  int64_t mode) {
+                  const at::Tensor& partials, int64_t blocks, int64_t fresh_from) {
   f32_rows(A1, "A1");
   f32_rows(G, "G");
   same_dev(G, A1, "G");
@@ -254,8 +259,7 @@ void wgrad_f32_op(const at::Tensor& A1, const c10::optional<at::Tensor>& A2,
     K2 = a2->size(1);
   }
   const int64_t K = A1.size(1) + K2;
-  TORCH_CHECK(mode == 1 ? wgrad_x3_supported(K, N) : wgrad_f32_supported(K, N),
-              "wgrad_f32: unsupported K=", K, " N=", N, " mode=", mode);
+  TORCH_CHECK(wgrad_f32_supported(K, N), "wgrad_f32: unsupported K=", K, " N=", N);
   TORCH_CHECK(partials.scalar_type() == at::kFloat && partials.is_contiguous() &&
                   partials.dim() == 3 && partials.size(1) == K && partials.size(2) == N,
               "partials must be contiguous float32 [P, K, N]");
@@ -263,14 +267,6 @@ void wgrad_f32_op(const at::Tensor& A1, const c10::optional<at::Tensor>& A2,
                   fresh_from <= partials.size(0),
               "wgrad_f32: 1 <= blocks <= P and 0 <= fresh_from <= P");
   c10::DeviceGuard g(A1.device());
-  if (mode == 1) {
-    DG_HIP_CHECK(wgrad_x3(A1.data_ptr<float>(), A1.stride(0), A1.size(1),
-                          a2 ? a2->data_ptr<float>() : nullptr, a2 ? a2->stride(0) : 0, K2, arp,
-                          G.data_ptr<float>(), G.stride(0), M, N, partials.data_ptr<float>(),
-                          static_cast<int>(blocks), static_cast<int>(fresh_from),
-                          stream_of(A1)));
-    return;
-  }
   DG_HIP_CHECK(wgrad_f32(A1.data_ptr<float>(), A1.stride(0), A1.size(1),
                          a2 ? a2->data_ptr<float>() : nullptr, a2 ? a2->stride(0) : 0, K2, arp,
                          G.data_ptr<float>(), G.stride(0), M, N, partials.data_ptr<float>(),
@@ -370,63 +366,25 @@ void set_spmm_f32_config_op(int64_t rowgroup, int64_t pass_cols) {
   set_spmm_f32_config(static_cast<int>(rowgroup), static_cast<int>(pass_cols));
 }
 
-void sage_fwd_f32_op(const at::Tensor& X, const at::Tensor& rowptr, const at::Tensor& col,
-                     const at::Tensor& inv_deg, const at::Tensor& Ws, const at::Tensor& Wn,
-                     const at::Tensor& bias, const at::Tensor& out, const at::Tensor& ring,
-                     const at::Tensor& err) {
-  f32_rows(X, "X");
-  f32_rows(out, "out");
-  const int64_t M = out.size(0), F = X.size(1);
-  TORCH_CHECK(F == 128 || F == 256, "sage_fwd_f32: input width must be 128 or 256");
-  TORCH_CHECK(out.size(1) == 256, "sage_fwd_f32: output width must be 256");
-  TORCH_CHECK(X.size(0) >= M && X.size(0) <= INT32_MAX, "sage_fwd_f32: X rows");
-  TORCH_CHECK(rowptr.scalar_type() == at::kLong && rowptr.is_contiguous() &&
-                  rowptr.numel() == M + 1, "sage_fwd_f32: rowptr must be int64 [M + 1]");
-  TORCH_CHECK(col.scalar_type() == at::kInt && col.is_contiguous(),
-              "sage_fwd_f32: col must be contiguous int32");
-  TORCH_CHECK(inv_deg.scalar_type() == at::kFloat && inv_deg.is_contiguous() &&
-                  inv_deg.numel() >= M, "sage_fwd_f32: inv_deg");
-  for (const at::Tensor* w : {&Ws, &Wn})
-    TORCH_CHECK(w->scalar_type() == at::kFloat && w->is_contiguous() && w->dim() == 2 &&
-                    w->size(0) == F && w->size(1) == 256, "sage_fwd_f32: weights must be [F, 256]");
-  TORCH_CHECK(bias.scalar_type() == at::kFloat && bias.is_contiguous() && bias.numel() == 256,
-              "sage_fwd_f32: bias [256]");
-  TORCH_CHECK(ring.scalar_type() == at::kFloat && ring.is_contiguous(), "sage_fwd_f32: ring");
-  TORCH_CHECK(err.scalar_type() == at::kInt && err.numel() >= 1, "sage_fwd_f32: err");
-  for (const at::Tensor* t : {&X, &rowptr, &col, &inv_deg, &Ws, &Wn, &bias, &ring, &err})
-    same_dev(*t, out, "operand");
-  c10::DeviceGuard g(out.device());
-  DG_HIP_CHECK(sage_fwd_f32(X.data_ptr<float>(), X.stride(0), static_cast<int>(F),
-                            rowptr.data_ptr<int64_t>(), col.data_ptr<int32_t>(),
-                            inv_deg.data_ptr<float>(), Ws.data_ptr<float>(), Wn.data_ptr<float>(),
-                            bias.data_ptr<float>(), out.data_ptr<float>(), out.stride(0), M,
-                            ring.data_ptr<float>(), ring.numel(), err.data_ptr<int>(),
-                            stream_of(out)));
-}
-
-void set_f32_sched_op(int64_t spmm_grid, int64_t gemm_tile) {
-  set_spmm_f32_grid(static_cast<int>(spmm_grid));
-  set_gemm_f32_tile(static_cast<int>(gemm_tile));
-}
+void set_f32_sched_op(int64_t spmm_grid) { set_spmm_f32_grid(static_cast<int>(spmm_grid)); }
 
 }  // namespace
 }  // namespace dgraph
 
 TORCH_LIBRARY_FRAGMENT(dgraph_amd, m) {
-  m.def("set_f32_sched(int spmm_grid, int gemm_tile) -> ()", &dgraph::set_f32_sched_op);
-  m.def("sage_fwd_f32(Tensor X, Tensor rowptr, Tensor col, Tensor inv_deg, Tensor Ws, "
-        "Tensor Wn, Tensor bias, Tensor(a!) out, Tensor(b!) ring, Tensor(c!) err) -> ()");
+  m.def("set_f32_sched(int spmm_grid) -> ()", &dgraph::set_f32_sched_op);
   m.def("set_spmm_f32_config(int rowgroup, int pass_cols=-1) -> ()",
         &dgraph::set_spmm_f32_config_op);
   m.def("spmm_f32_ex(Tensor rowptr, Tensor col, Tensor? edge_weight, Tensor? col_scale, "
         "Tensor? row_scale, Tensor? col_map, Tensor? row_ids, Tensor x, Tensor(a!) out, "
         "float beta=0., int cap=0, Tensor? row_map=None, Tensor? gate=None, "
-        "Tensor? self_add=None, Tensor? self_map=None, int self_row0=0) -> ()");
+        "Tensor? self_add=None, Tensor? self_map=None, int self_row0=0, Tensor? rowend=None, "
+        "Tensor? x2=None, int nsplit=0, int pass_cols=0) -> ()");
   m.def("gemm_f32(Tensor A1, Tensor B1, Tensor? A2, Tensor? B2, Tensor? a_rows, Tensor? bias, "
         "Tensor? cin, float beta, Tensor? gate, Tensor? o_rows, bool relu, Tensor(a!) out, "
-        "Tensor? row_scale=None, Tensor? b1x3=None, Tensor? b2x3=None) -> ()");
+        "Tensor? row_scale=None) -> ()");
   m.def("wgrad_f32(Tensor A1, Tensor? A2, Tensor? a1_rows, Tensor G, Tensor(a!) partials, "
-        "int blocks, int fresh_from, int mode=0) -> ()");
+        "int blocks, int fresh_from) -> ()");
   m.def("wgrad_f32_reduce(Tensor partials, Tensor(a!) out) -> ()");
   m.def("row_keep_bits(Tensor h, Tensor? rows, Tensor(a!) bits) -> ()");
   m.def("apply_keep_bits(Tensor(a!) g, Tensor bits) -> ()");
@@ -438,7 +396,6 @@ TORCH_LIBRARY_FRAGMENT(dgraph_amd, m) {
 TORCH_LIBRARY_IMPL(dgraph_amd, CUDA, m) {
   m.impl("spmm_f32_ex", &dgraph::spmm_f32_ex_op);
   m.impl("gemm_f32", &dgraph::gemm_f32_op);
-  m.impl("sage_fwd_f32", &dgraph::sage_fwd_f32_op);
   m.impl("wgrad_f32", &dgraph::wgrad_f32_op);
   m.impl("wgrad_f32_reduce", &dgraph::wgrad_f32_reduce_op);
   m.impl("row_keep_bits", &dgraph::row_keep_bits_op);

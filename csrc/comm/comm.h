@@ -25,4 +25,7 @@ hipError_t heap_signal(const uint64_t* peer_base, int64_t flag_off, int me, int 
 hipError_t heap_wait(const uint64_t* flags, int me, int world, uint64_t epoch,
                      int64_t max_spins, bool self_too, int* timed_out, hipStream_t st);
 
+// hold stream `st` for `us` microseconds of device wall-clock time (rehearsal link model)
+hipError_t link_delay(double us, hipStream_t st);
+
 }  // namespace dgraph

@@ -42,13 +42,9 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kBK = 32;
 
-// Two block shapes:
-//   * BM = 256 rows, 512 threads (8 waves, 2 per SIMD at ~240 VGPRs): the GEMM owns the
-//     whole register file of the CU — best when it runs alone;
-//   * "lean": BM = 128 rows, 256 threads (ONE wave per SIMD, 32 rows x N columns each),
-//     102 KB LDS: a memory-bound kernel on another stream (the next chunk's aggregation)
-//     keeps 2 waves per SIMD resident next to it, so the two overlap on every CU instead of
-//     taking turns (the matrix pipe and the vector-memory pipe are different units).
+// Block shape: BM = 256 rows, 512 threads (8 waves, 2 per SIMD at ~240 VGPRs): the GEMM owns
+// the whole register file of the CU (a 128-row one-wave-per-SIMD variant meant to co-reside
+// with the aggregation measured slower and was removed, PERFORMANCE.md).
 template <int BM, int N>
 struct GCfg;
 // (BM, N): (TM, TN, WM, WN) with 16*TM*WM = BM and 16*TN*WN = N; threads = 64*WM*WN
@@ -57,13 +53,8 @@ template <> struct GCfg<256, 192> { static constexpr int TM = 4, TN = 6, WM = 4,
 template <> struct GCfg<256, 176> { static constexpr int TM = 2, TN = 11, WM = 8, WN = 1; };
 template <> struct GCfg<256, 128> { static constexpr int TM = 2, TN = 8, WM = 8, WN = 1; };
 template <> struct GCfg<256, 64> { static constexpr int TM = 2, TN = 4, WM = 8, WN = 1; };
-template <> struct GCfg<128, 256> { static constexpr int TM = 2, TN = 16, WM = 4, WN = 1; };
-template <> struct GCfg<128, 192> { static constexpr int TM = 2, TN = 12, WM = 4, WN = 1; };
-template <> struct GCfg<128, 176> { static constexpr int TM = 2, TN = 11, WM = 4, WN = 1; };
-template <> struct GCfg<128, 128> { static constexpr int TM = 2, TN = 8, WM = 4, WN = 1; };
-template <> struct GCfg<128, 64> { static constexpr int TM = 2, TN = 4, WM = 4, WN = 1; };
 template <int BM>
-constexpr int threads_of() { return BM == 256 ? 512 : 256; }
+constexpr int threads_of() { return 512; }
 
 // A stage: 16-B chunk c of row r lives at chunk a_chunk(r, c) of the row (XOR swizzle by
 // row pair; table found by exhaustive search over the ds_read_b128 lane groups)
@@ -88,38 +79,7 @@ struct GLds {
 template <int BP>
 __device__ __forceinline__ int b_row(int k) { return k * BP + ((k >> 3) & 1) * 16; }
 
-// ---- fp32 as three bf16 parts (x = hi + mid + lo EXACTLY for normal x: hi and mid are
-// round-to-nearest-even bf16 of x and of x - hi, lo = x - hi - mid has <= 8 significant bits).
-typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
-__device__ __forceinline__ uint32_t rne_bf16_bits(float x) {
-  uint32_t u = __float_as_uint(x);
-  u += 0x7FFFu + ((u >> 16) & 1u);
-  return u & 0xFFFF0000u;
-}
-// 8 fp32 (k order) -> packed bf16x8 hi / mid / lo (element k in half k&1 of word k>>1)
-__device__ __forceinline__ void split3(const f32x4& f0, const f32x4& f1, uint4& H, uint4& M,
-                                       uint4& Lo) {
-  uint32_t h[8], m[8], l[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const float x = k < 4 ? f0[k] : f1[k - 4];
-    h[k] = rne_bf16_bits(x);
-    const float r1 = x - __uint_as_float(h[k]);
-    m[k] = rne_bf16_bits(r1);
-    l[k] = __float_as_uint(r1 - __uint_as_float(m[k]));
-  }
-  auto pk = [](uint32_t lo_e, uint32_t hi_e) { return __builtin_amdgcn_perm(hi_e, lo_e, 0x07060302u); };
-  H = uint4{pk(h[0], h[1]), pk(h[2], h[3]), pk(h[4], h[5]), pk(h[6], h[7])};
-  M = uint4{pk(m[0], m[1]), pk(m[2], m[3]), pk(m[4], m[5]), pk(m[6], m[7])};
-  Lo = uint4{pk(l[0], l[1]), pk(l[2], l[3]), pk(l[4], l[5]), pk(l[6], l[7])};
-}
-__device__ __forceinline__ f32x4 mfma_bf(const uint4& a, const uint4& b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
-                                                 __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
-}
-
-template <int BM, int N, bool HAS_A2, bool RELU, bool HAS_BIAS, bool HAS_CIN, bool HAS_GATE,
-          bool X3 = false>
+template <int BM, int N, bool HAS_A2, bool RELU, bool HAS_BIAS, bool HAS_CIN, bool HAS_GATE>
 __device__ __forceinline__ void gemm_f32_body(
     const float* __restrict__ A1, int64_t lda1, int K1, const float* __restrict__ B1,
     int64_t ldb1, const float* __restrict__ A2, int64_t lda2, int K2,
@@ -253,36 +213,7 @@ __device__ __forceinline__ void gemm_f32_body(
         af[a][1] = *reinterpret_cast<const f32x4*>(p + a_chunk(r, 2 * lh + 1) * 4);
       }
       const float* sbw = sb + b_row<L::BP>(8 * lh) + bcol_w + li;
-      if constexpr (X3) {
-        // one 16x16x32 bf16 MFMA per (a, b, product) covers the whole 32-deep stage: the six
-        // products of the split operands whose magnitude reaches fp32 rounding, smallest
-        // first (a_lo b_hi, a_hi b_lo, a_mid b_mid, a_mid b_hi, a_hi b_mid, a_hi b_hi); the
-        // dropped terms (mid*lo, lo*mid, lo*lo) are <= 2^-24 |a b| together
-        uint4 ah[TM], am[TM], al[TM];
-#pragma unroll
-        for (int a = 0; a < TM; ++a) split3(af[a][0], af[a][1], ah[a], am[a], al[a]);
-#pragma unroll
-        for (int b = 0; b < TN; ++b) {
-          f32x4 b0, b1;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            b0[j] = sbw[j * L::BP + b * 16];
-            b1[j] = sbw[(j + 4) * L::BP + b * 16];
-          }
-          uint4 bh, bm, bl;
-          split3(b0, b1, bh, bm, bl);
-#pragma unroll
-          for (int a = 0; a < TM; ++a) {
-            f32x4 c = acc[a][b];
-            c = mfma_bf(al[a], bh, c);
-            c = mfma_bf(ah[a], bl, c);
-            c = mfma_bf(am[a], bm, c);
-            c = mfma_bf(am[a], bh, c);
-            c = mfma_bf(ah[a], bm, c);
-            acc[a][b] = mfma_bf(ah[a], bh, c);
-          }
-        }
-      } else if constexpr (BM == 256) {
+      {
         // B fragments double-buffered across MFMA steps: step j+1's LDS reads are issued
         // before step j's TM*TN MFMAs
         float bf[2][TN];
@@ -300,29 +231,6 @@ __device__ __forceinline__ void gemm_f32_body(
 #pragma unroll
             for (int b = 0; b < TN; ++b)
               acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bf[j & 1][b], acc[a][b], 0, 0, 0);
-          }
-        }
-      } else {
-        // lean: ONE rolling set of B fragments — fragment b of step j+1 is read right after
-        // its last use in step j (TN MFMAs ahead of its own use), half the registers of a
-        // double buffer
-        float bf[TN];
-#pragma unroll
-        for (int b = 0; b < TN; ++b) bf[b] = sbw[b * 16];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-#pragma unroll
-          for (int a = 0; a + 1 < TM; ++a) {
-            const float av = af[a][j >> 2][j & 3];
-#pragma unroll
-            for (int b = 0; b < TN; ++b)
-              acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bf[b], acc[a][b], 0, 0, 0);
-          }
-          const float av = af[TM - 1][j >> 2][j & 3];
-#pragma unroll
-          for (int b = 0; b < TN; ++b) {
-            acc[TM - 1][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bf[b], acc[TM - 1][b], 0, 0, 0);
-            if (j + 1 < 8) bf[b] = sbw[(j + 1) * L::BP + b * 16];
           }
         }
       }
@@ -377,23 +285,6 @@ __global__ __launch_bounds__(512, 1) void gemm_f32_kernel(DG_GEMM_F32_ARGS) {
   gemm_f32_body<256, N, HAS_A2, RELU, HAS_BIAS, HAS_CIN, HAS_GATE>(DG_GEMM_F32_PASS);
 }
 
-// fp32 products as bf16x3 split MFMAs (same tile as gemm_f32_kernel)
-template <int N, bool HAS_A2, bool RELU, bool HAS_BIAS, bool HAS_CIN, bool HAS_GATE>
-__global__ __launch_bounds__(512, 1) void gemm_f32_x3_kernel(DG_GEMM_F32_ARGS) {
-  gemm_f32_body<256, N, HAS_A2, RELU, HAS_BIAS, HAS_CIN, HAS_GATE, true>(DG_GEMM_F32_PASS);
-}
-
-// lean tile: one wave per SIMD; its registers (<= 256) leave the rest of the file to a
-// co-resident kernel
-template <int N, bool HAS_A2, bool RELU, bool HAS_BIAS, bool HAS_CIN, bool HAS_GATE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void gemm_f32_lean_kernel(DG_GEMM_F32_ARGS) {
-  gemm_f32_body<128, N, HAS_A2, RELU, HAS_BIAS, HAS_CIN, HAS_GATE>(DG_GEMM_F32_PASS);
-}
-
-// row tile of the next launches: 256 (default) or 128 (lean; set_gemm_f32_tile); 3 = the
-// 256-row tile with bf16x3 split products
-int g_gemm_f32_bm = 256;
-
 template <int N, bool HAS_A2, bool RELU, bool HAS_BIAS, bool HAS_CIN, bool HAS_GATE>
 hipError_t launch_gemm_f32(const float* A1, int64_t lda1, int K1, const float* B1, int64_t ldb1,
                            const float* A2, int64_t lda2, int K2, const float* B2,
@@ -401,20 +292,15 @@ hipError_t launch_gemm_f32(const float* A1, int64_t lda1, int K1, const float* B
                            const float* cin, int64_t ldc, float beta, const float* gate,
                            int64_t ldg, const int64_t* o_rows, const float* rsc, float* out,
                            int64_t ldo, int64_t M, hipStream_t st) {
-  const bool lean = g_gemm_f32_bm == 128;
-  const bool x3 = g_gemm_f32_bm == 3;
-  auto kern = lean ? &gemm_f32_lean_kernel<N, HAS_A2, RELU, HAS_BIAS, HAS_CIN, HAS_GATE>
-              : x3 ? &gemm_f32_x3_kernel<N, HAS_A2, RELU, HAS_BIAS, HAS_CIN, HAS_GATE>
-                   : &gemm_f32_kernel<N, HAS_A2, RELU, HAS_BIAS, HAS_CIN, HAS_GATE>;
-  const int kBM = lean ? 128 : 256;
-  const size_t lds = lean ? GLds<128, N>::BYTES : GLds<256, N>::BYTES;
-  static_assert(GLds<256, N>::BYTES <= 160 * 1024, "LDS budget");
-  static bool attr[3] = {false, false, false};
-  const int ai = lean ? 1 : x3 ? 2 : 0;
-  if (!attr[ai]) {
+  auto kern = &gemm_f32_kernel<N, HAS_A2, RELU, HAS_BIAS, HAS_CIN, HAS_GATE>;
+  constexpr int kBM = 256;
+  constexpr size_t lds = GLds<256, N>::BYTES;
+  static_assert(lds <= 160 * 1024, "LDS budget");
+  static bool attr = false;
+  if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
-    attr[ai] = true;
+    attr = true;
   }
   static int num_cus = 0;
   if (num_cus == 0) {
@@ -427,7 +313,7 @@ hipError_t launch_gemm_f32(const float* A1, int64_t lda1, int K1, const float* B
   // persistent: one block per CU (LDS-limited), each walking tiles blockIdx + k * grid
   const int64_t ntiles = (M + kBM - 1) / kBM;
   const int64_t blocks = ntiles < num_cus ? ntiles : num_cus;
-  hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(blocks)), dim3(lean ? 256 : 512), lds, st, A1,
+  hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(blocks)), dim3(512), lds, st, A1,
                      lda1, K1, B1, ldb1, A2, lda2, K2, B2, ldb2, a_rows, bias, cin, ldc, beta,
                      gate, ldg, o_rows, rsc, out, ldo, M);
   return hipGetLastError();
@@ -480,8 +366,6 @@ hipError_t gemm_f32_n(const float* A1, int64_t lda1, int K1, const float* B1, in
 inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 }  // namespace
-
-void set_gemm_f32_tile(int bm) { g_gemm_f32_bm = (bm == 128 || bm == 3) ? bm : 256; }
 
 bool gemm_f32_supported(int64_t N, int64_t K1, int64_t K2) {
   return (N == 64 || N == 128 || N == 176 || N == 192 || N == 256) && K1 > 0 &&

@@ -52,12 +52,47 @@ hipError_t spmm_f32_rowgroup(IType it, const int64_t* rowptr, const void* col,
 // self_add (nullable): output row o also gets self_add[self_map[self_row0 + o]] (skipped
 // when < 0) after the row scale / beta and before the gate; gate (nullable, indexed like
 // out): the stored value is kept where gate > 0, else 0
+//
+// The full argument set of the same kernel: rowend (nullable) ends row rr's entries at
+// rowend[rr] instead of rowptr[rr + 1]; x2 (nullable): column c >= nsplit reads x2 row
+// c - nsplit (two sources in one pass; not with col_map / edge weights / col_scale);
+// pass_cols: column-pass width of this call (0 = the process default).
+struct SpmmF32Args {
+  const int64_t* rowptr = nullptr;
+  const int64_t* rowend = nullptr;
+  const void* col = nullptr;
+  IType it = IType::I32;
+  const float* ew = nullptr;
+  const float* col_scale = nullptr;
+  const float* row_scale = nullptr;
+  const int32_t* col_map = nullptr;
+  const int64_t* row_ids = nullptr;
+  const int64_t* row_map = nullptr;
+  const float* x = nullptr;
+  int64_t ldx = 0;
+  const float* x2 = nullptr;
+  int64_t ldx2 = 0;
+  int64_t nsplit = 0;
+  float* out = nullptr;
+  int64_t ldo = 0;
+  int64_t nrows = 0;
+  int F = 0;
+  float beta = 0.f;
+  int64_t cap = 0;
+  const float* gate = nullptr;
+  int64_t ldgate = 0;
+  const float* self_add = nullptr;
+  int64_t ld_self = 0;
+  const int32_t* self_map = nullptr;
+  int64_t self_row0 = 0;
+  int pass_cols = 0;
+};
+hipError_t spmm_f32_run(const SpmmF32Args& a, hipStream_t st);
 void set_spmm_f32_pass_cols(int cols);
 // rowgroup: 1 = fp32 row-group kernel (default), 0 = generic kernels; pass_cols: column
 // pass width (0 = default 64); negative arguments leave a setting unchanged
 void set_spmm_f32_config(int rowgroup, int pass_cols);
 void set_spmm_f32_grid(int blocks);   // 0 = uncapped
-void set_gemm_f32_tile(int bm);       // 256 (default) or 128 (lean, co-resident)
 
 // Hub-row splitting (rows whose degree exceeds `cap` are aggregated in three steps):
 //   1. spmm_csr(..., cap): every row sums at most its first `cap` entries;
@@ -208,26 +243,6 @@ hipError_t dual_gemm_bs(const void* A1, int64_t lda1, const void* B1t, int64_t K
 // operands with leading dimensions % 4 == 0. a_rows / o_rows nullable int64 [M].
 // gate (nullable, [*, N] with ldg): v = gate[o(i)][n] > 0 ? v : 0. cin may alias out.
 bool gemm_f32_supported(int64_t N, int64_t K1, int64_t K2);
-// the same dual GEMM as bf16x3 split-product MFMAs (gemm_x3.hip): B1p / B2p are the weights
-// pre-split into bf16 parts stored [3][N][K] (k contiguous); N in {64, 128, 192, 256}
-bool gemm_x3_supported(int64_t N, int64_t K1, int64_t K2);
-// fused fp32 SAGE hidden layer (sage_fwd_f32.hip): out = relu(X Ws + mean_N(X) Wn + b),
-// F in {128, 256}, 256 outputs; ring: >= min(tiles, CUs) * 2 * 128 * F floats; err: int flag
-hipError_t sage_fwd_f32(const float* X, int64_t ldx, int F, const int64_t* rowptr,
-                        const int32_t* col, const float* inv_deg, const float* Ws,
-                        const float* Wn, const float* bias, float* out, int64_t ldo, int64_t M,
-                        float* ring, int64_t ring_floats, int* err, hipStream_t st);
-// weight gradient as bf16x3 split products (wgrad_x3.hip), same contract as wgrad_f32
-bool wgrad_x3_supported(int64_t K, int64_t N);
-hipError_t wgrad_x3(const float* A1, int64_t lda1, int64_t K1, const float* A2, int64_t lda2,
-                    int64_t K2, const int64_t* a1_rows, const float* G, int64_t ldg, int64_t M,
-                    int64_t N, float* partials, int P, int fresh_from, hipStream_t st);
-hipError_t gemm_x3(const float* A1, int64_t lda1, int64_t K1, const uint16_t* B1p,
-                   const float* A2, int64_t lda2, int64_t K2, const uint16_t* B2p,
-                   const int64_t* a_rows, const float* bias, const float* cin, int64_t ldc,
-                   float beta, const float* gate, int64_t ldg, const int64_t* o_rows,
-                   const float* row_scale, bool relu, float* out, int64_t ldo, int64_t M,
-                   int64_t N, hipStream_t st);
 hipError_t gemm_f32(const float* A1, int64_t lda1, int64_t K1, const float* B1, int64_t ldb1,
                     const float* A2, int64_t lda2, int64_t K2, const float* B2, int64_t ldb2,
                     const int64_t* a_rows, const float* bias, const float* cin, int64_t ldc,

@@ -18,6 +18,12 @@
 //   * col_map (compile-time CMAP): column c reads x row col_map[c]; entries with
 //     col_map[c] < 0 are skipped (x is a row-compacted operand, e.g. a gradient that is
 //     nonzero only on the support rows and is stored only there).
+//   * rowend (runtime, nullable): row r's entries are [rowptr[rr], rowend[rr]) instead of
+//     [rowptr[rr], rowptr[rr + 1]) — one part of a row whose entries are stored in two runs
+//     (a vertex-partitioned rank's unified adjacency: interior columns, then halo columns);
+//   * two sources (compile-time TWO): column c < nsplit reads x row c, column c >= nsplit
+//     reads x2 row c - nsplit (the received halo rows) — interior and halo of a row in ONE
+//     pass when the halo is resident, instead of an interior pass plus a beta=1 halo pass.
 // Accumulation fp32 with packed FMAs in a fixed order per row: bitwise deterministic.
 #include "../common.h"
 #include "kernels.h"
@@ -27,38 +33,48 @@ namespace {
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-template <typename IdxT, int LPR, int WMODE, bool CMAP>
-__global__ __launch_bounds__(256) void spmm_f32_rowgroup_kernel(
-    const int64_t* __restrict__ rowptr, const IdxT* __restrict__ col,
-    const float* __restrict__ ew, const float* __restrict__ col_scale,
-    const float* __restrict__ row_scale, const int32_t* __restrict__ col_map,
-    const int64_t* __restrict__ row_ids, const float* __restrict__ x, int64_t ldx,
-    float* __restrict__ out, int64_t ldo, int64_t nrows, int F, float beta, int cap,
-    const int64_t* __restrict__ row_map, const float* __restrict__ gate, int64_t ldgate,
-    const float* __restrict__ self_add, int64_t ld_self, const int32_t* __restrict__ self_map,
-    int64_t self_row0) {
+template <typename IdxT, int LPR, int WMODE, bool CMAP, bool TWO>
+__global__ __launch_bounds__(256) void spmm_f32_rowgroup_kernel(SpmmF32Args a) {
   constexpr int VEC = 4;
   constexpr int G = kWave / LPR;
   constexpr int U = LPR < 8 ? LPR : 8;  // neighbour rows in flight per lane per batch
   constexpr bool HAS_EW = (WMODE & 1) != 0;
   constexpr bool HAS_CS = (WMODE & 2) != 0;
+  const IdxT* __restrict__ col = static_cast<const IdxT*>(a.col);
+  const int64_t* __restrict__ rowptr = a.rowptr;
   const int lane = threadIdx.x & (kWave - 1);
   const int g = lane / LPR;
   const int l = lane % LPR;
   const int wv = threadIdx.x >> 6;  // wave of the block (its row of the compaction table)
   __shared__ uint8_t inv[CMAP ? 4 * 64 : 1];
+  const int64_t nrows = a.nrows;
+  const int F = a.F;
   const int64_t ngroups = (nrows + G - 1) / G;
   const int64_t q0 = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
   const int64_t qstep = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
   const int f = l * VEC;  // launcher guarantees F <= LPR * VEC
   const bool active = f < F;
-  const float* xf = x + (active ? f : 0);
+  const float* xf = a.x + (active ? f : 0);
+  const float* x2f = TWO ? a.x2 + (active ? f : 0) : nullptr;
+  const uint64_t ldx = static_cast<uint64_t>(a.ldx);
+  const uint64_t ldx2 = static_cast<uint64_t>(a.ldx2);
+  const uint32_t ns = static_cast<uint32_t>(a.nsplit);
+  const int cap = a.cap;
+  // the row of x (or x2) that column id c reads
+  auto row_ptr = [&](uint32_t c) -> const float* {
+    if constexpr (TWO) {
+      return c < ns ? xf + static_cast<uint64_t>(c) * ldx
+                    : x2f + static_cast<uint64_t>(c - ns) * ldx2;
+    } else {
+      return xf + static_cast<uint64_t>(c) * ldx;
+    }
+  };
   for (int64_t q = q0; q < ngroups; q += qstep) {
     const int64_t r = q * G + g;
     const bool has_row = r < nrows;
-    const int64_t rr = has_row ? (row_ids ? row_ids[r] : r) : 0;
+    const int64_t rr = has_row ? (a.row_ids ? a.row_ids[r] : r) : 0;
     const int64_t s = has_row ? rowptr[rr] : 0;
-    const int64_t deg1 = has_row ? rowptr[rr + 1] - s : 0;
+    const int64_t deg1 = has_row ? (a.rowend ? a.rowend[rr] : rowptr[rr + 1]) - s : 0;
     const int deg = static_cast<int>(deg1 > cap ? cap : deg1);
     int maxdeg = deg;
 #pragma unroll
@@ -70,20 +86,21 @@ __global__ __launch_bounds__(256) void spmm_f32_rowgroup_kernel(
 #pragma unroll
     for (int i = 0; i < VEC / 2; ++i) acc[i] = f32x2{0.f, 0.f};
     // slot k of this group's row -> (row of x to read, weight); padding slots read the
-    // row of entry 0 (valid whenever maxdeg > 0) with weight 0
+    // row of the group's entry 0 (valid whenever deg > 0; a row without entries reads
+    // entry 0 of the whole column array, which exists whenever maxdeg > 0) with weight 0
     auto load_c = [&](int k) -> int64_t {
-      const IdxT c = col[k < deg ? s + k : 0];
+      const IdxT c = col[k < deg ? s + k : (deg > 0 ? s : 0)];
       return static_cast<int64_t>(c);
     };
     auto load_w = [&](int64_t& c, int k) -> float {
       float w = k < deg ? 1.f : 0.f;
       if constexpr (CMAP) {
-        const int32_t m = col_map[c];
+        const int32_t m = a.col_map[c];
         w = m >= 0 ? w : 0.f;
         c = m >= 0 ? m : 0;
       }
-      if constexpr (HAS_EW) w *= ew[k < deg ? s + k : 0];
-      if constexpr (HAS_CS) w *= col_scale[c];
+      if constexpr (HAS_EW) w *= a.ew[k < deg ? s + k : (deg > 0 ? s : 0)];
+      if constexpr (HAS_CS) w *= a.col_scale[c];
       return w;
     };
     int64_t my_c = 0;
@@ -127,9 +144,7 @@ __global__ __launch_bounds__(256) void spmm_f32_rowgroup_kernel(
             w[u] = j < cnt ? ww : 0.f;
           }
 #pragma unroll
-          for (int u = 0; u < U; ++u)
-            v[u] = *reinterpret_cast<const uint4*>(xf + static_cast<uint64_t>(c[u]) *
-                                                            static_cast<uint64_t>(ldx));
+          for (int u = 0; u < U; ++u) v[u] = *reinterpret_cast<const uint4*>(row_ptr(c[u]));
 #pragma unroll
           for (int u = 0; u < U; ++u) {
             const f32x2 ww{w[u], w[u]};
@@ -157,9 +172,7 @@ __global__ __launch_bounds__(256) void spmm_f32_rowgroup_kernel(
         // shuffles, unconditionally: past the end it re-reads entry 0)
         if (j0 == 0) nx_c = load_c(kn);
 #pragma unroll
-        for (int u = 0; u < U; ++u)
-          v[u] = *reinterpret_cast<const uint4*>(xf + static_cast<uint64_t>(c[u]) *
-                                                          static_cast<uint64_t>(ldx));
+        for (int u = 0; u < U; ++u) v[u] = *reinterpret_cast<const uint4*>(row_ptr(c[u]));
 #pragma unroll
         for (int u = 0; u < U; ++u) w[u] = __shfl(my_w, g * LPR + j0 + u, kWave);
 #pragma unroll
@@ -175,9 +188,10 @@ __global__ __launch_bounds__(256) void spmm_f32_rowgroup_kernel(
       my_c = nx_c;
     }
     if (has_row && active) {
-      const int64_t orow = row_map ? row_map[r] : r;
-      const float rs = row_scale ? row_scale[orow] : 1.f;
-      float* o = out + orow * ldo + f;
+      const int64_t orow = a.row_map ? a.row_map[r] : r;
+      const float rs = a.row_scale ? a.row_scale[orow] : 1.f;
+      float* o = a.out + orow * a.ldo + f;
+      const float beta = a.beta;
       float4 res;
       if (beta != 0.f) {
         const float4 old = *reinterpret_cast<const float4*>(o);
@@ -191,18 +205,18 @@ __global__ __launch_bounds__(256) void spmm_f32_rowgroup_kernel(
         res.z = acc[1].x * rs;
         res.w = acc[1].y * rs;
       }
-      if (self_add) {  // + the row's own term, stored row-compacted (row-uniform branch)
-        const int32_t m = self_map[self_row0 + orow];
+      if (a.self_add) {  // + the row's own term, stored row-compacted (row-uniform branch)
+        const int32_t m = a.self_map[a.self_row0 + orow];
         if (m >= 0) {
-          const float4 sv = *reinterpret_cast<const float4*>(self_add + m * ld_self + f);
+          const float4 sv = *reinterpret_cast<const float4*>(a.self_add + m * a.ld_self + f);
           res.x += sv.x;
           res.y += sv.y;
           res.z += sv.z;
           res.w += sv.w;
         }
       }
-      if (gate) {  // ReLU derivative from a stored activation (row-uniform branch)
-        const float4 gv = *reinterpret_cast<const float4*>(gate + orow * ldgate + f);
+      if (a.gate) {  // ReLU derivative from a stored activation (row-uniform branch)
+        const float4 gv = *reinterpret_cast<const float4*>(a.gate + orow * a.ldgate + f);
         res.x = gv.x > 0.f ? res.x : 0.f;
         res.y = gv.y > 0.f ? res.y : 0.f;
         res.z = gv.z > 0.f ? res.z : 0.f;
@@ -218,36 +232,37 @@ __global__ __launch_bounds__(256) void spmm_f32_rowgroup_kernel(
 // kernel of another stream (set_spmm_f32_grid)
 int g_f32_grid_cap = 0;
 
-template <typename IdxT, bool CMAP>
-hipError_t launch_f32_rg(const int64_t* rowptr, const IdxT* col, const float* ew,
-                         const float* cs, const float* rs, const int32_t* cmap,
-                         const int64_t* rids, const float* x, int64_t ldx, float* out,
-                         int64_t ldo, int64_t nrows, int F, float beta, int icap,
-                         const int64_t* row_map, const float* gate, int64_t ldgate,
-                         const float* sadd, int64_t ld_self, const int32_t* smap,
-                         int64_t srow0, hipStream_t st) {
-  const int lanes = (F + 3) / 4;
+template <typename IdxT>
+hipError_t launch_f32_rg(const SpmmF32Args& a, hipStream_t st) {
+  const int lanes = (a.F + 3) / 4;
   const int LPR = lanes <= 8 ? 8 : lanes <= 16 ? 16 : lanes <= 32 ? 32 : 64;
   const int64_t G = kWave / LPR;
-  const int64_t ngroups = (nrows + G - 1) / G;
+  const int64_t ngroups = (a.nrows + G - 1) / G;
   int64_t blocks = (ngroups + 3) / 4;  // in order: one row group per wave
   if (g_f32_grid_cap > 0 && blocks > g_f32_grid_cap) blocks = g_f32_grid_cap;
   if (blocks > 0x7fffffff) return hipErrorInvalidValue;
-  const int wmode = (ew != nullptr ? 1 : 0) | (cs != nullptr ? 2 : 0);
+  const int wmode = (a.ew != nullptr ? 1 : 0) | (a.col_scale != nullptr ? 2 : 0);
+  const bool cmap = a.col_map != nullptr;
+  const bool two = a.x2 != nullptr;
+  if (two && (cmap || wmode != 0)) return hipErrorInvalidValue;  // not instantiated
   dim3 grid(static_cast<unsigned>(blocks)), block(256);
-#define DG_F32_W(LPR_, W_)                                                                \
-  if (LPR == LPR_ && wmode == W_) {                                                       \
-    hipLaunchKernelGGL((spmm_f32_rowgroup_kernel<IdxT, LPR_, W_, CMAP>), grid, block, 0, \
-                       st, rowptr, col, ew, cs, rs, cmap, rids, x, ldx, out, ldo, nrows,  \
-                       F, beta, icap, row_map, gate, ldgate, sadd, ld_self, smap, srow0);  \
-    return hipGetLastError();                                                             \
+#define DG_F32_K(LPR_, W_, C_, T_)                                                          \
+  if (LPR == LPR_ && wmode == W_ && cmap == C_ && two == T_) {                              \
+    hipLaunchKernelGGL((spmm_f32_rowgroup_kernel<IdxT, LPR_, W_, C_, T_>), grid, block, 0, \
+                       st, a);                                                              \
+    return hipGetLastError();                                                               \
   }
-#define DG_F32(LPR_) DG_F32_W(LPR_, 0) DG_F32_W(LPR_, 1) DG_F32_W(LPR_, 2) DG_F32_W(LPR_, 3)
+#define DG_F32(LPR_)                                                                        \
+  DG_F32_K(LPR_, 0, false, false) DG_F32_K(LPR_, 1, false, false)                           \
+  DG_F32_K(LPR_, 2, false, false) DG_F32_K(LPR_, 3, false, false)                           \
+  DG_F32_K(LPR_, 0, true, false) DG_F32_K(LPR_, 1, true, false)                             \
+  DG_F32_K(LPR_, 2, true, false) DG_F32_K(LPR_, 3, true, false)                             \
+  DG_F32_K(LPR_, 0, false, true)
   DG_F32(8)
   DG_F32(16)
   DG_F32(32)
   DG_F32(64)
-#undef DG_F32_W
+#undef DG_F32_K
 #undef DG_F32
   return hipErrorInvalidValue;
 }
@@ -268,6 +283,36 @@ bool spmm_f32_rowgroup_ok(int F, int64_t ldx, int64_t ldo, const void* x, const 
          ldx < (int64_t(1) << 40);
 }
 
+hipError_t spmm_f32_run(const SpmmF32Args& args, hipStream_t st) {
+  if (args.nrows <= 0 || args.F <= 0) return hipSuccess;
+  auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  if (args.self_add && (!args.self_map || !al(args.self_add) || args.ld_self % 4))
+    return hipErrorInvalidValue;
+  if (args.gate && (!al(args.gate) || args.ldgate % 4)) return hipErrorInvalidValue;
+  if (!spmm_f32_rowgroup_ok(args.F, args.ldx, args.ldo, args.x, args.out))
+    return hipErrorInvalidValue;
+  if (args.x2 && (!al(args.x2) || args.ldx2 % 4 || args.nsplit < 0 ||
+                  args.nsplit >= (int64_t(1) << 32)))
+    return hipErrorInvalidValue;
+  SpmmF32Args a = args;
+  a.cap = (args.cap > 0 && args.cap < (int64_t(1) << 30)) ? args.cap : (1 << 30);
+  int pc = args.pass_cols > 0 ? args.pass_cols : g_f32_pass_cols;
+  pc = pc > 256 ? 256 : (pc < 16 ? 16 : pc - pc % 4);
+  for (int c0 = 0; c0 < args.F; c0 += pc) {
+    SpmmF32Args p = a;
+    p.F = args.F - c0 < pc ? args.F - c0 : pc;
+    p.x = args.x + c0;
+    p.x2 = args.x2 ? args.x2 + c0 : nullptr;
+    p.out = args.out + c0;
+    p.gate = args.gate ? args.gate + c0 : nullptr;
+    p.self_add = args.self_add ? args.self_add + c0 : nullptr;
+    const hipError_t err = args.it == IType::I32 ? launch_f32_rg<int32_t>(p, st)
+                                                 : launch_f32_rg<int64_t>(p, st);
+    if (err != hipSuccess) return err;
+  }
+  return hipSuccess;
+}
+
 hipError_t spmm_f32_rowgroup(IType it, const int64_t* rowptr, const void* col,
                              const float* ew, const float* col_scale, const float* row_scale,
                              const int32_t* col_map, const int64_t* row_ids, const float* x,
@@ -276,49 +321,31 @@ hipError_t spmm_f32_rowgroup(IType it, const int64_t* rowptr, const void* col,
                              hipStream_t st, const float* gate, int64_t ldgate,
                              const float* self_add, int64_t ld_self, const int32_t* self_map,
                              int64_t self_row0) {
-  if (nrows <= 0 || F <= 0) return hipSuccess;
-  if (self_add && (!self_map || (reinterpret_cast<uintptr_t>(self_add) & 15) || ld_self % 4))
-    return hipErrorInvalidValue;
-  if (gate && ((reinterpret_cast<uintptr_t>(gate) & 15) || ldgate % 4)) return hipErrorInvalidValue;
-  if (!spmm_f32_rowgroup_ok(F, ldx, ldo, x, out)) return hipErrorInvalidValue;
-  const int icap = (cap > 0 && cap < (int64_t(1) << 30)) ? static_cast<int>(cap) : (1 << 30);
-  int pc = g_f32_pass_cols;
-  pc = pc > 256 ? 256 : (pc < 16 ? 16 : pc - pc % 4);
-  for (int c0 = 0; c0 < F; c0 += pc) {
-    const int w = F - c0 < pc ? F - c0 : pc;
-    hipError_t err;
-    if (it == IType::I32) {
-      const auto* cp = static_cast<const int32_t*>(col);
-      err = col_map ? launch_f32_rg<int32_t, true>(rowptr, cp, ew, col_scale, row_scale,
-                                                   col_map, row_ids, x + c0, ldx, out + c0,
-                                                   ldo, nrows, w, beta, icap, row_map,
-                                                   gate ? gate + c0 : nullptr, ldgate,
-                                                   self_add ? self_add + c0 : nullptr, ld_self,
-                                                   self_map, self_row0, st)
-                    : launch_f32_rg<int32_t, false>(rowptr, cp, ew, col_scale, row_scale,
-                                                    nullptr, row_ids, x + c0, ldx, out + c0,
-                                                    ldo, nrows, w, beta, icap, row_map,
-                                                   gate ? gate + c0 : nullptr, ldgate,
-                                                   self_add ? self_add + c0 : nullptr, ld_self,
-                                                   self_map, self_row0, st);
-    } else {
-      const auto* cp = static_cast<const int64_t*>(col);
-      err = col_map ? launch_f32_rg<int64_t, true>(rowptr, cp, ew, col_scale, row_scale,
-                                                   col_map, row_ids, x + c0, ldx, out + c0,
-                                                   ldo, nrows, w, beta, icap, row_map,
-                                                   gate ? gate + c0 : nullptr, ldgate,
-                                                   self_add ? self_add + c0 : nullptr, ld_self,
-                                                   self_map, self_row0, st)
-                    : launch_f32_rg<int64_t, false>(rowptr, cp, ew, col_scale, row_scale,
-                                                    nullptr, row_ids, x + c0, ldx, out + c0,
-                                                    ldo, nrows, w, beta, icap, row_map,
-                                                   gate ? gate + c0 : nullptr, ldgate,
-                                                   self_add ? self_add + c0 : nullptr, ld_self,
-                                                   self_map, self_row0, st);
-    }
-    if (err != hipSuccess) return err;
-  }
-  return hipSuccess;
+  SpmmF32Args a{};
+  a.rowptr = rowptr;
+  a.col = col;
+  a.it = it;
+  a.ew = ew;
+  a.col_scale = col_scale;
+  a.row_scale = row_scale;
+  a.col_map = col_map;
+  a.row_ids = row_ids;
+  a.row_map = row_map;
+  a.x = x;
+  a.ldx = ldx;
+  a.out = out;
+  a.ldo = ldo;
+  a.nrows = nrows;
+  a.F = F;
+  a.beta = beta;
+  a.cap = cap;
+  a.gate = gate;
+  a.ldgate = ldgate;
+  a.self_add = self_add;
+  a.ld_self = ld_self;
+  a.self_map = self_map;
+  a.self_row0 = self_row0;
+  return spmm_f32_run(a, st);
 }
 
 }  // namespace dgraph

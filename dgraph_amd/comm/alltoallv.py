@@ -33,6 +33,17 @@ import torch.distributed as dist
 # 2-process-on-one-GPU equivalence test of the bench step uses it.
 A2A_IMPL = os.environ.get("DGRAPH_A2A_IMPL", "torch")
 
+# Link model of the LOOPBACK exchange (a W-way plan run by one process: bench.py
+# --rehearse-world). 0 = the copy completes at once (a loopback exposes nothing). > 0: the
+# copy is issued on a side stream behind a device-side wait of
+# latency + max-per-peer-bytes / (GBPS * 1e9) — each peer message rides its own xGMI link,
+# all links concurrently — and the call returns a PENDING work whose wait() is a stream
+# event wait, so the executor's overlap schedule meets a link-length transfer and its
+# exposed-exchange regions measure what a W-GPU run would expose (the reference timed its
+# exchange regions separately, experiments/OGB/GCN.py:101-116).
+LOOPBACK_LINK_GBPS = float(os.environ.get("DGRAPH_LOOPBACK_LINK_GBPS", "0"))
+LOOPBACK_LATENCY_US = float(os.environ.get("DGRAPH_LOOPBACK_LATENCY_US", "15"))
+
 _HEAPS: dict = {}
 
 
@@ -69,6 +80,32 @@ class _Done:
 
     def is_completed(self):
         return True
+
+
+class _EventWork:
+    """A pending exchange completed by a stream event: ``wait()`` makes the CURRENT stream
+    wait for it (no host synchronisation)."""
+
+    def __init__(self, event):
+        self.event = event
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.event)
+        return None
+
+    def is_completed(self):
+        return self.event.query()
+
+
+_SIDE: dict = {}
+
+
+def _side_stream(dev) -> "torch.cuda.Stream":
+    s = _SIDE.get(dev.index)
+    if s is None:
+        s = torch.cuda.Stream(dev)
+        _SIDE[dev.index] = s
+    return s
 
 
 class CommStats:
@@ -124,9 +161,7 @@ class AllToAllV:
             send = FaultInjector.before_exchange(
                 send, dist.get_rank() if dist.is_initialized() else 0)
         if self._world <= 1 or not dist.is_initialized() or dist.get_world_size(self.group) == 1:
-            if self.total_send:
-                out.copy_(send)
-            return (out, _Done()) if async_op else out
+            return self._loopback(send, out, row_bytes, async_op)
         send_c = send.contiguous()
         if A2A_IMPL == "shmem" and send_c.is_cuda:
             self._shmem(send_c, out)
@@ -148,6 +183,49 @@ class AllToAllV:
             return out, work
         return out
 
+
+    def link_us(self, row_bytes: int, gbps: float = 0.0) -> float:
+        """Modelled duration of this exchange on point-to-point links of ``gbps`` GB/s per
+        direction (default LOOPBACK_LINK_GBPS): latency + largest per-peer message / rate."""
+        gbps = gbps or LOOPBACK_LINK_GBPS
+        if gbps <= 0 or self._world <= 1:
+            return 0.0
+        peer = max(max(self.send_splits, default=0), max(self.recv_splits, default=0))
+        return LOOPBACK_LATENCY_US + peer * row_bytes / (gbps * 1e3)
+
+    def _loopback(self, send: torch.Tensor, out: torch.Tensor, row_bytes: int,
+                  async_op: bool):
+        """No peers: receive your own send rows (the first min(sent, received) rows; any
+        further received rows read as zero), optionally behind the link model."""
+        m = min(self.total_send, self.total_recv)
+        us = self.link_us(row_bytes) if send.is_cuda else 0.0
+        if us <= 0.0:
+            if m:
+                out[:m].copy_(send[:m])
+            if self.total_recv > m:
+                out[m:].zero_()
+            return (out, _Done()) if async_op else out
+        from .. import _native
+
+        dev = send.device
+        side = _side_stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            _native.ops().link_delay(float(us), int(dev.index))
+            if m:
+                out[:m].copy_(send[:m])
+            if self.total_recv > m:
+                out[m:].zero_()
+            ev = torch.cuda.Event()
+            ev.record(side)
+        # the allocator must not hand these blocks out again before the side stream is done
+        send.record_stream(side)
+        out.record_stream(side)
+        work = _EventWork(ev)
+        if async_op:
+            return out, work
+        work.wait()
+        return out
 
     def _shmem(self, send: torch.Tensor, out: torch.Tensor) -> None:
         """One-sided exchange: every rank puts its segment for peer p straight into p's

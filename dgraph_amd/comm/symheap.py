@@ -269,6 +269,11 @@ class SymmetricHeap:
                 break
         if slot is None:
             slot = self.alloc_tensor((max(n_max, 1), F), x2.dtype)
+        elif self.device_completion:
+            # a reused slot: peers' reads of its previous tensor (a remote_gather of the last
+            # epoch, still running on their GPUs) must be done before it is overwritten —
+            # the same write-after-read wait as the version-change path of _slot_for
+            self.wait(_DONE, self._epoch[_DONE])
         slot[: x2.shape[0]].copy_(x2)
         base = x._base if x._base is not None else x
         ent = {"ref": weakref.ref(base), "version": x._version, "slot": slot,

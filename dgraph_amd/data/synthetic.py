@@ -232,6 +232,38 @@ def localize_columns(csr: CSR, rank: int, offsets: List[int]):
     return out, halo, counts
 
 
+def _local_send_plan(csr: CSR, L: int, recv_splits: List[int]):
+    """For a SYMMETRIC graph: the local rows each peer p receives from this rank (rows with
+    an entry in a halo column owned by p), sorted by (p, row), and the per-peer counts."""
+    dev = csr.device
+    W = len(recv_splits)
+    recv_end = torch.cumsum(torch.tensor(recv_splits, dtype=torch.long, device=dev), 0)
+    keys = []
+    R = csr.num_rows
+    nnz = max(csr.col.numel(), 1)
+    step = max(1, int(R * (1 << 26) // nnz))
+    for r0 in range(0, R, step):
+        r1 = min(R, r0 + step)
+        a, b = int(csr.rowptr[r0]), int(csr.rowptr[r1])
+        if b == a:
+            continue
+        c = csr.col[a:b].long()
+        rows = torch.repeat_interleave(torch.arange(r0, r1, device=dev),
+                                       csr.rowptr[r0 + 1:r1 + 1] - csr.rowptr[r0:r1],
+                                       output_size=b - a)
+        h = c >= L
+        owner = torch.searchsorted(recv_end, c[h] - L, right=True)
+        keys.append(torch.unique(owner * L + rows[h]))
+        del c, rows, h, owner
+    key = torch.unique(torch.cat(keys)) if keys else torch.zeros(0, dtype=torch.long,
+                                                                 device=dev)
+    del keys
+    owner = torch.div(key, max(L, 1), rounding_mode="floor")
+    send_splits = [int(v) for v in torch.bincount(owner, minlength=W).tolist()]
+    send_local_idx = (key - owner * L).to(index_dtype_for(L)).contiguous()
+    return send_local_idx, send_splits
+
+
 def build_partition(shape: GraphShape, rank: int, world_size: int, device, seed: int = 0,
                     global_frac: float = 0.05, window: int = 1 << 14, group=None,
                     rehearse: bool = False):
@@ -254,15 +286,13 @@ def build_partition(shape: GraphShape, rank: int, world_size: int, device, seed:
     csr, halo, recv_splits = localize_columns(csr_g, rank, offsets)
     del csr_g
     if world_size > 1 and rehearse:
-        # one rank of a W-way job in a single process (no peers): the graph is symmetric,
-        # so the rows this rank must send mirror the rows it receives; send the matching
-        # number of local rows (spread over the partition) so every buffer, plan and
-        # kernel has its real shape while the exchange is a local loopback.
-        send_splits = list(recv_splits)
-        n_send = sum(send_splits)
-        idt = index_dtype_for(L)
-        send_local_idx = (torch.arange(n_send, device=device, dtype=torch.long) * 7919 % max(L, 1)
-                          ).to(idt)
+        # one rank of a W-way job in a single process (no peers). The graph is symmetric,
+        # so the rows peer p wants from this rank are exactly the local rows with a
+        # neighbour owned by p: the real send plan, computed locally (sorted by (p, row),
+        # as the peers' requests would be), so every buffer, plan and kernel has its real
+        # shape and the interior/boundary split is the real one; the exchange itself is a
+        # local loopback (comm/alltoallv.py; link-delayed with DGRAPH_LOOPBACK_LINK_GBPS).
+        send_local_idx, send_splits = _local_send_plan(csr, L, recv_splits)
         return dict(csr=csr, L=L, H=int(halo.numel()), halo_gids=halo,
                     send_local_idx=send_local_idx, send_splits=send_splits,
                     recv_splits=recv_splits, offsets=offsets)

@@ -9,7 +9,7 @@ their aggregates and gradients as large). This executor is a hand-scheduled forw
 backward over ROW CHUNKS that never materialises an aggregate, a logit matrix or a dense
 hidden gradient:
 
-forward (per row chunk c, interior + halo parts, every vertex of every layer):
+forward (per row chunk c, every vertex of every layer):
   F0  a_c = mean_N(x)_c            -> h1[c] = relu([x_c | a_c] [Ws0; Wn0] + b0)
   F1  a_c = mean_N(h1)_c           -> h2[c] = relu([h1_c | a_c] [Ws1; Wn1] + b1)
   F2  a_c = mean_N(h2)_c           -> z_c = [h2_c | a_c] [Ws2; Wn2] + b2 (all rows' logits)
@@ -25,26 +25,30 @@ Exact: every term the dense backward has is computed (the omitted products are w
 that are zero by construction). Live device memory at the papers100M shape, W=1: x 57 GB +
 CSR 14 GB + h1 114 GB + h2 114 GB + ~4 GB of chunk buffers; dZ1 and u1 live in h2's
 storage after its last use. Kernels: fp32 row-group SpMM with row lists / column maps /
-gates (csrc/kernels/spmm_f32.hip), MFMA f32 dual GEMM with bias/ReLU/gate/row-scatter
-epilogues (gemm_f32.hip), split-M MFMA weight gradients (wgrad_f32.hip), keep bits
-(bits.hip). Deterministic: fixed chunking, fixed reduction orders, no atomics.
+gates / two sources (csrc/kernels/spmm_f32.hip), MFMA f32 dual GEMM with
+bias/ReLU/gate/row-scatter epilogues (gemm_f32.hip), split-M MFMA weight gradients
+(wgrad_f32.hip), keep bits (bits.hip). Deterministic: fixed chunking, fixed reduction
+orders, no atomics.
 
-Vertex-partitioned graphs (W > 1): halo rows of x are exchanged once (static input), of
-h1/h2 once per forward — each issued asynchronously as soon as its layer is done and
-overlapped with the next layer's interior aggregation of every row (through a whole-layer
-aggregate buffer, or in place in the layer's own output buffer when there is no room for
-one); B2 sends the loss rows' contributions to remote support rows (restricted sub-plan of
-:class:`~dgraph_amd.parallel.dist_graph.DistGraph`), B1b sends the support rows'
-contributions to remote vertices (reverse halo exchange, issued before the B1a work so it
-overlaps it). The halo rows are part of the memory plan, which raises MemoryError before
-allocating when a configuration cannot fit.
+Vertex-partitioned graphs (W > 1). The rank's adjacency is ONE array per row: its interior
+entries (columns < L) then its halo entries (columns L + h), with a per-row split pointer,
+so an aggregation reads interior and halo of a row in one pass when the halo rows are
+resident (the input features' halo, exchanged once; the backward's S rows), and either part
+alone when they are not. With rows numbered interior-first (parallel/reorder.py: rows
+[0, L_int) have no halo neighbour and are sent to nobody), each forward layer whose halo
+exchange is in flight runs its interior rows to completion — aggregation, GEMM, loss, eval —
+then the interior part of its boundary rows into a store when one is free (the layer's own
+output buffer, or the whole-layer aggregate buffer), then waits and finishes the boundary
+rows; the backward's reverse exchange (B1b) overlaps the S-row work and the interior rows'
+input-layer gradient. Received halo rows are part of the memory plan, which raises
+MemoryError before allocating when a configuration cannot fit.
 
 Measured choices (profiles/r03/, PERFORMANCE.md): the SpMM column-pass width follows the
 graph's locality (64 columns on a windowed graph, full rows on a structureless one); the
 column-mapped transposed aggregation compacts each chunk's mapped entries before gathering;
-the chunks run on one stream (the two-stream pipeline and the one-kernel fused layer,
-DGRAPH_FUSED_PIPELINE / DGRAPH_FUSED_FWD, are correct but not faster: the fp32 GEMM's
-register footprint keeps the memory-bound and the MFMA-bound work from co-residing).
+the chunks run on one stream (a two-stream pipeline and a one-kernel fused layer were
+correct but not faster: the fp32 GEMM's register footprint keeps the memory-bound and the
+MFMA-bound work from co-residing; both were removed, PERFORMANCE.md keeps the numbers).
 """
 from __future__ import annotations
 
@@ -53,72 +57,26 @@ from typing import List, Optional, Tuple
 
 import torch
 
-from .. import _native
 from ..ops import f32 as F32
 from ..ops import kernels as K
 from ..parallel.dist_graph import DistGraph
+from ..parallel.reorder import graph_locality
 
 # rows per chunk of the row-chunked passes (0 = auto from free memory)
 CHUNK_ROWS = int(os.environ.get("DGRAPH_FUSED_CHUNK_ROWS", "0"))
-# fp32 GEMMs as bf16x3 split-product MFMAs (csrc/kernels/gemm_x3.hip: fp32-accurate, error vs
-# fp64 below the exact-f32 MFMA's); 0 = exact-f32 MFMAs (gemm_f32.hip)
-GEMM_X3 = os.environ.get("DGRAPH_GEMM_X3", "0") == "1"
-# W = 1: each hidden layer as ONE fused kernel (csrc/kernels/sage_fwd_f32.hip: gather waves
-# and MFMA waves co-resident on every CU) instead of chunked aggregation + GEMM launches
-FUSED_FWD = os.environ.get("DGRAPH_FUSED_FWD", "0") == "1"
-# W > 1: overlap each forward halo exchange with the next layer's interior aggregation
+# W > 1: overlap each forward halo exchange with work that does not need it
 OVERLAP_FWD = os.environ.get("DGRAPH_FUSED_OVERLAP", "1") != "0"
+# keep layer 0's input aggregate mean_N(x) from the forward for the backward when the
+# memory plan has room for it ("auto"), never ("off"), or require it ("on")
+KEEP_AGG0 = os.environ.get("DGRAPH_FUSED_KEEP_AGG0", "auto")
 
 
-def _ranges(n: int, step: int) -> List[Tuple[int, int]]:
-    return [(a, min(n, a + step)) for a in range(0, n, step)] or [(0, 0)]
+def _ranges(a: int, b: int, step: int) -> List[Tuple[int, int]]:
+    return [(r, min(b, r + step)) for r in range(a, b, step)]
 
 
 def _pad_to(n: int, m: int) -> int:
     return (n + m - 1) // m * m
-
-
-class _Pipe:
-    """Two-stage chunk pipeline: stage 1 (the memory-bound aggregation of chunk c into
-    buffer c % 2) on the current stream, stage 2 (MFMA GEMMs / weight gradients reading that
-    buffer) on a side stream, events ordering buffer reuse. OFF by default
-    (DGRAPH_FUSED_PIPELINE=1 turns it on): the fp32 GEMM block takes every SIMD's register
-    file, so the two kernels do not co-reside and the streams only add ordering overhead
-    (benchmarks/bench_overlap_f32.py: 127.9 ms piped vs 122.7 serial per layer at 1/4
-    scale; full step 2060 ms piped vs 2051 serial, profiles/r03/). Off = plain sequence."""
-
-    def __init__(self, dev):
-        self.cuda = dev.type == "cuda" and os.environ.get("DGRAPH_FUSED_PIPELINE", "0") == "1"
-        if self.cuda:
-            # DGRAPH_FUSED_SIDE_PRIO=1: the matrix stage's stream at high priority, so when a
-            # chunk's GEMM and the next chunk's aggregation become ready together the GEMM's
-            # (LDS-heavy, one-per-CU) blocks are placed first and the aggregation fills the
-            # registers left over, instead of the other way round
-            prio = -1 if os.environ.get("DGRAPH_FUSED_SIDE_PRIO", "0") == "1" else 0
-            self.side = torch.cuda.Stream(dev, priority=prio)
-            self.ready = [torch.cuda.Event() for _ in range(2)]
-            self.free = [torch.cuda.Event() for _ in range(2)]
-
-    def run(self, items, produce, consume):
-        if not self.cuda:
-            for k, it in enumerate(items):
-                consume(it, produce(it, k % 2), k % 2)
-            return
-        main = torch.cuda.current_stream()
-        self.side.wait_stream(main)
-        used = [False, False]
-        for k, it in enumerate(items):
-            b = k % 2
-            if used[b]:
-                main.wait_event(self.free[b])
-            res = produce(it, b)
-            self.ready[b].record(main)
-            with torch.cuda.stream(self.side):
-                self.side.wait_event(self.ready[b])
-                consume(it, res, b)
-                self.free[b].record(self.side)
-            used[b] = True
-        main.wait_stream(self.side)
 
 
 def supported(model, x: torch.Tensor) -> bool:
@@ -140,6 +98,71 @@ def _in_width(d0: int) -> int:
     return 64 if d0 <= 64 else 128
 
 
+class _Adj:
+    """A rank's adjacency in one column array: row r's interior entries (columns < L) are
+    ``col[rp[r]:mid[r]]``, its halo entries (columns L + h, h a received halo row) are
+    ``col[mid[r]:rp[r + 1]]``. Without a halo ``mid`` is None and the array is the interior
+    CSR itself (no copy)."""
+
+    def __init__(self, interior, halo, L: int):
+        self.L = L
+        if halo is None or halo.nnz == 0 and halo.num_rows == 0:
+            self.rp, self.col, self.mid = interior.rowptr, interior.col, None
+            self.nnz_int, self.nnz_halo = interior.nnz, 0
+            return
+        dev = interior.device
+        ideg = interior.rowptr[1:] - interior.rowptr[:-1]
+        hdeg = halo.rowptr[1:] - halo.rowptr[:-1]
+        rp = interior.rowptr + halo.rowptr
+        mid = (rp[:-1] + ideg).contiguous()
+        nnz = int(rp[-1])
+        if L + int(halo.num_cols) >= 2 ** 31:
+            raise ValueError("_Adj: local + halo rows must fit int32 column ids")
+        col = torch.empty(nnz, dtype=torch.int32, device=dev)
+        # chunked scatter of both parts (bounded temporaries at 10^9+ entries)
+        step = max(1, int(L * (1 << 26) // max(nnz, 1)))
+        for r0 in range(0, L, step):
+            r1 = min(L, r0 + step)
+            for src, deg, base, off in ((interior, ideg, rp, 0), (halo, hdeg, mid, L)):
+                a, b = int(src.rowptr[r0]), int(src.rowptr[r1])
+                if b == a:
+                    continue
+                shift = torch.repeat_interleave(base[r0:r1] - src.rowptr[r0:r1], deg[r0:r1],
+                                                output_size=b - a)
+                dst = torch.arange(a, b, device=dev, dtype=torch.long).add_(shift)
+                del shift
+                col[dst] = (src.col[a:b].to(torch.int32) + off) if off else \
+                    src.col[a:b].to(torch.int32)
+                del dst
+        self.rp, self.col, self.mid = rp.contiguous(), col, mid
+        self.nnz_int, self.nnz_halo = interior.nnz, halo.nnz
+
+    @property
+    def nnz(self) -> int:
+        return self.nnz_int + self.nnz_halo
+
+    def halo_degree(self) -> torch.Tensor:
+        if self.mid is None:
+            return torch.zeros(self.rp.numel() - 1, dtype=torch.long, device=self.rp.device)
+        return self.rp[1:] - self.mid
+
+    def rows(self, r0: int, r1: int, part: str):
+        """(rowptr, rowend) kernel arguments of rows [r0, r1): ``part`` "all" (interior and
+        halo entries), "int" (interior only) or "halo" (halo only)."""
+        if self.mid is None or part == "all":
+            if part == "halo":
+                raise ValueError("no halo entries")
+            return self.rp[r0:r1 + 1], None
+        if part == "int":
+            return self.rp[r0:r1], self.mid[r0:r1]
+        return self.mid[r0:r1], self.rp[r0 + 1:r1 + 1]
+
+    def memory_bytes(self) -> int:
+        if self.mid is None:
+            return 0  # the interior CSR's own arrays
+        return self.rp.numel() * 8 + self.mid.numel() * 8 + self.col.numel() * 4
+
+
 class FusedSAGE:
     """The fp32 training step of a 2- or 3-layer :class:`~dgraph_amd.models.sage.GraphSAGE`
     (mean aggregator, ReLU between layers, no dropout) over a :class:`DistGraph`.
@@ -148,11 +171,16 @@ class FusedSAGE:
     model's parameters and returns the loss (device scalar, this rank's share of the global
     mean: the sum over this rank's loss rows divided by the GLOBAL train-row count
     ``n_train``, so an all-reduce of the gradients gives the full-batch gradient).
-    ``self.correct`` holds (validation hits, test hits) of the same forward."""
+    ``self.correct`` holds (validation hits, test hits) of the same forward.
+
+    ``release_graph=True``: the graph's interior / halo CSRs are dropped once this
+    executor has built its own adjacency (DistGraph.release_csr) — the graph object is then
+    only an exchange plan."""
 
     def __init__(self, model, graph: DistGraph, x: torch.Tensor, train_idx: torch.Tensor,
                  y_train: torch.Tensor, eval_idx: torch.Tensor, y_eval: torch.Tensor,
-                 eval_is_val: torch.Tensor, n_train: int, chunk_rows: int = 0):
+                 eval_is_val: torch.Tensor, n_train: int, chunk_rows: int = 0,
+                 release_graph: bool = False):
         if not supported(model, x):
             raise ValueError("FusedSAGE: unsupported model/feature shape")
         dev = x.device
@@ -171,10 +199,8 @@ class FusedSAGE:
         self.nl = len(model.layers)
         self.hid = model.layers[0].out_dim
         self.C = model.layers[-1].out_dim
-        self.x3 = GEMM_X3 and dev.type == "cuda"
-        self._x3_cache: dict = {}
-        # logit GEMM width (the bf16x3 tile needs a multiple of 64)
-        self.Cp = (192 if self.x3 else 176) if self.C > 128 else (128 if self.C > 64 else 64)
+        # logit GEMM width
+        self.Cp = 176 if self.C > 128 else (128 if self.C > 64 else 64)
         self.Cg = _pad_to(self.C, 32) if self.C > 128 else self.Cp      # dz width (a K dim)
         if self.Cg not in (128, 176, 192, 256):
             self.Cg = 192
@@ -201,24 +227,39 @@ class FusedSAGE:
         self.posT = smap[self.T].long().contiguous()
         self.invdegS = self.inv_deg[S].contiguous()
         self.AT_S = it_t.select_rows(S)            # rows S (compact), cols T (compact)
+        del it_t
         self.sub = None
         if sub is not None:
             ht_nz, a2a_sub, st = sub[0], sub[1], sub[2]
             stc = st.compact_rows()
             self.sub = (ht_nz, a2a_sub, stc, smap[stc.row_map].long().contiguous())
-        # ---- interior / halo structures
-        self.it = graph.interior
-        self.halo = graph.halo
-        self.hcomp = graph.halo.compact_rows() if graph.halo is not None else None
+        # ---- adjacency: interior + halo entries of a row in one array
+        it = graph.interior
+        self.adj = _Adj(it, graph.halo, L)
+        # B1b's transposed interior aggregation: the interior part of the rows themselves
+        # when the interior block is symmetric, else its transpose
+        self.itT = None if it.symmetric else it.transpose()
         self.haloT = graph.halo.transpose() if graph.halo is not None else None
         self.send_st = graph.send_map.transpose_csr().compact_rows() \
             if graph.halo is not None else None
+        self.nnz_it, self.nnz_h = self.adj.nnz_int, self.adj.nnz_halo
         # entries of the S-row aggregation (B1a), counted on the host once
-        self.nnz_S = int((self.it.rowptr[S + 1] - self.it.rowptr[S]).sum())
-        if self.halo is not None:
-            self.nnz_S += int((self.halo.rowptr[S + 1] - self.halo.rowptr[S]).sum())
-        # ---- chunking (the planning above left cached temporaries: return them first, and
-        # count what the caching allocator still holds unused as free)
+        self.nnz_S = int((self.adj.rp[S + 1] - self.adj.rp[S]).sum())
+        # ---- interior prefix: rows [0, Li) have no halo entry and are sent to nobody
+        bnd = self.adj.halo_degree() > 0
+        if graph.send_map is not None and graph.send_map.idx.numel():
+            bnd[graph.send_map.idx.long()] = True
+        nzb = torch.nonzero(bnd)
+        self.Li = int(nzb[0, 0]) if nzb.numel() else L
+        del bnd, nzb
+        self.locality = getattr(graph, "locality_hint", None)
+        if self.locality is None and dev.type == "cuda":
+            self.locality = graph_locality(self.adj.rp, self.adj.col, L)
+        if release_graph:
+            graph.release_csr()
+            del it
+        # ---- memory plan (the planning above left cached temporaries: return them first,
+        # and count what the caching allocator still holds unused as free)
         if dev.type == "cuda":
             torch.cuda.empty_cache()
             free = torch.cuda.mem_get_info(dev)[0] + \
@@ -239,8 +280,7 @@ class FusedSAGE:
         # W > 1: the received halo rows live through the step — the input's (exchanged once,
         # kept), every hidden layer's (the backward reads them) — and each exchange's send
         # rows while it is in flight: planned here, not discovered by the allocator
-        H = graph.H if graph.halo is not None else 0
-        n_send = graph.send_map.idx.numel() if graph.halo is not None else 0
+        n_send = graph.send_map.idx.numel() if graph.send_map is not None else 0
         self.halo_bytes = 4 * (H * self.d0 + (self.nl - 1) * H * self.hid + n_send * self.hid)
         need_h += self.halo_bytes
         if dev.type == "cuda" and need_h + other + (1 << 28) > free:
@@ -250,35 +290,35 @@ class FusedSAGE:
                 f"FusedSAGE: activations {need_h / 2**30:.1f} GiB (halo rows "
                 f"{self.halo_bytes / 2**30:.1f}) + workspace {other / 2**30:.1f} GiB exceed the "
                 f"{free / 2**30:.1f} GiB free on {dev}")
-        # W > 1: a whole-layer aggregate buffer lets the interior aggregation of EVERY row run
-        # while the previous layer's halo rows are in flight (the halo part and the GEMMs
-        # follow once they land); without room for it the exchange is waited for up front
+        margin = 16 << 30 if dev.type == "cuda" else 0
+        # W > 1: a whole-layer aggregate buffer lets the interior part of the OUTPUT layer's
+        # boundary rows run while its halo rows are in flight (hidden layers use their own
+        # output buffer for that)
         self.agg_full = None
-        need_full = L * wA * 4
-        if graph.halo is not None and OVERLAP_FWD and free - need_h - other - need_full > (
-                16 << 30 if dev.type == "cuda" else 0):
-            self.agg_full = torch.empty(L, wA, dtype=torch.float32, device=dev)
+        need_full = (L - self.Li) * wA * 4
+        if graph.send_map is not None and OVERLAP_FWD and self.Li < L and \
+                free - need_h - other - need_full > margin:
+            self.agg_full = torch.empty(L - self.Li, wA, dtype=torch.float32, device=dev)
             other += need_full
-        # the fused hidden-layer kernel's per-block aggregate ring (W = 1, int32 columns)
-        self.fwd_ring = self.fwd_err = None
-        if (FUSED_FWD and dev.type == "cuda" and graph.halo is None
-                and self.it.col.dtype == torch.int32 and self.hid == 256):
-            ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-            self.fwd_ring = torch.empty(ncu * 2 * 128 * 256, dtype=torch.float32, device=dev)
-            self.fwd_err = torch.zeros(1, dtype=torch.int32, device=dev)
-            other += self.fwd_ring.numel() * 4
+        # layer 0's input aggregate kept from the forward for the backward (else recomputed)
+        self.agg0 = None
+        need0 = L * self.d0 * 4
+        if self.nl == 3 and KEEP_AGG0 != "off" and (
+                KEEP_AGG0 == "on" or free - need_h - other - need0 > margin):
+            self.agg0 = torch.empty(L, self.d0, dtype=torch.float32, device=dev)
+            other += need0
         spare = max(free - need_h - other, 1 << 28)
-        self.pipe = _Pipe(dev)
-        # chunk buffers: two of each when the two-stream pipeline runs (chunk c+1 is written
-        # while chunk c is read), one otherwise — the freed memory goes to larger chunks
-        self.nbuf = 2 if self.pipe.cuda else 1
-        per_row = 4 * self.nbuf * (wA + wB)  # aggregate + logit/gradient chunk buffers
+        per_row = 4 * (wA + wB)  # aggregate + logit/gradient chunk buffers
         cr = chunk_rows or CHUNK_ROWS
         if cr <= 0:
             cr = int(min(max(spare // per_row, 1 << 16), 1 << 21))
         self.cr = max(256, min(int(cr), max(L, 256)))
-        self.chunks = _ranges(L, self.cr)
-        self.s_chunks = _ranges(self.nS, self.cr)
+        # chunks never straddle the interior / boundary split
+        self.chunks = _ranges(0, self.Li, self.cr) + _ranges(self.Li, L, self.cr)
+        if not self.chunks:
+            self.chunks = [(0, 0)]
+        self.nA = sum(1 for r0, r1 in self.chunks if r1 <= self.Li and r1 > r0)
+        self.s_chunks = _ranges(0, self.nS, self.cr) or [(0, 0)]
         ss = lambda v, a: int(torch.searchsorted(v, torch.tensor(a, device=v.device)))  # noqa
         self.ch_T = [(ss(self.T, r0), ss(self.T, r1)) for r0, r1 in self.chunks]
         self.ch_E = [(ss(self.E, r0), ss(self.E, r1)) for r0, r1 in self.chunks]
@@ -289,8 +329,7 @@ class FusedSAGE:
                         for (r0, _), (a, b) in zip(self.chunks, self.ch_E)]
         self.ch_Sloc = [(self.S[a:b] - r0).contiguous()
                         for (r0, _), (a, b) in zip(self.chunks, self.ch_S)]
-        self.ch_halo = [self._halo_range(self.hcomp, r0, r1) for r0, r1 in self.chunks]
-        self.ch_send = [self._halo_range(self.send_st, r0, r1) for r0, r1 in self.chunks]
+        self.ch_send = [self._csr_range(self.send_st, r0, r1) for r0, r1 in self.chunks]
         # ---- persistent buffers (allocated once: no allocation in the steady state)
         f = dict(dtype=torch.float32, device=dev)
         self.h = [torch.empty(L, self.hid, **f) for _ in range(self.nl - 1)]
@@ -302,22 +341,14 @@ class FusedSAGE:
             n = self.nS * self.hid
             self.dZ = hl[:n].view(self.nS, self.hid)
             self.u = hl[n:2 * n].view(self.nS, self.hid) if self.nl == 3 else None
-        # ONE chunk arena: two of each chunk buffer (chunk c+1's aggregation, a memory-bound
-        # SpMM on the producer stream, runs while chunk c's MFMA GEMMs on the consumer
-        # stream read the other one) during the row-chunked passes, and the last hidden
-        # layer's keep bits (output-layer backward only, when no chunk buffer is live)
+        # ONE chunk arena: the aggregate and the logit / gradient chunk buffers during the
+        # row-chunked passes, and the last hidden layer's keep bits (output-layer backward
+        # only, when no chunk buffer is live)
         bits_words = self.nS * (self.hid // 32)
-        arena_fl = max(self.nbuf * self.cr * (wA + wB), bits_words)
+        arena_fl = max(self.cr * (wA + wB), bits_words)
         self.arena = torch.empty(arena_fl, **f)
-        o = 0
-        self.bufA2, self.bufB2 = [], []
-        for w, lst in ((wA, self.bufA2), (wB, self.bufB2)):
-            for _ in range(self.nbuf):
-                lst.append(self.arena[o:o + self.cr * w].view(self.cr, w))
-                o += self.cr * w
-            if self.nbuf == 1:  # index k % 2 reaches the single buffer either way
-                lst.append(lst[0])
-        self.bufA, self.bufB = self.bufA2[0], self.bufB2[0]
+        self.bufA = self.arena[:self.cr * wA].view(self.cr, wA)
+        self.bufB = self.arena[self.cr * wA:self.cr * (wA + wB)].view(self.cr, wB)
         self.bits = self.arena[:bits_words].view(torch.int32).view(self.nS, self.hid // 32)
         self.dz = torch.zeros(self.T.numel(), self.Cg, **f)  # output-layer gradient rows
         # the output layer's projected gradient rows (B2 only): the last hidden buffer's tail,
@@ -336,12 +367,12 @@ class FusedSAGE:
             elif dev.type != "cuda" or free - need_h > (4 * self.nS * self.hid + (8 << 30)):
                 self.v_self = torch.empty(self.nS, self.hid, **f)
             # else: no room — the self term runs as a row-scattered GEMM per chunk
-        self.acc_out_s = F32.WgradAcc(self.hid, self.Cg, dev, x3=self.x3)
-        self.acc_out_n = F32.WgradAcc(self.hid, self.Cg, dev, x3=self.x3)
+        self.acc_out_s = F32.WgradAcc(self.hid, self.Cg, dev)
+        self.acc_out_n = F32.WgradAcc(self.hid, self.Cg, dev)
         kh = self.hid if self.nl == 3 else self.d0
-        self.acc_hid_s = F32.WgradAcc(kh, self.hid, dev, x3=self.x3)
-        self.acc_hid_n = F32.WgradAcc(kh, self.hid, dev, x3=self.x3)
-        self.acc_in = F32.WgradAcc(2 * self.d0, self.hid, dev, x3=self.x3) if self.nl == 3 else None
+        self.acc_hid_s = F32.WgradAcc(kh, self.hid, dev)
+        self.acc_hid_n = F32.WgradAcc(kh, self.hid, dev)
+        self.acc_in = F32.WgradAcc(2 * self.d0, self.hid, dev) if self.nl == 3 else None
         self.row_loss = torch.zeros(nT, **f)
         self.hit = torch.zeros(self.E.numel(), dtype=torch.uint8, device=dev)
         self.E_val_l = self.E_val.long()
@@ -380,11 +411,6 @@ class FusedSAGE:
             out[name] = out.get(name, 0.0) + dt
         return out
 
-    def check_errors(self) -> None:
-        """Raise if a fused-kernel synchronisation wait timed out (host sync)."""
-        if self.fwd_err is not None and int(self.fwd_err.item()) != 0:
-            raise RuntimeError("FusedSAGE: sage_fwd_f32 role synchronisation timed out")
-
     @property
     def edges_aggregated(self) -> int:
         return self.g.edges_aggregated
@@ -393,30 +419,32 @@ class FusedSAGE:
     def edges_aggregated(self, v: int) -> None:
         self.g.edges_aggregated = v
 
+    @property
+    def schedule(self) -> dict:
+        """The overlap structure this executor runs (bench.py records it)."""
+        return {"interior_rows": self.Li, "boundary_rows": self.L - self.Li,
+                "chunk_rows": self.cr, "output_layer_store": self.agg_full is not None,
+                "keep_agg0": self.agg0 is not None}
+
     # ------------------------------------------------------------------ helpers
     def _gemm(self, A1, B1, A2=None, B2=None, **kw):
-        """fp32 dual GEMM: exact-f32 MFMAs, or bf16x3 split products with the weights split
-        once per step (``GEMM_X3``)."""
-        if self.x3:
-            kw["b1x3"] = self._split(B1)
-            if B2 is not None:
-                kw["b2x3"] = self._split(B2)
         return F32.gemm_f32(A1, B1, A2, B2, **kw)
-
-    def _split(self, B):
-        # keyed by address; the entry keeps B alive, so no other tensor can take its address
-        # while the cache (one step) lives
-        key = (B.data_ptr(), tuple(B.shape), B.stride())
-        v = self._x3_cache.get(key)
-        if v is None:
-            v = (B, F32.split_x3(B))
-            self._x3_cache[key] = v
-        return v[1]
 
     def _spmm(self, rowptr, col, x, out=None, **kw):
         """fp32 SpMM at the column-pass width tuned for ``x``'s width (``_tune_passes``)."""
         kw.setdefault("pass_cols", self.pass_for.get(x.shape[1], 0))
         return F32.spmm_f32(rowptr, col, x, out, **kw)
+
+    def _agg(self, hin: torch.Tensor, r0: int, r1: int, out: torch.Tensor, part: str = "all",
+             halo: Optional[torch.Tensor] = None, **kw) -> torch.Tensor:
+        """``out = mean over in-neighbours`` of rows [r0, r1), ``part`` of each row's entries
+        ("all" / "int" / "halo"); halo columns read ``halo`` (received rows). "all" without
+        ``halo`` is only valid for rows that have no halo entry."""
+        rp, re = self.adj.rows(r0, r1, part)
+        if part != "int" and halo is not None and self.adj.mid is not None:
+            kw.update(x2=halo, nsplit=self.L)
+        kw.setdefault("row_scale", self.inv_deg[r0:r1])
+        return self._spmm(rp, self.adj.col, hin, out, rowend=re, **kw)
 
     def _tune_passes(self) -> None:
         """Column-pass width per operand width, from the graph's locality: on a graph whose
@@ -425,36 +453,22 @@ class FusedSAGE:
         Cache (13.1 TB/s effective vs 9.8 at 128 columns on the bench graph); on a graph
         without that locality every neighbour row is a random HBM access and full-width
         passes read each row once, in one burst, instead of once per pass (structureless
-        papers100M step 5508 -> 3687 ms, profiles/r03/). The locality is the fraction of
-        the entries of 65536 evenly spaced rows within +-min(2^16, n/64) of their row (a timing-based
-        choice on one chunk proved noisy). DGRAPH_FUSED_PASS_COLS forces a width."""
+        papers100M step 5508 -> 3687 ms, profiles/r03/). The locality is
+        parallel/reorder.graph_locality of the graph's ORIGINAL order (a rank renumbered
+        interior-first carries it as ``locality_hint``). DGRAPH_FUSED_PASS_COLS forces a
+        width."""
         self.pass_for = {}
-        self.locality = None
         forced = int(os.environ.get("DGRAPH_FUSED_PASS_COLS", "0"))
         if forced:
             self.pass_for = {self.d0: min(forced, self.d0), self.hid: min(forced, self.hid)}
             return
-        if self.dev.type != "cuda":
+        if self.dev.type != "cuda" or self.locality is None:
             return
-        it = self.it
-        n = self.L
-        rows = torch.linspace(0, n - 1, steps=min(n, 65536), device=self.dev).long()
-        beg = it.rowptr[rows]
-        deg = (it.rowptr[rows + 1] - beg).clamp_max(64)
-        tot = int(deg.sum())
-        if tot == 0:
-            return
-        seg = torch.repeat_interleave(torch.arange(rows.numel(), device=self.dev), deg)
-        off = torch.cumsum(deg, 0) - deg
-        pos = beg[seg] + (torch.arange(tot, device=self.dev) - off[seg])
-        dist_ = (it.col[pos].long() - rows[seg]).abs()
-        win = max(1024, min(1 << 16, n // 64))  # small graphs: a window relative to n
-        self.locality = float((dist_ < win).float().mean())
         for w in (self.d0, self.hid):
             self.pass_for[w] = 64 if self.locality >= 0.5 else w
 
     @staticmethod
-    def _halo_range(csr, r0: int, r1: int):
+    def _csr_range(csr, r0: int, r1: int):
         """Rows [k0, k1) of a row-compacted CSR whose output rows fall in [r0, r1), with
         their chunk-local output rows."""
         if csr is None:
@@ -466,80 +480,71 @@ class FusedSAGE:
             return None
         return (csr.rowptr[k0:k1 + 1], (rm[k0:k1] - r0).contiguous(), k1 - k0)
 
-    def _agg_chunk(self, xin: torch.Tensor, xhalo: Optional[torch.Tensor], ci: int,
-                   out: torch.Tensor, gate=None) -> torch.Tensor:
-        """``out[:n] = mean over in-neighbours of rows chunk ci`` (interior + halo)."""
-        r0, r1 = self.chunks[ci]
-        n = r1 - r0
-        o = out[:n]
-        it = self.it
-        self._spmm(it.rowptr[r0:r1 + 1], it.col, xin, o, row_scale=self.inv_deg[r0:r1],
-                     gate=gate)
-        hr = self.ch_halo[ci]
-        if xhalo is not None and hr is not None:
-            rp, rmap, _ = hr
-            self._spmm(rp, self.hcomp.col, xhalo, o, row_scale=self.inv_deg[r0:r1], beta=1.0,
-                         row_map=rmap, gate=gate)
-        return o
-
     def _exchange(self, h: torch.Tensor):
         """Start the halo rows of ``h`` on their way from their owners (forward all-to-all-v,
         asynchronous): ``(recv, work)``, or None at W=1."""
         g = self.g
-        if g.halo is None:
+        if g.send_map is None:
             return None
         return g.a2a(K.gather_rows(h, g.send_map.idx), async_op=True)
 
     def _layer(self, hin: torch.Tensor, halo, consume, width: int, name: str,
-               store: Optional[torch.Tensor] = None):
-        """Aggregate every row chunk of ``hin`` (interior + halo part) and hand it to
-        ``consume(ci, agg, k)``. ``halo``: None (W=1), the received halo rows, or a pending
-        ``(recv, work)`` exchange. With a pending exchange and the whole-layer aggregate
-        buffer, the interior aggregation of all chunks runs first — while the halo rows are
-        on the links — then the exchange is waited for and the halo parts and the GEMMs
-        follow chunk by chunk. ``store`` (an [L, >= width] buffer that is free until the
-        consumer writes row chunk c, e.g. the layer's own output: the GEMM of chunk c reads
-        its aggregate rows before it overwrites them, tile by tile) stands in for the
-        whole-layer buffer when there is no room for one. Returns the halo rows (for the
-        backward)."""
+               store: Optional[torch.Tensor] = None, keep: Optional[torch.Tensor] = None):
+        """Aggregate every row chunk of ``hin`` and hand it to ``consume(ci, agg)``.
+        ``halo``: None (W=1), the received (resident) halo rows, or a pending
+        ``(recv, work)`` exchange. Resident / none: one pass per chunk. Pending: the
+        interior chunks [0, Li) first (they need no halo row); then, with a ``store``
+        ([>= L - Li, >= width] rows free until the consumer writes boundary row r, e.g.
+        the layer's own output buffer — the GEMM of a chunk reads its aggregate rows before
+        it overwrites them, tile by tile), the interior part of every boundary row; then
+        the exchange is waited for and the boundary chunks finish (halo part into the
+        store, or one pass). ``keep`` ([L, width]): aggregate there instead of the chunk
+        buffer (kept after the step). Returns the halo rows (for the backward)."""
         items = [ci for ci, (r0, r1) in enumerate(self.chunks) if r1 > r0]
-        if store is None and self.agg_full is not None:
-            store = self.agg_full
-        if isinstance(halo, tuple) and store is not None:
-            recv, work = halo
-            af = store[:, :width]
-            it = self.it
+        pending = isinstance(halo, tuple)
+
+        def buf(ci):
+            r0, r1 = self.chunks[ci]
+            return keep[r0:r1, :width] if keep is not None else self.bufA[:r1 - r0, :width]
+
+        if not pending:
             for ci in items:
                 r0, r1 = self.chunks[ci]
-                self._spmm(it.rowptr[r0:r1 + 1], it.col, hin, af[r0:r1],
-                             row_scale=self.inv_deg[r0:r1])
+                consume(ci, self._agg(hin, r0, r1, buf(ci), "all", halo))
+            return halo
+        recv, work = halo
+        seg_a = [ci for ci in items if ci < self.nA]
+        seg_b = [ci for ci in items if ci >= self.nA]
+        if not OVERLAP_FWD:
             self._mark(f"exchange_{name}")
             work.wait()
             self._mark(name)
-
-            def produce(ci, k):
+            for ci in items:
                 r0, r1 = self.chunks[ci]
-                hr = self.ch_halo[ci]
-                if hr is not None:
-                    rp, rmap, _ = hr
-                    self._spmm(rp, self.hcomp.col, recv, af[r0:r1], beta=1.0, row_map=rmap,
-                                 row_scale=self.inv_deg[r0:r1])
-                return af[r0:r1]
-
-            self.pipe.run(items, produce, consume)
+                consume(ci, self._agg(hin, r0, r1, buf(ci), "all", recv))
             return recv
-        if isinstance(halo, tuple):
-            recv, work = halo
-            self._mark(f"exchange_{name}")
-            work.wait()
-            self._mark(name)
-            halo = recv
-
-        def produce(ci, k):
-            return self._agg_chunk(hin, halo, ci, self.bufA2[k][:, :width])
-
-        self.pipe.run(items, produce, consume)
-        return halo
+        for ci in seg_a:
+            r0, r1 = self.chunks[ci]
+            consume(ci, self._agg(hin, r0, r1, buf(ci), "all"))
+        Li = self.Li
+        if store is not None and keep is None:
+            for ci in seg_b:
+                r0, r1 = self.chunks[ci]
+                self._agg(hin, r0, r1, store[r0 - Li:r1 - Li, :width], "int")
+        else:
+            store = None
+        self._mark(f"exchange_{name}")
+        work.wait()
+        self._mark(name)
+        for ci in seg_b:
+            r0, r1 = self.chunks[ci]
+            if store is not None:
+                a = store[r0 - Li:r1 - Li, :width]
+                self._agg(hin, r0, r1, a, "halo", recv, beta=1.0)
+            else:
+                a = self._agg(hin, r0, r1, buf(ci), "all", recv)
+            consume(ci, a)
+        return recv
 
     def _params(self):
         out = []
@@ -563,12 +568,10 @@ class FusedSAGE:
         P = self._params()
         dev = self.dev
         self._events = []
-        self._x3_cache = {}  # weights changed since the last step: split again
         self._mark("fwd_l0")
-        nnz_it = self.it.nnz
-        nnz_h = self.halo.nnz if self.halo is not None else 0
+        nnz = self.nnz_it + self.nnz_h
         # ---------------- forward: hidden layers
-        hin, hin_halo = x, (g._static_halo(x) if g.halo is not None else None)
+        hin, hin_halo = x, (g._static_halo(x) if g.send_map is not None else None)
         halos = []
         for l in range(nl - 1):
             ws, wn, b = P[l]
@@ -579,26 +582,18 @@ class FusedSAGE:
             hout = self.h[l]
             bias = b.detach()
 
-            def consume(ci, a, k, hin=hin, hout=hout, ws=ws, wn=wn, bias=bias):
+            def consume(ci, a, hin=hin, hout=hout, ws=ws, wn=wn, bias=bias):
                 r0, r1 = self.chunks[ci]
                 self._gemm(hin[r0:r1], ws, a, wn, bias=bias, relu=True, out=hout[r0:r1])
 
-            if self.fwd_ring is not None and not self.x3 and hin.shape[1] in (128, 256):
-                # aggregation + combine of the whole layer in one kernel
-                it = self.it
-                _native.ops().sage_fwd_f32(hin, it.rowptr, it.col, self.inv_deg, ws, wn,
-                                           bias.float().contiguous(), hout, self.fwd_ring,
-                                           self.fwd_err)
-                halos.append(None)
-            else:
-                # layer l >= 1 can aggregate in place in its own output buffer (same width)
-                inplace = hout if (OVERLAP_FWD and l > 0 and hin.shape[1] == hout.shape[1]) \
-                    else None
-                halos.append(self._layer(hin, hin_halo, consume, hin.shape[1], f"fwd_l{l}",
-                                         store=inplace))
-            self.edges_aggregated += nnz_it + nnz_h
+            # layer l >= 1 can store boundary-row aggregates in its own output buffer
+            store = hout[self.Li:] if (l > 0 and hin.shape[1] == hout.shape[1]) else None
+            keep = self.agg0 if l == 0 else None
+            halos.append(self._layer(hin, hin_halo, consume, hin.shape[1], f"fwd_l{l}",
+                                     store=store, keep=keep))
+            self.edges_aggregated += nnz
             hin = hout
-            # this layer's halo rows leave now and land while the next layer aggregates
+            # this layer's halo rows leave now and land while the next layer works
             hin_halo = self._exchange(hout)
             self._mark(f"fwd_l{l + 1}" if l + 1 < nl - 1 else "fwd_out")
         # ---------------- forward: output layer (all rows), loss and eval on the fly
@@ -612,26 +607,26 @@ class FusedSAGE:
         self.acc_out_s.reset()
         self.acc_out_n.reset()
         hl = hin
-        hl_halo = self._layer(hl, hin_halo, lambda ci, a, k: self._out_chunk(ci, a, k, hl, wsp,
-                                                                             wnp, bp),
-                              hid, "fwd_out")
+        hl_halo = self._layer(hl, hin_halo, lambda ci, a: self._out_chunk(ci, a, hl, wsp,
+                                                                          wnp, bp),
+                              hid, "fwd_out", store=self.agg_full)
         halos.append(hl_halo)
-        self.edges_aggregated += nnz_it + nnz_h
+        self.edges_aggregated += nnz
         # per-row losses / hits summed once, in a fixed order
         loss = self.row_loss.sum() * self.inv_n
         hv = self.hit.long()
         self.correct[0] = (hv * self.E_val_l).sum()
         self.correct[1] = (hv * (1 - self.E_val_l)).sum()
         self._mark("bwd_out")
-        return self._backward(P, halos, hl, hl_halo, loss, nnz_it, nnz_h)
+        return self._backward(P, halos, hl, hl_halo, loss)
 
-    def _out_chunk(self, ci, a, k, hl, wsp, wnp, bp):
-        """Output layer of row chunk ci (consumer stream): logits of every row, the loss
-        rows' cross-entropy gradient and output-layer weight gradients, eval hits."""
+    def _out_chunk(self, ci, a, hl, wsp, wnp, bp):
+        """Output layer of row chunk ci: logits of every row, the loss rows' cross-entropy
+        gradient and output-layer weight gradients, eval hits."""
         C, Cp = self.C, self.Cp
         r0, r1 = self.chunks[ci]
         n = r1 - r0
-        z = self._gemm(hl[r0:r1], wsp, a, wnp, bias=bp, out=self.bufB2[k][:n, :Cp])
+        z = self._gemm(hl[r0:r1], wsp, a, wnp, bias=bp, out=self.bufB[:n, :Cp])
         t0, t1 = self.ch_T[ci]
         if t1 > t0:
             # one fused kernel: per-row loss and the scaled softmax gradient rows
@@ -644,7 +639,7 @@ class FusedSAGE:
         if e1 > e0:
             F32.argmax_hits(z, self.ch_Eloc[ci], self.yE[e0:e1], self.hit[e0:e1], C)
 
-    def _backward(self, P, halos, hl, hl_halo, loss, nnz_it, nnz_h):
+    def _backward(self, P, halos, hl, hl_halo, loss):
         g, x, dev = self.g, self.x, self.dev
         nl, hid, C, Cg = self.nl, self.hid, self.C, self.Cg
         ws, wn, _ = P[nl - 1]
@@ -690,87 +685,35 @@ class FusedSAGE:
         work = None
         if nl == 3:
             # u1 = (dZ1 Wn1^T) / deg_S: its transposed aggregation feeds layer 0; the halo
-            # part is computed and sent first so the exchange overlaps the S-row work below
+            # part is computed and sent first so the exchange overlaps the S-row work and
+            # the interior rows of layer 0 below
             u = self._gemm(dZ, wn1.detach().t().contiguous(), row_scale=self.invdegS,
-                             out=self.u)
+                           out=self.u)
             if self.haloT is not None:
                 hg1 = self._spmm(self.haloT.rowptr, self.haloT.col, u, col_map=self.smap)
                 sg1, work = g.a2a_rev(hg1, async_op=True)
                 self.edges_aggregated += self.haloT.nnz
         self.acc_hid_s.reset()
         self.acc_hid_n.reset()
-        def produce_s(sr, k):
-            s0, s1 = sr
+        halo_l = hin_l_halo if self.adj.mid is not None else None
+        for s0, s1 in self.s_chunks:
+            if s1 <= s0:
+                continue
             rows = self.S[s0:s1]
-            aS = self.bufA2[k][:s1 - s0, :hin_l.shape[1]]
-            self._spmm(self.it.rowptr, self.it.col, hin_l, aS, row_ids=rows,
-                         row_scale=self.invdegS[s0:s1])
-            if hin_l_halo is not None:
-                self._spmm(self.halo.rowptr, self.halo.col, hin_l_halo, aS, row_ids=rows,
-                             row_scale=self.invdegS[s0:s1], beta=1.0)
-            return aS
-
-        def consume_s(sr, aS, k):
-            s0, s1 = sr
-            self.acc_hid_s.add(hin_l, dZ[s0:s1], a1_rows=self.S[s0:s1])
+            aS = self.bufA[:s1 - s0, :hin_l.shape[1]]
+            kw = dict(x2=halo_l, nsplit=self.L) if halo_l is not None else {}
+            self._spmm(self.adj.rp, self.adj.col, hin_l, aS, row_ids=rows,
+                       row_scale=self.invdegS[s0:s1], **kw)
+            self.acc_hid_s.add(hin_l, dZ[s0:s1], a1_rows=rows)
             self.acc_hid_n.add(aS, dZ[s0:s1])
-
-        self.pipe.run([sr for sr in self.s_chunks if sr[1] > sr[0]], produce_s, consume_s)
         self.edges_aggregated += self.nnz_S
         gw[(lh, 0)] = self.acc_hid_s.result()
         gw[(lh, 1)] = self.acc_hid_n.result()
         if lh == 0:
             gw[(0, 0)], gw[(0, 1)] = gw[(0, 0)][:self.d0_in], gw[(0, 1)][:self.d0_in]
         if nl == 3:
-            # ------------ layer 0: dZ0 by row chunks, consumed at once by its weight grads
-            ws1_t = ws1.detach().t().contiguous()
-            if work is not None:
-                self._mark("exchange_bwd_l0")
-                work.wait()
-            self._mark("bwd_l0")
-            self.acc_in.reset()
-            db0s = []
-            h1 = self.h[0]
-            x_halo = halos[0]
-            # the support rows' own term dZ1 Ws1^T, once over S (one full-size GEMM instead
-            # of a row-scattered one per chunk); added by the aggregation's epilogue
-            v = self._gemm(dZ, ws1_t, out=self.v_self) if self.v_self is not None else None
-
-            def produce_0(ci, k):
-                # memory-bound: the column-mapped transposed aggregation of u1 (gated by
-                # layer 0's ReLU) and the recomputed layer-0 input aggregate
-                r0, r1 = self.chunks[ci]
-                n = r1 - r0
-                gz = self.bufB2[k][:n, :hid]
-                self._spmm(self.it.rowptr[r0:r1 + 1], self.it.col, u, gz, col_map=self.smap,
-                             gate=h1[r0:r1], self_add=v,
-                             self_map=self.smap if v is not None else None, self_row0=r0)
-                sr = self.ch_send[ci]
-                if work is not None and sr is not None:
-                    rp, rmap, _ = sr
-                    self._spmm(rp, self.send_st.col, sg1, gz, beta=1.0, row_map=rmap,
-                                 gate=h1[r0:r1])
-                a0 = self._agg_chunk(x, x_halo, ci, self.bufA2[k][:, :self.d0])
-                return gz, a0
-
-            def consume_0(ci, ga, k):
-                gz, a0 = ga
-                r0, r1 = self.chunks[ci]
-                s0, s1 = self.ch_S[ci]
-                if v is None and s1 > s0:  # no room for v_self: scattered self term
-                    self._gemm(dZ[s0:s1], ws1_t, cin=gz, o_rows=self.ch_Sloc[ci],
-                                 gate=h1[r0:r1], out=gz)
-                self.acc_in.add(x[r0:r1], gz, A2=a0)
-                db0s.append(K.col_sum(gz))
-
-            self.pipe.run([ci for ci, (r0, r1) in enumerate(self.chunks) if r1 > r0],
-                          produce_0, consume_0)
-            db0 = torch.stack(db0s).sum(0) if db0s else torch.zeros(hid, device=dev)
-            self.edges_aggregated += 2 * nnz_it + nnz_h + \
-                (self.send_st.nnz if self.send_st is not None else 0)
-            w0 = self.acc_in.result()
-            gw[(0, 0)], gw[(0, 1)], gw[(0, 2)] = (w0[:self.d0_in],
-                                                  w0[self.d0:self.d0 + self.d0_in], db0)
+            self._input_layer_backward(P, halos, dZ, u, work, sg1 if work is not None else None,
+                                       gw)
         self._mark("grads")
         # ---------------- gradients into the parameters
         for l, (ws_, wn_, b_) in enumerate(P):
@@ -784,3 +727,66 @@ class FusedSAGE:
                     p.grad.copy_(gk)
         self._mark("end")
         return loss
+
+    def _input_layer_backward(self, P, halos, dZ, u, work, sg1, gw):
+        """B1b: dZ0 by row chunks, consumed at once by the input layer's weight gradients.
+        Interior chunks (no row receives from the reverse exchange) run before it is
+        waited for."""
+        x, dev, hid = self.x, self.dev, self.hid
+        ws1 = P[1][0]
+        ws1_t = ws1.detach().t().contiguous()
+        self._mark("bwd_l0")
+        self.acc_in.reset()
+        db0s = []
+        h1 = self.h[0]
+        x_halo = halos[0] if self.adj.mid is not None else None
+        # the support rows' own term dZ1 Ws1^T, once over S (one full-size GEMM instead
+        # of a row-scattered one per chunk); added by the aggregation's epilogue
+        v = self._gemm(dZ, ws1_t, out=self.v_self) if self.v_self is not None else None
+        items = [ci for ci, (r0, r1) in enumerate(self.chunks) if r1 > r0]
+        waited = work is None
+        for ci in items:
+            r0, r1 = self.chunks[ci]
+            n = r1 - r0
+            if not waited and ci >= self.nA:
+                self._mark("exchange_bwd_l0")
+                work.wait()
+                waited = True
+                self._mark("bwd_l0")
+            # memory-bound: the column-mapped transposed aggregation of u1 (gated by layer
+            # 0's ReLU) and the layer-0 input aggregate (kept from the forward or recomputed)
+            gz = self.bufB[:n, :hid]
+            sa = dict(gate=h1[r0:r1], self_add=v, self_map=self.smap if v is not None else None,
+                      self_row0=r0)
+            if self.itT is not None:
+                self._spmm(self.itT.rowptr[r0:r1 + 1], self.itT.col, u, gz, col_map=self.smap,
+                           **sa)
+            else:
+                rp, re = self.adj.rows(r0, r1, "int")
+                self._spmm(rp, self.adj.col, u, gz, rowend=re, col_map=self.smap, **sa)
+            sr = self.ch_send[ci]
+            if sg1 is not None and sr is not None:
+                rp_s, rmap, _ = sr
+                self._spmm(rp_s, self.send_st.col, sg1, gz, beta=1.0, row_map=rmap,
+                           gate=h1[r0:r1])
+            if self.agg0 is not None:
+                a0 = self.agg0[r0:r1]
+            else:
+                a0 = self._agg(x, r0, r1, self.bufA[:n, :self.d0], "all", x_halo)
+            s0, s1 = self.ch_S[ci]
+            if v is None and s1 > s0:  # no room for v_self: scattered self term
+                self._gemm(dZ[s0:s1], ws1_t, cin=gz, o_rows=self.ch_Sloc[ci],
+                           gate=h1[r0:r1], out=gz)
+            self.acc_in.add(x[r0:r1], gz, A2=a0)
+            db0s.append(K.col_sum(gz))
+        if not waited:
+            self._mark("exchange_bwd_l0")
+            work.wait()
+            self._mark("bwd_l0")
+        db0 = torch.stack(db0s).sum(0) if db0s else torch.zeros(hid, device=dev)
+        self.edges_aggregated += self.nnz_it + \
+            (self.send_st.nnz if self.send_st is not None else 0) + \
+            (0 if self.agg0 is not None else self.nnz_it + self.nnz_h)
+        w0 = self.acc_in.result()
+        gw[(0, 0)], gw[(0, 1)], gw[(0, 2)] = (w0[:self.d0_in],
+                                              w0[self.d0:self.d0 + self.d0_in], db0)

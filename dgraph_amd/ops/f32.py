@@ -18,8 +18,6 @@ from .. import _native
 
 
 # ------------------------------------------------------------------------------ SpMM
-DEFAULT_PASS_COLS = 64  # csrc/kernels/spmm_f32.hip g_f32_pass_cols
-
 
 def spmm_f32(rowptr: torch.Tensor, col: torch.Tensor, x: torch.Tensor,
              out: Optional[torch.Tensor] = None, *, row_scale=None, col_scale=None,
@@ -28,37 +26,40 @@ def spmm_f32(rowptr: torch.Tensor, col: torch.Tensor, x: torch.Tensor,
              row_map: Optional[torch.Tensor] = None,
              gate: Optional[torch.Tensor] = None, self_add: Optional[torch.Tensor] = None,
              self_map: Optional[torch.Tensor] = None, self_row0: int = 0,
-             pass_cols: int = 0) -> torch.Tensor:
-    """``out[o(i)] = row_scale[o(i)] * sum_j w_j x[m(col_j)] + beta * out[o(i)]`` over the
-    entries of CSR row ``row_ids[i]`` (all rows when None); ``m = col_map`` (entries with
-    ``col_map < 0`` skipped) or identity; ``o = row_map`` or identity. ``gate`` (indexed
-    like ``out``): the stored value is kept where ``gate > 0`` (a ReLU derivative).
-    ``self_add``: output row o also gets ``self_add[self_map[self_row0 + o]]`` (when >= 0),
-    before the gate. ``pass_cols`` (GPU): the column-pass width of this call (0 = the
-    current default, 64): narrow passes keep a locality window in the caches, full-width
-    passes make each random row access one long read (see FusedSAGE's autotune)."""
-    n = row_ids.numel() if row_ids is not None else rowptr.numel() - 1
+             pass_cols: int = 0, rowend: Optional[torch.Tensor] = None,
+             x2: Optional[torch.Tensor] = None, nsplit: int = 0) -> torch.Tensor:
+    """``out[o(i)] = row_scale[o(i)] * sum_j w_j X(m(col_j)) + beta * out[o(i)]`` over the
+    entries of CSR row ``r = row_ids[i]`` (all rows when None): ``[rowptr[r], rowptr[r+1])``,
+    or ``[rowptr[r], rowend[r])`` when ``rowend`` is given (one run of a row stored in two);
+    ``m = col_map`` (entries with ``col_map < 0`` skipped) or identity; ``X(c) = x[c]``, or
+    with ``x2`` (two sources in one pass) ``x2[c - nsplit]`` for ``c >= nsplit``; ``o =
+    row_map`` or identity. ``gate`` (indexed like ``out``): the stored value is kept where
+    ``gate > 0`` (a ReLU derivative). ``self_add``: output row o also gets
+    ``self_add[self_map[self_row0 + o]]`` (when >= 0), before the gate. ``pass_cols`` (GPU):
+    the column-pass width of this call (0 = the process default, 64): narrow passes keep a
+    locality window in the caches, full-width passes make each random row access one long
+    read (see FusedSAGE's autotune)."""
+    if row_ids is not None:
+        n = row_ids.numel()
+    else:
+        n = rowend.numel() if rowend is not None else rowptr.numel() - 1
     if out is None:
         if row_map is not None:
             raise ValueError("spmm_f32: row_map needs an explicit out")
         out = torch.empty(n, x.shape[1], dtype=x.dtype, device=x.device)
         beta = 0.0
     if x.is_cuda:
-        ops = _native.ops()
-        if pass_cols:
-            ops.set_spmm_f32_config(-1, int(pass_cols))
-        try:
-            ops.spmm_f32_ex(rowptr, col, edge_weight, col_scale, row_scale, col_map, row_ids, x,
-                            out, float(beta), 0, row_map, gate, self_add, self_map,
-                            int(self_row0))
-        finally:
-            if pass_cols:
-                ops.set_spmm_f32_config(-1, DEFAULT_PASS_COLS)
+        _native.ops().spmm_f32_ex(rowptr, col, edge_weight, col_scale, row_scale, col_map,
+                                  row_ids, x, out, float(beta), 0, row_map, gate, self_add,
+                                  self_map, int(self_row0), rowend, x2, int(nsplit),
+                                  int(pass_cols))
         return out
     # CPU reference (fp64 accumulation)
     rp = rowptr.long()
-    rows = torch.arange(rp.numel() - 1, device=rp.device) if row_ids is None else row_ids.long()
-    beg, end = rp[rows], rp[rows + 1]
+    nr = rowend.numel() if rowend is not None else rp.numel() - 1
+    rows = torch.arange(nr, device=rp.device) if row_ids is None else row_ids.long()
+    beg = rp[rows]
+    end = rowend.long()[rows] if rowend is not None else rp[rows + 1]
     deg = end - beg
     seg = torch.repeat_interleave(torch.arange(n, device=rp.device), deg)
     off = torch.zeros(n + 1, dtype=torch.long, device=rp.device)
@@ -77,7 +78,14 @@ def spmm_f32(rowptr: torch.Tensor, col: torch.Tensor, x: torch.Tensor,
         w = w * col_scale.double()[c]
     acc = torch.zeros(n, x.shape[1], dtype=torch.float64)
     if c.numel():
-        acc.index_add_(0, seg, x.double()[c] * w.unsqueeze(1))
+        if x2 is not None:
+            lo = c < nsplit
+            rows_x = torch.empty(c.numel(), x.shape[1], dtype=torch.float64)
+            rows_x[lo] = x.double()[c[lo]]
+            rows_x[~lo] = x2.double()[c[~lo] - nsplit]
+        else:
+            rows_x = x.double()[c]
+        acc.index_add_(0, seg, rows_x * w.unsqueeze(1))
     o = torch.arange(n) if row_map is None else row_map.long()
     if row_scale is not None:
         acc = acc * row_scale.double()[o].unsqueeze(1)
@@ -98,35 +106,12 @@ def gemm_f32_ok(N: int, K1: int, K2: int = 0) -> bool:
     return N in (64, 128, 176, 192, 256) and K1 % 32 == 0 and K1 > 0 and K2 % 32 == 0
 
 
-def split_x3(B: torch.Tensor, N: int = 0) -> torch.Tensor:
-    """fp32 ``B [K, N']`` -> its three bf16 parts ``[3, N, K]`` (hi, mid, lo; k contiguous;
-    columns past N' zero) with ``B == hi + mid + lo`` exactly for normal values: hi and mid
-    are round-to-nearest-even, lo carries the <= 8 remaining significant bits. The weight
-    operand of the bf16x3 GEMM (csrc/kernels/gemm_x3.hip), split once per call site."""
-    K, n0 = B.shape
-    N = N or n0
-    Bt = torch.zeros(N, K, dtype=torch.float32, device=B.device)
-    Bt[:n0] = B.t()
-    hi = Bt.to(torch.bfloat16)
-    r1 = Bt - hi.float()
-    mid = r1.to(torch.bfloat16)
-    lo = (r1 - mid.float()).to(torch.bfloat16)
-    return torch.stack([hi, mid, lo]).contiguous()
-
-
-def gemm_x3_ok(N: int, K1: int, K2: int = 0) -> bool:
-    return N in (64, 128, 192, 256) and K1 % 32 == 0 and K1 > 0 and K2 % 32 == 0
-
-
 def gemm_f32(A1: torch.Tensor, B1: torch.Tensor, A2=None, B2=None, *, a_rows=None, bias=None,
              cin=None, beta: float = 1.0, gate=None, o_rows=None, relu: bool = False,
-             out: Optional[torch.Tensor] = None, row_scale=None, b1x3=None,
-             b2x3=None) -> torch.Tensor:
+             out: Optional[torch.Tensor] = None, row_scale=None) -> torch.Tensor:
     """``out[o(i)] = relu?(gate?(rs[i] (A1[a(i)] @ B1 (+ A2[i] @ B2)) + bias +
     beta*cin[o(i)]))`` (csrc/kernels/gemm_f32.hip; B row-major [K, N]); ``gate``: keep
-    where gate > 0; ``row_scale`` (nullable [M]): per input row. ``b1x3`` / ``b2x3``
-    (``split_x3`` of B1 / B2): run the products as bf16x3 split-product MFMAs
-    (gemm_x3.hip; fp32-accurate) instead of exact-f32 MFMAs."""
+    where gate > 0; ``row_scale`` (nullable [M]): per input row."""
     M = a_rows.numel() if a_rows is not None else A1.shape[0]
     N = B1.shape[1]
     if out is None:
@@ -137,8 +122,7 @@ def gemm_f32(A1: torch.Tensor, B1: torch.Tensor, A2=None, B2=None, *, a_rows=Non
         _native.ops().gemm_f32(A1, B1.contiguous(), A2, None if B2 is None else B2.contiguous(),
                                a_rows, None if bias is None else bias.float().contiguous(),
                                cin, float(beta), gate, o_rows, bool(relu), out,
-                               None if row_scale is None else row_scale.float().contiguous(),
-                               b1x3, b2x3)
+                               None if row_scale is None else row_scale.float().contiguous())
         return out
     a = A1.double()[a_rows.long()] if a_rows is not None else A1[:M].double()
     v = a @ B1.double()
@@ -166,10 +150,8 @@ class WgradAcc:
 
     _P = 0
 
-    def __init__(self, K: int, N: int, device, blocks: int = 0, x3: bool = False):
+    def __init__(self, K: int, N: int, device, blocks: int = 0):
         self.K, self.N, self.device = int(K), int(N), torch.device(device)
-        # bf16x3 split-product MFMAs (wgrad_x3.hip) where the shape is supported
-        self.mode = 1 if (x3 and self.K in (128, 256) and self.N in (128, 192, 256)) else 0
         if self.device.type == "cuda":
             if blocks <= 0:
                 if WgradAcc._P == 0:
@@ -198,7 +180,7 @@ class WgradAcc:
         if self.device.type == "cuda":
             P = self.partials.shape[0]
             nb = max(1, min(P, -(-G.shape[0] // self.MIN_ROWS_PER_BLOCK)))
-            _native.ops().wgrad_f32(A1, A2, a1_rows, G, self.partials, nb, self.used, self.mode)
+            _native.ops().wgrad_f32(A1, A2, a1_rows, G, self.partials, nb, self.used)
             self.used = max(self.used, nb)
         else:
             M = G.shape[0]

@@ -144,12 +144,31 @@ class DistGraph:
 
     @property
     def device(self):
-        return self.interior.device
+        return self.interior.device if self.interior is not None else self._device
 
     @property
     def nnz(self) -> int:
         """Message edges aggregated at this rank's vertices (interior + halo)."""
+        if self.interior is None:
+            return self._nnz
         return self.interior.nnz + (self.halo.nnz if self.halo is not None else 0)
+
+    def release_csr(self) -> None:
+        """Drop the interior / halo CSRs (and everything cached from them). For an executor
+        that built its own adjacency from them (models/sage_fused.py keeps a rank's interior
+        and halo entries in ONE array) and needs only the exchange plans from here on: at
+        the papers100M shape the split copy is 6.5 GB per rank at W = 2. The aggregation
+        methods of this object cannot be used afterwards."""
+        if self.interior is None:
+            return
+        self._device = self.interior.device
+        self._nnz = self.nnz
+        self._had_halo = self.halo is not None
+        self.interior = None
+        self.halo = None
+        self._restrict_cache.clear()
+        self._restrict_fwd_cache.clear()
+        self._support_cache.clear()
 
     @staticmethod
     def from_pattern(cp, num_nbr_rows: Optional[int] = None, group=None,
@@ -375,10 +394,15 @@ class DistGraph:
             else:  # single-process rehearsal of a W-way rank: mirrored loopback plan
                 peer_cnt = cnt.clone()
             cnt_l, peer_l = [int(v) for v in cnt.tolist()], [int(v) for v in peer_cnt.tolist()]
-            peer_slot = _alltoallv_ids(slot, cnt_l, peer_l, self.a2a.group) if self._peers() \
-                else slot
+            send_sp = torch.tensor(self.a2a.send_splits, device=dev)
+            if self._peers():
+                peer_slot = _alltoallv_ids(slot, cnt_l, peer_l, self.a2a.group)
+            else:
+                # mirrored loopback: peer p's request for slot s lands in my send segment for
+                # p (whose length may differ from what I receive from p)
+                peer_slot = slot % send_sp[owner].clamp_min(1)
             send_off = torch.zeros(W + 1, dtype=torch.long, device=dev)
-            send_off[1:] = torch.cumsum(torch.tensor(self.a2a.send_splits, device=dev), 0)
+            send_off[1:] = torch.cumsum(send_sp, 0)
             base = torch.repeat_interleave(send_off[:-1], peer_cnt.to(dev))
             recv_local = self.send_map.idx.long()[base + peer_slot.to(dev)]
             sub = (ht_nz, AllToAllV(cnt_l, peer_l, self.a2a.group),

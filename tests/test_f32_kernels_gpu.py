@@ -172,12 +172,11 @@ def test_gemm_f32_cin_gate_rows():
     torch.testing.assert_close(cpu_out.double(), ref, atol=1e-4, rtol=1e-5)
 
 
-@pytest.mark.parametrize("x3", [False, True])
 @pytest.mark.parametrize("K1,K2,N", [(128, 128, 256), (256, 0, 256), (128, 0, 176),
                                      (256, 0, 128), (128, 0, 128), (128, 128, 192)])
-def test_wgrad_f32_vs_fp64(K1, K2, N, x3):
-    """exact-f32 (wgrad_f32.hip) and bf16x3 split-product (wgrad_x3.hip, where the shape is
-    supported) weight gradients against fp64, accumulated over two calls."""
+def test_wgrad_f32_vs_fp64(K1, K2, N):
+    """exact-f32 weight gradients (wgrad_f32.hip) against fp64, accumulated over two
+    calls."""
     g = torch.Generator().manual_seed(K1 * 7 + N)
     M1, M2 = 5003, 777
     src = torch.randn(8000, K1, generator=g)
@@ -187,9 +186,7 @@ def test_wgrad_f32_vs_fp64(K1, K2, N, x3):
     A1b = torch.randn(M2, K1, generator=g)
     A2b = torch.randn(M2, K2, generator=g) if K2 else None
     G2 = torch.randn(M2, N, generator=g)
-    acc = F32.WgradAcc(K1 + K2, N, DEV, x3=x3)
-    if x3 and acc.mode != 1:
-        pytest.skip("shape not covered by the bf16x3 kernel (exact-f32 path)")
+    acc = F32.WgradAcc(K1 + K2, N, DEV)
     acc.add(src.to(DEV), G1.to(DEV), None if A2a is None else A2a.to(DEV), rows1.to(DEV))
     acc.add(A1b.to(DEV), G2.to(DEV), None if A2b is None else A2b.to(DEV))
     out = acc.result()
@@ -284,155 +281,3 @@ def test_xent_argmax_rows_vs_cpu(C, W):
     F32.argmax_hits(z.to(DEV), rows.to(DEV), y.to(DEV), hitg, C)
     assert torch.equal(hitg.cpu(), hit)
     assert torch.equal(hit.bool(), z[rows][:, :C].argmax(1) == y)
-
-
-# ---------------------------------------------------------------- bf16x3 split-product GEMM
-def test_split_x3_is_exact():
-    """hi + mid + lo reproduces every fp32 weight exactly (normal range)."""
-    g = torch.Generator().manual_seed(5)
-    B = torch.randn(256, 176, generator=g) * torch.logspace(-6, 6, 176)
-    p = F32.split_x3(B, 192)
-    assert p.shape == (3, 192, 256) and p.dtype == torch.bfloat16
-    rec = (p[0].float() + p[1].float()) + p[2].float()
-    assert torch.equal(rec[:176].t(), B) and not rec[176:].any()
-
-
-@pytest.mark.parametrize("N", [64, 128, 192, 256])
-@pytest.mark.parametrize("K1,K2", [(128, 128), (256, 256), (256, 0), (32, 64)])
-def test_gemm_x3_vs_fp64_and_exact_f32(N, K1, K2):
-    """fp32-accurate: the bf16x3 products' error vs fp64, in units of sum|a b|, is no larger
-    than the exact-f32 MFMA kernel's on the same operands (plus slack for rounding luck)."""
-    g = torch.Generator().manual_seed(N + K1 + 3 * K2)
-    M = 1000
-    A1 = torch.randn(M, K1, generator=g)
-    B1 = torch.randn(K1, N, generator=g) / K1 ** 0.5
-    A2 = torch.randn(M, K2, generator=g) if K2 else None
-    B2 = torch.randn(K2, N, generator=g) / K2 ** 0.5 if K2 else None
-    bias = torch.randn(N, generator=g)
-    d = lambda t: None if t is None else t.to(DEV)  # noqa: E731
-    x3 = F32.gemm_f32(d(A1), d(B1), d(A2), d(B2), bias=d(bias), relu=True,
-                      b1x3=F32.split_x3(d(B1)), b2x3=None if B2 is None else F32.split_x3(d(B2)))
-    ex = F32.gemm_f32(d(A1), d(B1), d(A2), d(B2), bias=d(bias), relu=True)
-    ref = A1.double() @ B1.double() + bias.double()
-    scale = A1.abs().double() @ B1.abs().double() + bias.abs().double()
-    if K2:
-        ref = ref + A2.double() @ B2.double()
-        scale = scale + A2.abs().double() @ B2.abs().double()
-    ref = ref.clamp_min(0)
-    e_x3 = ((x3.double().cpu() - ref).abs() / scale).max().item()
-    e_ex = ((ex.double().cpu() - ref).abs() / scale).max().item()
-    assert e_x3 < 1e-6, e_x3
-    assert e_x3 <= 2.0 * e_ex + 1e-7, (e_x3, e_ex)
-
-
-def test_gemm_x3_rows_cin_gate_multi_tile():
-    """Gathered A1 rows, dense A2, row scale, cin/beta, gate and row-mapped output over more
-    128-row tiles than CUs (persistent walk with next-tile prefetch)."""
-    g = torch.Generator().manual_seed(77)
-    M, N = 128 * 256 * 2 + 555, 256
-    src = torch.randn(M + 3000, 128, generator=g)
-    a_rows = torch.randperm(M + 3000, generator=g)[:M]
-    A2 = torch.randn(M, 128, generator=g)
-    B1 = torch.randn(128, N, generator=g) / 11
-    B2 = torch.randn(128, N, generator=g) / 11
-    rs = torch.rand(M, generator=g) + 0.5
-    o_rows = torch.randperm(M + 64, generator=g)[:M]
-    out0 = torch.randn(M + 64, N, generator=g)
-    gate = torch.randn(M + 64, N, generator=g)
-    out = out0.clone().to(DEV)
-    F32.gemm_f32(src.to(DEV), B1.to(DEV), A2.to(DEV), B2.to(DEV), a_rows=a_rows.to(DEV),
-                 cin=out, beta=0.5, gate=gate.to(DEV), o_rows=o_rows.to(DEV), out=out,
-                 row_scale=rs.to(DEV), b1x3=F32.split_x3(B1.to(DEV)),
-                 b2x3=F32.split_x3(B2.to(DEV)))
-    ref = out0.double().clone()
-    v = (src[a_rows].double() @ B1.double() + A2.double() @ B2.double()) * rs.double()[:, None]
-    v = v + 0.5 * ref[o_rows]
-    ref[o_rows] = torch.where(gate[o_rows] > 0, v, torch.zeros_like(v))
-    torch.testing.assert_close(out.double().cpu(), ref, atol=2e-4, rtol=1e-5)
-
-
-def test_fused_step_x3_matches_exact():
-    """The fused executor with bf16x3 GEMMs tracks the exact-f32 one: loss and every weight
-    gradient of one step at fp32 rounding level."""
-    import dgraph_amd.models.sage_fused as sf
-    from test_sage_fused import _fused_grads
-
-    l0, g0, c0 = _fused_grads(0, 1, dev="cuda")
-    sf.GEMM_X3 = True
-    try:
-        l1, g1, c1 = _fused_grads(0, 1, dev="cuda")
-    finally:
-        sf.GEMM_X3 = False
-    torch.testing.assert_close(l1, l0, atol=1e-5, rtol=1e-5)
-    for a, b in zip(g1, g0):
-        torch.testing.assert_close(a, b, atol=1e-5, rtol=1e-4)
-    assert torch.equal(c1, c0)
-
-
-# ---------------------------------------------------------- fused hidden layer (one kernel)
-@pytest.mark.parametrize("F,skew", [(128, False), (256, False), (128, True), (256, True)])
-def test_sage_fwd_fused_kernel_matches_chunked(F, skew):
-    """sage_fwd_f32 (gather waves + MFMA waves in one persistent kernel) equals the chunked
-    path — fp32 row-group SpMM then the exact-f32 dual GEMM — BITWISE (same summation and
-    k orders), over more 128-row tiles than CUs with a partial last tile; and fp64.
-    ``skew``: many tiles per block and heavy-tailed degrees (every 13th row 150-400
-    neighbours), so the four gather waves drift apart by whole tiles — the case a shared
-    ready count got wrong."""
-    from dgraph_amd import _native
-
-    L = 128 * 256 * (12 if skew else 3) + 77
-    rp, col = _csr(L, L, 20, 31 + F)
-    if skew:
-        g0 = torch.Generator().manual_seed(99)
-        deg = (rp[1:] - rp[:-1]).cpu()
-        deg[::13] = torch.randint(150, 400, (deg[::13].numel(),), generator=g0)
-        rpc = torch.zeros(L + 1, dtype=torch.long)
-        rpc[1:] = torch.cumsum(deg, 0)
-        rp = rpc.to(DEV)
-        col = torch.randint(0, L, (int(rpc[-1]),), generator=g0).to(torch.int32).to(DEV)
-    g = torch.Generator().manual_seed(F)
-    x = torch.randn(L, F, generator=g).to(DEV)
-    Ws = (torch.randn(F, 256, generator=g) / F ** 0.5).to(DEV)
-    Wn = (torch.randn(F, 256, generator=g) / F ** 0.5).to(DEV)
-    b = torch.randn(256, generator=g).to(DEV)
-    deg = (rp[1:] - rp[:-1]).float()
-    inv = torch.where(deg > 0, 1.0 / deg.clamp_min(1), torch.zeros_like(deg)).contiguous()
-    ncu = torch.cuda.get_device_properties(0).multi_processor_count
-    ring = torch.empty(ncu * 2 * 128 * 256, device=DEV)
-    err = torch.zeros(1, dtype=torch.int32, device=DEV)
-    out = torch.empty(L, 256, device=DEV)
-    _native.ops().sage_fwd_f32(x, rp, col, inv, Ws, Wn, b, out, ring, err)
-    torch.cuda.synchronize()
-    assert int(err.item()) == 0
-    agg = F32.spmm_f32(rp, col, x, torch.empty(L, F, device=DEV), row_scale=inv)
-    ref = F32.gemm_f32(x, Ws, agg, Wn, bias=b, relu=True)
-    assert torch.equal(out, ref)
-    # and against fp64 on a sample of rows
-    rows = torch.randperm(L, generator=g)[:500]
-    rpc, colc = rp.cpu(), col.cpu().long()
-    a64 = torch.zeros(500, F, dtype=torch.float64)
-    xc = x.cpu().double()
-    for i, r in enumerate(rows.tolist()):
-        nb = colc[rpc[r]:rpc[r + 1]]
-        if nb.numel():
-            a64[i] = xc[nb].sum(0) / nb.numel()
-    r64 = (xc[rows] @ Ws.cpu().double() + a64 @ Wn.cpu().double() + b.cpu().double()).clamp_min(0)
-    torch.testing.assert_close(out[rows.to(DEV)].cpu().double(), r64, atol=1e-4, rtol=1e-5)
-
-
-def test_fused_step_fused_fwd_bitwise():
-    """The fused executor with the one-kernel hidden layers reproduces the chunked step
-    bitwise: loss, every weight gradient and the hit counts."""
-    import dgraph_amd.models.sage_fused as sf
-    from test_sage_fused import _fused_grads
-
-    l0, g0, c0 = _fused_grads(0, 1, dev="cuda")
-    sf.FUSED_FWD = True
-    try:
-        l1, g1, c1 = _fused_grads(0, 1, dev="cuda")
-    finally:
-        sf.FUSED_FWD = False
-    assert torch.equal(l1, l0)
-    for a, b in zip(g1, g0):
-        assert torch.equal(a, b)
-    assert torch.equal(c1, c0)

@@ -40,7 +40,7 @@ def _setup(rank, world, dev="cpu", layers=3, chunk_rows=300, gf=0.3, name="ogbn-
 
 
 def _fused_grads(rank, world, layers=3, chunk_rows=300, name="ogbn-papers100M",
-                 schedule="full", dev="cpu"):
+                 schedule="full", dev="cpu", gf=0.3):
     """schedule (W > 1): "full" = forward exchanges overlapped through the whole-layer
     aggregate buffer (output layer) and in place (hidden layers); "inplace" = no whole-layer
     buffer (hidden layers in place, the output layer's exchange waited for up front);
@@ -48,7 +48,7 @@ def _fused_grads(rank, world, layers=3, chunk_rows=300, name="ogbn-papers100M",
     import dgraph_amd.models.sage_fused as sf
 
     shape, g, x, y, split, tr, ev, n_tr, model = _setup(rank, world, dev=dev, layers=layers,
-                                                        name=name)
+                                                        name=name, gf=gf)
     sf.OVERLAP_FWD = schedule != "off"
     try:
         ex = FusedSAGE(model, g, x, tr, y[tr], ev, y[ev], split[ev] == SPLIT_VALID, n_tr,
@@ -109,3 +109,97 @@ def test_fused_partitioned_matches_w1(ranks, world, schedule, tmp_path):
     p = tmp_path / "ref.pt"
     torch.save({"loss": loss, "grads": grads, "corr": corr}, p)
     ranks(_dist_body, world, str(p), schedule)
+
+
+def _directed(csr, L, seed=0):
+    """Drop ~30 % of the entries of a symmetric local CSR: a directed graph (A != A^T)."""
+    from dgraph_amd.ops.csr import CSR
+
+    g = torch.Generator().manual_seed(seed)
+    keep = torch.rand(csr.col.numel(), generator=g) > 0.3
+    rows = csr.row_ids()[keep]
+    cols = csr.col[keep]
+    return CSR.from_coo(rows, cols, L, csr.num_cols, keep_perm=False)
+
+
+def test_fused_directed_graph_matches_autograd():
+    """on a non-symmetric graph B1b must aggregate over A^T, not A's own rows.
+    The fused executor equals the layer-stack autograd path on a directed graph."""
+    shape = SHAPES["ogbn-papers100M"].scaled(SCALE)
+    part = build_partition(shape, 0, 1, "cpu", global_frac=0.3, window=64)
+    L = part["L"]
+    part["csr"].num_cols = L
+    csr = _directed(part["csr"], L)
+    assert not torch.equal(csr.col, part["csr"].col)
+    offs = contiguous_offsets(shape.num_nodes, 1)
+    x, y, split = node_data(shape, 0, offs, "cpu", dtype=torch.float32, return_split=True)
+    tr = torch.nonzero(split == SPLIT_TRAIN).reshape(-1)
+    ev = torch.nonzero((split == SPLIT_VALID) | (split == SPLIT_TEST)).reshape(-1)
+    res = []
+    for fused in (False, True):
+        g = DistGraph(csr, L, 0, symmetric=False)
+        torch.manual_seed(0)
+        model = GraphSAGE(shape.num_features, 256, shape.num_classes, 3)
+        if fused:
+            ex = FusedSAGE(model, g, x, tr, y[tr], ev, y[ev], split[ev] == SPLIT_VALID,
+                           tr.numel(), chunk_rows=300)
+            assert ex.itT is not None
+            loss = ex.step()
+        else:
+            logits, _ = model(x, g, out_rows=tr, eval_rows=ev)
+            loss = torch.nn.functional.cross_entropy(logits.float(), y[tr],
+                                                     reduction="sum") / tr.numel()
+            loss.backward()
+        res.append((loss.detach(), [p.grad.clone() for p in model.parameters()]))
+    torch.testing.assert_close(res[1][0], res[0][0], atol=1e-5, rtol=1e-5)
+    for a, b in zip(res[1][1], res[0][1]):
+        torch.testing.assert_close(a, b, atol=2e-5, rtol=1e-4)
+
+
+def _interior_first_body(rank, world, ref_path, overlap):
+    """One rank of a W-way partition renumbered interior-first (parallel/reorder.py), the
+    fused executor's interior-then-boundary schedule, all-reduced against W=1."""
+    import dgraph_amd.models.sage_fused as sf
+    from dgraph_amd.parallel.reorder import interior_first
+
+    sf.OVERLAP_FWD = overlap
+    shape = SHAPES["ogbn-papers100M"].scaled(SCALE)
+    part = build_partition(shape, rank, world, "cpu", global_frac=0.05, window=64)
+    csr, send, perm, L_int, loc = interior_first(part["csr"], part["L"],
+                                                 part["send_local_idx"])
+    assert 0 < L_int < part["L"]
+    g = DistGraph(csr, part["L"], part["H"], send, part["send_splits"], part["recv_splits"],
+                  dist.group.WORLD, symmetric=True)
+    offs = contiguous_offsets(shape.num_nodes, world)
+    x, y, split = node_data(shape, rank, offs, "cpu", dtype=torch.float32, return_split=True)
+    x, y, split = x[perm], y[perm], split[perm]
+    tr = torch.nonzero(split == SPLIT_TRAIN).reshape(-1)
+    ev = torch.nonzero((split == SPLIT_VALID) | (split == SPLIT_TEST)).reshape(-1)
+    n_tr = torch.tensor([tr.numel()])
+    dist.all_reduce(n_tr)
+    torch.manual_seed(0)
+    model = GraphSAGE(shape.num_features, 256, shape.num_classes, 3)
+    ex = FusedSAGE(model, g, x, tr, y[tr], ev, y[ev], split[ev] == SPLIT_VALID, int(n_tr),
+                   chunk_rows=300, release_graph=True)
+    assert ex.Li == L_int and ex.nA >= 1
+    assert g.interior is None  # released: the executor runs on its own adjacency
+    loss = ex.step()
+    grads = [p.grad.clone() for p in model.parameters()]
+    corr = ex.correct.clone()
+    for t in grads:
+        dist.all_reduce(t)
+    dist.all_reduce(loss)
+    dist.all_reduce(corr)
+    ref = torch.load(ref_path)
+    torch.testing.assert_close(loss, ref["loss"], atol=1e-5, rtol=1e-5)
+    for a, b in zip(grads, ref["grads"]):
+        torch.testing.assert_close(a, b, atol=2e-5, rtol=1e-4)
+    assert torch.equal(corr, ref["corr"])
+
+
+@pytest.mark.parametrize("world,overlap", [(2, True), (4, True), (2, False)])
+def test_fused_interior_first_matches_w1(ranks, world, overlap, tmp_path):
+    loss, grads, corr = _fused_grads(0, 1, gf=0.05)
+    p = tmp_path / "ref.pt"
+    torch.save({"loss": loss, "grads": grads, "corr": corr}, p)
+    ranks(_interior_first_body, world, str(p), overlap)
