@@ -632,6 +632,7 @@ def main():
                           "final_loss_local": final_loss,
                           "executor": "fused" if use_fused else "stack",
                           "link_gbps": args.link_gbps,
+                          "allocator_in_timed_steps": alloc_timed,
                           **({"schedule": schedule} if schedule else {}),
                           **({"halo": halo} if halo else {}),
                           **({"regions": regions} if regions else {})}), flush=True)

@@ -29,9 +29,12 @@
 //     layout was 4-way conflicted), B rows 8..15 and 24..31 of a stage sit 16 floats further
 //     inside an (N+16)-float pitch
 //     (the two 16-lane halves of a ds_read_b32 fall in opposite bank halves: was 2-way);
-//   * persistent grid (one 512-thread block per CU) walking 256-row tiles: the next tile's
-//     first stage is loaded during the current tile's last stage, so the prologue's global
-//     latency and the epilogue's stores overlap MFMAs instead of idling the CU.
+//   * persistent grid (one 512-thread block per CU) pulling 256-row tiles from a work
+//     counter (dynamic: a block whose CU is held by another kernel, e.g. RCCL's during a
+//     halo exchange, starts late and finds the tiles taken, instead of running its static
+//     share after everyone else); the next tile's index is fetched during the current
+//     tile's first stage and its first stage is loaded during the current tile's last
+//     stage, so the prologue's global latency and the epilogue's stores overlap MFMAs.
 #include "../common.h"
 #include "kernels.h"
 
@@ -86,7 +89,8 @@ __device__ __forceinline__ void gemm_f32_body(
     const float* __restrict__ B2, int64_t ldb2, const int64_t* __restrict__ a_rows,
     const float* __restrict__ bias, const float* cin, int64_t ldc, float beta,
     const float* __restrict__ gate, int64_t ldg, const int64_t* __restrict__ o_rows,
-    const float* __restrict__ row_scale, float* out, int64_t ldo, int64_t M) {
+    const float* __restrict__ row_scale, float* out, int64_t ldo, int64_t M,
+    int* __restrict__ tile_ctr) {
   constexpr int kBM = BM;
   using C = GCfg<BM, N>;
   using L = GLds<BM, N>;
@@ -103,7 +107,10 @@ __device__ __forceinline__ void gemm_f32_body(
   const int K = K1 + K2;
   const int nst = K / kBK;
   const int64_t ntiles = (M + kBM - 1) / kBM;
-  int64_t tile = blockIdx.x;
+  __shared__ int s_tile;
+  if (tid == 0) s_tile = atomicAdd(tile_ctr, 1);
+  __syncthreads();
+  int64_t tile = s_tile;
   if (tile >= ntiles) return;  // block-uniform
 
   // ---- per-thread global load slots of a stage
@@ -183,9 +190,20 @@ __device__ __forceinline__ void gemm_f32_body(
   const int bcol_w = wn * TN * 16;  // this wave's first column
   int g = 0;                        // stages run by this block (LDS buffer parity)
   while (true) {
-    const int64_t next = tile + gridDim.x;
-    const bool has_next = next < ntiles;  // block-uniform
-    rows_of(has_next ? next : tile, nx_src_row);  // consumed at the tile's last stage
+    // the next tile: its counter fetch is issued now and read after stage 0 (one stage of
+    // MFMAs hides the atomic's latency); its A1 row indices are needed at the last stage
+    int nraw = 0;
+    if (tid == 0) nraw = atomicAdd(tile_ctr, 1);
+    int64_t next = 0;
+    bool has_next = false;  // block-uniform
+    if (nst == 1) {
+      __syncthreads();  // everyone has read s_tile / s_tile of the previous fetch
+      if (tid == 0) s_tile = nraw;
+      __syncthreads();
+      next = s_tile;
+      has_next = next < ntiles;
+      rows_of(has_next ? next : tile, nx_src_row);
+    }
     for (int s = 0; s < nst; ++s, ++g) {
       const int buf = g & 1;
       // the next stage, in flight during this stage's MFMAs; at the tile's last stage the
@@ -234,8 +252,14 @@ __device__ __forceinline__ void gemm_f32_body(
           }
         }
       }
+      if (s == 0 && nst > 1 && tid == 0) s_tile = nraw;
       store_stage(buf ^ 1);  // (the block's very last store lands in a buffer never read)
       __syncthreads();
+      if (s == 0 && nst > 1) {
+        next = s_tile;
+        has_next = next < ntiles;
+        rows_of(has_next ? next : tile, nx_src_row);  // consumed at the tile's last stage
+      }
     }
 
     // ---- epilogue: tile (a, b) register r of lane l is element
@@ -275,10 +299,10 @@ __device__ __forceinline__ void gemm_f32_body(
       const float *__restrict__ B2, int64_t ldb2, const int64_t *__restrict__ a_rows,         \
       const float *__restrict__ bias, const float *cin, int64_t ldc, float beta,              \
       const float *__restrict__ gate, int64_t ldg, const int64_t *__restrict__ o_rows,        \
-      const float *__restrict__ row_scale, float *out, int64_t ldo, int64_t M
+      const float *__restrict__ row_scale, float *out, int64_t ldo, int64_t M, int *tile_ctr
 #define DG_GEMM_F32_PASS                                                                       \
   A1, lda1, K1, B1, ldb1, A2, lda2, K2, B2, ldb2, a_rows, bias, cin, ldc, beta, gate, ldg,     \
-      o_rows, row_scale, out, ldo, M
+      o_rows, row_scale, out, ldo, M, tile_ctr
 
 template <int N, bool HAS_A2, bool RELU, bool HAS_BIAS, bool HAS_CIN, bool HAS_GATE>
 __global__ __launch_bounds__(512, 1) void gemm_f32_kernel(DG_GEMM_F32_ARGS) {
@@ -310,12 +334,14 @@ hipError_t launch_gemm_f32(const float* A1, int64_t lda1, int K1, const float* B
             hipSuccess || num_cus <= 0)
       num_cus = 256;
   }
-  // persistent: one block per CU (LDS-limited), each walking tiles blockIdx + k * grid
+  // persistent: one block per CU (LDS-limited), each pulling tiles from the work counter
   const int64_t ntiles = (M + kBM - 1) / kBM;
   const int64_t blocks = ntiles < num_cus ? ntiles : num_cus;
+  int* ctr = work_counter(st);
+  if (ctr == nullptr) return hipErrorOutOfMemory;
   hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(blocks)), dim3(512), lds, st, A1,
                      lda1, K1, B1, ldb1, A2, lda2, K2, B2, ldb2, a_rows, bias, cin, ldc, beta,
-                     gate, ldg, o_rows, rsc, out, ldo, M);
+                     gate, ldg, o_rows, rsc, out, ldo, M, ctr);
   return hipGetLastError();
 }
 
@@ -366,6 +392,24 @@ hipError_t gemm_f32_n(const float* A1, int64_t lda1, int K1, const float* B1, in
 inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 }  // namespace
+
+int* work_counter(hipStream_t st) {
+  constexpr int kSlots = 4096;
+  static int* ring[64] = {nullptr};
+  static unsigned next[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (ring[dev] == nullptr) {
+    if (hipMalloc(reinterpret_cast<void**>(&ring[dev]), kSlots * sizeof(int)) != hipSuccess)
+      return nullptr;
+    if (hipMemset(ring[dev], 0, kSlots * sizeof(int)) != hipSuccess) return nullptr;
+  }
+  // consecutive launches use distinct slots (a slot is reused 4096 launches later, long after
+  // its kernel finished); the reset is ordered before the launch on the same stream
+  int* c = ring[dev] + (next[dev]++ % kSlots) * 1;
+  if (hipMemsetAsync(c, 0, sizeof(int), st) != hipSuccess) return nullptr;
+  return c;
+}
 
 bool gemm_f32_supported(int64_t N, int64_t K1, int64_t K2) {
   return (N == 64 || N == 128 || N == 176 || N == 192 || N == 256) && K1 > 0 &&

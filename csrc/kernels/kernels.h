@@ -242,6 +242,13 @@ hipError_t dual_gemm_bs(const void* A1, int64_t lda1, const void* B1t, int64_t K
 // B row-major [K, N]; N in {64,128,176,192,256}; K1, K2 multiples of 32; 16-B aligned
 // operands with leading dimensions % 4 == 0. a_rows / o_rows nullable int64 [M].
 // gate (nullable, [*, N] with ldg): v = gate[o(i)][n] > 0 ? v : 0. cin may alias out.
+// Work counters of the dynamically scheduled persistent kernels (gemm_f32, wgrad_f32):
+// a zeroed int32 counter for ONE launch on `st` (a slot of a per-device ring; the reset is
+// an async memset enqueued on `st`, so it is stream-ordered and graph-capturable). Blocks
+// pull tiles / row units from it, so a block that cannot start (its CU held by another
+// stream's kernel, e.g. RCCL's during a halo exchange) costs nothing: the running blocks
+// take its work.
+int* work_counter(hipStream_t st);
 bool gemm_f32_supported(int64_t N, int64_t K1, int64_t K2);
 hipError_t gemm_f32(const float* A1, int64_t lda1, int64_t K1, const float* B1, int64_t ldb1,
                     const float* A2, int64_t lda2, int64_t K2, const float* B2, int64_t ldb2,
@@ -258,7 +265,8 @@ hipError_t wgrad_f32(const float* A1, int64_t lda1, int64_t K1, const float* A2,
                      int64_t K2, const int64_t* a1_rows, const float* G, int64_t ldg,
                      int64_t M, int64_t N, float* partials, int P, int fresh_from,
                      hipStream_t st);
-// (P blocks run; block b adds into slab b when b < fresh_from, else overwrites it)
+// (P row units, slab u = unit u, run by min(P, CUs) blocks pulling units dynamically; unit
+// u adds into slab u when u < fresh_from, else overwrites it)
 hipError_t wgrad_f32_reduce(const float* partials, int P, int64_t KN, float* out,
                             hipStream_t st);
 // 1-bit ReLU keep masks of selected rows (bits.hip): F % 32 == 0, F/32 words per row.

@@ -85,12 +85,11 @@ __global__ __launch_bounds__(256) void spmm_f32_rowgroup_kernel(SpmmF32Args a) {
     f32x2 acc[VEC / 2];
 #pragma unroll
     for (int i = 0; i < VEC / 2; ++i) acc[i] = f32x2{0.f, 0.f};
-    // slot k of this group's row -> (row of x to read, weight); padding slots read the
-    // row of the group's entry 0 (valid whenever deg > 0; a row without entries reads
-    // entry 0 of the whole column array, which exists whenever maxdeg > 0) with weight 0
+    // slot k of this group's row -> (row of x to read, weight); padding slots read row 0
+    // of x (column id 0: valid for x, col_map and col_scale whatever part of a row the
+    // call covers; an entry of the column array may be a halo column) with weight 0
     auto load_c = [&](int k) -> int64_t {
-      const IdxT c = col[k < deg ? s + k : (deg > 0 ? s : 0)];
-      return static_cast<int64_t>(c);
+      return k < deg ? static_cast<int64_t>(col[s + k]) : int64_t(0);
     };
     auto load_w = [&](int64_t& c, int k) -> float {
       float w = k < deg ? 1.f : 0.f;
@@ -99,7 +98,7 @@ __global__ __launch_bounds__(256) void spmm_f32_rowgroup_kernel(SpmmF32Args a) {
         w = m >= 0 ? w : 0.f;
         c = m >= 0 ? m : 0;
       }
-      if constexpr (HAS_EW) w *= a.ew[k < deg ? s + k : (deg > 0 ? s : 0)];
+      if constexpr (HAS_EW) w *= a.ew[k < deg ? s + k : 0];
       if constexpr (HAS_CS) w *= a.col_scale[c];
       return w;
     };

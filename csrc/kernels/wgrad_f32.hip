@@ -4,12 +4,14 @@
 //
 // The GraphSAGE weight gradients x^T g and agg^T g reduce over 10^7 - 10^8 vertex rows
 // into a 256 x 256 output: a library GEMM gets only (K/tile) x (N/tile) output tiles, i.e.
-// a handful of workgroups for 256 CUs. Here the REDUCTION is split: a persistent grid of
-// P blocks (at most one per CU, fewer for short inputs: >= 2048 rows each), block b owns a
-// contiguous range of rows and accumulates the whole [K, N] product in MFMA accumulators
-// (8 waves x TM x TN 16x16 tiles), then writes (or adds to) its private fp32 partial slab
-// partials[b]. wgrad_f32_reduce sums the slabs in block order — deterministic for a fixed
-// sequence of calls, which can accumulate over row chunks of one step before the reduce.
+// a handful of workgroups for 256 CUs. Here the REDUCTION is split into U units of
+// contiguous rows; a persistent grid of at most one block per CU pulls units from a work
+// counter (a block whose CU is held by another stream's kernel — RCCL's during a halo
+// exchange — starts late and finds the units taken), accumulates the whole [K, N] product of
+// a unit in MFMA accumulators (8 waves x TM x TN 16x16 tiles) and writes (or adds to) the
+// UNIT's fp32 partial slab partials[u]. wgrad_f32_reduce sums the slabs in unit order —
+// deterministic whichever block ran a unit, for a fixed sequence of calls, which can
+// accumulate over row chunks of one step before the reduce.
 // Data flow per 32-row stage: A and G rows -> registers (issued one stage ahead) -> padded
 // LDS [32][K+4] / [32][N+4]; MFMA step j uses rows 8h + j (lane group h = lane >> 4) of both
 // (the k-slot permutation of gemm_f32.hip, here over the reduced row index). Stage rows with
@@ -49,19 +51,26 @@ template <int K, int N>
 __global__ __launch_bounds__(kThr, 1) void wgrad_f32_kernel(
     const float* __restrict__ A1, int64_t lda1, int K1, const float* __restrict__ A2,
     int64_t lda2, const int64_t* __restrict__ a1_rows, const float* __restrict__ G,
-    int64_t ldg, int64_t M, int64_t rows_per_block, float* __restrict__ partials,
-    int fresh_from) {
+    int64_t ldg, int64_t M, int64_t rows_per_unit, int units, float* __restrict__ partials,
+    int fresh_from, int* __restrict__ unit_ctr) {
   using C = WCfg<K, N>;
   constexpr int TM = C::TM, TN = C::TN, WN = C::WN;
   extern __shared__ __attribute__((aligned(16))) float lds[];
+  __shared__ int s_unit;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   const int li = lane & 15;
   const int lh = lane >> 4;
-  const int64_t m_begin = static_cast<int64_t>(blockIdx.x) * rows_per_block;
-  int64_t m_end = m_begin + rows_per_block;
+  for (;;) {
+  __syncthreads();  // the previous unit's LDS reads and s_unit reads are done
+  if (tid == 0) s_unit = atomicAdd(unit_ctr, 1);
+  __syncthreads();
+  const int unit = s_unit;
+  if (unit >= units) return;  // block-uniform
+  const int64_t m_begin = static_cast<int64_t>(unit) * rows_per_unit;
+  int64_t m_end = m_begin + rows_per_unit;
   m_end = m_end < M ? m_end : M;
   const int64_t nst = m_end > m_begin ? (m_end - m_begin + kRows - 1) / kRows : 0;
 
@@ -176,7 +185,7 @@ __global__ __launch_bounds__(kThr, 1) void wgrad_f32_kernel(
     }
   }
   // register r of tile (a, b), lane l: C[kw + 16a + 4(l>>4) + r][nw + 16b + (l&15)]
-  float* slab = partials + static_cast<int64_t>(blockIdx.x) * K * N;
+  float* slab = partials + static_cast<int64_t>(unit) * K * N;
 #pragma unroll
   for (int a = 0; a < TM; ++a)
 #pragma unroll
@@ -187,9 +196,10 @@ __global__ __launch_bounds__(kThr, 1) void wgrad_f32_kernel(
         float* p = slab + k * N + nw + b * 16 + li;
         // slabs below fresh_from hold this step's earlier calls: accumulate; the rest are
         // written fresh (a call may use fewer blocks than an earlier one)
-        *p = static_cast<int>(blockIdx.x) < fresh_from ? *p + acc[a][b][r] : acc[a][b][r];
+        *p = unit < fresh_from ? *p + acc[a][b][r] : acc[a][b][r];
       }
     }
+  }  // units
 }
 
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ partials,
@@ -216,10 +226,22 @@ hipError_t launch_wgrad(const float* A1, int64_t lda1, int K1, const float* A2, 
                               static_cast<int>(C::BYTES));
     attr = true;
   }
-  int64_t rpb = (M + P - 1) / P;
-  rpb = (rpb + kRows - 1) / kRows * kRows;
-  hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(P)), dim3(kThr), C::BYTES, st, A1, lda1,
-                     K1, A2, lda2, a1_rows, G, ldg, M, rpb, partials, fresh_from);
+  // P units (slabs) of whole 32-row stages, run by at most one block per CU
+  int64_t rpu = (M + P - 1) / P;
+  rpu = (rpu + kRows - 1) / kRows * kRows;
+  static int num_cus = 0;
+  if (num_cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&num_cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+            hipSuccess || num_cus <= 0)
+      num_cus = 256;
+  }
+  const int blocks = P < num_cus ? P : num_cus;
+  int* ctr = work_counter(st);
+  if (ctr == nullptr) return hipErrorOutOfMemory;
+  hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(blocks)), dim3(kThr), C::BYTES, st, A1,
+                     lda1, K1, A2, lda2, a1_rows, G, ldg, M, rpu, P, partials, fresh_from, ctr);
   return hipGetLastError();
 }
 

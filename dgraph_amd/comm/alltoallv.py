@@ -164,8 +164,11 @@ class AllToAllV:
             return self._loopback(send, out, row_bytes, async_op)
         send_c = send.contiguous()
         if A2A_IMPL == "shmem" and send_c.is_cuda:
-            self._shmem(send_c, out)
-            return (out, _Done()) if async_op else out
+            work = self._shmem(send_c, out, async_op)
+            if async_op:
+                return out, work
+            work.wait()
+            return out
         if A2A_IMPL == "native" and send_c.is_cuda:
             from .rccl_exec import RCCLExecutor
 
@@ -227,13 +230,21 @@ class AllToAllV:
         work.wait()
         return out
 
-    def _shmem(self, send: torch.Tensor, out: torch.Tensor) -> None:
+    def _shmem(self, send: torch.Tensor, out: torch.Tensor, async_op: bool = False):
         """One-sided exchange: every rank puts its segment for peer p straight into p's
         symmetric receive slot at the offset where p expects rows from this rank (the
         prefix of p's receive splits), then copies its own slot out. Completion is
         stream-ordered on separate GPUs and host-ordered for ranks sharing one
         (SymmetricHeap.put_rows). The first call per (plan, row shape, dtype) is collective:
-        the slot is sized for the largest receiver and the offsets are exchanged once."""
+        the slot is sized for the largest receiver and the offsets are exchanged once.
+
+        Separate GPUs (device completion) and ``async_op``: the puts, the completion
+        signals / waits and the copy-out run on the device's comm side stream (every
+        one-sided exchange rides it, in issue order, so the heap's epoch counters stay in
+        step on all ranks) behind the current stream's work, and the returned work's
+        ``wait()`` is a stream-event wait — the exchange overlaps whatever the caller
+        issues next, as the RCCL path does (the reference's put was synchronous,
+        DGraph/distributed/Engine.py:67-86). Returns the work object."""
         heap = shmem_heap(self.group, send.device)
         if self._shm_offsets is None:
             from ..plan.pattern import _alltoall_counts
@@ -251,9 +262,23 @@ class AllToAllV:
             rmax = max(_allgather_obj(int(self.total_recv), self.group))
             slot = heap.alloc_tensor((max(rmax, 1),) + tuple(send.shape[1:]), send.dtype)
             self._shm_slots[key] = slot
+        if async_op and heap.device_completion:
+            dev = send.device
+            side = _side_stream(dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                heap.put_rows(send, slot, self.send_splits, self._shm_offsets)
+                if self.total_recv:
+                    out.copy_(slot[: self.total_recv])
+                ev = torch.cuda.Event()
+                ev.record(side)
+            send.record_stream(side)
+            out.record_stream(side)
+            return _EventWork(ev)
         heap.put_rows(send, slot, self.send_splits, self._shm_offsets)
         if self.total_recv:
             out.copy_(slot[: self.total_recv])
+        return _Done()
 
 
 def torch_alltoallv_with_comm_map(contiguous_send_tensor: torch.Tensor,

@@ -274,7 +274,8 @@ class FusedSAGE:
         # dz rows, wgrad slabs, (u_out when it cannot live in the last hidden buffer) and
         # allocator / temporary slack; the chunk arena gets the rest
         self.u_sep = 2 * self.nS + nT > L
-        other = 4 * nT * self.Cg + 5 * 4 * 256 * 256 * 256 + (3 << 29) + \
+        other = 4 * nT * self.Cg + 5 * 4 * 256 * 256 * 256 * F32.WgradAcc.UNITS_PER_CU + \
+            (3 << 29) + \
             (4 * nT * self.hid if self.u_sep else 0)
         wA, wB = max(self.hid, self.d0), max(self.Cp, self.hid)
         # W > 1: the received halo rows live through the step — the input's (exchanged once,

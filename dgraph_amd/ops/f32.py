@@ -145,8 +145,13 @@ def gemm_f32(A1: torch.Tensor, B1: torch.Tensor, A2=None, B2=None, *, a_rows=Non
 
 class WgradAcc:
     """``dW += [A1[a1_rows] | A2]^T G`` accumulated over calls (row chunks of one step) in
-    per-block fp32 partial slabs (csrc/kernels/wgrad_f32.hip), reduced once in a fixed
-    order by :meth:`result` — deterministic for a fixed chunking."""
+    per-unit fp32 partial slabs (csrc/kernels/wgrad_f32.hip: a call's rows are cut into
+    units, one slab each, pulled dynamically by at most one block per CU), reduced once in
+    a fixed order by :meth:`result` — deterministic for a fixed chunking. Two units per CU
+    by default, so a CU held by another stream's kernel costs a share of one unit, not a
+    whole block's."""
+
+    UNITS_PER_CU = 2
 
     _P = 0
 
@@ -156,7 +161,7 @@ class WgradAcc:
             if blocks <= 0:
                 if WgradAcc._P == 0:
                     WgradAcc._P = torch.cuda.get_device_properties(self.device).multi_processor_count
-                blocks = WgradAcc._P
+                blocks = WgradAcc._P * self.UNITS_PER_CU
             self.partials = torch.empty(blocks, self.K, self.N, dtype=torch.float32,
                                         device=self.device)
         else:
