@@ -161,8 +161,11 @@ class Job:
                                global_frac=global_frac, window=args.window,
                                rehearse=self.rehearse)
         ex = getattr(args, "executor", "auto")
+        from dgraph_amd.models.sage_fused import HIDDEN_WIDTHS
+
         self.use_fused = ex == "fused" or (ex == "auto" and dtype == torch.float32 and
-                                           args.layers in (2, 3) and args.hidden == 256)
+                                           args.layers in (2, 3) and
+                                           args.hidden in HIDDEN_WIDTHS)
         csr = part["csr"]
         if p_world == 1:
             csr.num_cols = part["L"]

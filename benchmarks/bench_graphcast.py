@@ -40,7 +40,9 @@ def main():
                          "(BASELINE config 5)")
     ap.add_argument("--profile-ops", default="",
                     help="torch.profiler per-op device-time table of one step -> PATH")
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--dtype", default="fp32", choices=["bf16", "fp32"],
+                    help="fp32 (default) = the reference's precision (experiments/GraphCast has no "
+                         "casts); bf16 = bf16 compute with fp32 master weights")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--cuda-graph", action="store_true",

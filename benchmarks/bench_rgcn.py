@@ -55,6 +55,10 @@ def parse(argv=None):
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--rehearse-world", type=int, default=0)
     ap.add_argument("--rehearse-rank", type=int, default=0)
+    ap.add_argument("--dtype", choices=("fp32", "bf16"), default="fp32",
+                    help="compute/storage dtype (fp32 = the reference's precision: "
+                         "experiments/OGB-LSC/RGAT.py has no casts; bf16 = autocast with fp32 "
+                         "master weights, a secondary)")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args(argv)
 
@@ -88,7 +92,7 @@ def main(argv=None):
                                   global_frac=args.global_frac, window=args.window,
                                   group=comm.group, rehearse=rehearse, relations=needed)
     graph = HeteroGraph.from_partition(part, EDGE_TYPES, group=comm.group, rank=p_rank)
-    dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
+    dtype = torch.bfloat16 if (dev.type == "cuda" and args.dtype == "bf16") else torch.float32
     heap = None
     alloc = None
     if args.backend != "nccl" and dev.type == "cuda" and p_world > 1 and not rehearse:
@@ -99,7 +103,8 @@ def main(argv=None):
         need_b = 0
         for t in range(3):
             n_max = max(offs[t][r + 1] - offs[t][r] for r in range(p_world))
-            need_b += (n_max * shape.num_features * 2 + 511) // 256 * 256
+            need_b += (n_max * shape.num_features * torch.empty((), dtype=dtype).element_size()
+                       + 511) // 256 * 256
         heap = SymmetricHeap(need_b + (1 << 20), comm.group)
 
         def alloc(t, shp, dt, _o=offs):
@@ -140,7 +145,7 @@ def main(argv=None):
     opt = torch.optim.Adam(model.parameters(), lr=args.lr, fused=dev.type == "cuda")
     sync = GradSync(model.parameters(), group=comm.group) if world > 1 else None
     inv_n = 1.0 / max(n_train, 1)
-    use_amp = dev.type == "cuda"
+    use_amp = dev.type == "cuda" and dtype == torch.bfloat16
 
     def step():
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=use_amp):
@@ -198,7 +203,8 @@ def main(argv=None):
         rec = {"rehearsal": True, "rank": p_rank, "world": p_world,
                "ms_per_step_compute_loopback": ms_step, "messages_local": E_step,
                "halo_rows": halo_total, "peak_mem_gb": round(peak, 2),
-               "final_loss_local": float(lt.item())}
+               "final_loss_local": float(lt.item()),
+               "dtype": "bf16" if dtype == torch.bfloat16 else "fp32"}
     if rank == 0:
         print(json.dumps(rec), flush=True)
     if heap is not None:

@@ -79,23 +79,38 @@ def _pad_to(n: int, m: int) -> int:
     return (n + m - 1) // m * m
 
 
+HIDDEN_WIDTHS = (128, 256, 384, 512)  # multiples of 128: wgrad K-blocks, GEMM N-blocks
+MAX_IN_WIDTH = 1024
+
+
 def supported(model, x: torch.Tensor) -> bool:
-    """Shapes the fused executor runs (the GraphSAGE of bench.py / the OGB shapes)."""
+    """Shapes the fused executor runs: 2 or 3 mean-aggregating layers, no dropout, hidden
+    width in HIDDEN_WIDTHS (wider products run as several kernel tiles), input width up to
+    MAX_IN_WIDTH (zero-padded to the kernels' multiple), at most 256 classes."""
     layers = list(model.layers)
     if len(layers) not in (2, 3) or getattr(model, "dropout", 0.0) != 0.0:
         return False
     hid = layers[0].out_dim
     d0 = x.shape[1]
-    # input widths up to 128 (narrower features are zero-padded to 64 / 128 columns)
-    return (x.dtype == torch.float32 and 0 < d0 <= 128
-            and hid == 256 and all(l.out_dim == hid for l in layers[:-1])
-            and layers[-1].out_dim <= 176)
+    return (x.dtype == torch.float32 and 0 < d0 <= MAX_IN_WIDTH
+            and hid in HIDDEN_WIDTHS and all(l.out_dim == hid for l in layers[:-1])
+            and 0 < layers[-1].out_dim <= 256)
 
 
-def _in_width(d0: int) -> int:
-    """Input width the kernels run at: the layer-0 GEMM's K (a multiple of 32) and the
-    input weight gradient's K = 2 * width (128 or 256)."""
-    return 64 if d0 <= 64 else 128
+def _in_width(d0: int, nl: int = 3) -> int:
+    """Input width the kernels run at (zero-padded features): the layer-0 GEMM's K (a
+    multiple of 32), the input weight gradient's K = 2 * width (3 layers: a multiple of
+    128) or K = width (2 layers: a multiple of 128)."""
+    if nl == 3:
+        return 64 if d0 <= 64 else _pad_to(d0, 64)
+    return _pad_to(d0, 128)
+
+
+def _width_at_least(c: int, widths) -> int:
+    for w in widths:
+        if w >= c:
+            return w
+    raise ValueError(f"no kernel width >= {c}")
 
 
 class _Adj:
@@ -186,7 +201,7 @@ class FusedSAGE:
         dev = x.device
         self.dev = dev
         self.d0_in = x.shape[1]
-        self.d0 = _in_width(self.d0_in)
+        self.d0 = _in_width(self.d0_in, len(model.layers))
         if self.d0 != self.d0_in:
             # zero feature columns: their aggregates are zero, their weight rows get
             # gradients that are dropped (ogbn-products: 100 -> 128)
@@ -199,11 +214,11 @@ class FusedSAGE:
         self.nl = len(model.layers)
         self.hid = model.layers[0].out_dim
         self.C = model.layers[-1].out_dim
-        # logit GEMM width
-        self.Cp = 176 if self.C > 128 else (128 if self.C > 64 else 64)
-        self.Cg = _pad_to(self.C, 32) if self.C > 128 else self.Cp      # dz width (a K dim)
-        if self.Cg not in (128, 176, 192, 256):
-            self.Cg = 192
+        # logit GEMM width (N of the output GEMM) and the dz width (N of the output-layer
+        # weight gradients, K of the projections of dz)
+        self.Cp = _width_at_least(self.C, (64, 128, 176, 192, 256))
+        self.Cg = _width_at_least(_pad_to(self.C, 32) if self.C > 128 else self.C,
+                                  (128, 176, 192, 256))
         self.inv_n = 1.0 / max(int(n_train), 1)
         # ---- loss / eval rows, sorted (chunk ranges are searchsorted)
         t, tp = torch.sort(train_idx.long())
@@ -274,7 +289,12 @@ class FusedSAGE:
         # dz rows, wgrad slabs, (u_out when it cannot live in the last hidden buffer) and
         # allocator / temporary slack; the chunk arena gets the rest
         self.u_sep = 2 * self.nS + nT > L
-        other = 4 * nT * self.Cg + 5 * 4 * 256 * 256 * 256 * F32.WgradAcc.UNITS_PER_CU + \
+        ncu = torch.cuda.get_device_properties(dev).multi_processor_count \
+            if dev.type == "cuda" else 1
+        kh = self.hid if self.nl == 3 else self.d0
+        slab_floats = (2 * self.hid * self.Cg + 2 * kh * self.hid +
+                       (2 * self.d0 * self.hid if self.nl == 3 else 0))
+        other = 4 * nT * self.Cg + 4 * slab_floats * ncu * F32.WgradAcc.UNITS_PER_CU + \
             (3 << 29) + \
             (4 * nT * self.hid if self.u_sep else 0)
         wA, wB = max(self.hid, self.d0), max(self.Cp, self.hid)

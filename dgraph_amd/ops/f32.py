@@ -119,10 +119,21 @@ def gemm_f32(A1: torch.Tensor, B1: torch.Tensor, A2=None, B2=None, *, a_rows=Non
             raise ValueError("gemm_f32: o_rows needs an explicit out")
         out = torch.empty(M, N, dtype=torch.float32, device=A1.device)
     if A1.is_cuda:
-        _native.ops().gemm_f32(A1, B1.contiguous(), A2, None if B2 is None else B2.contiguous(),
-                               a_rows, None if bias is None else bias.float().contiguous(),
-                               cin, float(beta), gate, o_rows, bool(relu), out,
-                               None if row_scale is None else row_scale.float().contiguous())
+        B1 = B1.contiguous()
+        B2 = None if B2 is None else B2.contiguous()
+        bias = None if bias is None else bias.float().contiguous()
+        rs = None if row_scale is None else row_scale.float().contiguous()
+        ops = _native.ops()
+        # N beyond one kernel tile (a 512-wide hidden layer): column blocks, A read per block
+        blocks = [(0, N)] if N <= 256 else _blocks(N, lambda w: w in (128, 176, 192, 256))
+        for n0, n1 in blocks:
+            full = (n0, n1) == (0, N)
+            ops.gemm_f32(A1, B1 if full else B1[:, n0:n1], A2,
+                         None if B2 is None else (B2 if full else B2[:, n0:n1]), a_rows,
+                         None if bias is None else bias[n0:n1], None if cin is None else
+                         (cin if full else cin[:, n0:n1]), float(beta),
+                         None if gate is None else (gate if full else gate[:, n0:n1]), o_rows,
+                         bool(relu), out if full else out[:, n0:n1], rs)
         return out
     a = A1.double()[a_rows.long()] if a_rows is not None else A1[:M].double()
     v = a @ B1.double()
@@ -143,50 +154,106 @@ def gemm_f32(A1: torch.Tensor, B1: torch.Tensor, A2=None, B2=None, *, a_rows=Non
     return out
 
 
+def _wgrad_n_ok(n: int) -> bool:
+    return n in (128, 176, 192, 256)
+
+
+def _blocks(n: int, ok, widths=(256, 192, 176, 128)):
+    """Cut ``n`` columns into blocks whose widths satisfy ``ok`` (greedy, widest first)."""
+    out, c = [], 0
+    while c < n:
+        for w in widths:
+            if n - c >= w and ok(w) and (n - c - w == 0 or n - c - w >= min(widths)):
+                out.append((c, c + w))
+                c += w
+                break
+        else:
+            raise ValueError(f"no kernel block decomposition of {n} columns")
+    return out
+
+
+class _WgradTile:
+    """One native accumulator: ``dW[K, N] += [A1[a1_rows] | A2]^T G`` for K in {128, 256},
+    N in {128, 176, 192, 256} (csrc/kernels/wgrad_f32.hip: a call's rows are cut into
+    units, one fp32 partial slab each, pulled dynamically by at most one block per CU),
+    reduced once in unit order — deterministic for a fixed chunking."""
+
+    def __init__(self, K: int, N: int, device, units: int):
+        self.K, self.N = K, N
+        self.partials = torch.empty(units, K, N, dtype=torch.float32, device=device)
+        self.used = 0
+
+    def add(self, A1, G, A2, a1_rows, min_rows: int) -> None:
+        P = self.partials.shape[0]
+        nb = max(1, min(P, -(-G.shape[0] // min_rows)))
+        _native.ops().wgrad_f32(A1, A2, a1_rows, G, self.partials, nb, self.used)
+        self.used = max(self.used, nb)
+
+    def result(self, out: torch.Tensor) -> torch.Tensor:
+        _native.ops().wgrad_f32_reduce(self.partials[: self.used], out)
+        return out
+
+
 class WgradAcc:
-    """``dW += [A1[a1_rows] | A2]^T G`` accumulated over calls (row chunks of one step) in
-    per-unit fp32 partial slabs (csrc/kernels/wgrad_f32.hip: a call's rows are cut into
-    units, one slab each, pulled dynamically by at most one block per CU), reduced once in
-    a fixed order by :meth:`result` — deterministic for a fixed chunking. Two units per CU
-    by default, so a CU held by another stream's kernel costs a share of one unit, not a
-    whole block's."""
+    """``dW += [A1[a1_rows] | A2]^T G`` accumulated over calls (row chunks of one step),
+    deterministic for a fixed chunking (the fp32 weight gradients of the fused executors).
+
+    GPU: native split-M MFMA accumulators (:class:`_WgradTile`); a ``[K, N]`` product wider
+    than one kernel tile (K > 256: a wide input layer, ``[x | mean_N(x)]`` of a 768-wide
+    feature; N > 256: a 512-wide hidden layer) is cut into K-blocks of the concatenated
+    ``[A1 | A2]`` columns and N-blocks of G's columns, one accumulator each (G is read once
+    per K-block). Two row units per CU, so a CU held by another stream's kernel costs a
+    share of one unit, not a whole block's. CPU: one fp64 accumulator (the numerics
+    oracle)."""
 
     UNITS_PER_CU = 2
+    # rows per unit of a short call: fewer units -> fewer partial slabs read and written,
+    # but each unit's rows run serially (2048: a 1.4K-row call took 0.4 ms on one CU; 64
+    # spreads it over ~22)
+    MIN_ROWS_PER_BLOCK = 64
 
     _P = 0
 
     def __init__(self, K: int, N: int, device, blocks: int = 0):
         self.K, self.N, self.device = int(K), int(N), torch.device(device)
+        self.fresh = True
+        self.tiles = []
         if self.device.type == "cuda":
             if blocks <= 0:
                 if WgradAcc._P == 0:
                     WgradAcc._P = torch.cuda.get_device_properties(self.device).multi_processor_count
                 blocks = WgradAcc._P * self.UNITS_PER_CU
-            self.partials = torch.empty(blocks, self.K, self.N, dtype=torch.float32,
-                                        device=self.device)
+            kb = _blocks(self.K, lambda w: w in (128, 256), (256, 128))
+            nb = _blocks(self.N, _wgrad_n_ok)
+            for k0, k1 in kb:
+                for n0, n1 in nb:
+                    self.tiles.append(((k0, k1), (n0, n1),
+                                       _WgradTile(k1 - k0, n1 - n0, self.device, blocks)))
         else:
             self.partials = torch.zeros(1, self.K, self.N, dtype=torch.float64)
-        self.fresh = True
-        self.used = 0  # slabs written since reset
-
-    # rows per block of a short call: fewer blocks -> fewer partial slabs read and
-    # written, but each block's rows run serially (2048: a 1.4K-row call took 0.4 ms on
-    # one CU; 64 spreads it over ~22)
-    MIN_ROWS_PER_BLOCK = 64
 
     def reset(self):
         self.fresh = True
-        self.used = 0
+        for t in self.tiles:
+            t[2].used = 0
 
     def add(self, A1: torch.Tensor, G: torch.Tensor, A2: Optional[torch.Tensor] = None,
             a1_rows: Optional[torch.Tensor] = None) -> None:
         if G.shape[0] == 0:
             return
         if self.device.type == "cuda":
-            P = self.partials.shape[0]
-            nb = max(1, min(P, -(-G.shape[0] // self.MIN_ROWS_PER_BLOCK)))
-            _native.ops().wgrad_f32(A1, A2, a1_rows, G, self.partials, nb, self.used)
-            self.used = max(self.used, nb)
+            K1 = A1.shape[1] if A2 is not None else self.K
+            if A2 is None and A1.shape[1] != self.K:
+                A1 = A1[:, : self.K]
+            for (k0, k1), (n0, n1), t in self.tiles:
+                g = G if (n0, n1) == (0, G.shape[1]) else G[:, n0:n1]
+                if k1 <= K1:  # A1 columns only (rows through a1_rows)
+                    a = A1 if (k0, k1) == (0, A1.shape[1]) else A1[:, k0:k1]
+                    t.add(a, g, None, a1_rows, self.MIN_ROWS_PER_BLOCK)
+                elif k0 >= K1:  # A2 columns only (dense rows)
+                    t.add(A2[:, k0 - K1:k1 - K1], g, None, None, self.MIN_ROWS_PER_BLOCK)
+                else:  # straddles: the kernel's dual form
+                    t.add(A1[:, k0:K1], g, A2[:, : k1 - K1], a1_rows, self.MIN_ROWS_PER_BLOCK)
         else:
             M = G.shape[0]
             a = A1.double()[a1_rows.long()] if a1_rows is not None else A1[:M].double()
@@ -205,7 +272,12 @@ class WgradAcc:
         if self.fresh:
             return out.zero_()
         if self.device.type == "cuda":
-            _native.ops().wgrad_f32_reduce(self.partials[: self.used], out)
+            if len(self.tiles) == 1 and out.is_contiguous():
+                self.tiles[0][2].result(out)
+                return out
+            for (k0, k1), (n0, n1), t in self.tiles:
+                blk = torch.empty(k1 - k0, n1 - n0, dtype=torch.float32, device=self.device)
+                out[k0:k1, n0:n1] = t.result(blk)
         else:
             out.copy_(self.partials[0].to(out.dtype))
         return out

@@ -203,3 +203,41 @@ def test_fused_interior_first_matches_w1(ranks, world, overlap, tmp_path):
     p = tmp_path / "ref.pt"
     torch.save({"loss": loss, "grads": grads, "corr": corr}, p)
     ranks(_interior_first_body, world, str(p), overlap)
+
+
+@pytest.mark.parametrize("hidden,feat", [(128, 100), (512, 128), (256, 300)])
+def test_fused_widths_match_stack(hidden, feat):
+    """Hidden 128 / 512 and a wide (zero-padded) input run on the fused executor and equal
+    the layer-stack autograd path."""
+    from dgraph_amd.data.synthetic import GraphShape
+
+    base = SHAPES["ogbn-papers100M"].scaled(SCALE)
+    shape = GraphShape("w", base.num_nodes, base.num_directed_edges, feat, 40, 0.3, 0.1, 0.1)
+    part = build_partition(shape, 0, 1, "cpu", global_frac=0.3, window=64)
+    L = part["L"]
+    part["csr"].num_cols = L
+    offs = contiguous_offsets(shape.num_nodes, 1)
+    x, y, split = node_data(shape, 0, offs, "cpu", dtype=torch.float32, return_split=True)
+    tr = torch.nonzero(split == SPLIT_TRAIN).reshape(-1)
+    ev = torch.nonzero((split == SPLIT_VALID) | (split == SPLIT_TEST)).reshape(-1)
+    res = []
+    for fused in (False, True):
+        g = DistGraph(part["csr"], L, 0, symmetric=True)
+        torch.manual_seed(0)
+        model = GraphSAGE(feat, hidden, 40, 3)
+        if fused:
+            from dgraph_amd.models.sage_fused import supported
+
+            assert supported(model, x)
+            ex = FusedSAGE(model, g, x, tr, y[tr], ev, y[ev], split[ev] == SPLIT_VALID,
+                           tr.numel(), chunk_rows=300)
+            loss = ex.step()
+        else:
+            logits, _ = model(x, g, out_rows=tr, eval_rows=ev)
+            loss = torch.nn.functional.cross_entropy(logits.float(), y[tr],
+                                                     reduction="sum") / tr.numel()
+            loss.backward()
+        res.append((loss.detach(), [p.grad.clone() for p in model.parameters()]))
+    torch.testing.assert_close(res[1][0], res[0][0], atol=1e-5, rtol=1e-5)
+    for a, b in zip(res[1][1], res[0][1]):
+        torch.testing.assert_close(a, b, atol=2e-5, rtol=1e-4)
