@@ -44,6 +44,14 @@ import time
 # (expandable segments are unsupported on ROCm; forbid splitting huge cached blocks so a
 #  freed 57 GB activation block is never carved up by a 38 GB request)
 os.environ.setdefault("PYTORCH_ALLOC_CONF", "max_split_size_mb:512")
+# hardware queues per process, set before the HIP runtime starts (torch only initialises it
+# on first use). With HIP's default of 4, the streams of one process (default, compute,
+# the communication stream of the halo exchange, ...) share queues round-robin, and a
+# stream sharing the compute stream's queue runs IN ORDER with it: the exchange is then
+# serialised with the kernels it should overlap (measured: a W=8 rank's step 355 ms with
+# 4 queues vs 309 ms with 8 or 16, the exposed exchange moving into the compute regions,
+# profiles/r04/). Override with DGRAPH_HW_QUEUES.
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("DGRAPH_HW_QUEUES", "8")
 
 import torch
 import torch.distributed as dist

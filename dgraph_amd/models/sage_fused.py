@@ -354,6 +354,16 @@ class FusedSAGE:
         # ---- persistent buffers (allocated once: no allocation in the steady state)
         f = dict(dtype=torch.float32, device=dev)
         self.h = [torch.empty(L, self.hid, **f) for _ in range(self.nl - 1)]
+        # W > 1: the exchange buffers, resident — an exchange's buffers are in use on the
+        # comm stream until it completes, so per-step buffers would make the caching
+        # allocator map fresh blocks (a synchronous hipMalloc of GBs) every step. One send
+        # buffer (forward sends, then the reverse exchange's receive), one received-halo
+        # buffer per hidden layer (the last one is the reverse exchange's send after the
+        # output layer's forward); the memory plan above counted exactly these
+        self.send_buf, self.halo_buf = None, []
+        if graph.send_map is not None:
+            self.send_buf = torch.empty(n_send, self.hid, **f)
+            self.halo_buf = [torch.empty(H, self.hid, **f) for _ in range(self.nl - 1)]
         if self.store_sep:
             self.dZ = torch.empty(self.nS, self.hid, **f)
             self.u = torch.empty(self.nS, self.hid, **f) if self.nl == 3 else None
@@ -501,13 +511,15 @@ class FusedSAGE:
             return None
         return (csr.rowptr[k0:k1 + 1], (rm[k0:k1] - r0).contiguous(), k1 - k0)
 
-    def _exchange(self, h: torch.Tensor):
-        """Start the halo rows of ``h`` on their way from their owners (forward all-to-all-v,
-        asynchronous): ``(recv, work)``, or None at W=1."""
+    def _exchange(self, h: torch.Tensor, l: int):
+        """Start the halo rows of hidden layer ``l``'s output ``h`` on their way from their
+        owners (forward all-to-all-v, asynchronous, resident buffers): ``(recv, work)``, or
+        None at W=1."""
         g = self.g
         if g.send_map is None:
             return None
-        return g.a2a(K.gather_rows(h, g.send_map.idx), async_op=True)
+        K.copy_rows(h, src_idx=g.send_map.idx, out=self.send_buf)
+        return g.a2a(self.send_buf, out=self.halo_buf[l], async_op=True)
 
     def _layer(self, hin: torch.Tensor, halo, consume, width: int, name: str,
                store: Optional[torch.Tensor] = None, keep: Optional[torch.Tensor] = None):
@@ -615,7 +627,7 @@ class FusedSAGE:
             self.edges_aggregated += nnz
             hin = hout
             # this layer's halo rows leave now and land while the next layer works
-            hin_halo = self._exchange(hout)
+            hin_halo = self._exchange(hout, l)
             self._mark(f"fwd_l{l + 1}" if l + 1 < nl - 1 else "fwd_out")
         # ---------------- forward: output layer (all rows), loss and eval on the fly
         ws, wn, b = P[nl - 1]
@@ -711,8 +723,11 @@ class FusedSAGE:
             u = self._gemm(dZ, wn1.detach().t().contiguous(), row_scale=self.invdegS,
                            out=self.u)
             if self.haloT is not None:
-                hg1 = self._spmm(self.haloT.rowptr, self.haloT.col, u, col_map=self.smap)
-                sg1, work = g.a2a_rev(hg1, async_op=True)
+                # the output layer's received halo rows are dead: its buffer sends, the
+                # forward send buffer receives
+                hg1 = self._spmm(self.haloT.rowptr, self.haloT.col, u, self.halo_buf[-1],
+                                 col_map=self.smap)
+                sg1, work = g.a2a_rev(hg1, out=self.send_buf, async_op=True)
                 self.edges_aggregated += self.haloT.nnz
         self.acc_hid_s.reset()
         self.acc_hid_n.reset()

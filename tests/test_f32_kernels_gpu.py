@@ -343,18 +343,21 @@ def test_fused_wide_gpu_matches_cpu(hidden, feat, layers):
 
     base = SHAPES["ogbn-papers100M"].scaled(1e-4)
     shape = GraphShape("w", base.num_nodes, base.num_directed_edges, feat, 47, 0.2, 0.1, 0.1)
+    # one graph and one data set (the generators differ per device), moved to each device
+    part = build_partition(shape, 0, 1, "cpu", global_frac=0.1, window=256)
+    L = part["L"]
+    part["csr"].num_cols = L
+    x0, y0, split0 = node_data(shape, 0, contiguous_offsets(shape.num_nodes, 1), "cpu",
+                               dtype=torch.float32, return_split=True)
     res = []
     for dev in ("cpu", DEV):
-        part = build_partition(shape, 0, 1, dev, global_frac=0.1, window=256)
-        L = part["L"]
-        part["csr"].num_cols = L
-        x, y, split = node_data(shape, 0, contiguous_offsets(shape.num_nodes, 1), dev,
-                                dtype=torch.float32, return_split=True)
+        x, y, split = x0.to(dev), y0.to(dev), split0.to(dev)
+        csr = part["csr"].to(dev)
         tr = torch.nonzero(split == SPLIT_TRAIN).reshape(-1)
         ev = torch.nonzero((split == SPLIT_VALID) | (split == SPLIT_TEST)).reshape(-1)
         torch.manual_seed(0)
         model = GraphSAGE(feat, hidden, 47, layers).to(dev)
-        g = DistGraph(part["csr"], L, 0, symmetric=True)
+        g = DistGraph(csr, L, 0, symmetric=True)
         ex = FusedSAGE(model, g, x, tr, y[tr], ev, y[ev], split[ev] == SPLIT_VALID,
                        tr.numel(), chunk_rows=2048)
         loss = ex.step()

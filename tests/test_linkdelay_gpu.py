@@ -21,6 +21,8 @@ DEV = torch.device("cuda", 0)
 
 def test_link_delay_holds_stream():
     _native.load()
+    _native.ops().link_delay(10.0, 0)  # first launch loads the code object
+    torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for us in (200.0, 5000.0):
         torch.cuda.synchronize()
