@@ -102,6 +102,9 @@ def parse():
                          "per-peer message / GBPS (one xGMI link per peer pair) on a side "
                          "stream, so the exposed-exchange regions measure the overlap "
                          "schedule against link-length transfers (0 = instant loopback)")
+    ap.add_argument("--link-cus", type=int, default=-1,
+                    help="rehearsal link model: CUs the modelled collective holds during a "
+                         "transfer (default DGRAPH_LOOPBACK_CUS = 16)")
     ap.add_argument("--no-interior-first", dest="interior_first", action="store_false",
                     help="W>1 fused executor: keep the original row order (no interior-first "
                          "renumbering, parallel/reorder.py)")
@@ -354,6 +357,12 @@ class Job:
             setattr(self, k, None)
 
 
+def _link_cus():
+    from dgraph_amd.comm import alltoallv as _a2a
+
+    return _a2a.LOOPBACK_CUS
+
+
 def _offsets(n, w):
     from dgraph_amd.data.synthetic import contiguous_offsets
 
@@ -509,6 +518,8 @@ def main():
         from dgraph_amd.comm import alltoallv as _a2a
 
         _a2a.LOOPBACK_LINK_GBPS = args.link_gbps
+        if args.link_cus >= 0:
+            _a2a.LOOPBACK_CUS = args.link_cus
     cfg = RunConfig.from_env()  # DGRAPH_<SECTION>_<FIELD> overrides (kernel knobs etc.)
     cfg.model.hidden, cfg.model.num_layers, cfg.model.dtype = args.hidden, args.layers, args.dtype
     cfg.data.dataset, cfg.data.global_frac = args.shape, args.global_frac
@@ -643,6 +654,7 @@ def main():
                           "final_loss_local": final_loss,
                           "executor": "fused" if use_fused else "stack",
                           "link_gbps": args.link_gbps,
+                          "link_cus": _link_cus() if args.link_gbps > 0 else 0,
                           "allocator_in_timed_steps": alloc_timed,
                           **({"schedule": schedule} if schedule else {}),
                           **({"halo": halo} if halo else {}),

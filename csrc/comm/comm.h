@@ -26,6 +26,6 @@ hipError_t heap_wait(const uint64_t* flags, int me, int world, uint64_t epoch,
                      int64_t max_spins, bool self_too, int* timed_out, hipStream_t st);
 
 // hold stream `st` for `us` microseconds of device wall-clock time (rehearsal link model)
-hipError_t link_delay(double us, hipStream_t st);
+hipError_t link_delay(double us, hipStream_t st, int blocks = 1);
 
 }  // namespace dgraph

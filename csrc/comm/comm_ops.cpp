@@ -278,16 +278,17 @@ void rccl_allreduce(int64_t h, const at::Tensor& t) {
 
 // Hold the current stream of `device` for `us` microseconds (device-side wait; the link
 // model of the single-process rehearsal's loopback exchange, comm/alltoallv.py)
-void link_delay_op(double us, int64_t device) {
+void link_delay_op(double us, int64_t device, int64_t blocks) {
   c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, static_cast<c10::DeviceIndex>(device)));
-  DG_HIP_CHECK(link_delay(us, c10::hip::getCurrentHIPStream(device).stream()));
+  DG_HIP_CHECK(link_delay(us, c10::hip::getCurrentHIPStream(device).stream(),
+                          static_cast<int>(blocks)));
 }
 
 }  // namespace
 }  // namespace dgraph
 
 TORCH_LIBRARY_FRAGMENT(dgraph_amd, m) {
-  m.def("link_delay(float us, int device) -> ()", &dgraph::link_delay_op);
+  m.def("link_delay(float us, int device, int blocks=1) -> ()", &dgraph::link_delay_op);
   m.def("heap_alloc(int nbytes, int device) -> Tensor", &dgraph::heap_alloc);
   m.def("ipc_get_handle(Tensor heap) -> Tensor", &dgraph::ipc_get_handle);
   m.def("ipc_open_handle(Tensor handle, int device) -> int", &dgraph::ipc_open_handle);

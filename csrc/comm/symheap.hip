@@ -198,17 +198,18 @@ hipError_t heap_put_rows(DType dt, const uint64_t* peer_base, int64_t dst_off,
 
 // ---------------------------------------------------------------------------------------
 // Link-time model of a loopback exchange (single-process rehearsal of a W-way rank): one
-// lane of one wave waits `ticks` of the constant-rate wall clock (s_memrealtime, read by
-// wall_clock64) with s_sleep between polls, so the stream it runs on is held for the time
-// the exchange's largest per-peer message would take on one xGMI link. Occupies one wave
-// slot of one CU and no memory bandwidth.
+// lane of each one-wave block waits `ticks` of the constant-rate wall clock (s_memrealtime,
+// read by wall_clock64) with s_sleep between polls, so the stream it runs on is held for
+// the time the exchange's largest per-peer message would take on one xGMI link. Each block
+// holds a wave slot of a CU (and no memory bandwidth) — several blocks stand for the CUs a
+// collective's kernel occupies while it moves data.
 __global__ __launch_bounds__(64) void link_delay_kernel(uint64_t ticks) {
   if (threadIdx.x != 0) return;
   const uint64_t t0 = wall_clock64();
   while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(32);
 }
 
-hipError_t link_delay(double us, hipStream_t st) {
+hipError_t link_delay(double us, hipStream_t st, int blocks) {
   if (!(us > 0.0)) return hipSuccess;
   static int khz = 0;
   if (khz == 0) {
@@ -220,7 +221,7 @@ hipError_t link_delay(double us, hipStream_t st) {
   }
   const double t = us * 1e-3 * static_cast<double>(khz);
   const uint64_t ticks = t > 1.8e19 ? ~0ull : static_cast<uint64_t>(t);
-  hipLaunchKernelGGL(link_delay_kernel, dim3(1), dim3(64), 0, st, ticks);
+  hipLaunchKernelGGL(link_delay_kernel, dim3(blocks > 0 ? blocks : 1), dim3(64), 0, st, ticks);
   return hipGetLastError();
 }
 

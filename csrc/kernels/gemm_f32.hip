@@ -108,9 +108,13 @@ __device__ __forceinline__ void gemm_f32_body(
   const int nst = K / kBK;
   const int64_t ntiles = (M + kBM - 1) / kBM;
   __shared__ int s_tile;
-  if (tid == 0) s_tile = atomicAdd(tile_ctr, 1);
-  __syncthreads();
-  int64_t tile = s_tile;
+  // tile_ctr == nullptr: static schedule (block b walks tiles b, b + grid, ...)
+  const bool dyn = tile_ctr != nullptr;
+  if (dyn) {
+    if (tid == 0) s_tile = atomicAdd(tile_ctr, 1);
+    __syncthreads();
+  }
+  int64_t tile = dyn ? s_tile : blockIdx.x;
   if (tile >= ntiles) return;  // block-uniform
 
   // ---- per-thread global load slots of a stage
@@ -193,10 +197,12 @@ __device__ __forceinline__ void gemm_f32_body(
     // the next tile: its counter fetch is issued now and read after stage 0 (one stage of
     // MFMAs hides the atomic's latency); its A1 row indices are needed at the last stage
     int nraw = 0;
-    if (tid == 0) nraw = atomicAdd(tile_ctr, 1);
-    int64_t next = 0;
-    bool has_next = false;  // block-uniform
-    if (nst == 1) {
+    if (dyn && tid == 0) nraw = atomicAdd(tile_ctr, 1);
+    int64_t next = tile + gridDim.x;
+    bool has_next = next < ntiles;  // block-uniform
+    if (!dyn) {
+      rows_of(has_next ? next : tile, nx_src_row);
+    } else if (nst == 1) {
       __syncthreads();  // everyone has read s_tile / s_tile of the previous fetch
       if (tid == 0) s_tile = nraw;
       __syncthreads();
@@ -252,10 +258,10 @@ __device__ __forceinline__ void gemm_f32_body(
           }
         }
       }
-      if (s == 0 && nst > 1 && tid == 0) s_tile = nraw;
+      if (dyn && s == 0 && nst > 1 && tid == 0) s_tile = nraw;
       store_stage(buf ^ 1);  // (the block's very last store lands in a buffer never read)
       __syncthreads();
-      if (s == 0 && nst > 1) {
+      if (dyn && s == 0 && nst > 1) {
         next = s_tile;
         has_next = next < ntiles;
         rows_of(has_next ? next : tile, nx_src_row);  // consumed at the tile's last stage
@@ -337,8 +343,11 @@ hipError_t launch_gemm_f32(const float* A1, int64_t lda1, int K1, const float* B
   // persistent: one block per CU (LDS-limited), each pulling tiles from the work counter
   const int64_t ntiles = (M + kBM - 1) / kBM;
   const int64_t blocks = ntiles < num_cus ? ntiles : num_cus;
-  int* ctr = work_counter(st);
-  if (ctr == nullptr) return hipErrorOutOfMemory;
+  int* ctr = nullptr;
+  if (g_f32_dynamic) {
+    ctr = work_counter(st);
+    if (ctr == nullptr) return hipErrorOutOfMemory;
+  }
   hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(blocks)), dim3(512), lds, st, A1,
                      lda1, K1, B1, ldb1, A2, lda2, K2, B2, ldb2, a_rows, bias, cin, ldc, beta,
                      gate, ldg, o_rows, rsc, out, ldo, M, ctr);
@@ -392,6 +401,9 @@ hipError_t gemm_f32_n(const float* A1, int64_t lda1, int K1, const float* B1, in
 inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 }  // namespace
+
+bool g_f32_dynamic = true;
+void set_f32_dynamic(bool on) { g_f32_dynamic = on; }
 
 int* work_counter(hipStream_t st) {
   constexpr int kSlots = 4096;

@@ -249,6 +249,10 @@ hipError_t dual_gemm_bs(const void* A1, int64_t lda1, const void* B1t, int64_t K
 // stream's kernel, e.g. RCCL's during a halo exchange) costs nothing: the running blocks
 // take its work.
 int* work_counter(hipStream_t st);
+// dynamic (work counter, default) or static (block b: tiles b, b + grid, ...) schedule of
+// the fp32 GEMM and weight-gradient kernels launched from now on
+extern bool g_f32_dynamic;
+void set_f32_dynamic(bool on);
 bool gemm_f32_supported(int64_t N, int64_t K1, int64_t K2);
 hipError_t gemm_f32(const float* A1, int64_t lda1, int64_t K1, const float* B1, int64_t ldb1,
                     const float* A2, int64_t lda2, int64_t K2, const float* B2, int64_t ldb2,

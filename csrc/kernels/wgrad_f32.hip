@@ -63,11 +63,18 @@ __global__ __launch_bounds__(kThr, 1) void wgrad_f32_kernel(
   const int wm = wave / WN, wn = wave % WN;
   const int li = lane & 15;
   const int lh = lane >> 4;
-  for (;;) {
-  __syncthreads();  // the previous unit's LDS reads and s_unit reads are done
-  if (tid == 0) s_unit = atomicAdd(unit_ctr, 1);
-  __syncthreads();
-  const int unit = s_unit;
+  // unit_ctr == nullptr: static schedule (block b runs units b, b + grid, ...)
+  for (int it = 0;; ++it) {
+  int unit;
+  if (unit_ctr != nullptr) {
+    __syncthreads();  // the previous unit's LDS reads and s_unit reads are done
+    if (tid == 0) s_unit = atomicAdd(unit_ctr, 1);
+    __syncthreads();
+    unit = s_unit;
+  } else {
+    if (it > 0) __syncthreads();  // the previous unit's LDS reads are done
+    unit = static_cast<int>(blockIdx.x) + it * static_cast<int>(gridDim.x);
+  }
   if (unit >= units) return;  // block-uniform
   const int64_t m_begin = static_cast<int64_t>(unit) * rows_per_unit;
   int64_t m_end = m_begin + rows_per_unit;
@@ -238,8 +245,11 @@ hipError_t launch_wgrad(const float* A1, int64_t lda1, int K1, const float* A2, 
       num_cus = 256;
   }
   const int blocks = P < num_cus ? P : num_cus;
-  int* ctr = work_counter(st);
-  if (ctr == nullptr) return hipErrorOutOfMemory;
+  int* ctr = nullptr;
+  if (g_f32_dynamic) {
+    ctr = work_counter(st);
+    if (ctr == nullptr) return hipErrorOutOfMemory;
+  }
   hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(blocks)), dim3(kThr), C::BYTES, st, A1,
                      lda1, K1, A2, lda2, a1_rows, G, ldg, M, rpu, P, partials, fresh_from, ctr);
   return hipGetLastError();

@@ -43,6 +43,11 @@ A2A_IMPL = os.environ.get("DGRAPH_A2A_IMPL", "torch")
 # exchange regions separately, experiments/OGB/GCN.py:101-116).
 LOOPBACK_LINK_GBPS = float(os.environ.get("DGRAPH_LOOPBACK_LINK_GBPS", "0"))
 LOOPBACK_LATENCY_US = float(os.environ.get("DGRAPH_LOOPBACK_LATENCY_US", "15"))
+# CUs the modelled collective's kernel holds while the transfer runs (one wave each): RCCL
+# moves an all-to-all with one workgroup per channel, each resident on a CU for the whole
+# transfer; a block of another kernel that needs the whole CU (the fp32 GEMM) cannot start
+# there until it ends
+LOOPBACK_CUS = int(os.environ.get("DGRAPH_LOOPBACK_CUS", "16"))
 
 _HEAPS: dict = {}
 
@@ -214,7 +219,7 @@ class AllToAllV:
         side = _side_stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
-            _native.ops().link_delay(float(us), int(dev.index))
+            _native.ops().link_delay(float(us), int(dev.index), LOOPBACK_CUS)
             if m:
                 out[:m].copy_(send[:m])
             if self.total_recv > m:
