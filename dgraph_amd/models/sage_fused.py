@@ -518,8 +518,20 @@ class FusedSAGE:
         g = self.g
         if g.send_map is None:
             return None
-        K.copy_rows(h, src_idx=g.send_map.idx, out=self.send_buf)
-        return g.a2a(self.send_buf, out=self.halo_buf[l], async_op=True)
+        if self.dev.type != "cuda":
+            K.copy_rows(h, src_idx=g.send_map.idx, out=self.send_buf)
+            return g.a2a(self.send_buf, out=self.halo_buf[l], async_op=True)
+        # pack and send on the communication stream: the pack (a streaming gather of the
+        # send rows) overlaps the next layer's interior work instead of preceding it. It
+        # reads h (complete: the stream waits for the compute stream) and writes the send
+        # buffer, whose previous exchange the compute stream has already waited for
+        from ..comm.alltoallv import _side_stream
+
+        side = _side_stream(self.dev)
+        side.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(side):
+            K.copy_rows(h, src_idx=g.send_map.idx, out=self.send_buf)
+            return g.a2a(self.send_buf, out=self.halo_buf[l], async_op=True)
 
     def _layer(self, hin: torch.Tensor, halo, consume, width: int, name: str,
                store: Optional[torch.Tensor] = None, keep: Optional[torch.Tensor] = None):
