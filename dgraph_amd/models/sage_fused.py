@@ -69,6 +69,17 @@ OVERLAP_FWD = os.environ.get("DGRAPH_FUSED_OVERLAP", "1") != "0"
 # keep layer 0's input aggregate mean_N(x) from the forward for the backward when the
 # memory plan has room for it ("auto"), never ("off"), or require it ("on")
 KEEP_AGG0 = os.environ.get("DGRAPH_FUSED_KEEP_AGG0", "auto")
+# W > 1, a forward layer whose exchange is in flight: after its interior rows, aggregate the
+# interior part of the boundary rows into a store before waiting ("on"), or wait and run the
+# boundary rows in one two-source pass ("off"); "auto" stores only when the modelled
+# exchange outlasts the interior rows' work (the store costs a second pass over the boundary
+# rows and a read-modify-write of their aggregates: ~10 ms per layer at W = 8)
+BOUNDARY_STORE = os.environ.get("DGRAPH_FUSED_BOUNDARY_STORE", "auto")
+# planning rates of the "auto" choice: xGMI per link and direction, fp32 SpMM gather
+# (effective) and fp32 MFMA GEMM rates measured on MI355X (PERFORMANCE.md)
+PLAN_LINK_GBPS = float(os.environ.get("DGRAPH_PLAN_LINK_GBPS", "153"))
+PLAN_SPMM_TBPS = 10.0
+PLAN_GEMM_TFPS = 100.0
 
 
 def _ranges(a: int, b: int, step: int) -> List[Tuple[int, int]]:
@@ -315,10 +326,11 @@ class FusedSAGE:
         # W > 1: a whole-layer aggregate buffer lets the interior part of the OUTPUT layer's
         # boundary rows run while its halo rows are in flight (hidden layers use their own
         # output buffer for that)
+        self.use_store = self._plan_store()
         self.agg_full = None
         need_full = (L - self.Li) * wA * 4
         if graph.send_map is not None and OVERLAP_FWD and self.Li < L and \
-                free - need_h - other - need_full > margin:
+                self.use_store["out"] and free - need_h - other - need_full > margin:
             self.agg_full = torch.empty(L - self.Li, wA, dtype=torch.float32, device=dev)
             other += need_full
         # layer 0's input aggregate kept from the forward for the backward (else recomputed)
@@ -455,6 +467,7 @@ class FusedSAGE:
         """The overlap structure this executor runs (bench.py records it)."""
         return {"interior_rows": self.Li, "boundary_rows": self.L - self.Li,
                 "chunk_rows": self.cr, "output_layer_store": self.agg_full is not None,
+                "boundary_store": dict(self.use_store),
                 "keep_agg0": self.agg0 is not None}
 
     # ------------------------------------------------------------------ helpers
@@ -532,6 +545,26 @@ class FusedSAGE:
         with torch.cuda.stream(side):
             K.copy_rows(h, src_idx=g.send_map.idx, out=self.send_buf)
             return g.a2a(self.send_buf, out=self.halo_buf[l], async_op=True)
+
+    def _plan_store(self) -> dict:
+        """Per forward layer (by output width): pre-aggregate the boundary rows' interior
+        part while the exchange is in flight? Only when the modelled exchange (largest
+        per-peer message / PLAN_LINK_GBPS) outlasts the interior rows' work (their SpMM
+        bytes and GEMM flops at the planning rates) — otherwise the interior rows alone
+        hide it and the boundary rows run in one pass after the wait."""
+        g = self.g
+        if BOUNDARY_STORE in ("on", "off") or g.send_map is None or self.Li >= self.L:
+            return {k: BOUNDARY_STORE == "on" for k in ("hidden", "out")}
+        a2a = g.a2a
+        peer_rows = max(max(a2a.send_splits, default=0), max(a2a.recv_splits, default=0))
+        t_x = peer_rows * self.hid * 4 / (PLAN_LINK_GBPS * 1e9)
+        nnz_a = int(self.adj.rp[self.Li]) if self.Li > 0 else 0
+        out = {}
+        for key, n_out in (("hidden", self.hid), ("out", self.Cp)):
+            t_a = nnz_a * self.hid * 4 / (PLAN_SPMM_TBPS * 1e12) + \
+                2.0 * self.Li * 2 * self.hid * n_out / (PLAN_GEMM_TFPS * 1e12)
+            out[key] = t_x > 0.8 * t_a
+        return out
 
     def _layer(self, hin: torch.Tensor, halo, consume, width: int, name: str,
                store: Optional[torch.Tensor] = None, keep: Optional[torch.Tensor] = None):
@@ -632,7 +665,8 @@ class FusedSAGE:
                 self._gemm(hin[r0:r1], ws, a, wn, bias=bias, relu=True, out=hout[r0:r1])
 
             # layer l >= 1 can store boundary-row aggregates in its own output buffer
-            store = hout[self.Li:] if (l > 0 and hin.shape[1] == hout.shape[1]) else None
+            store = hout[self.Li:] if (l > 0 and hin.shape[1] == hout.shape[1] and
+                                       self.use_store["hidden"]) else None
             keep = self.agg0 if l == 0 else None
             halos.append(self._layer(hin, hin_halo, consume, hin.shape[1], f"fwd_l{l}",
                                      store=store, keep=keep))
@@ -654,7 +688,8 @@ class FusedSAGE:
         hl = hin
         hl_halo = self._layer(hl, hin_halo, lambda ci, a: self._out_chunk(ci, a, hl, wsp,
                                                                           wnp, bp),
-                              hid, "fwd_out", store=self.agg_full)
+                              hid, "fwd_out",
+                              store=self.agg_full if self.use_store["out"] else None)
         halos.append(hl_halo)
         self.edges_aggregated += nnz
         # per-row losses / hits summed once, in a fixed order

@@ -156,13 +156,14 @@ def test_fused_directed_graph_matches_autograd():
         torch.testing.assert_close(a, b, atol=2e-5, rtol=1e-4)
 
 
-def _interior_first_body(rank, world, ref_path, overlap):
+def _interior_first_body(rank, world, ref_path, overlap, store="auto"):
     """One rank of a W-way partition renumbered interior-first (parallel/reorder.py), the
     fused executor's interior-then-boundary schedule, all-reduced against W=1."""
     import dgraph_amd.models.sage_fused as sf
     from dgraph_amd.parallel.reorder import interior_first
 
     sf.OVERLAP_FWD = overlap
+    sf.BOUNDARY_STORE = store
     shape = SHAPES["ogbn-papers100M"].scaled(SCALE)
     part = build_partition(shape, rank, world, "cpu", global_frac=0.05, window=64)
     csr, send, perm, L_int, loc = interior_first(part["csr"], part["L"],
@@ -182,6 +183,8 @@ def _interior_first_body(rank, world, ref_path, overlap):
     ex = FusedSAGE(model, g, x, tr, y[tr], ev, y[ev], split[ev] == SPLIT_VALID, int(n_tr),
                    chunk_rows=300, release_graph=True)
     assert ex.Li == L_int and ex.nA >= 1
+    if store != "auto":
+        assert ex.use_store == {"hidden": store == "on", "out": store == "on"}
     assert g.interior is None  # released: the executor runs on its own adjacency
     loss = ex.step()
     grads = [p.grad.clone() for p in model.parameters()]
@@ -197,12 +200,14 @@ def _interior_first_body(rank, world, ref_path, overlap):
     assert torch.equal(corr, ref["corr"])
 
 
-@pytest.mark.parametrize("world,overlap", [(2, True), (4, True), (2, False)])
-def test_fused_interior_first_matches_w1(ranks, world, overlap, tmp_path):
+@pytest.mark.parametrize("world,overlap,store", [(2, True, "on"), (2, True, "off"),
+                                                (4, True, "on"), (4, True, "off"),
+                                                (2, False, "auto")])
+def test_fused_interior_first_matches_w1(ranks, world, overlap, store, tmp_path):
     loss, grads, corr = _fused_grads(0, 1, gf=0.05)
     p = tmp_path / "ref.pt"
     torch.save({"loss": loss, "grads": grads, "corr": corr}, p)
-    ranks(_interior_first_body, world, str(p), overlap)
+    ranks(_interior_first_body, world, str(p), overlap, store)
 
 
 @pytest.mark.parametrize("hidden,feat", [(128, 100), (512, 128), (256, 300)])
