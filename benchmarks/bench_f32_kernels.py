@@ -26,7 +26,6 @@ def main():
     ap.add_argument("--rows", type=int, default=1438388)
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--global-frac", type=float, default=0.05)
-    ap.add_argument("--variants", default="0", help="SpMM tuning variants to time")
     a = ap.parse_args()
     from dgraph_amd import _native
     from dgraph_amd.data.synthetic import SHAPES, build_partition
@@ -57,23 +56,13 @@ def main():
         res[name] = r
         print(name, r, flush=True)
 
-    ops = _native.ops()
     for F in (128, 256):
         x = torch.randn(L, F, device=dev)
         out = torch.empty(L, F, device=dev)
-        ref = None
-        for var in [int(v) for v in a.variants.split(",")]:
-            ops.set_f32_sched(-1, -1, var)
-            tag = "" if var == 0 else f"_v{var}"
-            timed(f"spmm_f32_F{F}{tag}", lambda: F32.spmm_f32(csr.rowptr, csr.col, x, out,
-                                                              row_scale=inv, pass_cols=64),
-                  nbytes=csr.nnz * (F * 4 + 4) + L * F * 4)
-            if ref is None:
-                ref = out.clone()
-            else:
-                assert torch.equal(ref, out), f"variant {var} differs"
-        ops.set_f32_sched(-1, -1, 0)
-        del x, out, ref
+        timed(f"spmm_f32_F{F}", lambda: F32.spmm_f32(csr.rowptr, csr.col, x, out,
+                                                     row_scale=inv, pass_cols=64),
+              nbytes=csr.nnz * (F * 4 + 4) + L * F * 4)
+        del x, out
     # column-mapped: u stored on ~30 % of the rows
     g = torch.Generator(device=dev).manual_seed(0)
     S = torch.nonzero(torch.rand(L, generator=g, device=dev) < 0.3).reshape(-1)

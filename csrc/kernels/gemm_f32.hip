@@ -32,9 +32,9 @@
 //   * persistent grid (one 512-thread block per CU) pulling 256-row tiles from a work
 //     counter (dynamic: a block whose CU is held by another kernel, e.g. RCCL's during a
 //     halo exchange, starts late and finds the tiles taken, instead of running its static
-//     share after everyone else); the next tile's index is fetched during the current
-//     tile's first stage and its first stage is loaded during the current tile's last
-//     stage, so the prologue's global latency and the epilogue's stores overlap MFMAs.
+//     share after everyone else); tile indices are fetched a tile ahead, and the next
+//     tile's first stage is loaded during the current tile's last stage, so the prologue's
+//     global latency and the epilogue's stores overlap MFMAs.
 #include "../common.h"
 #include "kernels.h"
 
@@ -108,13 +108,20 @@ __device__ __forceinline__ void gemm_f32_body(
   const int nst = K / kBK;
   const int64_t ntiles = (M + kBM - 1) / kBM;
   __shared__ int s_tile;
-  // tile_ctr == nullptr: static schedule (block b walks tiles b, b + grid, ...)
+  // tile_ctr == nullptr: static schedule (block b walks tiles b, b + grid, ...). Dynamic:
+  // thread 0 keeps ONE counter fetch in flight a whole tile ahead (``pending``) and
+  // publishes it through LDS at the top of the next tile, so the atomic's latency is never
+  // waited for; readfirstlane keeps the block-uniform indices in scalar registers
   const bool dyn = tile_ctr != nullptr;
+  int pending = 0;
   if (dyn) {
-    if (tid == 0) s_tile = atomicAdd(tile_ctr, 1);
+    if (tid == 0) {
+      s_tile = atomicAdd(tile_ctr, 1);
+      pending = atomicAdd(tile_ctr, 1);
+    }
     __syncthreads();
   }
-  int64_t tile = dyn ? s_tile : blockIdx.x;
+  int64_t tile = dyn ? __builtin_amdgcn_readfirstlane(s_tile) : blockIdx.x;
   if (tile >= ntiles) return;  // block-uniform
 
   // ---- per-thread global load slots of a stage
@@ -194,22 +201,17 @@ __device__ __forceinline__ void gemm_f32_body(
   const int bcol_w = wn * TN * 16;  // this wave's first column
   int g = 0;                        // stages run by this block (LDS buffer parity)
   while (true) {
-    // the next tile: its counter fetch is issued now and read after stage 0 (one stage of
-    // MFMAs hides the atomic's latency); its A1 row indices are needed at the last stage
-    int nraw = 0;
-    if (dyn && tid == 0) nraw = atomicAdd(tile_ctr, 1);
     int64_t next = tile + gridDim.x;
-    bool has_next = next < ntiles;  // block-uniform
-    if (!dyn) {
-      rows_of(has_next ? next : tile, nx_src_row);
-    } else if (nst == 1) {
-      __syncthreads();  // everyone has read s_tile / s_tile of the previous fetch
-      if (tid == 0) s_tile = nraw;
+    if (dyn) {
+      if (tid == 0) {
+        s_tile = pending;  // fetched a tile ago
+        pending = atomicAdd(tile_ctr, 1);
+      }
       __syncthreads();
-      next = s_tile;
-      has_next = next < ntiles;
-      rows_of(has_next ? next : tile, nx_src_row);
+      next = __builtin_amdgcn_readfirstlane(s_tile);
     }
+    const bool has_next = next < ntiles;  // block-uniform
+    rows_of(has_next ? next : tile, nx_src_row);  // consumed at the tile's last stage
     for (int s = 0; s < nst; ++s, ++g) {
       const int buf = g & 1;
       // the next stage, in flight during this stage's MFMAs; at the tile's last stage the
@@ -258,14 +260,8 @@ __device__ __forceinline__ void gemm_f32_body(
           }
         }
       }
-      if (dyn && s == 0 && nst > 1 && tid == 0) s_tile = nraw;
       store_stage(buf ^ 1);  // (the block's very last store lands in a buffer never read)
       __syncthreads();
-      if (dyn && s == 0 && nst > 1) {
-        next = s_tile;
-        has_next = next < ntiles;
-        rows_of(has_next ? next : tile, nx_src_row);  // consumed at the tile's last stage
-      }
     }
 
     // ---- epilogue: tile (a, b) register r of lane l is element

@@ -93,7 +93,6 @@ void set_spmm_f32_pass_cols(int cols);
 // pass width (0 = default 64); negative arguments leave a setting unchanged
 void set_spmm_f32_config(int rowgroup, int pass_cols);
 void set_spmm_f32_grid(int blocks);   // 0 = uncapped
-void set_spmm_f32_variant(int v);     // tuning variant of the row-group kernel (0 default)
 
 // Hub-row splitting (rows whose degree exceeds `cap` are aggregated in three steps):
 //   1. spmm_csr(..., cap): every row sums at most its first `cap` entries;

@@ -33,17 +33,15 @@ namespace {
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-// VAR (tuning variants, set_spmm_f32_variant; A/B in benchmarks/bench_f32_kernels.py):
-//   0 = batches of 8 neighbour rows per lane; 1 = one batch of LPR rows (all loads of a
-//   chunk in flight before its FMAs); 2 / 3 = as 0 with at least 6 / 8 waves per SIMD
-template <typename IdxT, int LPR, int WMODE, bool CMAP, bool TWO, int VAR>
-__global__ __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu(VAR == 2 ? 6 : VAR == 3 ? 8 : 1)))
-void spmm_f32_rowgroup_kernel(SpmmF32Args a) {
+// Batches of 8 neighbour rows per lane (98 VGPRs, 4 waves per SIMD). Measured against one
+// batch of all LPR rows (all loads of a chunk before its FMAs: -3 %) and against forcing 6 or
+// 8 waves per SIMD (fewer registers, fewer loads in flight: -28 % / -38 %),
+// profiles/r04/spmm_f32_variants_ab.log.
+template <typename IdxT, int LPR, int WMODE, bool CMAP, bool TWO>
+__global__ __launch_bounds__(256) void spmm_f32_rowgroup_kernel(SpmmF32Args a) {
   constexpr int VEC = 4;
   constexpr int G = kWave / LPR;
-  // neighbour rows in flight per lane per batch
-  constexpr int U = VAR == 1 ? LPR : (LPR < 8 ? LPR : 8);
+  constexpr int U = LPR < 8 ? LPR : 8;  // neighbour rows in flight per lane per batch
   constexpr bool HAS_EW = (WMODE & 1) != 0;
   constexpr bool HAS_CS = (WMODE & 2) != 0;
   const IdxT* __restrict__ col = static_cast<const IdxT*>(a.col);
@@ -95,7 +93,10 @@ void spmm_f32_rowgroup_kernel(SpmmF32Args a) {
     // of x (column id 0: valid for x, col_map and col_scale whatever part of a row the
     // call covers; an entry of the column array may be a halo column) with weight 0
     auto load_c = [&](int k) -> int64_t {
-      return k < deg ? static_cast<int64_t>(col[s + k]) : int64_t(0);
+      // unconditional load (entry 0 for padding slots: a load under a branch is waited for
+      // at the join), its value replaced by column 0 for padding
+      const IdxT c = col[k < deg ? s + k : 0];
+      return k < deg ? static_cast<int64_t>(c) : int64_t(0);
     };
     auto load_w = [&](int64_t& c, int k) -> float {
       float w = k < deg ? 1.f : 0.f;
@@ -232,8 +233,6 @@ void spmm_f32_rowgroup_kernel(SpmmF32Args a) {
   }
 }
 
-int g_f32_variant = 0;
-
 // grid cap (0 = one row group per wave, the whole graph in one launch): the kernel is
 // grid-strided, so a capped grid is a persistent one that leaves room on every CU for a
 // kernel of another stream (set_spmm_f32_grid)
@@ -252,22 +251,13 @@ hipError_t launch_f32_rg(const SpmmF32Args& a, hipStream_t st) {
   const bool cmap = a.col_map != nullptr;
   const bool two = a.x2 != nullptr;
   if (two && (cmap || wmode != 0)) return hipErrorInvalidValue;  // not instantiated
-  const int var = (wmode == 0 && !cmap) ? g_f32_variant : 0;
   dim3 grid(static_cast<unsigned>(blocks)), block(256);
-#define DG_F32_KV(LPR_, W_, C_, T_, V_)                                                     \
-  if (LPR == LPR_ && wmode == W_ && cmap == C_ && two == T_ && var == V_) {                 \
-    hipLaunchKernelGGL((spmm_f32_rowgroup_kernel<IdxT, LPR_, W_, C_, T_, V_>), grid, block, \
-                       0, st, a);                                                           \
+#define DG_F32_K(LPR_, W_, C_, T_)                                                          \
+  if (LPR == LPR_ && wmode == W_ && cmap == C_ && two == T_) {                              \
+    hipLaunchKernelGGL((spmm_f32_rowgroup_kernel<IdxT, LPR_, W_, C_, T_>), grid, block, 0, \
+                       st, a);                                                              \
     return hipGetLastError();                                                               \
   }
-// the tuning variants exist for the hot (unweighted, uncompacted) instantiations; every
-// other combination runs variant 0
-#define DG_F32_K(LPR_, W_, C_, T_)                                                          \
-  if (W_ == 0 && !C_) {                                                                     \
-    DG_F32_KV(LPR_, W_, C_, T_, 1) DG_F32_KV(LPR_, W_, C_, T_, 2)                          \
-    DG_F32_KV(LPR_, W_, C_, T_, 3)                                                          \
-  }                                                                                         \
-  DG_F32_KV(LPR_, W_, C_, T_, 0)
 #define DG_F32(LPR_)                                                                        \
   DG_F32_K(LPR_, 0, false, false) DG_F32_K(LPR_, 1, false, false)                           \
   DG_F32_K(LPR_, 2, false, false) DG_F32_K(LPR_, 3, false, false)                           \
@@ -279,7 +269,6 @@ hipError_t launch_f32_rg(const SpmmF32Args& a, hipStream_t st) {
   DG_F32(32)
   DG_F32(64)
 #undef DG_F32_K
-#undef DG_F32_KV
 #undef DG_F32
   return hipErrorInvalidValue;
 }
@@ -293,8 +282,6 @@ int g_f32_pass_cols = 64;
 void set_spmm_f32_pass_cols(int cols) { g_f32_pass_cols = cols > 0 ? cols : 64; }
 
 void set_spmm_f32_grid(int blocks) { g_f32_grid_cap = blocks > 0 ? blocks : 0; }
-
-void set_spmm_f32_variant(int v) { g_f32_variant = (v >= 0 && v <= 3) ? v : 0; }
 
 bool spmm_f32_rowgroup_ok(int F, int64_t ldx, int64_t ldo, const void* x, const void* out) {
   auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) % 16) == 0; };

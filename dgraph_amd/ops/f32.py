@@ -10,6 +10,7 @@ ops are what :mod:`dgraph_amd.models.sage_fused` is built from.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -202,11 +203,12 @@ class WgradAcc:
     than one kernel tile (K > 256: a wide input layer, ``[x | mean_N(x)]`` of a 768-wide
     feature; N > 256: a 512-wide hidden layer) is cut into K-blocks of the concatenated
     ``[A1 | A2]`` columns and N-blocks of G's columns, one accumulator each (G is read once
-    per K-block). Two row units per CU, so a CU held by another stream's kernel costs a
-    share of one unit, not a whole block's. CPU: one fp64 accumulator (the numerics
-    oracle)."""
+    per K-block); row units are pulled dynamically by the blocks. CPU: one fp64 accumulator
+    (the numerics oracle). One row unit per CU by default (``DGRAPH_WGRAD_UNITS_PER_CU``): two cost 8 ms
+    per papers100M step in slab traffic, and the kernel's blocks share a CU with another
+    stream's waves without slowing down (profiles/r04/gemm_wgrad_static_vs_dynamic_ab.log)."""
 
-    UNITS_PER_CU = 2
+    UNITS_PER_CU = int(os.environ.get("DGRAPH_WGRAD_UNITS_PER_CU", "1"))
     # rows per unit of a short call: fewer units -> fewer partial slabs read and written,
     # but each unit's rows run serially (2048: a 1.4K-row call took 0.4 ms on one CU; 64
     # spreads it over ~22)
