@@ -75,6 +75,12 @@ KEEP_AGG0 = os.environ.get("DGRAPH_FUSED_KEEP_AGG0", "auto")
 # exchange outlasts the interior rows' work (the store costs a second pass over the boundary
 # rows and a read-modify-write of their aggregates: ~10 ms per layer at W = 8)
 BOUNDARY_STORE = os.environ.get("DGRAPH_FUSED_BOUNDARY_STORE", "auto")
+# W > 1: hidden-layer halos exchanged and consumed in column blocks ("stream") instead of
+# kept at full width for the whole step — "auto" when the full-width plan does not fit (a
+# structureless graph's halo is nearly every remote vertex), "on" / "off" to force
+HALO_STREAM = os.environ.get("DGRAPH_FUSED_HALO_STREAM", "auto")
+# (column block, ring buffers) of the streamed plan, in order of preference
+STREAM_SHAPES = ((64, 2), (64, 1), (32, 2), (32, 1))
 # planning rates of the "auto" choice: xGMI per link and direction, fp32 SpMM gather
 # (effective) and fp32 MFMA GEMM rates measured on MI355X (PERFORMANCE.md)
 PLAN_LINK_GBPS = float(os.environ.get("DGRAPH_PLAN_LINK_GBPS", "153"))
@@ -317,7 +323,26 @@ class FusedSAGE:
         # kept), every hidden layer's (the backward reads them) — and each exchange's send
         # rows while it is in flight: planned here, not discovered by the allocator
         n_send = graph.send_map.idx.numel() if graph.send_map is not None else 0
+        self.n_send = n_send
         self.halo_bytes = 4 * (H * self.d0 + (self.nl - 1) * H * self.hid + n_send * self.hid)
+        self.stream, self.cw, self.nbuf = False, 0, 0
+        full_ok = dev.type != "cuda" or need_h + self.halo_bytes + other + (1 << 28) <= free
+        if graph.send_map is not None and (HALO_STREAM == "on" or
+                                           (HALO_STREAM == "auto" and not full_ok)):
+            # streamed halos: the input's halo stays resident (static), the hidden layers'
+            # cross in column blocks of cw through a ring of nbuf send/receive buffers, and
+            # whole-row aggregates land in stores (the output layer's, the S rows' of the
+            # re-fetched h1, the reverse exchange's input-layer gradient)
+            stores = L * max(self.hid, self.d0) * 4 + self.nS * self.hid * 4 + \
+                (L * self.hid * 4 if self.nl == 3 else 0)
+            for cw, nb in STREAM_SHAPES:
+                if self.hid % cw:
+                    continue
+                ring = nb * (H + n_send) * cw * 4
+                hb = 4 * H * self.d0 + ring + stores
+                if dev.type != "cuda" or need_h + hb + other + (1 << 28) <= free:
+                    self.stream, self.cw, self.nbuf, self.halo_bytes = True, cw, nb, hb
+                    break
         need_h += self.halo_bytes
         if dev.type == "cuda" and need_h + other + (1 << 28) > free:
             # fail here, before any allocation (and after every collective of the setup), so a
@@ -333,8 +358,8 @@ class FusedSAGE:
         self.use_store = self._plan_store()
         self.agg_full = None
         need_full = (L - self.Li) * wA * 4
-        if graph.send_map is not None and OVERLAP_FWD and self.Li < L and \
-                self.use_store["out"] and free - need_h - other - need_full > margin:
+        if graph.send_map is not None and OVERLAP_FWD and self.Li < L and not self.stream \
+                and self.use_store["out"] and free - need_h - other - need_full > margin:
             self.agg_full = torch.empty(L - self.Li, wA, dtype=torch.float32, device=dev)
             other += need_full
         # layer 0's input aggregate kept from the forward for the backward (else recomputed)
@@ -377,9 +402,17 @@ class FusedSAGE:
         # buffer per hidden layer (the last one is the reverse exchange's send after the
         # output layer's forward); the memory plan above counted exactly these
         self.send_buf, self.halo_buf = None, []
-        if graph.send_map is not None:
+        self.ring_send, self.ring_recv = [], []
+        self.aS_full = self.gz_full = None
+        if graph.send_map is not None and not self.stream:
             self.send_buf = torch.empty(n_send, self.hid, **f)
             self.halo_buf = [torch.empty(H, self.hid, **f) for _ in range(self.nl - 1)]
+        elif self.stream:
+            self.ring_send = [torch.empty(n_send, self.cw, **f) for _ in range(self.nbuf)]
+            self.ring_recv = [torch.empty(H, self.cw, **f) for _ in range(self.nbuf)]
+            self.agg_full = torch.empty(L, max(self.hid, self.d0), **f)
+            self.aS_full = torch.empty(self.nS, self.hid, **f)
+            self.gz_full = torch.empty(L, self.hid, **f) if self.nl == 3 else None
         if self.store_sep:
             self.dZ = torch.empty(self.nS, self.hid, **f)
             self.u = torch.empty(self.nS, self.hid, **f) if self.nl == 3 else None
@@ -472,6 +505,8 @@ class FusedSAGE:
         return {"interior_rows": self.Li, "boundary_rows": self.L - self.Li,
                 "chunk_rows": self.cr, "output_layer_store": self.agg_full is not None,
                 "boundary_store": dict(self.use_store),
+                "halo_stream": ({"column_block": self.cw, "buffers": self.nbuf}
+                                if self.stream else False),
                 "keep_agg0": self.agg0 is not None}
 
     # ------------------------------------------------------------------ helpers
@@ -628,6 +663,88 @@ class FusedSAGE:
             consume(ci, a)
         return recv
 
+    def _on_comm_stream(self, fn):
+        """Run ``fn()`` (a pack + an asynchronous exchange) on the communication stream,
+        behind the compute stream's work so far (CPU: inline)."""
+        if self.dev.type != "cuda":
+            return fn()
+        from ..comm.alltoallv import _side_stream
+
+        side = _side_stream(self.dev)
+        side.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(side):
+            return fn()
+
+    def _stream_fwd(self, h: torch.Tensor, out: torch.Tensor, name: str,
+                    rows: Optional[torch.Tensor] = None) -> None:
+        """Streamed halo: ``out[:, c] = mean over in-neighbours of h[:, c]`` for every row
+        (or for the adjacency rows ``rows``, output row i <- rows[i]), with h's halo rows
+        exchanged in column blocks of ``cw`` through the buffer ring — block k+1 is on the
+        links while block k is aggregated (two-source: local and received rows in one
+        pass). A block's buffers are reused only after the compute stream consumed them
+        (the comm stream waits for it before every pack)."""
+        g, L, cw, nb = self.g, self.L, self.cw, self.nbuf
+        blocks = _ranges(0, h.shape[1], cw)
+
+        def issue(k):
+            c0, c1 = blocks[k]
+            b = k % nb
+
+            def go():
+                K.copy_rows(h[:, c0:c1], src_idx=g.send_map.idx, out=self.ring_send[b])
+                return g.a2a(self.ring_send[b], out=self.ring_recv[b], async_op=True)
+            return self._on_comm_stream(go)
+
+        works = {0: issue(0)}
+        for k, (c0, c1) in enumerate(blocks):
+            if nb > 1 and k + 1 < len(blocks):
+                works[k + 1] = issue(k + 1)
+            recv, work = works.pop(k)
+            self._mark(f"exchange_{name}")
+            work.wait()
+            self._mark(name)
+            if rows is None:
+                self._spmm(self.adj.rp, self.adj.col, h[:, c0:c1], out[:, c0:c1], x2=recv,
+                           nsplit=L, row_scale=self.inv_deg, pass_cols=c1 - c0)
+            else:
+                self._spmm(self.adj.rp, self.adj.col, h[:, c0:c1], out[:, c0:c1],
+                           row_ids=rows, x2=recv, nsplit=L, row_scale=self.invdegS,
+                           pass_cols=c1 - c0)
+            if nb == 1 and k + 1 < len(blocks):
+                works[k + 1] = issue(k + 1)
+
+    def _stream_rev(self, u: torch.Tensor, gz: torch.Tensor, gate: torch.Tensor,
+                    name: str) -> None:
+        """Streamed reverse exchange of B1b: for every column block, the halo rows'
+        contributions ``A_halo^T u`` (column-mapped onto S) are sent to their owners and
+        summed into ``gz`` (zeroed first; the ReLU gate of layer 0 applied), block k+1's
+        contributions computed while block k is on the links."""
+        g, cw, nb = self.g, self.cw, self.nbuf
+        blocks = _ranges(0, u.shape[1], cw)
+        gz.zero_()
+        st = self.send_st
+
+        def issue(k):
+            c0, c1 = blocks[k]
+            b = k % nb
+            hg = self.ring_recv[b]
+            self._spmm(self.haloT.rowptr, self.haloT.col, u[:, c0:c1], hg, col_map=self.smap)
+            return self._on_comm_stream(
+                lambda: g.a2a_rev(hg, out=self.ring_send[b], async_op=True))
+
+        works = {0: issue(0)}
+        for k, (c0, c1) in enumerate(blocks):
+            if nb > 1 and k + 1 < len(blocks):
+                works[k + 1] = issue(k + 1)
+            sg, work = works.pop(k)
+            self._mark(f"exchange_{name}")
+            work.wait()
+            self._mark(name)
+            self._spmm(st.rowptr, st.col, sg, gz[:, c0:c1], beta=1.0, row_map=st.row_map,
+                       gate=gate[:, c0:c1])
+            if nb == 1 and k + 1 < len(blocks):
+                works[k + 1] = issue(k + 1)
+
     def _params(self):
         out = []
         for l in self.model.layers:
@@ -668,16 +785,25 @@ class FusedSAGE:
                 r0, r1 = self.chunks[ci]
                 self._gemm(hin[r0:r1], ws, a, wn, bias=bias, relu=True, out=hout[r0:r1])
 
-            # layer l >= 1 can store boundary-row aggregates in its own output buffer
-            store = hout[self.Li:] if (l > 0 and hin.shape[1] == hout.shape[1] and
-                                       self.use_store["hidden"]) else None
-            keep = self.agg0 if l == 0 else None
-            halos.append(self._layer(hin, hin_halo, consume, hin.shape[1], f"fwd_l{l}",
-                                     store=store, keep=keep))
+            if self.stream and l > 0:
+                # streamed halo: every row's aggregate into the layer's own output buffer
+                # (column block by column block), then the GEMMs in place, chunk by chunk
+                self._stream_fwd(hin, hout, f"fwd_l{l}")
+                for ci, (r0, r1) in enumerate(self.chunks):
+                    if r1 > r0:
+                        consume(ci, hout[r0:r1])
+                halos.append(None)
+            else:
+                # layer l >= 1 can store boundary-row aggregates in its own output buffer
+                store = hout[self.Li:] if (l > 0 and hin.shape[1] == hout.shape[1] and
+                                           self.use_store["hidden"]) else None
+                keep = self.agg0 if l == 0 else None
+                halos.append(self._layer(hin, hin_halo, consume, hin.shape[1], f"fwd_l{l}",
+                                         store=store, keep=keep))
             self.edges_aggregated += nnz
             hin = hout
             # this layer's halo rows leave now and land while the next layer works
-            hin_halo = self._exchange(hout, l)
+            hin_halo = None if self.stream else self._exchange(hout, l)
             self._mark(f"fwd_l{l + 1}" if l + 1 < nl - 1 else "fwd_out")
         # ---------------- forward: output layer (all rows), loss and eval on the fly
         ws, wn, b = P[nl - 1]
@@ -690,10 +816,17 @@ class FusedSAGE:
         self.acc_out_s.reset()
         self.acc_out_n.reset()
         hl = hin
-        hl_halo = self._layer(hl, hin_halo, lambda ci, a: self._out_chunk(ci, a, hl, wsp,
-                                                                          wnp, bp),
-                              hid, "fwd_out",
-                              store=self.agg_full if self.use_store["out"] else None)
+        if self.stream:
+            self._stream_fwd(hl, self.agg_full, "fwd_out")
+            for ci, (r0, r1) in enumerate(self.chunks):
+                if r1 > r0:
+                    self._out_chunk(ci, self.agg_full[r0:r1, :hid], hl, wsp, wnp, bp)
+            hl_halo = None
+        else:
+            hl_halo = self._layer(hl, hin_halo, lambda ci, a: self._out_chunk(ci, a, hl, wsp,
+                                                                              wnp, bp),
+                                  hid, "fwd_out",
+                                  store=self.agg_full if self.use_store["out"] else None)
         halos.append(hl_halo)
         self.edges_aggregated += nnz
         # per-row losses / hits summed once, in a fixed order
@@ -773,7 +906,11 @@ class FusedSAGE:
             # the interior rows of layer 0 below
             u = self._gemm(dZ, wn1.detach().t().contiguous(), row_scale=self.invdegS,
                            out=self.u)
-            if self.haloT is not None:
+            if self.haloT is not None and self.stream:
+                # streamed reverse exchange into the input-layer gradient store
+                self._stream_rev(u, self.gz_full, self.h[0], f"bwd_l{lh}")
+                self.edges_aggregated += self.haloT.nnz
+            elif self.haloT is not None:
                 # the output layer's received halo rows are dead: its buffer sends, the
                 # forward send buffer receives
                 hg1 = self._spmm(self.haloT.rowptr, self.haloT.col, u, self.halo_buf[-1],
@@ -783,14 +920,21 @@ class FusedSAGE:
         self.acc_hid_s.reset()
         self.acc_hid_n.reset()
         halo_l = hin_l_halo if self.adj.mid is not None else None
+        streamed = self.stream and lh > 0
+        if streamed:
+            # the S rows' aggregate of h1, its halo rows re-fetched in column blocks
+            self._stream_fwd(hin_l, self.aS_full, f"bwd_l{lh}", rows=self.S)
         for s0, s1 in self.s_chunks:
             if s1 <= s0:
                 continue
             rows = self.S[s0:s1]
-            aS = self.bufA[:s1 - s0, :hin_l.shape[1]]
-            kw = dict(x2=halo_l, nsplit=self.L) if halo_l is not None else {}
-            self._spmm(self.adj.rp, self.adj.col, hin_l, aS, row_ids=rows,
-                       row_scale=self.invdegS[s0:s1], **kw)
+            if streamed:
+                aS = self.aS_full[s0:s1]
+            else:
+                aS = self.bufA[:s1 - s0, :hin_l.shape[1]]
+                kw = dict(x2=halo_l, nsplit=self.L) if halo_l is not None else {}
+                self._spmm(self.adj.rp, self.adj.col, hin_l, aS, row_ids=rows,
+                           row_scale=self.invdegS[s0:s1], **kw)
             self.acc_hid_s.add(hin_l, dZ[s0:s1], a1_rows=rows)
             self.acc_hid_n.add(aS, dZ[s0:s1])
         self.edges_aggregated += self.nnz_S
@@ -852,7 +996,9 @@ class FusedSAGE:
                 rp, re = self.adj.rows(r0, r1, "int")
                 self._spmm(rp, self.adj.col, u, gz, rowend=re, col_map=self.smap, **sa)
             sr = self.ch_send[ci]
-            if sg1 is not None and sr is not None:
+            if self.gz_full is not None:  # streamed reverse exchange: gated, summed
+                gz.add_(self.gz_full[r0:r1])
+            elif sg1 is not None and sr is not None:
                 rp_s, rmap, _ = sr
                 self._spmm(rp_s, self.send_st.col, sg1, gz, beta=1.0, row_map=rmap,
                            gate=h1[r0:r1])

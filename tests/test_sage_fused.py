@@ -156,7 +156,7 @@ def test_fused_directed_graph_matches_autograd():
         torch.testing.assert_close(a, b, atol=2e-5, rtol=1e-4)
 
 
-def _interior_first_body(rank, world, ref_path, overlap, store="auto"):
+def _interior_first_body(rank, world, ref_path, overlap, store="auto", stream="off"):
     """One rank of a W-way partition renumbered interior-first (parallel/reorder.py), the
     fused executor's interior-then-boundary schedule, all-reduced against W=1."""
     import dgraph_amd.models.sage_fused as sf
@@ -164,6 +164,9 @@ def _interior_first_body(rank, world, ref_path, overlap, store="auto"):
 
     sf.OVERLAP_FWD = overlap
     sf.BOUNDARY_STORE = store
+    sf.HALO_STREAM = "on" if stream != "off" else "off"
+    if stream == "single":  # one ring buffer: exchange and aggregation alternate
+        sf.STREAM_SHAPES = ((64, 1),)
     shape = SHAPES["ogbn-papers100M"].scaled(SCALE)
     part = build_partition(shape, rank, world, "cpu", global_frac=0.05, window=64)
     csr, send, perm, L_int, loc = interior_first(part["csr"], part["L"],
@@ -185,6 +188,9 @@ def _interior_first_body(rank, world, ref_path, overlap, store="auto"):
     assert ex.Li == L_int and ex.nA >= 1
     if store != "auto":
         assert ex.use_store == {"hidden": store == "on", "out": store == "on"}
+    assert ex.stream == (stream != "off")
+    if stream == "single":
+        assert ex.nbuf == 1
     assert g.interior is None  # released: the executor runs on its own adjacency
     loss = ex.step()
     grads = [p.grad.clone() for p in model.parameters()]
@@ -200,14 +206,16 @@ def _interior_first_body(rank, world, ref_path, overlap, store="auto"):
     assert torch.equal(corr, ref["corr"])
 
 
-@pytest.mark.parametrize("world,overlap,store", [(2, True, "on"), (2, True, "off"),
-                                                (4, True, "on"), (4, True, "off"),
-                                                (2, False, "auto")])
-def test_fused_interior_first_matches_w1(ranks, world, overlap, store, tmp_path):
+@pytest.mark.parametrize("world,overlap,store,stream", [
+    (2, True, "on", "off"), (2, True, "off", "off"), (4, True, "on", "off"),
+    (4, True, "off", "off"), (2, False, "auto", "off"),
+    # streamed halos (column blocks through a buffer ring; the structureless-graph plan)
+    (2, True, "auto", "on"), (4, True, "auto", "on"), (2, True, "auto", "single")])
+def test_fused_interior_first_matches_w1(ranks, world, overlap, store, stream, tmp_path):
     loss, grads, corr = _fused_grads(0, 1, gf=0.05)
     p = tmp_path / "ref.pt"
     torch.save({"loss": loss, "grads": grads, "corr": corr}, p)
-    ranks(_interior_first_body, world, str(p), overlap, store)
+    ranks(_interior_first_body, world, str(p), overlap, store, stream)
 
 
 @pytest.mark.parametrize("hidden,feat", [(128, 100), (512, 128), (256, 300)])
