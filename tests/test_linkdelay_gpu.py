@@ -49,7 +49,7 @@ def test_delayed_loopback_is_pending_then_lands(monkeypatch):
     assert torch.equal(out, send)
 
 
-def _rehearsal_step(gbps, steps=2):
+def _rehearsal_step(gbps, steps=2, stream="off"):
     """Rank 0 of a 2-way partition of a scaled papers100M graph, alone (loopback exchange),
     interior-first, on the fused fp32 executor: losses and the last step's gradients."""
     from dgraph_amd.data.synthetic import (SHAPES, SPLIT_TEST, SPLIT_TRAIN, SPLIT_VALID,
@@ -59,7 +59,10 @@ def _rehearsal_step(gbps, steps=2):
     from dgraph_amd.parallel.dist_graph import DistGraph
     from dgraph_amd.parallel.reorder import interior_first
 
+    import dgraph_amd.models.sage_fused as sf
+
     A.LOOPBACK_LINK_GBPS = gbps
+    sf.HALO_STREAM = stream
     try:
         shape = SHAPES["ogbn-papers100M"].scaled(2e-4)
         part = build_partition(shape, 0, 2, DEV, global_frac=0.05, window=256, rehearse=True)
@@ -78,7 +81,7 @@ def _rehearsal_step(gbps, steps=2):
         model = GraphSAGE(shape.num_features, 256, shape.num_classes, 3).to(DEV)
         ex = FusedSAGE(model, g, x, tr, y[tr], ev, y[ev], split[ev] == SPLIT_VALID,
                        tr.numel(), chunk_rows=512, release_graph=True)
-        assert ex.nA >= 1
+        assert ex.nA >= 1 and ex.stream == (stream == "on")
         losses = []
         for _ in range(steps):
             ex.record = True
@@ -92,11 +95,14 @@ def _rehearsal_step(gbps, steps=2):
         return torch.stack(losses), grads, ex.correct.clone(), reg
     finally:
         A.LOOPBACK_LINK_GBPS = 0.0
+        sf.HALO_STREAM = "auto"
 
 
-def test_rehearsal_delayed_equals_instant_bitwise():
-    l0, g0, c0, r0 = _rehearsal_step(0.0)
-    l1, g1, c1, r1 = _rehearsal_step(0.5)  # a 0.5 GB/s "link": every exchange is long
+@pytest.mark.parametrize("stream", ["off", "on"])
+def test_rehearsal_delayed_equals_instant_bitwise(stream):
+    l0, g0, c0, r0 = _rehearsal_step(0.0, stream=stream)
+    # a 0.5 GB/s "link": every exchange (or column block of one) is long
+    l1, g1, c1, r1 = _rehearsal_step(0.5, stream=stream)
     assert torch.equal(l0, l1)
     for a, b in zip(g0, g1):
         assert torch.equal(a, b)
