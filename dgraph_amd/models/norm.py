@@ -91,6 +91,96 @@ def _vec(p: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
     return None if p is None else p.reshape(-1).float().contiguous()
 
 
+class BNState:
+    """What the backward (and a recompute of the output) of one ``act(BN(x))`` needs: the
+    global statistics, the affine parameters and the dropout seed — never the output."""
+
+    __slots__ = ("mean", "rstd", "g", "b", "N", "relu", "p", "seed", "native", "group",
+                 "gshape", "gdtype")
+
+
+def bn_act_forward(x: torch.Tensor, gamma, beta, eps: float, group, relu: bool = False,
+                   drop_p: float = 0.0):
+    """``y = dropout(act(BN(x)))`` with global statistics -> ``(y, state, var)``.
+
+    GPU (fp32/bf16 [N, F]): native kernels (csrc/kernels/batchnorm.hip) — one pass for the
+    statistics and one fused normalise/affine/ReLU/dropout pass. The dropout keep mask is a
+    function of (seed, element index) that :func:`bn_act_backward` and
+    :func:`bn_act_recompute` regenerate."""
+    st = BNState()
+    N, mean, var = global_moments(x, group)
+    st.seed = int(torch.randint(0, 1 << 62, (1,), dtype=torch.int64).item()) \
+        if drop_p > 0 else 0
+    st.p = float(drop_p)
+    st.N, st.relu, st.group = N, relu, group
+    st.mean, st.rstd = mean, torch.rsqrt(var + eps)
+    st.gshape = None if gamma is None else gamma.shape
+    st.gdtype = None if gamma is None else gamma.dtype
+    st.g, st.b = _vec(gamma), _vec(beta)
+    st.native = _native_ok(x)
+    return bn_act_recompute(st, x), st, var
+
+
+def bn_act_recompute(st: BNState, x: torch.Tensor) -> torch.Tensor:
+    """The forward output again, bit for bit, from the saved input and state."""
+    if st.native:
+        return _ops().bn_apply(x, None, st.mean, st.rstd, st.g, st.b, None, None, st.relu, 0,
+                               st.p, st.seed)
+    y = (x.to(st.mean.dtype) - st.mean) * st.rstd
+    if st.g is not None:
+        y = y * st.g.to(st.mean.dtype) + st.b.to(st.mean.dtype)
+    if st.relu:
+        y = torch.relu(y)
+    if st.p > 0:
+        y = y * dropout_keep_mask(st.seed, *x.shape, x.device, st.p).to(y.dtype) / \
+            (1.0 - st.p)
+    return y.to(x.dtype)
+
+
+def bn_act_backward(st: BNState, x: torch.Tensor, dy: torch.Tensor, xhat=None):
+    """``(dx, dgamma, dbeta)`` of :func:`bn_act_forward` (``dgamma``/``dbeta`` rank-local;
+    ``xhat``: the saved normalised input when the reference path did not recompute)."""
+    mean, rstd, g, b = st.mean, st.rstd, st.g, st.b
+    F = mean.numel()
+    Nf = max(st.N, 1.0)
+    p, seed = st.p, st.seed
+    if st.native:
+        dy = dy.to(x.dtype)
+        if dy.stride(1) != 1 or dy.shape != x.shape:
+            dy = dy.contiguous()
+        s = _ops().bn_reduce(x, dy, mean, rstd, g, b, st.relu, 1, p, seed).float()
+        sum_dy, sum_dy_xhat = s[0], s[1]
+    else:
+        if xhat is None:
+            xhat = (x.to(mean.dtype) - mean) * rstd
+        dyf = dy.to(mean.dtype)
+        if p > 0:
+            dyf = dyf * dropout_keep_mask(seed, *dyf.shape, dyf.device, p).to(dyf.dtype) / \
+                (1.0 - p)
+        if st.relu:
+            pre = xhat * g.to(mean.dtype) + b.to(mean.dtype) if g is not None else xhat
+            dyf = dyf * (pre > 0)
+        sum_dy = dyf.sum(0)
+        sum_dy_xhat = (dyf * xhat).sum(0)
+    dgamma = dbeta = None
+    if st.gshape is not None:
+        dgamma = sum_dy_xhat.reshape(st.gshape).to(st.gdtype)
+        dbeta = sum_dy.reshape(st.gshape).to(st.gdtype)
+    glob = torch.cat([sum_dy, sum_dy_xhat])
+    if _world(st.group) > 1:
+        dist.all_reduce(glob, group=st.group)
+    m_dy, m_dyx = glob[:F] / Nf, glob[F:] / Nf
+    if st.native:
+        dx = _ops().bn_apply(x, dy, mean, rstd, g, b, m_dy.contiguous(), m_dyx.contiguous(),
+                             st.relu, 1, p, seed)
+    else:
+        dx = (dyf - m_dy - xhat * m_dyx) * rstd
+        if g is not None:
+            dx = dx * g.to(mean.dtype)
+        dx = dx.to(dy.dtype)
+    return dx, dgamma, dbeta
+
+
 class _SyncBNFn(Function):
     """``y = act(BN(x))`` with global statistics; ``act`` is ReLU when ``relu``.
 
@@ -102,78 +192,24 @@ class _SyncBNFn(Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, eps: float, group, recompute: bool, box: list,
                 relu: bool = False, drop_p: float = 0.0):
-        N, mean, var = global_moments(x, group)
-        # dropout fused after the activation: the keep mask is a function of (seed, element
-        # index) that the backward regenerates (native kernels and reference alike)
-        seed = int(torch.randint(0, 1 << 62, (1,), dtype=torch.int64).item()) \
-            if drop_p > 0 else 0
-        ctx.drop = (float(drop_p), seed)
-        box.append(N)
-        rstd = torch.rsqrt(var + eps)
-        ctx.group, ctx.N, ctx.relu = group, N, relu
-        ctx.has_affine = gamma is not None
-        ctx.gshape = None if gamma is None else gamma.shape
-        ctx.gdtype = None if gamma is None else gamma.dtype
-        ctx.native = _native_ok(x)
-        g, b = _vec(gamma), _vec(beta)
-        if ctx.native:
-            y = _ops().bn_apply(x, None, mean, rstd, g, b, None, None, relu, 0, float(drop_p),
-                                seed)
-            ctx.save_for_backward(x, mean, rstd, g, b)
-            return y, mean, var
-        ctx.recompute = recompute
-        xhat = (x.to(mean.dtype) - mean) * rstd
-        y = xhat
-        if gamma is not None:
-            y = y * g.to(mean.dtype) + b.to(mean.dtype)
-        if relu:
-            y = torch.relu(y)
-        if drop_p > 0:
-            y = y * dropout_keep_mask(seed, *x.shape, x.device, drop_p).to(y.dtype) / \
-                (1.0 - drop_p)
-        ctx.save_for_backward(x if recompute else xhat, mean, rstd, g, b)
-        return y.to(x.dtype), mean, var
+        y, st, var = bn_act_forward(x, gamma, beta, eps, group, relu, drop_p)
+        box.append(st.N)
+        ctx.st = st
+        ctx.keep_xhat = not st.native and not recompute
+        if ctx.keep_xhat:
+            ctx.save_for_backward((x.to(st.mean.dtype) - st.mean) * st.rstd)
+            ctx.xdtype = x.dtype
+        else:
+            ctx.save_for_backward(x)
+        return y, st.mean, var
 
     @staticmethod
     def backward(ctx, dy, _dm, _dv):
-        saved, mean, rstd, g, b = ctx.saved_tensors
-        F = mean.numel()
-        Nf = max(ctx.N, 1.0)
-        p, seed = ctx.drop
-        if ctx.native:
-            x = saved
-            dy = dy.to(x.dtype)
-            if dy.stride(1) != 1 or dy.shape != x.shape:
-                dy = dy.contiguous()
-            s = _ops().bn_reduce(x, dy, mean, rstd, g, b, ctx.relu, 1, p, seed).float()
-            sum_dy, sum_dy_xhat = s[0], s[1]
+        (saved,) = ctx.saved_tensors
+        if ctx.keep_xhat:
+            dx, dgamma, dbeta = bn_act_backward(ctx.st, saved, dy, xhat=saved)
         else:
-            xhat = (saved.to(mean.dtype) - mean) * rstd if ctx.recompute else saved
-            dyf = dy.to(mean.dtype)
-            if p > 0:
-                dyf = dyf * dropout_keep_mask(seed, *dyf.shape, dyf.device, p).to(dyf.dtype) / \
-                    (1.0 - p)
-            if ctx.relu:
-                pre = xhat * g.to(mean.dtype) + b.to(mean.dtype) if g is not None else xhat
-                dyf = dyf * (pre > 0)
-            sum_dy = dyf.sum(0)
-            sum_dy_xhat = (dyf * xhat).sum(0)
-        dgamma = dbeta = None
-        if ctx.has_affine:
-            dgamma = sum_dy_xhat.reshape(ctx.gshape).to(ctx.gdtype)
-            dbeta = sum_dy.reshape(ctx.gshape).to(ctx.gdtype)
-        glob = torch.cat([sum_dy, sum_dy_xhat])
-        if _world(ctx.group) > 1:
-            dist.all_reduce(glob, group=ctx.group)
-        m_dy, m_dyx = glob[:F] / Nf, glob[F:] / Nf
-        if ctx.native:
-            dx = _ops().bn_apply(saved, dy, mean, rstd, g, b, m_dy.contiguous(),
-                                 m_dyx.contiguous(), ctx.relu, 1, p, seed)
-        else:
-            dx = (dyf - m_dy - xhat * m_dyx) * rstd
-            if g is not None:
-                dx = dx * g.to(mean.dtype)
-            dx = dx.to(dy.dtype)
+            dx, dgamma, dbeta = bn_act_backward(ctx.st, saved, dy)
         return dx, dgamma, dbeta, None, None, None, None, None, None
 
 
@@ -222,6 +258,15 @@ class DistributedBatchNorm1D(nn.Module):
         self.recompute = recompute
         self.group = group
 
+    def _update_running(self, n: float, mean: torch.Tensor, var: torch.Tensor) -> None:
+        if not self.track_running_stats:
+            return
+        with torch.no_grad():
+            self.num_batches_tracked += 1
+            unbiased = var * (n / max(n - 1.0, 1.0))
+            self.running_mean.mul_(1 - self.momentum).add_(self.momentum * mean)
+            self.running_var.mul_(1 - self.momentum).add_(self.momentum * unbiased)
+
     def forward(self, x: torch.Tensor, relu: bool = False, dropout: float = 0.0) -> torch.Tensor:
         """``BN(x)``, or ``relu(BN(x))`` fused into the same kernels when ``relu``; in
         training, ``dropout`` > 0 applies dropout after the activation in the same pass
@@ -238,13 +283,8 @@ class DistributedBatchNorm1D(nn.Module):
             y, mean, var = _SyncBNFn.apply(x, self.gamma, self.beta, self.eps, self.group,
                                            self.recompute, box, relu,
                                            float(dropout) if self.training else 0.0)
-            if self.training and self.track_running_stats:
-                with torch.no_grad():
-                    self.num_batches_tracked += 1
-                    n = box[0]
-                    unbiased = var * (n / max(n - 1.0, 1.0))
-                    self.running_mean.mul_(1 - self.momentum).add_(self.momentum * mean)
-                    self.running_var.mul_(1 - self.momentum).add_(self.momentum * unbiased)
+            if self.training:
+                self._update_running(box[0], mean, var)
         else:
             y = (x.to(_cdt(x)) - self.running_mean) * torch.rsqrt(self.running_var + self.eps)
             if self.gamma is not None:

@@ -8,9 +8,13 @@ type — so it plugs into the same trainer:
 
     h_d^{l+1} = dropout(relu(BN( skip_l(h_d^l) + sum_{r: s->d} mean_{j in N_r(i)} h_s^l[j] W_r^l )))
 
-Two execution paths:
+Execution paths:
 
-* :class:`HeteroGraph` (``dgraph_amd.parallel.hetero_graph``; built by
+* :class:`HeteroGraph`, fp32 (the reference's precision) — :meth:`_forward_hetero_lean`:
+  transform-first at every layer, BN'd activations recomputed in backward instead of saved,
+  relation aggregations added in place into the destinations' pre-activations, GEMMs on the
+  exact-f32 MFMA kernels; fits rank 1 of the 8-way MAG240M partition on one GPU.
+* :class:`HeteroGraph`, bf16 autocast (``dgraph_amd.parallel.hetero_graph``; built by
   ``dgraph_amd.data.mag.build_hetero_partition``) — the MI355X hot path. Layer 0 is
   transform-first: ONE GEMM per source type ``X_s [W_r1 | W_r2 ...]`` on the local rows
   and on the halo feature rows fetched once (one-sided heap get, or one all-to-all-v), then
@@ -30,10 +34,11 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops.act_linear import act_linears
 from ..ops.aggregate import aggregate
 from ..ops.dense import linear as _dense_linear
 from ..ops.dense import linear_sum
-from ..parallel.hetero_graph import SourceGraph, source_aggregate
+from ..parallel.hetero_graph import SourceGraph, source_aggregate, source_aggregate_into
 from .norm import DistributedBatchNorm1D
 
 
@@ -82,6 +87,7 @@ class CommAwareRGCN(nn.Module):
         self.edge_types = list(edge_types) if edge_types is not None else None
         self.target = target_type
         self.num_node_types = num_node_types
+        self.lean: Optional[bool] = None  # None: by the compute dtype (see forward)
         self.convs = nn.ModuleList()
         self.skips = nn.ModuleList()
         for i in range(num_layers):
@@ -118,8 +124,17 @@ class CommAwareRGCN(nn.Module):
 
     def forward(self, xs, graph, edge_types=None) -> torch.Tensor:
         """``forward(xs, HeteroGraph)`` (hot path), or the RelationGraph path with either
-        argument order: ``(xs, graphs, edge_types)`` or RGAT's ``(xs, edge_types, graphs)``."""
+        argument order: ``(xs, graphs, edge_types)`` or RGAT's ``(xs, edge_types, graphs)``.
+
+        HeteroGraph inputs computed in fp32 (the reference's precision) take the
+        memory-lean path (:meth:`_forward_hetero_lean`); under bf16 autocast the
+        aggregate-first path with the bf16 MFMA dual GEMM (:meth:`_forward_hetero`)."""
         if isinstance(graph, HeteroGraph):
+            x0 = next(iter(xs.values()))
+            lean = self.lean if self.lean is not None else (
+                x0.dtype == torch.float32 and not (torch.is_autocast_enabled() and x0.is_cuda))
+            if lean:
+                return self._forward_hetero_lean(xs, graph)
             return self._forward_hetero(xs, graph)
         if edge_types is not None and len(graph) and isinstance(graph[0], tuple):
             graph, edge_types = edge_types, graph
@@ -164,6 +179,62 @@ class CommAwareRGCN(nn.Module):
                 tmp[t] = linear_sum(tl, self.skips[l].bias)
             h = {t: self._finish(l, v) for t, v in tmp.items()}
         return self._head(h[self.target])
+
+    def _forward_hetero_lean(self, xs: Dict[int, torch.Tensor], g: HeteroGraph) -> torch.Tensor:
+        """Transform-first at EVERY layer, BN'd activations recomputed instead of stored:
+
+            pre_t^l = skip_l(h_t) + sum_{r: s->t} mean_r(h_s W_r^l),  h = act(BN(pre^{l-1}))
+
+        per source type ONE :func:`~dgraph_amd.ops.act_linears` call builds ``act(BN(pre_s))``
+        transiently and runs the skip GEMM (straight into ``pre_s``, bias fused) and the
+        stacked relation GEMM ``[W_r1 | W_r2 ...]``; the relation aggregations then add into
+        the destinations' ``pre`` in place (one halo exchange per source type, of the
+        transformed rows). Saved per step: the inputs, one ``pre`` per (layer, type) and the
+        head's hidden pre-activation — no BN output, aggregate or relation output (the
+        aggregate-first path saves each of those: 274 GB at fp32 on one GPU's 1/8 MAG240M
+        share, profiles/r04/rgcn_fp32_eighth.json). Same math as :meth:`_forward_hetero`."""
+        ets = g.edge_types
+        avail = [r for s in g.sources.values() for r in s.ranges]
+        need, rels = layer_plan(ets, self.num_layers, self.target, avail)
+        C = self.hidden
+        pre: Dict[int, torch.Tensor] = {}
+        for l in range(self.num_layers):
+            by_src: Dict[int, List[int]] = {}
+            for r in rels[l]:
+                by_src.setdefault(ets[r][0], []).append(r)
+            new: Dict[int, torch.Tensor] = {}
+            zs = []
+            for s in sorted(set(need[l]) | set(by_src)):
+                rs = by_src.get(s, [])
+                Ws = [self.skips[l].weight] if s in need[l] else []
+                if rs:
+                    Ws.append(torch.cat([self.convs[l][r].weight for r in rs], 0)
+                              if len(rs) > 1 else self.convs[l][rs[0]].weight)
+                inp = xs[s] if l == 0 else pre[s]
+                bn = self.bns[l - 1] if l else None
+                outs = act_linears(inp, Ws, self.skips[l].bias if s in need[l] else None,
+                                   bn=bn, relu=l > 0, dropout=self.dropout if l else 0.0)
+                if s in need[l]:
+                    new[s] = outs[0]
+                if rs:
+                    zh = None
+                    if l == 0:  # read-only features: halo rows fetched once, transformed here
+                        xh = g.sources[s].static_halo(xs[s])
+                        zh = act_linears(xh, Ws[-1:])[0] if xh is not None else None
+                    zs.append((s, rs, outs[-1], zh))
+            for s, rs, z, zh in zs:
+                spec = [(r, i * C, (i + 1) * C) for i, r in enumerate(rs)]
+                res = source_aggregate_into(z, g.sources[s], spec,
+                                            [new[ets[r][1]] for r in rs], static_halo=zh)
+                for r, o in zip(rs, res):
+                    new[ets[r][1]] = o
+            pre = new
+        lin1, bn, _, drop, lin2 = self.mlp
+        t = self.target
+        p1 = act_linears(pre[t], [lin1.weight], lin1.bias, bn=self.bns[self.num_layers - 1],
+                         relu=True, dropout=self.dropout)[0]
+        return act_linears(p1, [lin2.weight], lin2.bias, bn=bn, relu=True,
+                           dropout=drop.p)[0]
 
     # ------------------------------------------------------------------ RelationGraph path
     def _forward_relations(self, xs: List[torch.Tensor], edge_types, graphs) -> torch.Tensor:

@@ -1,0 +1,157 @@
+"""``outs_i = act(x) W_i^T (+ b)`` with ``act`` = dropout(ReLU(BatchNorm(x))) recomputed in
+backward instead of stored (the fp32 R-GCN's memory-lean layer, ``models/rgcn.py``).
+
+A BN'd activation feeds exactly the GEMMs of the next layer (skip and relation transforms
+of one source type, or an MLP linear); only the pre-BN input is saved, the normalised
+activation is rebuilt for the weight gradients (one elementwise pass) — at MAG240M scale
+that drops one [rows, hidden] fp32 tensor per (layer, node type) from the saved set (15.6 GB
+each on one GPU's 1/8 share). The reference keeps both (experiments/OGB-LSC/RGAT.py:320-349
+runs BN, ReLU, dropout and the next layer's linears as separate autograd nodes;
+distributed_layers.py:77-214 saves ``x_hat`` unless recomputing).
+
+GPU fp32: the GEMMs run on the exact-f32 MFMA kernel (``ops.f32.gemm_f32``, bias fused),
+``dy = sum_i g_i W_i`` two terms per call with the running sum chained through ``cin``,
+and ``dW_i`` on the split-M MFMA weight-gradient accumulator (``ops.f32.WgradAcc``); widths
+the kernels do not tile (e.g. 153 classes) fall back to the library GEMM. Elsewhere
+(CPU, bf16): plain PyTorch math, the numerics oracle.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence
+
+import torch
+from torch.autograd import Function
+
+from . import f32 as F32
+from . import kernels as K
+
+
+def _f32_gpu(t: torch.Tensor) -> bool:
+    return t.is_cuda and t.dtype == torch.float32
+
+
+def _tileable(n: int) -> bool:
+    """Output widths the fp32 GEMM covers (one tile or 128/176/192/256 column blocks)."""
+    if F32.gemm_f32_ok(n, 32):
+        return True
+    try:
+        F32._blocks(n, lambda w: w in (128, 176, 192, 256))
+        return n > 256
+    except ValueError:
+        return False
+
+
+def _wgrad_ok(K: int, N: int) -> bool:
+    try:
+        F32._blocks(K, lambda w: w in (128, 256), (256, 128))
+        F32._blocks(N, F32._wgrad_n_ok)
+        return True
+    except ValueError:
+        return False
+
+
+def _gemm(y: torch.Tensor, W: torch.Tensor, b: Optional[torch.Tensor]) -> torch.Tensor:
+    """``y W^T + b`` (W: [N, K], torch Linear layout)."""
+    N, K = W.shape
+    if _f32_gpu(y) and K % 32 == 0 and _tileable(N) and y.stride(1) == 1:
+        return F32.gemm_f32(y, W.t().contiguous(), bias=b)
+    return torch.nn.functional.linear(y, W.to(y.dtype), None if b is None else b.to(y.dtype))
+
+
+def _dy(gs: Sequence[torch.Tensor], Ws: Sequence[torch.Tensor]) -> torch.Tensor:
+    """``sum_i g_i W_i`` (two terms per MFMA call, running sum chained through ``cin``)."""
+    K = Ws[0].shape[1]
+    if all(_f32_gpu(g) and g.shape[1] % 32 == 0 for g in gs) and _tileable(K):
+        out = None
+        for k in range(0, len(gs), 2):
+            two = k + 1 < len(gs)
+            out = F32.gemm_f32(gs[k], Ws[k].contiguous(), gs[k + 1] if two else None,
+                               Ws[k + 1].contiguous() if two else None, cin=out, out=out)
+        return out
+    out = gs[0] @ Ws[0].to(gs[0].dtype)
+    for g, W in zip(gs[1:], Ws[1:]):
+        out = out + g @ W.to(g.dtype)
+    return out
+
+
+def _wgrad(g: torch.Tensor, y: torch.Tensor, W: torch.Tensor) -> torch.Tensor:
+    """``g^T y`` in W's layout [N, K]."""
+    N, K = W.shape
+    if _f32_gpu(g) and _f32_gpu(y) and _wgrad_ok(K, N) and y.stride(1) == 1 \
+            and g.stride(1) == 1:
+        acc = F32.WgradAcc(K, N, g.device)
+        acc.add(y, g)
+        return acc.result().t().contiguous().to(W.dtype)
+    adt = torch.float64 if g.dtype == torch.float64 else torch.float32
+    return (g.t().to(adt) @ y.to(adt)).to(W.dtype)
+
+
+class _ActLinearsFn(Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, bias, bn, relu: bool, drop_p: float, *Ws):
+        st = None
+        if bn is not None:
+            from ..models.norm import bn_act_forward
+
+            y, st, var = bn_act_forward(x, gamma, beta, bn.eps, bn.group, relu, drop_p)
+            bn._update_running(st.N, st.mean, var)
+        else:
+            y = x
+        outs = [_gemm(y, W, bias if i == 0 else None) for i, W in enumerate(Ws)]
+        del y
+        ctx.st = st
+        ctx.has_bias = bias is not None
+        ctx.save_for_backward(x, *Ws)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *gs):
+        x, *Ws = ctx.saved_tensors
+        st = ctx.st
+        if st is not None:
+            from ..models.norm import bn_act_recompute
+
+            y = bn_act_recompute(st, x)
+        else:
+            y = x
+        live = any(g is not None for g in gs)
+        gs_c = [None if g is None else (g if g.stride(1) == 1 and g.is_contiguous()
+                                        else g.contiguous()) for g in gs]
+        dWs = []
+        for g, W in zip(gs_c, Ws):
+            dWs.append(None if g is None else _wgrad(g, y, W))
+        db = None
+        if ctx.has_bias and ctx.needs_input_grad[3] and gs_c[0] is not None:
+            g0 = gs_c[0]
+            db = (K.col_sum(g0) if g0.is_cuda else g0.sum(0)).to(Ws[0].dtype)
+        dx = dgamma = dbeta = None
+        need_x = ctx.needs_input_grad[0] or (st is not None and (ctx.needs_input_grad[1]
+                                                                 or ctx.needs_input_grad[2]))
+        if need_x and live:
+            dy = _dy([g for g, W in zip(gs_c, Ws) if g is not None],
+                     [W for g, W in zip(gs_c, Ws) if g is not None])
+            if st is not None:
+                from ..models.norm import bn_act_backward
+
+                del y
+                dx, dgamma, dbeta = bn_act_backward(st, x, dy)
+            else:
+                dx = dy
+        return (dx, dgamma, dbeta, db, None, None, None, *dWs)
+
+
+def act_linears(x: torch.Tensor, Ws: Sequence[torch.Tensor], bias=None, bn=None,
+                relu: bool = False, dropout: float = 0.0) -> List[torch.Tensor]:
+    """``[act(x) W_i^T (+ bias on the first)]`` with ``act`` = dropout(relu?(bn(x))) when
+    ``bn`` (a :class:`~dgraph_amd.models.norm.DistributedBatchNorm1D` in training mode) is
+    given, identity otherwise. Saves ``x`` only."""
+    if bn is not None and not bn.training:
+        x = bn(x, relu=relu)
+        bn = None
+    elif bn is None and (relu or dropout):
+        raise ValueError("act_linears: relu/dropout need a BatchNorm")
+    gamma = beta = None
+    if bn is not None:
+        gamma, beta = bn.gamma, bn.beta
+    return list(_ActLinearsFn.apply(x, gamma, beta, bias, bn, bool(relu),
+                                    float(dropout) if bn is not None else 0.0, *Ws))

@@ -159,18 +159,25 @@ class SourceGraph:
     # ------------------------------------------------------------------ forward / adjoint
     def forward_rels(self, z: torch.Tensor, z_halo: Optional[torch.Tensor],
                      spec: Sequence[Tuple[int, int, int]], mean: bool = True,
-                     exchange: bool = True) -> List[torch.Tensor]:
+                     exchange: bool = True,
+                     into: Optional[Sequence[torch.Tensor]] = None) -> List[torch.Tensor]:
         """``out_r = A_r[:, local] z[:, c0:c1] + A_r[:, halo] halo(z)[:, c0:c1]`` for every
         ``(r, c0, c1)`` in ``spec``. With ``exchange`` the halo rows of ``z`` are moved by
-        an all-to-all-v overlapped with the interior SpMMs; else ``z_halo`` is used."""
+        an all-to-all-v overlapped with the interior SpMMs; else ``z_halo`` is used.
+        ``into``: one existing tensor per spec entry that ``out_r`` is ADDED to (the
+        destination's skip term: no separate output and add pass)."""
         recv, work = z_halo, None
         if self.halo is not None and exchange:
             recv, work = self.a2a(K.gather_rows(z, self.send_map.idx), async_op=True)
             if not self.overlap:
                 work.wait()
         outs = []
-        for rid, c0, c1 in spec:
+        for i, (rid, c0, c1) in enumerate(spec):
             p = self.part("interior", rid)
+            if into is not None:
+                outs.append(K.spmm(p.rowptr, p.col, z[:, c0:c1], into[i],
+                                   row_scale=self.scale(rid) if mean else None, beta=1.0))
+                continue
             outs.append(K.spmm(p.rowptr, p.col, z[:, c0:c1],
                                row_scale=self.scale(rid) if mean else None))
         if self.halo is not None:
@@ -240,6 +247,49 @@ class _SourceAggFn(Function):
         gz, gz_halo = ctx.graph.backward_rels(grads, ctx.spec, ctx.width, ctx.dtype, ctx.mean,
                                               ctx.exchange)
         return gz, (gz_halo if ctx.has_halo else None), None, None, None, None
+
+
+class _SourceAggIntoFn(Function):
+    @staticmethod
+    def forward(ctx, z, z_halo, graph: SourceGraph, spec, mean: bool, exchange: bool,
+                slots, *targets):
+        ctx.graph, ctx.spec, ctx.mean, ctx.exchange = graph, spec, mean, exchange
+        ctx.width, ctx.dtype = z.shape[1], z.dtype
+        ctx.has_halo = z_halo is not None
+        ctx.slots = slots
+        graph.forward_rels(z, z_halo, spec, mean, exchange, into=[targets[i] for i in slots])
+        ctx.mark_dirty(*targets)
+        return targets
+
+    @staticmethod
+    def backward(ctx, *gts):
+        grads = [gts[i] for i in ctx.slots]
+        gz, gz_halo = ctx.graph.backward_rels(grads, ctx.spec, ctx.width, ctx.dtype, ctx.mean,
+                                              ctx.exchange)
+        return (gz, (gz_halo if ctx.has_halo else None), None, None, None, None, None, *gts)
+
+
+def source_aggregate_into(z: torch.Tensor, graph: SourceGraph,
+                          spec: Sequence[Tuple[int, int, int]],
+                          targets: Sequence[torch.Tensor], mean: bool = True,
+                          static_halo: Optional[torch.Tensor] = None) -> List[torch.Tensor]:
+    """:func:`source_aggregate` whose per-relation results are ADDED in place to
+    ``targets`` (one per spec entry; the same tensor may appear more than once). Returns
+    the updated targets in spec order (autograd: the targets' gradients pass through)."""
+    uniq: List[torch.Tensor] = []
+    slots = []
+    for t in targets:
+        for j, u in enumerate(uniq):
+            if u is t:
+                slots.append(j)
+                break
+        else:
+            slots.append(len(uniq))
+            uniq.append(t)
+    exchange = static_halo is None
+    outs = _SourceAggIntoFn.apply(z.contiguous() if z.stride(1) != 1 else z, static_halo,
+                                  graph, tuple(spec), mean, exchange, tuple(slots), *uniq)
+    return [outs[j] for j in slots]
 
 
 def source_aggregate(z: torch.Tensor, graph: SourceGraph,

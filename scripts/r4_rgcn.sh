@@ -1,0 +1,22 @@
+#!/usr/bin/env bash
+# fp32 R-GCN (lean path): GPU tests, 1/8-scale step, W=8 rank-1 rehearsal, kernel stats
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+cd "$R" && mkdir -p gpurun_out/rgcn
+O=gpurun_out/rgcn
+fatal() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
+step() {
+  local name=$1 t=$2; shift 2
+  timeout -k 10 "$t" "$@" > "$O/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"; grep -E '^\{|passed|failed|Error' "$O/$name.log" | cut -c1-900
+  if fatal $rc; then echo "FATAL at $name"; exit $rc; fi
+}
+step tests 300 python -u -m pytest tests/test_rgcn.py -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider
+step eighth 500 python -u benchmarks/bench_rgcn.py --scale 0.125 --steps 3 --warmup 1
+step w8r1 600 python -u benchmarks/bench_rgcn.py --rehearse-world 8 --rehearse-rank 1 --steps 3 --warmup 1
+if [ "${PROF:-1}" = 1 ]; then
+  cd /tmp && export TMPDIR=/tmp && cd "$R"
+  step prof 500 rocprofv3 --kernel-trace --stats -d "$O/prof" -o rgcn -- python3 benchmarks/bench_rgcn.py --scale 0.125 --steps 2 --warmup 1
+  find "$O/prof" -name "*kernel_stats.csv" | head -3
+fi

@@ -1,9 +1,10 @@
 """R-GCN on MAG-shaped heterogeneous graphs (BASELINE config 4).
 
 * the device-side MAG generator keeps exactly the W=1 edges on every partition;
-* the relation-stacked hot path (``SourceGraph``: layer-0 transform-first with static halo
-  rows, later layers aggregate-first with one exchange per source type) matches a plain
-  PyTorch model of the same math, forward and gradients;
+* the relation-stacked hot paths (``SourceGraph``; aggregate-first: layer-0 transform-first
+  with static halo rows, later layers aggregate-first with one exchange per source type;
+  lean: transform-first everywhere, BN outputs recomputed, aggregations added in place)
+  match a plain PyTorch model of the same math, forward and gradients;
 * W = 2, 3 gloo training follows the W=1 loss curve (halo exchange, adjoint, SyncBN);
 * the RelationGraph path (RGAT dataset objects) trains too.
 """
@@ -65,8 +66,9 @@ def _dense_reference(model, xs, csrs):
     return model.mlp(h[0])
 
 
+@pytest.mark.parametrize("lean", [True, False])
 @pytest.mark.parametrize("layers", [2, 3])
-def test_hot_path_matches_dense_reference(layers):
+def test_hot_path_matches_dense_reference(layers, lean):
     part = build_hetero_partition(SHAPE, 0, 1, "cpu", global_frac=0.2, window=64)
     g = HeteroGraph.from_partition(part, EDGE_TYPES)
     csrs, _ = build_relation_csrs(SHAPE, 0, 1, "cpu", global_frac=0.2, window=64)
@@ -74,6 +76,7 @@ def test_hot_path_matches_dense_reference(layers):
     feats = {t: v[:, :32].contiguous() for t, v in feats.items()}
     torch.manual_seed(0)
     m = CommAwareRGCN(32, 16, SHAPE.num_classes, 5, layers, dropout=0.0)
+    m.lean = lean
     out = m(feats, g)
     loss = F.cross_entropy(out[tr], y[tr])
     loss.backward()
@@ -162,11 +165,12 @@ def test_relation_graph_path_trains():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("gpu_dtype", ["fp32", "bf16"])
-def test_hot_path_gpu_matches_cpu(gpu_dtype):
+@pytest.mark.parametrize("gpu_dtype,width", [("fp32", 64), ("fp32", 128), ("bf16", 64)])
+def test_hot_path_gpu_matches_cpu(gpu_dtype, width):
     """R-GCN on the MI355X (native SpMM over strided relation column slices, native
-    BN+ReLU, tall-skinny linears) vs the fp32 CPU run of the same model and graph: tight
-    in fp32 (same math), loose in bf16 autocast (two BN backwards amplify bf16 rounding)."""
+    BN+ReLU; fp32: the lean path's exact-f32 MFMA GEMMs and, at width 128, MFMA weight
+    gradients) vs the fp32 CPU run of the same model and graph: tight in fp32 (same math),
+    loose in bf16 autocast (two BN backwards amplify bf16 rounding)."""
     shape = HETERO_SHAPES["mag240m"].scaled(1e-4)
     # graph and data generated once on the CPU (device RNG streams differ), then moved
     part_cpu = build_hetero_partition(shape, 0, 1, "cpu", global_frac=0.2, window=256)
@@ -180,10 +184,10 @@ def test_hot_path_gpu_matches_cpu(gpu_dtype):
             for s, d in part_cpu["sources"].items()}}
         g = HeteroGraph.from_partition(part, EDGE_TYPES)
         dt = torch.bfloat16 if (bf16 and dev == "cuda") else torch.float32
-        feats = {t: v[:, :64].to(dt).to(dev).contiguous() for t, v in feats_cpu.items()}
+        feats = {t: v[:, :width].to(dt).to(dev).contiguous() for t, v in feats_cpu.items()}
         y, tr = y_cpu.to(dev), tr_cpu.to(dev)
         torch.manual_seed(0)
-        m = CommAwareRGCN(64, 64, shape.num_classes, 5, 2, dropout=0.0).to(dev)
+        m = CommAwareRGCN(width, width, shape.num_classes, 5, 2, dropout=0.0).to(dev)
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=bf16 and dev == "cuda"):
             out = m(feats, g)
         loss = F.cross_entropy(out[tr].float(), y[tr])
