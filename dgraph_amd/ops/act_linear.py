@@ -17,7 +17,7 @@ the kernels do not tile (e.g. 153 classes) fall back to the library GEMM. Elsewh
 """
 from __future__ import annotations
 
-from typing import List, Optional, Sequence
+from typing import List, Sequence
 
 import torch
 from torch.autograd import Function
@@ -26,62 +26,11 @@ from . import f32 as F32
 from . import kernels as K
 
 
-def _f32_gpu(t: torch.Tensor) -> bool:
-    return t.is_cuda and t.dtype == torch.float32
-
-
-def _tileable(n: int) -> bool:
-    """Output widths the fp32 GEMM covers (one tile or 128/176/192/256 column blocks)."""
-    if F32.gemm_f32_ok(n, 32):
-        return True
-    try:
-        F32._blocks(n, lambda w: w in (128, 176, 192, 256))
-        return n > 256
-    except ValueError:
-        return False
-
-
-def _wgrad_ok(K: int, N: int) -> bool:
-    try:
-        F32._blocks(K, lambda w: w in (128, 256), (256, 128))
-        F32._blocks(N, F32._wgrad_n_ok)
-        return True
-    except ValueError:
-        return False
-
-
-def _gemm(y: torch.Tensor, W: torch.Tensor, b: Optional[torch.Tensor]) -> torch.Tensor:
-    """``y W^T + b`` (W: [N, K], torch Linear layout)."""
-    N, K = W.shape
-    if _f32_gpu(y) and K % 32 == 0 and _tileable(N) and y.stride(1) == 1:
-        return F32.gemm_f32(y, W.t().contiguous(), bias=b)
-    return torch.nn.functional.linear(y, W.to(y.dtype), None if b is None else b.to(y.dtype))
-
-
-def _dy(gs: Sequence[torch.Tensor], Ws: Sequence[torch.Tensor]) -> torch.Tensor:
-    """``sum_i g_i W_i`` (two terms per MFMA call, running sum chained through ``cin``)."""
-    K = Ws[0].shape[1]
-    if all(_f32_gpu(g) and g.shape[1] % 32 == 0 for g in gs) and _tileable(K):
-        out = None
-        for k in range(0, len(gs), 2):
-            two = k + 1 < len(gs)
-            out = F32.gemm_f32(gs[k], Ws[k].contiguous(), gs[k + 1] if two else None,
-                               Ws[k + 1].contiguous() if two else None, cin=out, out=out)
-        return out
-    out = gs[0] @ Ws[0].to(gs[0].dtype)
-    for g, W in zip(gs[1:], Ws[1:]):
-        out = out + g @ W.to(g.dtype)
-    return out
-
-
 def _wgrad(g: torch.Tensor, y: torch.Tensor, W: torch.Tensor) -> torch.Tensor:
     """``g^T y`` in W's layout [N, K]."""
-    N, K = W.shape
-    if _f32_gpu(g) and _f32_gpu(y) and _wgrad_ok(K, N) and y.stride(1) == 1 \
-            and g.stride(1) == 1:
-        acc = F32.WgradAcc(K, N, g.device)
-        acc.add(y, g)
-        return acc.result().t().contiguous().to(W.dtype)
+    dW = F32.linear_wgrad(g, y, W)
+    if dW is not None:
+        return dW
     adt = torch.float64 if g.dtype == torch.float64 else torch.float32
     return (g.t().to(adt) @ y.to(adt)).to(W.dtype)
 
@@ -97,7 +46,7 @@ class _ActLinearsFn(Function):
             bn._update_running(st.N, st.mean, var)
         else:
             y = x
-        outs = [_gemm(y, W, bias if i == 0 else None) for i, W in enumerate(Ws)]
+        outs = [F32.linear_fwd(y, W, bias if i == 0 else None) for i, W in enumerate(Ws)]
         del y
         ctx.st = st
         ctx.has_bias = bias is not None
@@ -128,7 +77,7 @@ class _ActLinearsFn(Function):
         need_x = ctx.needs_input_grad[0] or (st is not None and (ctx.needs_input_grad[1]
                                                                  or ctx.needs_input_grad[2]))
         if need_x and live:
-            dy = _dy([g for g, W in zip(gs_c, Ws) if g is not None],
+            dy = F32.linear_dgrad([g for g, W in zip(gs_c, Ws) if g is not None],
                      [W for g, W in zip(gs_c, Ws) if g is not None])
             if st is not None:
                 from ..models.norm import bn_act_backward

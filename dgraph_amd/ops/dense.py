@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import torch
 
+from . import f32 as F32
 from . import kernels as K
 
 
@@ -121,6 +122,8 @@ class _LinearFn(torch.autograd.Function):
     def forward(ctx, x, W, b):
         ctx.save_for_backward(x, W)
         ctx.has_b = b is not None
+        if x.dim() == 2:  # fp32 on the GPU: the exact-f32 MFMA GEMM, bias fused
+            return F32.linear_fwd(x, W, b)
         return torch.nn.functional.linear(x, W, b)
 
     @staticmethod
@@ -131,15 +134,16 @@ class _LinearFn(torch.autograd.Function):
         x2 = x.reshape(-1, W.shape[1])
         dx = dW = db = None
         if ctx.needs_input_grad[0]:
-            dx = (g2 @ W.to(g2.dtype)).reshape(x.shape)
+            dx = F32.linear_dgrad([g2], [W]).reshape(x.shape)
         if ctx.needs_input_grad[1]:
-            if g2.is_cuda:
+            dW = F32.linear_wgrad(g2, x2, W)  # fp32: split-M MFMA accumulator
+            if dW is None and g2.is_cuda:
                 # >= 8M rows (R-GCN relation linears): the 2^14-row split-K default
                 # (1/8 MAG240M step 378 -> 357 ms); fewer rows (GraphCast, 1-2M): >= 4096
                 # rows x <= 128 chunks (50.5 -> 46.4 ms)
                 L2 = g2.shape[0]
                 dW = wgrad(g2, x2.contiguous(), 0 if L2 >= 1 << 23 else _auto_rows_per_chunk(L2))
-            else:
+            elif dW is None:
                 dW = g2.t().to(torch.float64 if g2.dtype == torch.float64 else torch.float32) @ \
                     x2.to(torch.float64 if g2.dtype == torch.float64 else torch.float32)
             dW = dW.to(W.dtype)
@@ -223,6 +227,20 @@ class _LinearSumFn(torch.autograd.Function):
                           bias=b if k == 0 else None, cin=cin, out=out)
                 cin = out
             return out
+        if xs[0].is_cuda and xs[0].dtype == torch.float32 and F32.LINEAR_ON and all(
+                x.dim() == 2 and x.stride(1) == 1 and x.shape[1] % 32 == 0 for x in xs) \
+                and F32.tileable(Ws[0].shape[0]):
+            # fp32: the exact-f32 MFMA GEMM two terms per call, the running sum (and acc)
+            # chained through cin
+            out = None
+            cin = acc
+            for k in range(0, len(xs), 2):
+                two = k + 1 < len(xs)
+                out = F32.gemm_f32(xs[k], Ws[k].t().contiguous(), xs[k + 1] if two else None,
+                                   Ws[k + 1].t().contiguous() if two else None,
+                                   bias=b if k == 0 else None, cin=cin, out=out)
+                cin = out
+            return out
         out = torch.nn.functional.linear(xs[0], Ws[0], b)
         for x, W in zip(xs[1:], Ws[1:]):
             out = out + torch.nn.functional.linear(x, W)
@@ -240,12 +258,13 @@ class _LinearSumFn(torch.autograd.Function):
                 if ctx.native and dual_gemm_shape_ok(x.shape[1], W.shape[0]):
                     dx = dual_gemm(g, W.to(g.dtype).t().contiguous())
                 else:
-                    dx = g @ W.to(g.dtype)
+                    dx = F32.linear_dgrad([g], [W])
             if ctx.needs_input_grad[3 + 2 * i]:
-                if g.is_cuda:
+                dW = F32.linear_wgrad(g, x, W)  # fp32: split-M MFMA accumulator
+                if dW is None and g.is_cuda:
                     L = g.shape[0]
                     dW = wgrad(g, x, 0 if L >= 1 << 23 else _auto_rows_per_chunk(L))
-                else:
+                elif dW is None:
                     adt = torch.float64 if g.dtype == torch.float64 else torch.float32
                     dW = g.t().to(adt) @ x.to(adt)
                 dW = dW.to(W.dtype)

@@ -285,6 +285,76 @@ class WgradAcc:
         return out
 
 
+# ------------------------------------------------------------------------------ Linear
+# ``y = x W^T + b`` layers (torch Linear layout, W: [N, K]) at fp32 on the kernels above,
+# for any model's linears (ops.dense.linear / linear_sum, ops.act_linear): the library fp32
+# GEMM is the fallback for widths the kernels do not tile (e.g. 153 classes) and for
+# non-fp32 / CPU tensors. Switch: DGRAPH_F32_LINEAR=0 -> library GEMMs everywhere.
+LINEAR_ON = os.environ.get("DGRAPH_F32_LINEAR", "1") != "0"
+
+
+def tileable(n: int) -> bool:
+    """Output widths the fp32 GEMM covers (one tile, or 128/176/192/256 column blocks)."""
+    if gemm_f32_ok(n, 32):
+        return True
+    try:
+        _blocks(n, lambda w: w in (128, 176, 192, 256))
+        return n > 256
+    except ValueError:
+        return False
+
+
+def wgrad_ok(K: int, N: int) -> bool:
+    try:
+        _blocks(K, lambda w: w in (128, 256), (256, 128))
+        _blocks(N, _wgrad_n_ok)
+        return True
+    except ValueError:
+        return False
+
+
+def _on(*ts) -> bool:
+    return LINEAR_ON and all(t.is_cuda and t.dtype == torch.float32 and t.dim() == 2
+                             and t.stride(1) == 1 and t.shape[0] > 0 for t in ts)
+
+
+def linear_fwd(x: torch.Tensor, W: torch.Tensor, b: Optional[torch.Tensor] = None):
+    """``x W^T + b``."""
+    N, K = W.shape
+    if _on(x) and K % 32 == 0 and tileable(N):
+        return gemm_f32(x, W.t().contiguous(), bias=b)
+    return torch.nn.functional.linear(x, W.to(x.dtype), None if b is None else b.to(x.dtype))
+
+
+def linear_dgrad(gs, Ws) -> torch.Tensor:
+    """``sum_i g_i W_i`` (two terms per kernel call, the running sum chained through
+    ``cin``)."""
+    K = Ws[0].shape[1]
+    gs = [g if g.stride(-1) == 1 else g.contiguous() for g in gs]
+    if _on(*gs) and all(g.shape[1] % 32 == 0 for g in gs) and tileable(K):
+        out = None
+        for k in range(0, len(gs), 2):
+            two = k + 1 < len(gs)
+            out = gemm_f32(gs[k], Ws[k].contiguous(), gs[k + 1] if two else None,
+                           Ws[k + 1].contiguous() if two else None, cin=out, out=out)
+        return out
+    out = gs[0] @ Ws[0].to(gs[0].dtype)
+    for g, W in zip(gs[1:], Ws[1:]):
+        out = out + g @ W.to(g.dtype)
+    return out
+
+
+def linear_wgrad(g: torch.Tensor, x: torch.Tensor, W: torch.Tensor):
+    """``g^T x`` in W's layout [N, K] (split-M MFMA accumulator), or None when the kernels
+    do not tile the shape (callers then use their own library path)."""
+    N, K = W.shape
+    if _on(g, x) and wgrad_ok(K, N):
+        acc = WgradAcc(K, N, g.device)
+        acc.add(x, g)
+        return acc.result().t().contiguous().to(W.dtype)
+    return None
+
+
 # ------------------------------------------------------------------------------ bits
 def row_keep_bits(h: torch.Tensor, rows: Optional[torch.Tensor] = None,
                   out: Optional[torch.Tensor] = None) -> torch.Tensor:

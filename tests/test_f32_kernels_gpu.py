@@ -366,3 +366,40 @@ def test_fused_wide_gpu_matches_cpu(hidden, feat, layers):
     assert abs(res[0][0] - res[1][0]) < 1e-4 * max(1.0, abs(res[0][0]))
     for a, b in zip(res[0][1], res[1][1]):
         torch.testing.assert_close(b, a, atol=5e-5, rtol=2e-3)
+
+
+@pytest.mark.parametrize("M,K,N", [(5000, 384, 128), (3000, 768, 512), (2000, 256, 153)])
+def test_dense_linear_f32_vs_fp64(M, K, N):
+    """``ops.dense.linear`` / ``linear_sum`` / ``act_linears`` at fp32 on the GPU (MFMA
+    GEMM + split-M weight gradient; 153 columns on the library fallback) vs fp64 CPU."""
+    from dgraph_amd.ops.act_linear import act_linears
+    from dgraph_amd.ops.dense import linear, linear_sum
+
+    g = torch.Generator().manual_seed(M + N)
+    x = torch.randn(M, K, generator=g)
+    x2 = torch.randn(M, K, generator=g)
+    W = torch.randn(N, K, generator=g) / K ** 0.5
+    W2 = torch.randn(N, K, generator=g) / K ** 0.5
+    b = torch.randn(N, generator=g)
+    go = torch.randn(M, N, generator=g)
+
+    def run(dev, dt, fn):
+        ts = [t.to(dev, dt, copy=True).requires_grad_() for t in (x, x2, W, W2, b)]
+        out = fn(*ts)
+        out.backward(go.to(dev, dt))
+        return [out.detach().double().cpu()] + [t.grad.double().cpu() for t in ts
+                                                 if t.grad is not None]
+
+    fns = {
+        "linear": lambda a, a2, w, w2, bb: linear(a, w, bb),
+        "linear_sum": lambda a, a2, w, w2, bb: linear_sum([(a, w), (a2, w2)], bb),
+        "act_linears": lambda a, a2, w, w2, bb: act_linears(a, [w, w2], bb)[0]
+        + act_linears(a, [w, w2], bb)[1],
+    }
+    for name, fn in fns.items():
+        got = run(DEV, torch.float32, fn)
+        ref = run("cpu", torch.float64, fn)
+        assert len(got) == len(ref), name
+        for a, r in zip(got, ref):
+            err = float((a - r).abs().max() / r.abs().max().clamp_min(1e-6))
+            assert err < 2e-5, (name, err)
