@@ -223,6 +223,23 @@ def grid_placement_from_mesh(g: GlobalGraphCastGraph, mesh_part: torch.Tensor) -
     return mesh_part.long()[torch.from_numpy(first)]
 
 
+def grid_placement_from_g2m(g: GlobalGraphCastGraph, mesh_part: torch.Tensor) -> torch.Tensor:
+    """The reference's grid placement for a given mesh placement
+    (experiments/GraphCast/data_utils/graphcast_graph.py:287-324): every grid vertex takes
+    the rank of the mesh destination of its grid2mesh edges — edges visited in ascending
+    rank order, the last write kept, i.e. the largest such rank — and a grid vertex with no
+    grid2mesh edge stays on rank 0. (The reference's loop pairs the rank-sorted edge
+    sources with the unsorted edge ranks, :316-322; this is the rule that loop is written
+    to implement, with the pairing intact.)"""
+    src, dst = g.g2m
+    n_grid = g.grid_shape[0] * g.grid_shape[1]
+    r = mesh_part.long()[torch.from_numpy(np.asarray(dst, dtype=np.int64))]
+    out = torch.zeros(n_grid, dtype=torch.long)
+    out.scatter_reduce_(0, torch.from_numpy(np.asarray(src, dtype=np.int64)), r, "amax",
+                        include_self=True)
+    return out
+
+
 def load_mesh_placement(path: str, num_mesh: int, world_size: int) -> torch.Tensor:
     """``mesh_vertex_rank_placement.pt`` of the reference (experiments/GraphCast/dataset.py:
     244, microbenchmark_graphcast.py:35): an int tensor [V_mesh] of ranks. Loaded with
@@ -325,11 +342,16 @@ def _edge_set(agg_g: np.ndarray, other_g: np.ndarray, agg_part: torch.Tensor,
 def partition_graphcast_graph(g: GlobalGraphCastGraph, rank: int, world_size: int,
                               grid_part: Optional[torch.Tensor] = None,
                               mesh_part: Optional[torch.Tensor] = None,
-                              group=None) -> DistributedGraphCastGraph:
+                              group=None, grid_rule: str = "g2m") -> DistributedGraphCastGraph:
     """Per-rank view (collective when ``world_size > 1``). Local vertices keep increasing
-    global-id order."""
+    global-id order. Given only a mesh placement, the grid placement follows it by
+    ``grid_rule``: ``"g2m"`` (the reference's: :func:`grid_placement_from_g2m`) or
+    ``"m2g"`` (:func:`grid_placement_from_mesh`: decoder edges stay rank-local)."""
     if mesh_part is not None and grid_part is None:
-        grid_part = grid_placement_from_mesh(g, mesh_part)
+        if grid_rule not in ("g2m", "m2g"):
+            raise ValueError(f"grid_rule {grid_rule!r}: expected 'g2m' or 'm2g'")
+        grid_part = (grid_placement_from_g2m if grid_rule == "g2m"
+                     else grid_placement_from_mesh)(g, mesh_part)
     if grid_part is None or mesh_part is None:
         grid_part, mesh_part = latitude_partition(g, world_size)
     m_src, m_dst = g.m2m

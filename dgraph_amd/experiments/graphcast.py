@@ -74,7 +74,8 @@ class GraphCastTrainer:
         mesh_part = None
         if mesh_vertex_placement:
             # the reference's mesh_vertex_rank_placement.pt (GraphCast/dataset.py:244); the
-            # grid placement follows it (data/graphcast_graph.grid_placement_from_mesh)
+            # grid placement follows it by the reference's rule: each grid vertex on the
+            # rank of its grid2mesh mesh destination (graphcast_graph.grid_placement_from_g2m)
             mesh_part = load_mesh_placement(mesh_vertex_placement, g.mesh_xyz.shape[0],
                                             self.psize)
         self.graph = partition_graphcast_graph(g, self.prank, self.psize, mesh_part=mesh_part,

@@ -165,8 +165,9 @@ def test_mlp_reference_layout():
 
 def test_graphcast_mesh_placement_file(ranks, tmp_path):
     """A reference-style ``mesh_vertex_rank_placement.pt`` (random, non-contiguous ranks)
-    drives the partition (grid vertices follow their mesh2grid source) and reproduces W=1."""
-    from dgraph_amd.data.graphcast_graph import grid_placement_from_mesh
+    drives the partition (grid vertices on the rank of their grid2mesh mesh destination, the
+    reference's rule) and reproduces W=1."""
+    from dgraph_amd.data.graphcast_graph import grid_placement_from_g2m, grid_placement_from_mesh
 
     d = str(tmp_path)
     g = build_global_graph(2, (19, 36))
@@ -176,6 +177,11 @@ def test_graphcast_mesh_placement_file(ranks, tmp_path):
     torch.save(place.int(), path)
     gp = grid_placement_from_mesh(g, place)
     assert gp.numel() == 19 * 36 and int(gp.max()) < world
+    gg = grid_placement_from_g2m(g, place)
+    src, dst = (torch.from_numpy(a).long() for a in g.g2m)
+    for v in range(0, 19 * 36, 7):  # max rank over the vertex's g2m edges, else rank 0
+        e = dst[src == v]
+        assert int(gg[v]) == (int(place[e].max()) if e.numel() else 0)
     ranks(_gc_dist, 1, d)
     ranks(_gc_dist, world, d, path)
     r1 = torch.load(f"{d}/gc_w1.pt", weights_only=True)
