@@ -147,6 +147,8 @@ def main(argv=None):
     inv_n = 1.0 / max(n_train, 1)
     use_amp = dev.type == "cuda" and dtype == torch.bfloat16
 
+    lean = model.lean if model.lean is not None else (dtype == torch.float32)
+
     def step():
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=use_amp):
             logits = model(feats, graph)
@@ -198,12 +200,16 @@ def main(argv=None):
                    "parallelism": f"graph-partition{p_world}" + (" (rehearsal)" if rehearse
                                                                   else "")},
         "final_loss": float(lt.item()), "peak_mem_gb_rank0": round(peak, 2),
+        "path": "lean" if lean else "aggregate-first",
+        "layer0_halo": ("kept" if (not lean or model._keep_static_halo(feats, graph))
+                        else "exchanged per step"),
     }
     if rehearse:
         rec = {"rehearsal": True, "rank": p_rank, "world": p_world,
                "ms_per_step_compute_loopback": ms_step, "messages_local": E_step,
                "halo_rows": halo_total, "peak_mem_gb": round(peak, 2),
-               "final_loss_local": float(lt.item()),
+               "final_loss_local": float(lt.item()), "path": rec["path"],
+               "layer0_halo": rec["layer0_halo"],
                "dtype": "bf16" if dtype == torch.bfloat16 else "fp32"}
     if rank == 0:
         print(json.dumps(rec), flush=True)

@@ -88,6 +88,7 @@ class CommAwareRGCN(nn.Module):
         self.target = target_type
         self.num_node_types = num_node_types
         self.lean: Optional[bool] = None  # None: by the compute dtype (see forward)
+        self.static_halo: Optional[bool] = None  # lean path; None: by memory
         self.convs = nn.ModuleList()
         self.skips = nn.ModuleList()
         for i in range(num_layers):
@@ -180,23 +181,42 @@ class CommAwareRGCN(nn.Module):
             h = {t: self._finish(l, v) for t, v in tmp.items()}
         return self._head(h[self.target])
 
+    def _keep_static_halo(self, xs: Dict[int, torch.Tensor], g: HeteroGraph) -> bool:
+        """Keep the layer-0 feature halo rows for the whole run (fetched once, no layer-0
+        communication) unless they would take more than ``STATIC_HALO_FRAC`` of the
+        device; then the transformed rows of every relation are exchanged per step
+        instead (256 instead of 768 columns, and nothing resident)."""
+        if self.static_halo is not None:
+            return bool(self.static_halo)
+        nbytes = sum(sg.H * xs[s].shape[1] * xs[s].element_size()
+                     for s, sg in g.sources.items() if s in xs)
+        x0 = next(iter(xs.values()))
+        if not x0.is_cuda or nbytes == 0:
+            return True
+        total = torch.cuda.get_device_properties(x0.device).total_memory
+        return nbytes <= self.STATIC_HALO_FRAC * total
+
+    STATIC_HALO_FRAC = 0.08
+
     def _forward_hetero_lean(self, xs: Dict[int, torch.Tensor], g: HeteroGraph) -> torch.Tensor:
         """Transform-first at EVERY layer, BN'd activations recomputed instead of stored:
 
             pre_t^l = skip_l(h_t) + sum_{r: s->t} mean_r(h_s W_r^l),  h = act(BN(pre^{l-1}))
 
         per source type ONE :func:`~dgraph_amd.ops.act_linears` call builds ``act(BN(pre_s))``
-        transiently and runs the skip GEMM (straight into ``pre_s``, bias fused) and the
-        stacked relation GEMM ``[W_r1 | W_r2 ...]``; the relation aggregations then add into
-        the destinations' ``pre`` in place (one halo exchange per source type, of the
-        transformed rows). Saved per step: the inputs, one ``pre`` per (layer, type) and the
+        transiently and runs the skip GEMM (straight into ``pre_s``, bias fused) and one GEMM
+        per relation; each relation's aggregation then adds into its destination's ``pre``
+        in place, exchanging that relation's transformed halo rows (one [H, hidden] buffer
+        live at a time). Saved per step: the inputs, one ``pre`` per (layer, type) and the
         head's hidden pre-activation — no BN output, aggregate or relation output (the
         aggregate-first path saves each of those: 274 GB at fp32 on one GPU's 1/8 MAG240M
-        share, profiles/r04/rgcn_fp32_eighth.json). Same math as :meth:`_forward_hetero`."""
+        share, profiles/r04/rgcn_fp32_eighth.json). Layer 0's feature halo rows are kept
+        (fetched once) when :meth:`_keep_static_halo` allows. Same math as
+        :meth:`_forward_hetero`."""
         ets = g.edge_types
         avail = [r for s in g.sources.values() for r in s.ranges]
         need, rels = layer_plan(ets, self.num_layers, self.target, avail)
-        C = self.hidden
+        keep_halo = self._keep_static_halo(xs, g)
         pre: Dict[int, torch.Tensor] = {}
         for l in range(self.num_layers):
             by_src: Dict[int, List[int]] = {}
@@ -206,28 +226,29 @@ class CommAwareRGCN(nn.Module):
             zs = []
             for s in sorted(set(need[l]) | set(by_src)):
                 rs = by_src.get(s, [])
-                Ws = [self.skips[l].weight] if s in need[l] else []
-                if rs:
-                    Ws.append(torch.cat([self.convs[l][r].weight for r in rs], 0)
-                              if len(rs) > 1 else self.convs[l][rs[0]].weight)
+                skip = s in need[l]
+                Ws = ([self.skips[l].weight] if skip else []) + \
+                    [self.convs[l][r].weight for r in rs]
                 inp = xs[s] if l == 0 else pre[s]
                 bn = self.bns[l - 1] if l else None
-                outs = act_linears(inp, Ws, self.skips[l].bias if s in need[l] else None,
+                outs = act_linears(inp, Ws, self.skips[l].bias if skip else None,
                                    bn=bn, relu=l > 0, dropout=self.dropout if l else 0.0)
-                if s in need[l]:
+                if skip:
                     new[s] = outs[0]
-                if rs:
-                    zh = None
-                    if l == 0:  # read-only features: halo rows fetched once, transformed here
-                        xh = g.sources[s].static_halo(xs[s])
-                        zh = act_linears(xh, Ws[-1:])[0] if xh is not None else None
-                    zs.append((s, rs, outs[-1], zh))
-            for s, rs, z, zh in zs:
-                spec = [(r, i * C, (i + 1) * C) for i, r in enumerate(rs)]
-                res = source_aggregate_into(z, g.sources[s], spec,
-                                            [new[ets[r][1]] for r in rs], static_halo=zh)
-                for r, o in zip(rs, res):
-                    new[ets[r][1]] = o
+                zr = outs[1:] if skip else outs
+                zh = [None] * len(rs)
+                if l == 0 and keep_halo:
+                    # read-only features: halo rows fetched once, transformed here
+                    xh = g.sources[s].static_halo(xs[s])
+                    if xh is not None:
+                        zh = act_linears(xh, Ws[len(Ws) - len(rs):])
+                zs += [(s, r, z, h) for r, z, h in zip(rs, zr, zh)]
+            while zs:  # each relation output is released right after its aggregation
+                s, r, z, zh = zs.pop(0)
+                d = ets[r][1]
+                new[d] = source_aggregate_into(z, g.sources[s], [(r, 0, z.shape[1])],
+                                               [new[d]], static_halo=zh)[0]
+                del z, zh
             pre = new
         lin1, bn, _, drop, lin2 = self.mlp
         t = self.target

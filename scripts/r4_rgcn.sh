@@ -14,11 +14,15 @@ step() {
 }
 step tests 400 python -u -m pytest tests/test_rgcn.py tests/test_f32_kernels_gpu.py tests/test_graphcast.py -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider -k "rgcn or dense_linear or graphcast or gemm or wgrad"
 step eighth 500 python -u benchmarks/bench_rgcn.py --scale 0.125 --steps 3 --warmup 1
-step gc73_mfma 300 python -u benchmarks/bench_graphcast.py --steps 10 --warmup 3
-step gc73_lib 300 env DGRAPH_F32_LINEAR=0 python -u benchmarks/bench_graphcast.py --steps 10 --warmup 3
-step w8r1 600 python -u benchmarks/bench_rgcn.py --rehearse-world 8 --rehearse-rank 1 --steps 3 --warmup 1
+step eighth_lib 500 env DGRAPH_F32_LINEAR=0 python -u benchmarks/bench_rgcn.py --scale 0.125 --steps 3 --warmup 1
+step w8r1 600 python -u benchmarks/bench_rgcn.py --rehearse-world 8 --rehearse-rank 1 --steps 3 --warmup 1 --backend rocshmem
+step w8r1_exp 600 env PYTORCH_ALLOC_CONF=expandable_segments:True python -u benchmarks/bench_rgcn.py --rehearse-world 8 --rehearse-rank 1 --steps 3 --warmup 1 --backend rocshmem
 if [ "${PROF:-1}" = 1 ]; then
-  cd /tmp && export TMPDIR=/tmp && cd "$R"
-  step prof 500 rocprofv3 --kernel-trace --stats -d "$O/prof" -o rgcn -- python3 benchmarks/bench_rgcn.py --scale 0.125 --steps 2 --warmup 1
-  find "$O/prof" -name "*kernel_stats.csv" | head -3
+  cd /tmp && export TMPDIR=/tmp
+  timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/prof" -o run \
+    -- python3 "$R/benchmarks/bench_rgcn.py" --scale 0.125 --steps 2 --warmup 1 > "$R/$O/prof.log" 2>&1
+  rc=$?; cd "$R"; echo "== prof rc=$rc"
+  python3 scripts/prof_summary.py "$O/prof" 40 > "$O/prof_summary.txt" 2>&1; head -45 "$O/prof_summary.txt"
+  find "$O/prof" -name "*kernel_stats.csv" -exec cp {} "$O/" \;
+  rm -rf "$O/prof"
 fi

@@ -91,7 +91,7 @@ def test_hot_path_matches_dense_reference(layers, lean):
             torch.testing.assert_close(a, p.grad, atol=1e-5, rtol=1e-4)
 
 
-def _train(rank, world, steps, out):
+def _train(rank, world, steps, out, static_halo=None):
     import torch.distributed as dist
 
     from dgraph_amd.parallel.grad_sync import GradSync
@@ -106,6 +106,7 @@ def _train(rank, world, steps, out):
         dist.all_reduce(n)
     torch.manual_seed(0)
     m = CommAwareRGCN(24, 16, SHAPE.num_classes, 5, 2, dropout=0.0)
+    m.static_halo = static_halo
     opt = torch.optim.Adam(m.parameters(), lr=1e-2)
     sync = GradSync(m.parameters())
     losses = []
@@ -124,10 +125,13 @@ def _train(rank, world, steps, out):
         torch.save(torch.tensor(losses), out)
 
 
-@pytest.mark.parametrize("world", [2, 3, 8])
-def test_distributed_training_matches_single_rank(ranks, tmp_path, world):
+@pytest.mark.parametrize("world,static_halo", [(2, None), (3, None), (8, None), (2, False),
+                                               (3, False)])
+def test_distributed_training_matches_single_rank(ranks, tmp_path, world, static_halo):
+    """(``static_halo=False``: layer 0 exchanges each relation's transformed halo rows per
+    step, forward and reverse, instead of keeping the feature halo.)"""
     _train(0, 1, 3, tmp_path / "w1.pt")
-    ranks(_train, world, 3, str(tmp_path / "wn.pt"))
+    ranks(_train, world, 3, str(tmp_path / "wn.pt"), static_halo)
     a = torch.load(tmp_path / "w1.pt", weights_only=True)
     b = torch.load(tmp_path / "wn.pt", weights_only=True)
     torch.testing.assert_close(a, b, atol=2e-5, rtol=2e-5)
