@@ -4,8 +4,9 @@
 the MeshGraphMLP hidden layers of GraphCast (Linear -> SiLU, experiments/GraphCast/
 layers.py:24-75; the node block's first Linear over ``[x || agg]`` is two terms, so no
 concatenation and no separate add). GPU:
-  forward  — the bias-free product (native MFMA dual GEMM, two terms per launch, or the
-             library GEMM) then ONE fused bias + activation pass (csrc/kernels/act.hip);
+  forward  — the bias-free product (native MFMA dual GEMM, two terms per launch — bf16, or
+             exact-f32 at fp32 — or the library GEMM for untiled widths) then ONE fused
+             bias + activation pass (csrc/kernels/act.hip);
   backward — ONE pass computes ``dz = dy * act'(z + b)`` and the bias gradient's column
              sums together; ``dx_i = dz W_i``, ``dW_i`` by the split-K weight gradient.
 PyTorch's path is addmm + silu forward and silu_backward + a column reduction (an extra
@@ -19,6 +20,7 @@ import torch
 import torch.nn.functional as Fn
 
 from .. import _native
+from . import f32 as F32
 from .dense import (_auto_rows_per_chunk, _native_linear_sum_ok, dual_gemm, dual_gemm_shape_ok,
                     wgrad)
 
@@ -31,6 +33,13 @@ def _act_ref(z: torch.Tensor, act: int) -> torch.Tensor:
     if act == 2:
         return torch.relu(z)
     return z
+
+
+def _f32_mm_ok(xs, Ws) -> bool:
+    return (F32.LINEAR_ON and xs[0].is_cuda and xs[0].shape[0] > 0
+            and all(x.dtype == torch.float32 and x.dim() == 2 and x.stride(1) == 1
+                    and x.shape[1] % 32 == 0 for x in xs)
+            and F32.tileable(Ws[0].shape[0]))
 
 
 def _native_ok(z: torch.Tensor) -> bool:
@@ -60,6 +69,13 @@ class _LinearActFn(torch.autograd.Function):
                 dual_gemm(xs[k], Ws[k].to(xs[k].dtype), xs[k + 1] if two else None,
                           Ws[k + 1].to(xs[k].dtype) if two else None, cin=cin, out=z)
                 cin = z
+        elif _f32_mm_ok(xs, Ws):
+            # fp32: the exact-f32 MFMA GEMM, two terms per launch, running sum through cin
+            z = None
+            for k in range(0, len(xs), 2):
+                two = k + 1 < len(xs)
+                z = F32.gemm_f32(xs[k], Ws[k].t().contiguous(), xs[k + 1] if two else None,
+                                 Ws[k + 1].t().contiguous() if two else None, cin=z, out=z)
         else:
             z = Fn.linear(xs[0], Ws[0])
             for x, W in zip(xs[1:], Ws[1:]):
@@ -99,13 +115,14 @@ class _LinearActFn(torch.autograd.Function):
                 if ctx.native_mm and dual_gemm_shape_ok(x.shape[1], W.shape[0]):
                     dx = dual_gemm(dz, W.to(dz.dtype).t().contiguous())
                 else:
-                    dx = dz @ W.to(dz.dtype)
+                    dx = F32.linear_dgrad([dz], [W])
             if ctx.needs_input_grad[3 + 2 * i]:
-                if dz.is_cuda:
+                dW = F32.linear_wgrad(dz, x, W)  # fp32: split-M MFMA accumulator
+                if dW is None and dz.is_cuda:
                     L = dz.shape[0]
                     dW = wgrad(dz, x.contiguous(),
                                0 if L >= 1 << 23 else _auto_rows_per_chunk(L))
-                else:
+                elif dW is None:
                     adt = torch.float64 if dz.dtype == torch.float64 else torch.float32
                     dW = dz.t().to(adt) @ x.to(adt)
                 dW = dW.to(W.dtype)

@@ -12,8 +12,10 @@ step() {
   echo "== $name rc=$rc"; grep -E '^\{|passed|failed|Error' "$O/$name.log" | cut -c1-900
   if fatal $rc; then echo "FATAL at $name"; exit $rc; fi
 }
-step tests 400 python -u -m pytest tests/test_rgcn.py tests/test_f32_kernels_gpu.py tests/test_graphcast.py -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider -k "rgcn or dense_linear or graphcast or gemm or wgrad"
+step tests 400 python -u -m pytest tests/test_rgcn.py tests/test_f32_kernels_gpu.py tests/test_graphcast.py tests/test_act_gpu.py -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider -k "rgcn or dense_linear or graphcast or gemm or wgrad or act"
 step eighth 500 python -u benchmarks/bench_rgcn.py --scale 0.125 --steps 3 --warmup 1
+step gc73_mfma 300 python -u benchmarks/bench_graphcast.py --steps 10 --warmup 3
+step gc73_lib 300 env DGRAPH_F32_LINEAR=0 python -u benchmarks/bench_graphcast.py --steps 10 --warmup 3
 step eighth_lib 500 env DGRAPH_F32_LINEAR=0 python -u benchmarks/bench_rgcn.py --scale 0.125 --steps 3 --warmup 1
 step w8r1 600 python -u benchmarks/bench_rgcn.py --rehearse-world 8 --rehearse-rank 1 --steps 3 --warmup 1 --backend rocshmem
 step w8r1_exp 600 env PYTORCH_ALLOC_CONF=expandable_segments:True python -u benchmarks/bench_rgcn.py --rehearse-world 8 --rehearse-rank 1 --steps 3 --warmup 1 --backend rocshmem
