@@ -59,6 +59,8 @@ def parse(argv=None):
                     help="compute/storage dtype (fp32 = the reference's precision: "
                          "experiments/OGB-LSC/RGAT.py has no casts; bf16 = autocast with fp32 "
                          "master weights, a secondary)")
+    ap.add_argument("--path", choices=("auto", "lean", "aggregate-first"), default="auto",
+                    help="R-GCN execution path (auto: lean at fp32, aggregate-first under bf16)")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args(argv)
 
@@ -142,6 +144,8 @@ def main(argv=None):
     model = CommAwareRGCN(shape.num_features, args.hidden, shape.num_classes, len(EDGE_TYPES),
                           args.layers, dropout=args.dropout, comm=comm,
                           bn_group=comm.group).to(dev)
+    if args.path != "auto":
+        model.lean = args.path == "lean"
     opt = torch.optim.Adam(model.parameters(), lr=args.lr, fused=dev.type == "cuda")
     sync = GradSync(model.parameters(), group=comm.group) if world > 1 else None
     inv_n = 1.0 / max(n_train, 1)
