@@ -1,10 +1,10 @@
 #!/usr/bin/env bash
-# Round-4 GPU session: GPU tests, the 1-GPU headline, link-delayed rehearsals of W = 2/4/8.
+# GPU session: GPU tests, the 1-GPU headline, link-delayed rehearsals of W = 2/4/8.
 # Stops at the first fault-like exit (timeout / abort / segfault); plain test failures go on.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
-cd "$R" && mkdir -p gpurun_out/r4
-O=gpurun_out/r4
+cd "$R" && mkdir -p gpurun_out/round
+O=gpurun_out/round
 fatal() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
 step() {  # step <name> <timeout> <cmd...>
   local name=$1 t=$2; shift 2

@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# 1-GPU headline under knob variants (same box): VARS="name:ENV=V,ENV2=V2 ..."
+# 1-GPU headline under knob variants on one box: VARS="name:ENV=V,ENV2=V2 ..."
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 cd "$R" && mkdir -p gpurun_out/w1var

@@ -1,9 +1,13 @@
 #!/usr/bin/env bash
-# A/B of the W-way rehearsal: link delay on/off, interior-first on/off (+ optional trace).
+# W-way rehearsals of the headline step, one rank on one GPU with the link-delayed loopback
+# exchange (bench.py --rehearse-world W --link-gbps G): RUNS="W:GBPS[:HWQ] ..." (GBPS 0 = no
+# delay; HWQ = DGRAPH_HW_QUEUES), EXTRA = more bench.py args (e.g. --global-frac 1.0),
+# TESTS=1 runs the fp32 / link-delay / multi-process GPU tests first.
+# Output: gpurun_out/rehearse/*.log, all.jsonl (one "rehearsal" JSON line per run).
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
-cd "$R" && mkdir -p gpurun_out/r4ab
-O=gpurun_out/r4ab
+cd "$R" && mkdir -p gpurun_out/rehearse
+O=gpurun_out/rehearse
 fatal() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
 run() {  # run <name> <W> <args...>
   local name=$1 W=$2; shift 2
@@ -30,7 +34,7 @@ for spec in ${RUNS:-8:153 8:0 2:153 4:153}; do
   W=${spec%%:*}; rest=${spec#*:}; G=${rest%%:*}; Q=${rest#*:}
   [ "$Q" = "$rest" ] && Q=""
   if [ -n "$Q" ]; then
-    GPU_MAX_HW_QUEUES=$Q run w${W}_g${G}_q${Q} $W --link-gbps $G ${EXTRA:-}
+    DGRAPH_HW_QUEUES=$Q run w${W}_g${G}_q${Q} $W --link-gbps $G ${EXTRA:-}
   else
     run w${W}_g${G} $W --link-gbps $G ${EXTRA:-}
   fi
