@@ -27,13 +27,13 @@
 // Persistent grid (occupancy x CUs), tiles round-robin over blocks.
 #include "../common.h"
 #include "kernels.h"
+#include "lds_dma.h"
 
 namespace dgraph {
 namespace {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
-typedef __attribute__((address_space(3))) void* lds_void_t;
 
 __device__ __forceinline__ bf16x8 as_bf16x8_bs(uint4 v) { return __builtin_bit_cast(bf16x8, v); }
 
@@ -41,27 +41,6 @@ constexpr int kTR = 32;       // rows per tile (one MFMA row block)
 constexpr int kEWs = 40;      // epilogue tile row (32 + 8 pad, elements)
 constexpr int kPiece = 1040;  // LDS stride of one 1 KB DMA piece (+16 B: bank rotation)
 constexpr int kLdsMax = 160 * 1024;
-
-// One LDS-DMA wave-instruction: lane l's 16 B from `src` land at lds_base + 16 l. Issued
-// as inline asm on purpose: hipcc tracks __builtin_amdgcn_global_load_lds as an LDS write
-// it cannot disambiguate and then waits vmcnt(0) before EVERY ds_read of the tile loop
-// (draining the prefetch); completion is tracked by the counted waits below instead.
-__device__ __forceinline__ void glds16(const void* src, void* lds_base) {
-  const uint32_t l = __builtin_amdgcn_readfirstlane(
-      static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void_t)lds_base)));
-  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off"
-               :
-               : "v"(src), "s"(l)
-               : "memory", "m0");
-}
-
-// s_waitcnt vmcnt(n) (gfx9 encoding: vmcnt[3:0] | vmcnt[5:4] << 14; expcnt/lgkmcnt left
-// at their maxima, i.e. not waited for)
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
-}
 
 // wait until at most BASE + n * STEP vector-memory ops are outstanding, n = min(i, MAXN)
 template <int BASE, int STEP, int MAXN>

@@ -18,8 +18,12 @@
 // (TM*TN*4 accumulator registers). K runs in 32-deep stages through two LDS buffers:
 //   * A stage [256][32] fp32 (32 KB), B stage [32][N+4] fp32 (row pad: the 8-apart k rows
 //     one b32 fragment read touches fall in different banks);
-//   * global -> registers for stage s+1 is issued before the MFMAs of stage s and written
-//     to the other buffer after them (one barrier per stage);
+//   * stage s+1 is staged global -> LDS by LDS-DMA (global_load_lds_dwordx4: no staging
+//     registers; 212-218 VGPRs instead of 240) into the other buffer while stage s's MFMAs
+//     run, retired by vmcnt(0) + one barrier per stage. Measured against register staging,
+//     against B-fragment reads pinned a whole MFMA step ahead, and against the next stage's
+//     fragments prefetched behind the last MFMA step: all within +-0.3 % on the papers100M
+//     step (profiles/r04/gemm_f32_staging_ab.log), so the simplest form is kept;
 //   * k order inside a stage: lane group h = lane>>4 takes k = 8h + j in MFMA step j, so a
 //     lane's A fragments of the stage are two 16-B pieces (2 x ds_read_b128) and its B
 //     fragment of step j is row 8h + j (the permutation is applied to A and B alike; the
@@ -37,6 +41,7 @@
 //     global latency and the epilogue's stores overlap MFMAs.
 #include "../common.h"
 #include "kernels.h"
+#include "lds_dma.h"
 
 namespace dgraph {
 namespace {
@@ -44,6 +49,7 @@ namespace {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kBK = 32;
+
 
 // Block shape: BM = 256 rows, 512 threads (8 waves, 2 per SIMD at ~240 VGPRs): the GEMM owns
 // the whole register file of the CU (a 128-row one-wave-per-SIMD variant meant to co-reside
@@ -74,8 +80,6 @@ struct GLds {
   static constexpr int B_FL = kBK * BP;                 // B stage floats
   static constexpr int STAGE = A_FL + B_FL;
   static constexpr size_t BYTES = 2 * STAGE * sizeof(float);
-  static constexpr int A_V4 = A_FL / 4 / kThreads;      // float4 per thread (A stage) = 4
-  static constexpr int B_V4 = (kBK * N / 4 + kThreads - 1) / kThreads;  // float4 (B stage)
 };
 
 // B stage row k starts at b_row(k): rows with bit 3 set are shifted by 16 floats
@@ -124,67 +128,49 @@ __device__ __forceinline__ void gemm_f32_body(
   int64_t tile = dyn ? __builtin_amdgcn_readfirstlane(s_tile) : blockIdx.x;
   if (tile >= ntiles) return;  // block-uniform
 
-  // ---- per-thread global load slots of a stage
-  // A: float4 q = tid + kThreads*u -> row q / 8, 16-B chunk q % 8 of the stage's 32 k.
-  // Row indices are kept as 32-bit (the launcher checks every operand has < 2^31 rows).
-  int32_t a_src_row[L::A_V4];   // A1 rows of the tile being loaded (through a_rows)
-  int32_t nx_src_row[L::A_V4];  // the next tile's A1 rows (index loads issued early)
-  int64_t ld_tile = tile;       // the tile whose stages load_stage reads (A2 rows dense)
+  // ---- LDS-DMA staging of a stage (no staging registers): wave w issues 4 A pieces
+  // (piece P = 4w + u = rows 8P..8P+7 of the tile, 1 KB, lane l -> row 8P + l/8, LDS slot
+  // l%8 of the row, which holds global chunk (l%8) ^ swz(row): the A swizzle moved to the
+  // per-lane SOURCE address) and 4 B rows (row kr = 4w + u, lane l < N/4 -> columns
+  // 4l..4l+3). Row indices are 32-bit (the launcher checks every operand has < 2^31 rows).
+  static_assert(kThreads == 512 && kBM == 256 && kBK == 32, "staging map");
+  int32_t a_src_row[4];   // A1 rows of the tile being loaded (through a_rows)
+  int32_t nx_src_row[4];  // the next tile's A1 rows (index loads issued early)
+  int64_t ld_tile = tile; // the tile whose stages issue_stage reads (A2 rows dense)
+  const int a_slot = lane & 7;
   auto rows_of = [&](int64_t t, int32_t* a1) {
 #pragma unroll
-    for (int u = 0; u < L::A_V4; ++u) {
-      const int q = tid + kThreads * u;
-      int64_t r = t * kBM + q / 8;
+    for (int u = 0; u < 4; ++u) {
+      int64_t r = t * kBM + (4 * wave + u) * 8 + (lane >> 3);
       r = r < M ? r : M - 1;  // rows past M read a valid row (never stored)
       a1[u] = static_cast<int32_t>(a_rows ? a_rows[r] : r);
     }
   };
   rows_of(tile, a_src_row);
-  f32x4 ra[L::A_V4];
-  f32x4 rb[L::B_V4];
-  auto load_stage = [&](int s) {
+  auto issue_stage = [&](int s, int buf) {
     const int k0 = s * kBK;
     const bool first = !HAS_A2 || k0 < K1;
     const float* Ab = first ? A1 : A2;
     const int64_t lda = first ? lda1 : lda2;
     const int ka = first ? k0 : k0 - K1;
+    float* sa = lds + buf * L::STAGE;
+    float* sb = sa + L::A_FL;
 #pragma unroll
-    for (int u = 0; u < L::A_V4; ++u) {
-      const int q = tid + kThreads * u;
-      int64_t r2 = ld_tile * kBM + q / 8;
+    for (int u = 0; u < 4; ++u) {
+      const int r = (4 * wave + u) * 8 + (lane >> 3);  // row within the tile
+      int64_t r2 = ld_tile * kBM + r;
       r2 = r2 < M ? r2 : M - 1;
       const int64_t ar = first ? static_cast<int64_t>(a_src_row[u]) : r2;
-      ra[u] = *reinterpret_cast<const f32x4*>(Ab + ar * lda + ka + (q % 8) * 4);
+      const int c = a_chunk(r, a_slot);  // XOR swizzle: its own inverse
+      glds16(Ab + ar * lda + ka + c * 4, sa + (4 * wave + u) * 8 * kBK);
     }
     const float* Bb = first ? B1 : B2;
     const int64_t ldb = first ? ldb1 : ldb2;
 #pragma unroll
-    for (int u = 0; u < L::B_V4; ++u) {
-      // unconditional (slots past the stage re-read its last float4; store_stage skips
-      // them): a load under a branch makes the compiler wait for it at the join
-      int q = tid + kThreads * u;
-      q = q < kBK * N / 4 ? q : kBK * N / 4 - 1;
-      const int kr = q / (N / 4), c4 = q % (N / 4);
-      rb[u] = *reinterpret_cast<const f32x4*>(Bb + static_cast<int64_t>(ka + kr) * ldb + c4 * 4);
-    }
-  };
-  auto store_stage = [&](int buf) {
-    float* sa = lds + buf * L::STAGE;
-    float* sb = sa + L::A_FL;
-#pragma unroll
-    for (int u = 0; u < L::A_V4; ++u) {
-      const int q = tid + kThreads * u;
-      const int r = q / 8;
-      *reinterpret_cast<f32x4*>(sa + r * kBK + a_chunk(r, q % 8) * 4) = ra[u];
-    }
-#pragma unroll
-    for (int u = 0; u < L::B_V4; ++u) {
-      // clamped like the load: surplus slots rewrite the last float4 with its own value
-      // (no branch, so the compiler cannot sink the load into one)
-      int q = tid + kThreads * u;
-      q = q < kBK * N / 4 ? q : kBK * N / 4 - 1;
-      const int kr = q / (N / 4), c4 = q % (N / 4);
-      *reinterpret_cast<f32x4*>(sb + b_row<L::BP>(kr) + c4 * 4) = rb[u];
+    for (int u = 0; u < 4; ++u) {
+      const int kr = 4 * wave + u;
+      if (lane < N / 4)
+        glds16(Bb + static_cast<int64_t>(ka + kr) * ldb + lane * 4, sb + b_row<L::BP>(kr));
     }
   };
 
@@ -194,8 +180,8 @@ __device__ __forceinline__ void gemm_f32_body(
 #pragma unroll
     for (int b = 0; b < TN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  load_stage(0);
-  store_stage(0);
+  issue_stage(0, 0);
+  wait_vmcnt<0>();
   __syncthreads();
   const int arow_w = wm * TM * 16;  // this wave's first row within the block tile
   const int bcol_w = wn * TN * 16;  // this wave's first column
@@ -221,11 +207,10 @@ __device__ __forceinline__ void gemm_f32_body(
       const bool last = s + 1 == nst;
       const bool switch_tile = last && has_next;
 #pragma unroll
-      for (int u = 0; u < L::A_V4; ++u) a_src_row[u] = switch_tile ? nx_src_row[u] : a_src_row[u];
+      for (int u = 0; u < 4; ++u) a_src_row[u] = switch_tile ? nx_src_row[u] : a_src_row[u];
       ld_tile = switch_tile ? next : ld_tile;
-      load_stage(last ? 0 : s + 1);
-      // keep the loads HERE: without this fence the scheduler sinks them next to their use
-      // (store_stage after the MFMAs) and their latency is exposed every stage
+      // the other buffer was last read in the previous stage (before its barrier)
+      issue_stage(last ? 0 : s + 1, buf ^ 1);
       __builtin_amdgcn_sched_barrier(0);
       const float* sa = lds + buf * L::STAGE;
       const float* sb = sa + L::A_FL;
@@ -260,7 +245,8 @@ __device__ __forceinline__ void gemm_f32_body(
           }
         }
       }
-      store_stage(buf ^ 1);  // (the block's very last store lands in a buffer never read)
+      // this stage's DMAs landed (the block's very last ones fill a buffer never read)
+      wait_vmcnt<0>();
       __syncthreads();
     }
 
