@@ -10,7 +10,7 @@ all-reduced gradients, every parameter after 3 Adam steps and the validation/tes
 counts (reference: tests/test_NCCLCommPlan.py:85-124,242-359, replicated ground truth).
 
 Covered: fp32 on the fused row-chunked executor (the headline path) in both graph
-localities; bf16 on the layer-stack path with halo recomputation off and on and the
+localities, at W = 2, 3 and 4; bf16 on the layer-stack path with halo recomputation off and on and the
 gradient support prepared (the round-2 fused bf16 path).
 """
 import argparse
@@ -87,7 +87,7 @@ def _body(rank, world, kw, dt):
     close_shmem_heaps()
     if rank != 0:
         return
-    assert got["halo"] > 0, "the W=2 partition has no halo: nothing crossed the boundary"
+    assert got["halo"] > 0, f"the W={world} partition has no halo: nothing crossed the boundary"
     assert ref["E_msg"] == got["E_msg"]
     if dt == "fp32":
         torch.testing.assert_close(got["losses"], ref["losses"], atol=1e-5, rtol=1e-5)
@@ -96,7 +96,7 @@ def _body(rank, world, kw, dt):
         # parts in another order
         for a, b in zip(got["grads"], ref["grads"]):
             rel = float((a - b).norm() / b.norm().clamp_min(1e-30))
-            assert rel < 1e-5, f"W=2 gradient differs from W=1 by {rel:.2e} (relative)"
+            assert rel < 1e-5, f"W={world} gradient differs from W=1 by {rel:.2e} (relative)"
             assert float((a - b).abs().max()) <= 1e-5 * float(b.abs().max()) + 1e-9
         # after 3 Adam steps: Adam divides by sqrt(v), so a near-zero (cancelling) gradient
         # entry whose fp32 rounding differs moves by up to a whole lr step; everything else
@@ -133,12 +133,21 @@ def test_bench_step_two_processes_one_gpu(monkeypatch, dt, kw):
     run_ranks(_body, 2, kw, dt, timeout=240)
 
 
-def test_alltoallv_shmem_two_processes(monkeypatch):
+@pytest.mark.parametrize("world", [3, 4])
+def test_bench_step_more_processes_one_gpu(monkeypatch, world):
+    """W = 3 and 4 ranks (every rank exchanging with several peers at once) against W=1."""
+    monkeypatch.setenv("DGRAPH_A2A_IMPL", "shmem")
+    monkeypatch.setenv("DGRAPH_SYMHEAP_BYTES", str(1 << 30))
+    run_ranks(_body, world, dict(global_frac=0.05), "fp32", timeout=110)
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_alltoallv_shmem_processes(monkeypatch, world):
     """The shmem transport alone: random splits, two widths, two dtypes, repeated calls
     (slot reuse across calls must not leak into the next exchange)."""
     monkeypatch.setenv("DGRAPH_A2A_IMPL", "shmem")
     monkeypatch.setenv("DGRAPH_SYMHEAP_BYTES", str(64 << 20))
-    run_ranks(_a2a_body, 2, timeout=120)
+    run_ranks(_a2a_body, world, timeout=120)
 
 
 def _a2a_body(rank, world):
