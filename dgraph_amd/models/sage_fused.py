@@ -324,8 +324,13 @@ class FusedSAGE:
         # rows while it is in flight: planned here, not discovered by the allocator
         n_send = graph.send_map.idx.numel() if graph.send_map is not None else 0
         self.n_send = n_send
+        # the input's halo exchange (once, at the first step): its send/receive blocks live
+        # next to everything planned here
+        x_tr = 4 * (n_send + H) * graph.static_halo_block(self.d0) \
+            if graph.send_map is not None else 0
         self.halo_bytes = 4 * (H * self.d0 + (self.nl - 1) * H * self.hid + n_send * self.hid)
         self.stream, self.cw, self.nbuf = False, 0, 0
+        other += x_tr
         full_ok = dev.type != "cuda" or need_h + self.halo_bytes + other + (1 << 28) <= free
         if graph.send_map is not None and (HALO_STREAM == "on" or
                                            (HALO_STREAM == "auto" and not full_ok)):

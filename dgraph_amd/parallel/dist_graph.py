@@ -194,9 +194,30 @@ class DistGraph:
             return c["recv"]
         # a weak reference, not the address: a freed tensor's storage can be reused
         c.clear()
-        c.update(ref=weakref.ref(x), version=x._version,
-                 recv=self.a2a(K.gather_rows(x, self.send_map.idx)))
+        cb = self.static_halo_block(x.shape[1], x.element_size())
+        if cb >= x.shape[1]:
+            recv = self.a2a(K.gather_rows(x, self.send_map.idx))
+        else:
+            # a large halo (structureless graph): packed and exchanged in column blocks, so
+            # the transient send/receive buffers stay small next to the kept halo rows
+            recv = torch.empty(self.a2a.total_recv, x.shape[1], dtype=x.dtype, device=x.device)
+            for c0 in range(0, x.shape[1], cb):
+                c1 = min(c0 + cb, x.shape[1])
+                recv[:, c0:c1] = self.a2a(K.gather_rows(x[:, c0:c1], self.send_map.idx))
+        c.update(ref=weakref.ref(x), version=x._version, recv=recv)
         return c["recv"]
+
+    STATIC_BLOCK_BYTES = 4 << 30
+
+    def static_halo_block(self, F: int, elem: int = 4) -> int:
+        """Column-block width of the static halo exchange: whole rows unless the packed send
+        rows exceed ``STATIC_BLOCK_BYTES``. Its transient (send + receive blocks) is
+        ``(n_send + H) * block * elem`` bytes on top of the kept ``H * F`` halo rows."""
+        n_send = self.send_map.idx.numel() if self.send_map is not None else 0
+        if n_send * F * elem <= self.STATIC_BLOCK_BYTES:
+            return F
+        cb = max(16, (self.STATIC_BLOCK_BYTES // max(n_send * elem, 1)) // 16 * 16)
+        return min(cb, F)
 
     def aggregate(self, x: torch.Tensor, mean: bool = True,
                   out: Optional[torch.Tensor] = None, static: bool = False,

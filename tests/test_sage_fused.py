@@ -167,6 +167,8 @@ def _interior_first_body(rank, world, ref_path, overlap, store="auto", stream="o
     sf.HALO_STREAM = "on" if stream != "off" else "off"
     if stream == "single":  # one ring buffer: exchange and aggregation alternate
         sf.STREAM_SHAPES = ((64, 1),)
+    if stream != "off":  # the input's static halo exchanged in 16-column blocks too
+        DistGraph.STATIC_BLOCK_BYTES = 1024
     shape = SHAPES["ogbn-papers100M"].scaled(SCALE)
     part = build_partition(shape, rank, world, "cpu", global_frac=0.05, window=64)
     csr, send, perm, L_int, loc = interior_first(part["csr"], part["L"],
