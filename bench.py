@@ -79,6 +79,9 @@ def parse():
                          "for fp32 shapes it supports")
     ap.add_argument("--no-bf16-extra", action="store_true",
                     help="skip the secondary bf16 (layer-stack) measurement of the headline graph")
+    ap.add_argument("--plan-reserve-gb", type=float, default=None,
+                    help="GB the fused executor's memory plan leaves free (default: 24 for the "
+                         "structureless extra at W > 1, else 0)")
     ap.add_argument("--global-frac", type=float, default=0.05,
                     help="fraction of uniformly random (non-local) edges of the headline "
                          "graph; the rest join ids within +-window")
@@ -268,9 +271,15 @@ class Job:
 
             if not supported(self.model, self.x):
                 raise SystemExit("[bench] --executor fused does not support this shape/dtype")
+            # a secondary graph (the structureless extra) at W > 1 plans with 24 GB of
+            # headroom: its halo sizes differ from rank to rank, and an OOM on one rank
+            # mid-step would take the whole job (and its headline line) down
+            reserve = (24 << 30) if (global_frac != args.global_frac and self.world > 1) else 0
+            if getattr(args, "plan_reserve_gb", None) is not None:
+                reserve = int(args.plan_reserve_gb * (1 << 30))
             self.fused = FusedSAGE(self.model, self.graph, self.x, self.train_idx, self.y_train,
                                    self.eval_idx, self.y_eval, self.eval_is_val, self.n_train,
-                                   release_graph=True)
+                                   release_graph=True, reserve_bytes=reserve)
         self.steppers = {}
         if getattr(args, "cuda_graph", False) and dev.type == "cuda":
             from dgraph_amd.utils.graphed import GraphedStep, make_capturable

@@ -212,7 +212,7 @@ class FusedSAGE:
     def __init__(self, model, graph: DistGraph, x: torch.Tensor, train_idx: torch.Tensor,
                  y_train: torch.Tensor, eval_idx: torch.Tensor, y_eval: torch.Tensor,
                  eval_is_val: torch.Tensor, n_train: int, chunk_rows: int = 0,
-                 release_graph: bool = False):
+                 release_graph: bool = False, reserve_bytes: int = 0):
         if not supported(model, x):
             raise ValueError("FusedSAGE: unsupported model/feature shape")
         dev = x.device
@@ -302,6 +302,9 @@ class FusedSAGE:
                 torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
         else:
             free = 64 << 30
+        # headroom the caller keeps out of the plan (a secondary measurement that must not
+        # run the device to its last GB: rank-to-rank halo sizes and allocator rounding vary)
+        free -= int(reserve_bytes)
         need_h = (self.nl - 1) * L * self.hid * 4
         self.store_sep = 2 * self.nS > L   # dZ and u do not fit in the last hidden buffer
         if self.store_sep:

@@ -16,7 +16,8 @@ from conftest import run_ranks
 def _args(**kw):
     a = argparse.Namespace(shape="ogbn-papers100M", scale=2e-5, hidden=128, layers=3, lr=1e-2,
                            dtype="fp32", global_frac=0.05, window=64, seed=0,
-                           no_overlap=False, rehearse_world=0, rehearse_rank=0)
+                           no_overlap=False, rehearse_world=0, rehearse_rank=0,
+                           executor="stack")  # the layer-stack path (fused: below)
     for k, v in kw.items():
         setattr(a, k, v)
     return a
