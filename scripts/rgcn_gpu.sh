@@ -18,7 +18,8 @@ step() {  # step <name> <timeout> <cmd...>
   echo "== $name rc=$rc"; grep -E '^\{|passed|failed|Error' "$O/$name.log" | cut -c1-900
   if fatal $rc; then echo "FATAL at $name"; exit $rc; fi
 }
-B="benchmarks/bench_rgcn.py --dtype ${DTYPE:-fp32}"
+S=benchmarks/bench_rgcn.py
+B="$S --dtype ${DTYPE:-fp32}"
 for run in ${RUNS:-tests eighth w8r1}; do
   case $run in
     tests) step tests 400 python -u -m pytest tests/test_rgcn.py tests/test_f32_kernels_gpu.py \
@@ -31,7 +32,7 @@ for run in ${RUNS:-tests eighth w8r1}; do
     prof) for p in ${PATHS:-auto}; do
             cd /tmp && export TMPDIR=/tmp
             timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv \
-              -d "$R/$O/prof_$p" -o run -- python3 "$R/$B" --path $p --scale 0.125 --steps 2 \
+              -d "$R/$O/prof_$p" -o run -- python3 "$R/$S" --dtype ${DTYPE:-fp32} --path $p --scale 0.125 --steps 2 \
               --warmup 1 > "$R/$O/prof_$p.log" 2>&1
             rc=$?; cd "$R"; echo "== prof_$p rc=$rc"
             python3 scripts/prof_summary.py "$O/prof_$p" 40 > "$O/prof_$p.txt" 2>&1
