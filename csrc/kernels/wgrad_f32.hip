@@ -209,13 +209,27 @@ __global__ __launch_bounds__(kThr, 1) void wgrad_f32_kernel(
   }  // units
 }
 
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ partials,
-                                                           int P, int64_t KN,
-                                                           float* __restrict__ out) {
+// out[i] = sum of the P slabs' element i, added in slab order (deterministic). Each lane
+// keeps 16 slab loads in flight ahead of the (ordered) adds: a 128 x 128 product over 256
+// slabs is only 64 blocks, and one dependent load per add made the reduce latency-bound
+// (63 us per call, a third of a GraphCast weight gradient: profiles/r04).
+__global__ __launch_bounds__(64) void wgrad_reduce_kernel(const float* __restrict__ partials,
+                                                          int P, int64_t KN,
+                                                          float* __restrict__ out) {
+  constexpr int D = 16;
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= KN) return;
+  const float* p = partials + i;
   float s = 0.f;
-  for (int b = 0; b < P; ++b) s += partials[b * KN + i];  // fixed block order
+  int b = 0;
+  for (; b + D <= P; b += D) {
+    float v[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) v[j] = p[static_cast<int64_t>(b + j) * KN];
+#pragma unroll
+    for (int j = 0; j < D; ++j) s += v[j];
+  }
+  for (; b < P; ++b) s += p[static_cast<int64_t>(b) * KN];
   out[i] = s;
 }
 
@@ -286,8 +300,8 @@ hipError_t wgrad_f32(const float* A1, int64_t lda1, int64_t K1, const float* A2,
 hipError_t wgrad_f32_reduce(const float* partials, int P, int64_t KN, float* out,
                             hipStream_t st) {
   if (KN <= 0) return hipSuccess;
-  const int64_t blocks = (KN + 255) / 256;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, st,
+  const int64_t blocks = (KN + 63) / 64;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(static_cast<unsigned>(blocks)), dim3(64), 0, st,
                      partials, P, KN, out);
   return hipGetLastError();
 }
