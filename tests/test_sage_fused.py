@@ -212,7 +212,8 @@ def _interior_first_body(rank, world, ref_path, overlap, store="auto", stream="o
     (2, True, "on", "off"), (2, True, "off", "off"), (4, True, "on", "off"),
     (4, True, "off", "off"), (2, False, "auto", "off"),
     # streamed halos (column blocks through a buffer ring; the structureless-graph plan)
-    (2, True, "auto", "on"), (4, True, "auto", "on"), (2, True, "auto", "single")])
+    (2, True, "auto", "on"), (4, True, "auto", "on"), (8, True, "auto", "on"),
+    (2, True, "auto", "single")])
 def test_fused_interior_first_matches_w1(ranks, world, overlap, store, stream, tmp_path):
     loss, grads, corr = _fused_grads(0, 1, gf=0.05)
     p = tmp_path / "ref.pt"
