@@ -242,7 +242,8 @@ void gemm_f32_op(const at::Tensor& A1, const at::Tensor& B1, const c10::optional
 
 void wgrad_f32_op(const at::Tensor& A1, const c10::optional<at::Tensor>& A2,
                   const c10::optional<at::Tensor>& a1_rows, const at::Tensor& G,
-                  const at::Tensor& partials, int64_t blocks, int64_t fresh_from) {
+                  const at::Tensor& partials, int64_t blocks, int64_t fresh_from,
+                  const c10::optional<at::Tensor>& col_partials) {
   f32_rows(A1, "A1");
   f32_rows(G, "G");
   same_dev(G, A1, "G");
@@ -266,12 +267,19 @@ void wgrad_f32_op(const at::Tensor& A1, const c10::optional<at::Tensor>& A2,
   TORCH_CHECK(blocks >= 1 && blocks <= partials.size(0) && fresh_from >= 0 &&
                   fresh_from <= partials.size(0),
               "wgrad_f32: 1 <= blocks <= P and 0 <= fresh_from <= P");
+  const at::Tensor* cp = opt(col_partials);
+  if (cp) {
+    same_dev(*cp, A1, "col_partials");
+    TORCH_CHECK(cp->scalar_type() == at::kFloat && cp->is_contiguous() && cp->dim() == 2 &&
+                    cp->size(0) >= partials.size(0) && cp->size(1) == N,
+                "col_partials must be contiguous float32 [>= P, N]");
+  }
   c10::DeviceGuard g(A1.device());
   DG_HIP_CHECK(wgrad_f32(A1.data_ptr<float>(), A1.stride(0), A1.size(1),
                          a2 ? a2->data_ptr<float>() : nullptr, a2 ? a2->stride(0) : 0, K2, arp,
                          G.data_ptr<float>(), G.stride(0), M, N, partials.data_ptr<float>(),
                          static_cast<int>(blocks), static_cast<int>(fresh_from),
-                         stream_of(A1)));
+                         cp ? cp->data_ptr<float>() : nullptr, stream_of(A1)));
 }
 
 void wgrad_f32_reduce_op(const at::Tensor& partials, const at::Tensor& out) {
@@ -387,7 +395,7 @@ TORCH_LIBRARY_FRAGMENT(dgraph_amd, m) {
         "Tensor? cin, float beta, Tensor? gate, Tensor? o_rows, bool relu, Tensor(a!) out, "
         "Tensor? row_scale=None) -> ()");
   m.def("wgrad_f32(Tensor A1, Tensor? A2, Tensor? a1_rows, Tensor G, Tensor(a!) partials, "
-        "int blocks, int fresh_from) -> ()");
+        "int blocks, int fresh_from, Tensor(b!)? col_partials=None) -> ()");
   m.def("wgrad_f32_reduce(Tensor partials, Tensor(a!) out) -> ()");
   m.def("row_keep_bits(Tensor h, Tensor? rows, Tensor(a!) bits) -> ()");
   m.def("apply_keep_bits(Tensor(a!) g, Tensor bits) -> ()");

@@ -268,9 +268,10 @@ bool wgrad_f32_supported(int64_t K, int64_t N);
 hipError_t wgrad_f32(const float* A1, int64_t lda1, int64_t K1, const float* A2, int64_t lda2,
                      int64_t K2, const int64_t* a1_rows, const float* G, int64_t ldg,
                      int64_t M, int64_t N, float* partials, int P, int fresh_from,
-                     hipStream_t st);
+                     float* col_partials, hipStream_t st);
 // (P row units, slab u = unit u, run by min(P, CUs) blocks pulling units dynamically; unit
-// u adds into slab u when u < fresh_from, else overwrites it)
+// u adds into slab u when u < fresh_from, else overwrites it; col_partials (nullable,
+// [P, N]): unit u's column sums of G, same accumulate rule — a bias gradient)
 hipError_t wgrad_f32_reduce(const float* partials, int P, int64_t KN, float* out,
                             hipStream_t st);
 // 1-bit ReLU keep masks of selected rows (bits.hip): F % 32 == 0, F/32 words per row.

@@ -52,7 +52,7 @@ __global__ __launch_bounds__(kThr, 1) void wgrad_f32_kernel(
     const float* __restrict__ A1, int64_t lda1, int K1, const float* __restrict__ A2,
     int64_t lda2, const int64_t* __restrict__ a1_rows, const float* __restrict__ G,
     int64_t ldg, int64_t M, int64_t rows_per_unit, int units, float* __restrict__ partials,
-    int fresh_from, int* __restrict__ unit_ctr) {
+    int fresh_from, int* __restrict__ unit_ctr, float* __restrict__ col_partials) {
   using C = WCfg<K, N>;
   constexpr int TM = C::TM, TN = C::TN, WN = C::WN;
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -147,6 +147,7 @@ __global__ __launch_bounds__(kThr, 1) void wgrad_f32_kernel(
 #pragma unroll
     for (int b = 0; b < TN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int kw = wm * TM * 16, nw = wn * TN * 16;
+  float csum = 0.f;
   if (nst > 0) {
     load_idx(0);
     load_data(0);
@@ -165,6 +166,12 @@ __global__ __launch_bounds__(kThr, 1) void wgrad_f32_kernel(
       const float* sg = sa + C::A_FL;
       // operand fragments double-buffered across MFMA steps (reads of step j+1 are in
       // flight during step j's MFMAs); rows 8 lh + j, j < 8, share srow's shift
+      if (col_partials != nullptr && tid < N) {
+        // the bias gradient's column sums ride along: column tid of this stage's G rows,
+        // added in row order (rows past the unit were stored as zeros)
+#pragma unroll 8
+        for (int rr = 0; rr < kRows; ++rr) csum += sg[srow<C::GP>(rr) + tid];
+      }
       const float* saw = sa + srow<C::AP>(8 * lh) + kw + li;
       const float* sgw = sg + srow<C::GP>(8 * lh) + nw + li;
       float av[2][TM], gv[2][TN];
@@ -206,6 +213,10 @@ __global__ __launch_bounds__(kThr, 1) void wgrad_f32_kernel(
         *p = unit < fresh_from ? *p + acc[a][b][r] : acc[a][b][r];
       }
     }
+  if (col_partials != nullptr && tid < N) {
+    float* p = col_partials + static_cast<int64_t>(unit) * N + tid;
+    *p = unit < fresh_from ? *p + csum : csum;
+  }
   }  // units
 }
 
@@ -236,7 +247,8 @@ __global__ __launch_bounds__(64) void wgrad_reduce_kernel(const float* __restric
 template <int K, int N>
 hipError_t launch_wgrad(const float* A1, int64_t lda1, int K1, const float* A2, int64_t lda2,
                         const int64_t* a1_rows, const float* G, int64_t ldg, int64_t M,
-                        float* partials, int P, int fresh_from, hipStream_t st) {
+                        float* partials, int P, int fresh_from, float* col_partials,
+                        hipStream_t st) {
   using C = WCfg<K, N>;
   auto kern = &wgrad_f32_kernel<K, N>;
   static_assert(C::BYTES <= 160 * 1024, "LDS budget");
@@ -265,7 +277,8 @@ hipError_t launch_wgrad(const float* A1, int64_t lda1, int K1, const float* A2, 
     if (ctr == nullptr) return hipErrorOutOfMemory;
   }
   hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(blocks)), dim3(kThr), C::BYTES, st, A1,
-                     lda1, K1, A2, lda2, a1_rows, G, ldg, M, rpu, P, partials, fresh_from, ctr);
+                     lda1, K1, A2, lda2, a1_rows, G, ldg, M, rpu, P, partials, fresh_from, ctr,
+                     col_partials);
   return hipGetLastError();
 }
 
@@ -280,7 +293,7 @@ bool wgrad_f32_supported(int64_t K, int64_t N) {
 hipError_t wgrad_f32(const float* A1, int64_t lda1, int64_t K1, const float* A2, int64_t lda2,
                      int64_t K2, const int64_t* a1_rows, const float* G, int64_t ldg,
                      int64_t M, int64_t N, float* partials, int P, int fresh_from,
-                     hipStream_t st) {
+                     float* col_partials, hipStream_t st) {
   const int64_t K = K1 + (A2 ? K2 : 0);
   if (!wgrad_f32_supported(K, N) || P <= 0) return hipErrorInvalidValue;
   if (K1 % 4 || !al16w(A1) || lda1 % 4 || !al16w(G) || ldg % 4) return hipErrorInvalidValue;
@@ -290,7 +303,7 @@ hipError_t wgrad_f32(const float* A1, int64_t lda1, int64_t K1, const float* A2,
 #define DG_WG(K_, N_)                                                                      \
   if (K == K_ && N == N_)                                                                  \
     return launch_wgrad<K_, N_>(A1, lda1, k1, A2, lda2, a1_rows, G, ldg, M, partials, P,  \
-                                fresh_from, st);
+                                fresh_from, col_partials, st);
   DG_WG(256, 256) DG_WG(256, 176) DG_WG(256, 192) DG_WG(256, 128)
   DG_WG(128, 256) DG_WG(128, 176) DG_WG(128, 192) DG_WG(128, 128)
 #undef DG_WG

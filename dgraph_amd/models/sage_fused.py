@@ -458,9 +458,12 @@ class FusedSAGE:
         self.acc_out_s = F32.WgradAcc(self.hid, self.Cg, dev)
         self.acc_out_n = F32.WgradAcc(self.hid, self.Cg, dev)
         kh = self.hid if self.nl == 3 else self.d0
-        self.acc_hid_s = F32.WgradAcc(kh, self.hid, dev)
+        # (the bias gradients are the column sums of the same G: computed in the same
+        # weight-gradient pass instead of separate column-sum passes)
+        self.acc_hid_s = F32.WgradAcc(kh, self.hid, dev, colsum=True)
         self.acc_hid_n = F32.WgradAcc(kh, self.hid, dev)
-        self.acc_in = F32.WgradAcc(2 * self.d0, self.hid, dev) if self.nl == 3 else None
+        self.acc_in = F32.WgradAcc(2 * self.d0, self.hid, dev, colsum=True) \
+            if self.nl == 3 else None
         self.row_loss = torch.zeros(nT, **f)
         self.hit = torch.zeros(self.E.numel(), dtype=torch.uint8, device=dev)
         self.E_val_l = self.E_val.long()
@@ -905,7 +908,6 @@ class FusedSAGE:
         ws1, wn1, _ = P[lh]
         hin_l = x if lh == 0 else self.h[lh - 1]
         hin_l_halo = halos[lh]
-        gw[(lh, 2)] = K.col_sum(dZ)
         u = None
         work = None
         if nl == 3:
@@ -948,6 +950,7 @@ class FusedSAGE:
         self.edges_aggregated += self.nnz_S
         gw[(lh, 0)] = self.acc_hid_s.result()
         gw[(lh, 1)] = self.acc_hid_n.result()
+        gw[(lh, 2)] = self.acc_hid_s.col_result()
         if lh == 0:
             gw[(0, 0)], gw[(0, 1)] = gw[(0, 0)][:self.d0_in], gw[(0, 1)][:self.d0_in]
         if nl == 3:
@@ -976,7 +979,6 @@ class FusedSAGE:
         ws1_t = ws1.detach().t().contiguous()
         self._mark("bwd_l0")
         self.acc_in.reset()
-        db0s = []
         h1 = self.h[0]
         x_halo = halos[0] if self.adj.mid is not None else None
         # the support rows' own term dZ1 Ws1^T, once over S (one full-size GEMM instead
@@ -1019,12 +1021,11 @@ class FusedSAGE:
                 self._gemm(dZ[s0:s1], ws1_t, cin=gz, o_rows=self.ch_Sloc[ci],
                            gate=h1[r0:r1], out=gz)
             self.acc_in.add(x[r0:r1], gz, A2=a0)
-            db0s.append(K.col_sum(gz))
         if not waited:
             self._mark("exchange_bwd_l0")
             work.wait()
             self._mark("bwd_l0")
-        db0 = torch.stack(db0s).sum(0) if db0s else torch.zeros(hid, device=dev)
+        db0 = self.acc_in.col_result()
         self.edges_aggregated += self.nnz_it + \
             (self.send_st.nnz if self.send_st is not None else 0) + \
             (0 if self.agg0 is not None else self.nnz_it + self.nnz_h)

@@ -179,19 +179,26 @@ class _WgradTile:
     units, one fp32 partial slab each, pulled dynamically by at most one block per CU),
     reduced once in unit order — deterministic for a fixed chunking."""
 
-    def __init__(self, K: int, N: int, device, units: int):
+    def __init__(self, K: int, N: int, device, units: int, colsum: bool = False):
         self.K, self.N = K, N
         self.partials = torch.empty(units, K, N, dtype=torch.float32, device=device)
+        # G's column sums per unit (a bias gradient), computed by the same kernel pass
+        self.col = torch.empty(units, N, dtype=torch.float32, device=device) if colsum \
+            else None
         self.used = 0
 
     def add(self, A1, G, A2, a1_rows, min_rows: int) -> None:
         P = self.partials.shape[0]
         nb = max(1, min(P, -(-G.shape[0] // min_rows)))
-        _native.ops().wgrad_f32(A1, A2, a1_rows, G, self.partials, nb, self.used)
+        _native.ops().wgrad_f32(A1, A2, a1_rows, G, self.partials, nb, self.used, self.col)
         self.used = max(self.used, nb)
 
     def result(self, out: torch.Tensor) -> torch.Tensor:
         _native.ops().wgrad_f32_reduce(self.partials[: self.used], out)
+        return out
+
+    def col_result(self, out: torch.Tensor) -> torch.Tensor:
+        _native.ops().wgrad_f32_reduce(self.col[: self.used].unsqueeze(1), out)
         return out
 
 
@@ -216,9 +223,10 @@ class WgradAcc:
 
     _P = 0
 
-    def __init__(self, K: int, N: int, device, blocks: int = 0):
+    def __init__(self, K: int, N: int, device, blocks: int = 0, colsum: bool = False):
         self.K, self.N, self.device = int(K), int(N), torch.device(device)
         self.fresh = True
+        self.colsum = bool(colsum)
         self.tiles = []
         if self.device.type == "cuda":
             if blocks <= 0:
@@ -229,10 +237,13 @@ class WgradAcc:
             nb = _blocks(self.N, _wgrad_n_ok)
             for k0, k1 in kb:
                 for n0, n1 in nb:
+                    # the column sums ride on the first K-block of every N-block
                     self.tiles.append(((k0, k1), (n0, n1),
-                                       _WgradTile(k1 - k0, n1 - n0, self.device, blocks)))
+                                       _WgradTile(k1 - k0, n1 - n0, self.device, blocks,
+                                                  colsum=self.colsum and k0 == 0)))
         else:
             self.partials = torch.zeros(1, self.K, self.N, dtype=torch.float64)
+            self.cols = torch.zeros(self.N, dtype=torch.float64)
 
     def reset(self):
         self.fresh = True
@@ -266,7 +277,34 @@ class WgradAcc:
                 self.partials[0].copy_(p)
             else:
                 self.partials[0] += p
+            if self.colsum:
+                cs = G.double().sum(0)
+                if self.fresh:
+                    self.cols.copy_(cs)
+                else:
+                    self.cols += cs
         self.fresh = False
+
+    def col_result(self, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Column sums of every G added since the last reset (``colsum=True``): the bias
+        gradient that goes with the weight gradient, from the same kernel pass."""
+        if not self.colsum:
+            raise ValueError("WgradAcc: built without colsum")
+        if out is None:
+            out = torch.empty(self.N, dtype=torch.float32, device=self.device)
+        if self.fresh:
+            return out.zero_()
+        if self.device.type == "cuda":
+            for (k0, k1), (n0, n1), t in self.tiles:
+                if k0 == 0:
+                    if (n0, n1) == (0, self.N):
+                        t.col_result(out)
+                    else:
+                        blk = torch.empty(n1 - n0, dtype=torch.float32, device=self.device)
+                        out[n0:n1] = t.col_result(blk)
+        else:
+            out.copy_(self.cols.to(out.dtype))
+        return out
 
     def result(self, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         if out is None:

@@ -319,7 +319,7 @@ def test_wgrad_tiles_vs_fp64(K1, K2, N):
     rows = torch.randperm(6000, generator=g)[:M]
     A2 = torch.randn(M, K2, generator=g)
     G = torch.randn(M, N, generator=g)
-    acc = F32.WgradAcc(K1 + K2, N, DEV)
+    acc = F32.WgradAcc(K1 + K2, N, DEV, colsum=True)
     half = M // 2
     acc.add(src.to(DEV), G[:half].to(DEV), A2[:half].to(DEV), rows[:half].to(DEV))
     acc.add(src.to(DEV), G[half:].to(DEV), A2[half:].to(DEV), rows[half:].to(DEV))
@@ -327,6 +327,13 @@ def test_wgrad_tiles_vs_fp64(K1, K2, N):
     a = torch.cat([src.double()[rows], A2.double()], 1)
     ref = a.t() @ G.double()
     torch.testing.assert_close(out.double().cpu(), ref, atol=5e-3, rtol=1e-5)
+    # the fused column sums (bias gradient) of the same G
+    torch.testing.assert_close(acc.col_result().double().cpu(), G.double().sum(0),
+                               atol=1e-3, rtol=1e-5)
+    acc.reset()  # a fresh accumulation overwrites every slab it uses
+    acc.add(src.to(DEV), G[:100].to(DEV), A2[:100].to(DEV), rows[:100].to(DEV))
+    torch.testing.assert_close(acc.col_result().double().cpu(), G[:100].double().sum(0),
+                               atol=1e-4, rtol=1e-5)
 
 
 @pytest.mark.parametrize("hidden,feat,layers", [(512, 300, 3), (128, 100, 2), (384, 768, 3)])
