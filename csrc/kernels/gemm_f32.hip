@@ -57,13 +57,15 @@ constexpr int kBK = 32;
 template <int BM, int N>
 struct GCfg;
 // (BM, N): (TM, TN, WM, WN) with 16*TM*WM = BM and 16*TN*WN = N; threads = 64*WM*WN
+// (a 4-wave block with a 128 x 128 tile per wave — 256 accumulators, one wave per SIMD —
+// compiles to 256 VGPRs + 256 AGPRs with scratch spills on gfx950/hipcc 7.2: not used)
 template <> struct GCfg<256, 256> { static constexpr int TM = 4, TN = 8, WM = 4, WN = 2; };
 template <> struct GCfg<256, 192> { static constexpr int TM = 4, TN = 6, WM = 4, WN = 2; };
 template <> struct GCfg<256, 176> { static constexpr int TM = 2, TN = 11, WM = 8, WN = 1; };
 template <> struct GCfg<256, 128> { static constexpr int TM = 2, TN = 8, WM = 8, WN = 1; };
 template <> struct GCfg<256, 64> { static constexpr int TM = 2, TN = 4, WM = 8, WN = 1; };
-template <int BM>
-constexpr int threads_of() { return 512; }
+template <int BM, int N>
+constexpr int threads_of() { return 64 * GCfg<BM, N>::WM * GCfg<BM, N>::WN; }
 
 // A stage: 16-B chunk c of row r lives at chunk a_chunk(r, c) of the row (XOR swizzle by
 // row pair; table found by exhaustive search over the ds_read_b128 lane groups)
@@ -74,7 +76,7 @@ __device__ __forceinline__ int a_chunk(int r, int c) {
 
 template <int BM, int N>
 struct GLds {
-  static constexpr int kThreads = threads_of<BM>();
+  static constexpr int kThreads = threads_of<BM, N>();
   static constexpr int BP = N + 16;  // B stage row pitch (floats): room for b_row's shift
   static constexpr int A_FL = BM * kBK;                 // A stage floats
   static constexpr int B_FL = kBK * BP;                 // B stage floats
@@ -133,15 +135,17 @@ __device__ __forceinline__ void gemm_f32_body(
   // l%8 of the row, which holds global chunk (l%8) ^ swz(row): the A swizzle moved to the
   // per-lane SOURCE address) and 4 B rows (row kr = 4w + u, lane l < N/4 -> columns
   // 4l..4l+3). Row indices are 32-bit (the launcher checks every operand has < 2^31 rows).
-  static_assert(kThreads == 512 && kBM == 256 && kBK == 32, "staging map");
-  int32_t a_src_row[4];   // A1 rows of the tile being loaded (through a_rows)
-  int32_t nx_src_row[4];  // the next tile's A1 rows (index loads issued early)
+  constexpr int NW = kThreads / 64;  // waves
+  constexpr int PW = 32 / NW;         // A pieces and B rows per wave per stage
+  static_assert(32 % NW == 0 && kBM == 256 && kBK == 32, "staging map");
+  int32_t a_src_row[PW];   // A1 rows of the tile being loaded (through a_rows)
+  int32_t nx_src_row[PW];  // the next tile's A1 rows (index loads issued early)
   int64_t ld_tile = tile; // the tile whose stages issue_stage reads (A2 rows dense)
   const int a_slot = lane & 7;
   auto rows_of = [&](int64_t t, int32_t* a1) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      int64_t r = t * kBM + (4 * wave + u) * 8 + (lane >> 3);
+    for (int u = 0; u < PW; ++u) {
+      int64_t r = t * kBM + (PW * wave + u) * 8 + (lane >> 3);
       r = r < M ? r : M - 1;  // rows past M read a valid row (never stored)
       a1[u] = static_cast<int32_t>(a_rows ? a_rows[r] : r);
     }
@@ -156,19 +160,19 @@ __device__ __forceinline__ void gemm_f32_body(
     float* sa = lds + buf * L::STAGE;
     float* sb = sa + L::A_FL;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int r = (4 * wave + u) * 8 + (lane >> 3);  // row within the tile
+    for (int u = 0; u < PW; ++u) {
+      const int r = (PW * wave + u) * 8 + (lane >> 3);  // row within the tile
       int64_t r2 = ld_tile * kBM + r;
       r2 = r2 < M ? r2 : M - 1;
       const int64_t ar = first ? static_cast<int64_t>(a_src_row[u]) : r2;
       const int c = a_chunk(r, a_slot);  // XOR swizzle: its own inverse
-      glds16(Ab + ar * lda + ka + c * 4, sa + (4 * wave + u) * 8 * kBK);
+      glds16(Ab + ar * lda + ka + c * 4, sa + (PW * wave + u) * 8 * kBK);
     }
     const float* Bb = first ? B1 : B2;
     const int64_t ldb = first ? ldb1 : ldb2;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int kr = 4 * wave + u;
+    for (int u = 0; u < PW; ++u) {
+      const int kr = PW * wave + u;
       if (lane < N / 4)
         glds16(Bb + static_cast<int64_t>(ka + kr) * ldb + lane * 4, sb + b_row<L::BP>(kr));
     }
@@ -207,7 +211,7 @@ __device__ __forceinline__ void gemm_f32_body(
       const bool last = s + 1 == nst;
       const bool switch_tile = last && has_next;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) a_src_row[u] = switch_tile ? nx_src_row[u] : a_src_row[u];
+      for (int u = 0; u < PW; ++u) a_src_row[u] = switch_tile ? nx_src_row[u] : a_src_row[u];
       ld_tile = switch_tile ? next : ld_tile;
       // the other buffer was last read in the previous stage (before its barrier)
       issue_stage(last ? 0 : s + 1, buf ^ 1);
@@ -293,7 +297,7 @@ __device__ __forceinline__ void gemm_f32_body(
       o_rows, row_scale, out, ldo, M, tile_ctr
 
 template <int N, bool HAS_A2, bool RELU, bool HAS_BIAS, bool HAS_CIN, bool HAS_GATE>
-__global__ __launch_bounds__(512, 1) void gemm_f32_kernel(DG_GEMM_F32_ARGS) {
+__global__ __launch_bounds__((threads_of<256, N>()), 1) void gemm_f32_kernel(DG_GEMM_F32_ARGS) {
   gemm_f32_body<256, N, HAS_A2, RELU, HAS_BIAS, HAS_CIN, HAS_GATE>(DG_GEMM_F32_PASS);
 }
 
@@ -330,7 +334,7 @@ hipError_t launch_gemm_f32(const float* A1, int64_t lda1, int K1, const float* B
     ctr = work_counter(st);
     if (ctr == nullptr) return hipErrorOutOfMemory;
   }
-  hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(blocks)), dim3(512), lds, st, A1,
+  hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(blocks)), dim3((threads_of<256, N>())), lds, st, A1,
                      lda1, K1, B1, ldb1, A2, lda2, K2, B2, ldb2, a_rows, bias, cin, ldc, beta,
                      gate, ldg, o_rows, rsc, out, ldo, M, ctr);
   return hipGetLastError();
