@@ -861,7 +861,8 @@ class FusedSAGE:
             tl = self.ch_Tloc[ci]
             dzt = self.dz[t0:t1]
             F32.xent_rows(z, tl, self.yT[t0:t1], self.inv_n, dzt, self.row_loss[t0:t1], C)
-            self.acc_out_s.add(hl, dzt, a1_rows=self.T[t0:t1])
+            # (the self-term weight gradient h[T]^T dz runs once over all loss rows in the
+            # backward; the aggregate rows a[T] exist only per chunk)
             self.acc_out_n.add(a, dzt, a1_rows=tl)
         e0, e1 = self.ch_E[ci]
         if e1 > e0:
@@ -876,6 +877,7 @@ class FusedSAGE:
         F32.row_keep_bits(hlast, self.S, self.bits)  # the last hidden ReLU derivative on S
         del hl_halo, halos[-1]
         gw = {}
+        self.acc_out_s.add(hlast, self.dz, a1_rows=self.T)  # one call over every loss row
         dws2 = self.acc_out_s.result()[:, :C]
         dwn2 = self.acc_out_n.result()[:, :C]
         gw[(nl - 1, 0)], gw[(nl - 1, 1)] = dws2, dwn2
