@@ -26,13 +26,17 @@ from . import f32 as F32
 from . import kernels as K
 
 
-def _wgrad(g: torch.Tensor, y: torch.Tensor, W: torch.Tensor) -> torch.Tensor:
-    """``g^T y`` in W's layout [N, K]."""
-    dW = F32.linear_wgrad(g, y, W)
-    if dW is not None:
-        return dW
+def _wgrad(g: torch.Tensor, y: torch.Tensor, W: torch.Tensor, bias: bool = False):
+    """``g^T y`` in W's layout [N, K] (``bias``: and ``g``'s column sums, from the same
+    kernel pass on the GPU)."""
+    r = F32.linear_wgrad(g, y, W, bias=bias)
+    if r is not None:
+        return r
     adt = torch.float64 if g.dtype == torch.float64 else torch.float32
-    return (g.t().to(adt) @ y.to(adt)).to(W.dtype)
+    dW = (g.t().to(adt) @ y.to(adt)).to(W.dtype)
+    if not bias:
+        return dW
+    return dW, (K.col_sum(g) if g.is_cuda else g.sum(0))
 
 
 class _ActLinearsFn(Function):
@@ -67,12 +71,17 @@ class _ActLinearsFn(Function):
         gs_c = [None if g is None else (g if g.stride(1) == 1 and g.is_contiguous()
                                         else g.contiguous()) for g in gs]
         dWs = []
-        for g, W in zip(gs_c, Ws):
-            dWs.append(None if g is None else _wgrad(g, y, W))
         db = None
-        if ctx.has_bias and ctx.needs_input_grad[3] and gs_c[0] is not None:
-            g0 = gs_c[0]
-            db = (K.col_sum(g0) if g0.is_cuda else g0.sum(0)).to(Ws[0].dtype)
+        want_b = ctx.has_bias and ctx.needs_input_grad[3] and gs_c[0] is not None
+        for i, (g, W) in enumerate(zip(gs_c, Ws)):
+            if g is None:
+                dWs.append(None)
+            elif i == 0 and want_b:
+                dW, db = _wgrad(g, y, W, bias=True)
+                dWs.append(dW)
+                db = db.to(Ws[0].dtype)
+            else:
+                dWs.append(_wgrad(g, y, W))
         dx = dgamma = dbeta = None
         need_x = ctx.needs_input_grad[0] or (st is not None and (ctx.needs_input_grad[1]
                                                                  or ctx.needs_input_grad[2]))

@@ -135,8 +135,14 @@ class _LinearFn(torch.autograd.Function):
         dx = dW = db = None
         if ctx.needs_input_grad[0]:
             dx = F32.linear_dgrad([g2], [W]).reshape(x.shape)
+        want_b = ctx.has_b and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1]:
-            dW = F32.linear_wgrad(g2, x2, W)  # fp32: split-M MFMA accumulator
+            # fp32: split-M MFMA accumulator (and the bias gradient from the same pass)
+            dW = F32.linear_wgrad(g2, x2, W, bias=want_b)
+            if isinstance(dW, tuple):
+                dW, db = dW
+                db = db.to(W.dtype)
+                want_b = False
             if dW is None and g2.is_cuda:
                 # >= 8M rows (R-GCN relation linears): the 2^14-row split-K default
                 # (1/8 MAG240M step 378 -> 357 ms); fewer rows (GraphCast, 1-2M): >= 4096
@@ -147,7 +153,7 @@ class _LinearFn(torch.autograd.Function):
                 dW = g2.t().to(torch.float64 if g2.dtype == torch.float64 else torch.float32) @ \
                     x2.to(torch.float64 if g2.dtype == torch.float64 else torch.float32)
             dW = dW.to(W.dtype)
-        if ctx.has_b and ctx.needs_input_grad[2]:
+        if want_b:
             db = (col_sum_f32(g2) if g2.is_cuda else g2.sum(0)).to(W.dtype)
         return dx, dW, db
 

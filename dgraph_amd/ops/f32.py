@@ -382,14 +382,16 @@ def linear_dgrad(gs, Ws) -> torch.Tensor:
     return out
 
 
-def linear_wgrad(g: torch.Tensor, x: torch.Tensor, W: torch.Tensor):
+def linear_wgrad(g: torch.Tensor, x: torch.Tensor, W: torch.Tensor, bias: bool = False):
     """``g^T x`` in W's layout [N, K] (split-M MFMA accumulator), or None when the kernels
-    do not tile the shape (callers then use their own library path)."""
+    do not tile the shape (callers then use their own library path). ``bias``: returns
+    ``(dW, g.sum(0))``, the column sums from the same kernel pass."""
     N, K = W.shape
     if _on(g, x) and wgrad_ok(K, N):
-        acc = WgradAcc(K, N, g.device)
+        acc = WgradAcc(K, N, g.device, colsum=bias)
         acc.add(x, g)
-        return acc.result().t().contiguous().to(W.dtype)
+        dW = acc.result().t().contiguous().to(W.dtype)
+        return (dW, acc.col_result()) if bias else dW
     return None
 
 
