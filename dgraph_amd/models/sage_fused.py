@@ -79,6 +79,11 @@ BOUNDARY_STORE = os.environ.get("DGRAPH_FUSED_BOUNDARY_STORE", "auto")
 # kept at full width for the whole step — "auto" when the full-width plan does not fit (a
 # structureless graph's halo is nearly every remote vertex), "on" / "off" to force
 HALO_STREAM = os.environ.get("DGRAPH_FUSED_HALO_STREAM", "auto")
+# input-layer backward: the transposed aggregation of u (stored on the support rows S only)
+# over an adjacency compacted to the S columns once, with the columns already mapped to S
+# positions (a plain SpMM over ~S/L of the entries), instead of the column-mapped pass over
+# every entry — when the memory plan has room for it (auto), always (on) or never (off)
+COMPACT_T = os.environ.get("DGRAPH_FUSED_COMPACT_T", "auto")
 # (column block, ring buffers) of the streamed plan, in order of preference
 STREAM_SHAPES = ((64, 2), (64, 1), (32, 2), (32, 1))
 # planning rates of the "auto" choice: xGMI per link and direction, fp32 SpMM gather
@@ -128,6 +133,48 @@ def _width_at_least(c: int, widths) -> int:
         if w >= c:
             return w
     raise ValueError(f"no kernel width >= {c}")
+
+
+def _compact_by_map(rowptr: torch.Tensor, col: torch.Tensor, rowend: Optional[torch.Tensor],
+                    cmap: torch.Tensor, nrows: int, count_only: bool = False):
+    """Entries ``[rowptr[r], rowend[r] or rowptr[r + 1])`` of rows ``r < nrows`` whose column
+    maps (``cmap[c] >= 0``), in entry order, with the column replaced by ``cmap[c]``:
+    ``(rowptr int64 [nrows + 1], col int32)``. Row chunks of ~2^26 entries (bounded
+    temporaries). ``count_only``: just the number of kept entries."""
+    dev = col.device
+    start = rowptr[:nrows]
+    deg = (rowend[:nrows] if rowend is not None else rowptr[1:nrows + 1]) - start
+    total = int(deg.sum())
+    step = max(1, int(nrows * (1 << 26) // max(total, 1)))
+    chunks = [(r0, min(nrows, r0 + step)) for r0 in range(0, nrows, step)]
+
+    def entries(r0, r1):
+        d = deg[r0:r1]
+        n = int(d.sum())
+        if n == 0:
+            return None, None
+        rows = torch.repeat_interleave(torch.arange(r1 - r0, device=dev), d, output_size=n)
+        first = torch.cumsum(d, 0) - d
+        pos = start[r0:r1][rows] + torch.arange(n, device=dev) - first[rows]
+        m = cmap[col[pos].long()]
+        return rows, m
+
+    counts = torch.zeros(nrows, dtype=torch.long, device=dev)
+    for r0, r1 in chunks:
+        rows, m = entries(r0, r1)
+        if rows is not None:
+            counts[r0:r1] = torch.bincount(rows[m >= 0], minlength=r1 - r0)
+    if count_only:
+        return int(counts.sum())
+    rp = torch.zeros(nrows + 1, dtype=torch.long, device=dev)
+    torch.cumsum(counts, 0, out=rp[1:])
+    del counts
+    out = torch.empty(int(rp[-1]), dtype=torch.int32, device=dev)
+    for r0, r1 in chunks:
+        rows, m = entries(r0, r1)
+        if rows is not None:
+            out[int(rp[r0]):int(rp[r1])] = m[m >= 0].to(torch.int32)
+    return rp, out
 
 
 class _Adj:
@@ -360,6 +407,21 @@ class FusedSAGE:
                 f"{self.halo_bytes / 2**30:.1f}) + workspace {other / 2**30:.1f} GiB exceed the "
                 f"{free / 2**30:.1f} GiB free on {dev}")
         margin = 16 << 30 if dev.type == "cuda" else 0
+        # the input-layer backward's S-compacted transposed adjacency (COMPACT_T): built when
+        # it leaves at least 1 GB for the chunk arena (it shrinks the arena, not the plan)
+        self.TS = None
+        if self.nl == 3 and COMPACT_T != "off":
+            if self.itT is not None:
+                src = (self.itT.rowptr, self.itT.col, None)
+            else:
+                src = (self.adj.rp, self.adj.col, self.adj.mid)
+            nnz_ts = _compact_by_map(src[0], src[1], src[2], self.smap, L, count_only=True) \
+                if L else 0
+            ts_bytes = nnz_ts * 4 + (L + 1) * 8
+            room = free - need_h - other - (1 << 28)
+            if COMPACT_T == "on" or dev.type != "cuda" or room - ts_bytes >= (1 << 30):
+                self.TS = _compact_by_map(src[0], src[1], src[2], self.smap, L)
+                other += ts_bytes
         # W > 1: a whole-layer aggregate buffer lets the interior part of the OUTPUT layer's
         # boundary rows run while its halo rows are in flight (hidden layers use their own
         # output buffer for that)
@@ -518,7 +580,7 @@ class FusedSAGE:
                 "boundary_store": dict(self.use_store),
                 "halo_stream": ({"column_block": self.cw, "buffers": self.nbuf}
                                 if self.stream else False),
-                "keep_agg0": self.agg0 is not None}
+                "keep_agg0": self.agg0 is not None, "compact_T": self.TS is not None}
 
     # ------------------------------------------------------------------ helpers
     def _gemm(self, A1, B1, A2=None, B2=None, **kw):
@@ -1001,7 +1063,9 @@ class FusedSAGE:
             gz = self.bufB[:n, :hid]
             sa = dict(gate=h1[r0:r1], self_add=v, self_map=self.smap if v is not None else None,
                       self_row0=r0)
-            if self.itT is not None:
+            if self.TS is not None:
+                self._spmm(self.TS[0][r0:r1 + 1], self.TS[1], u, gz, **sa)
+            elif self.itT is not None:
                 self._spmm(self.itT.rowptr[r0:r1 + 1], self.itT.col, u, gz, col_map=self.smap,
                            **sa)
             else:
