@@ -422,6 +422,19 @@ class FusedSAGE:
             if COMPACT_T == "on" or dev.type != "cuda" or room - ts_bytes >= (1 << 30):
                 self.TS = _compact_by_map(src[0], src[1], src[2], self.smap, L)
                 other += ts_bytes
+        # the same for the halo rows' transposed aggregation of u (the reverse exchange's
+        # payload, computed before the S-row work so the exchange overlaps it)
+        self.HTS = None
+        if self.TS is not None and self.haloT is not None:
+            Hn = self.haloT.rowptr.numel() - 1
+            nnz_h = _compact_by_map(self.haloT.rowptr, self.haloT.col, None, self.smap, Hn,
+                                    count_only=True)
+            hts_bytes = nnz_h * 4 + (Hn + 1) * 8
+            if COMPACT_T == "on" or dev.type != "cuda" or \
+                    free - need_h - other - (1 << 28) - hts_bytes >= (1 << 30):
+                self.HTS = _compact_by_map(self.haloT.rowptr, self.haloT.col, None, self.smap,
+                                           Hn)
+                other += hts_bytes
         # W > 1: a whole-layer aggregate buffer lets the interior part of the OUTPUT layer's
         # boundary rows run while its halo rows are in flight (hidden layers use their own
         # output buffer for that)
@@ -580,7 +593,8 @@ class FusedSAGE:
                 "boundary_store": dict(self.use_store),
                 "halo_stream": ({"column_block": self.cw, "buffers": self.nbuf}
                                 if self.stream else False),
-                "keep_agg0": self.agg0 is not None, "compact_T": self.TS is not None}
+                "keep_agg0": self.agg0 is not None, "compact_T": self.TS is not None,
+                "compact_halo_T": self.HTS is not None}
 
     # ------------------------------------------------------------------ helpers
     def _gemm(self, A1, B1, A2=None, B2=None, **kw):
@@ -801,7 +815,11 @@ class FusedSAGE:
             c0, c1 = blocks[k]
             b = k % nb
             hg = self.ring_recv[b]
-            self._spmm(self.haloT.rowptr, self.haloT.col, u[:, c0:c1], hg, col_map=self.smap)
+            if self.HTS is not None:
+                self._spmm(self.HTS[0], self.HTS[1], u[:, c0:c1], hg)
+            else:
+                self._spmm(self.haloT.rowptr, self.haloT.col, u[:, c0:c1], hg,
+                           col_map=self.smap)
             return self._on_comm_stream(
                 lambda: g.a2a_rev(hg, out=self.ring_send[b], async_op=True))
 
@@ -987,8 +1005,11 @@ class FusedSAGE:
             elif self.haloT is not None:
                 # the output layer's received halo rows are dead: its buffer sends, the
                 # forward send buffer receives
-                hg1 = self._spmm(self.haloT.rowptr, self.haloT.col, u, self.halo_buf[-1],
-                                 col_map=self.smap)
+                if self.HTS is not None:
+                    hg1 = self._spmm(self.HTS[0], self.HTS[1], u, self.halo_buf[-1])
+                else:
+                    hg1 = self._spmm(self.haloT.rowptr, self.haloT.col, u, self.halo_buf[-1],
+                                     col_map=self.smap)
                 sg1, work = g.a2a_rev(hg1, out=self.send_buf, async_op=True)
                 self.edges_aggregated += self.haloT.nnz
         self.acc_hid_s.reset()
