@@ -70,8 +70,9 @@ def main():
     smap[S] = torch.arange(S.numel(), dtype=torch.int32, device=dev)
     u = torch.randn(S.numel(), 256, device=dev)
     out = torch.empty(L, 256, device=dev)
-    timed("spmm_f32_cmap_F256", lambda: F32.spmm_f32(csr.rowptr, csr.col, u, out,
-                                                     col_map=smap, pass_cols=64))
+    for pc in (64, 128, 256):
+        timed(f"spmm_f32_cmap_F256_pc{pc}", lambda pc=pc: F32.spmm_f32(
+            csr.rowptr, csr.col, u, out, col_map=smap, pass_cols=pc))
     del u, out
     M = a.rows
     A1 = torch.randn(M, 256, device=dev)
