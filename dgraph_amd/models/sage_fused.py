@@ -605,6 +605,17 @@ class FusedSAGE:
         kw.setdefault("pass_cols", self.pass_for.get(x.shape[1], 0))
         return F32.spmm_f32(rowptr, col, x, out, **kw)
 
+    def _spmm_u(self, rowptr, col, u, out=None, **kw):
+        """SpMM reading ``u``, a gradient stored on the support rows S only (through a
+        column map, or an adjacency compacted to S): full-width passes. The operand is
+        ~S/L of a full activation, so one whole-row pass gathers about as many bytes per
+        row window as a 64-column pass over full rows, and the entries (and their column
+        map) are walked once instead of once per pass: column-mapped F=256 at 30 % of
+        rows 48.9 -> 30.2 ms (64- vs 256-column passes, profiles/r04/)."""
+        forced = int(os.environ.get("DGRAPH_FUSED_PASS_COLS", "0"))
+        kw.setdefault("pass_cols", min(forced, u.shape[1]) if forced else min(u.shape[1], 256))
+        return F32.spmm_f32(rowptr, col, u, out, **kw)
+
     def _agg(self, hin: torch.Tensor, r0: int, r1: int, out: torch.Tensor, part: str = "all",
              halo: Optional[torch.Tensor] = None, **kw) -> torch.Tensor:
         """``out = mean over in-neighbours`` of rows [r0, r1), ``part`` of each row's entries
@@ -816,10 +827,10 @@ class FusedSAGE:
             b = k % nb
             hg = self.ring_recv[b]
             if self.HTS is not None:
-                self._spmm(self.HTS[0], self.HTS[1], u[:, c0:c1], hg)
+                self._spmm_u(self.HTS[0], self.HTS[1], u[:, c0:c1], hg)
             else:
-                self._spmm(self.haloT.rowptr, self.haloT.col, u[:, c0:c1], hg,
-                           col_map=self.smap)
+                self._spmm_u(self.haloT.rowptr, self.haloT.col, u[:, c0:c1], hg,
+                             col_map=self.smap)
             return self._on_comm_stream(
                 lambda: g.a2a_rev(hg, out=self.ring_send[b], async_op=True))
 
@@ -971,10 +982,10 @@ class FusedSAGE:
         work = None
         if self.sub is not None:
             ht_nz, a2a_sub, stc, stc_rows = self.sub
-            hg = self._spmm(ht_nz.rowptr, ht_nz.col, u2)
+            hg = self._spmm_u(ht_nz.rowptr, ht_nz.col, u2)
             sg, work = a2a_sub(hg, async_op=True)
             self.edges_aggregated += ht_nz.nnz
-        self._spmm(self.AT_S.rowptr, self.AT_S.col, u2, dZ)
+        self._spmm_u(self.AT_S.rowptr, self.AT_S.col, u2, dZ)
         self.edges_aggregated += self.AT_S.nnz
         if work is not None:
             self._mark("exchange_bwd_out")
@@ -1006,10 +1017,10 @@ class FusedSAGE:
                 # the output layer's received halo rows are dead: its buffer sends, the
                 # forward send buffer receives
                 if self.HTS is not None:
-                    hg1 = self._spmm(self.HTS[0], self.HTS[1], u, self.halo_buf[-1])
+                    hg1 = self._spmm_u(self.HTS[0], self.HTS[1], u, self.halo_buf[-1])
                 else:
-                    hg1 = self._spmm(self.haloT.rowptr, self.haloT.col, u, self.halo_buf[-1],
-                                     col_map=self.smap)
+                    hg1 = self._spmm_u(self.haloT.rowptr, self.haloT.col, u, self.halo_buf[-1],
+                                       col_map=self.smap)
                 sg1, work = g.a2a_rev(hg1, out=self.send_buf, async_op=True)
                 self.edges_aggregated += self.haloT.nnz
         self.acc_hid_s.reset()
@@ -1085,13 +1096,13 @@ class FusedSAGE:
             sa = dict(gate=h1[r0:r1], self_add=v, self_map=self.smap if v is not None else None,
                       self_row0=r0)
             if self.TS is not None:
-                self._spmm(self.TS[0][r0:r1 + 1], self.TS[1], u, gz, **sa)
+                self._spmm_u(self.TS[0][r0:r1 + 1], self.TS[1], u, gz, **sa)
             elif self.itT is not None:
-                self._spmm(self.itT.rowptr[r0:r1 + 1], self.itT.col, u, gz, col_map=self.smap,
-                           **sa)
+                self._spmm_u(self.itT.rowptr[r0:r1 + 1], self.itT.col, u, gz,
+                             col_map=self.smap, **sa)
             else:
                 rp, re = self.adj.rows(r0, r1, "int")
-                self._spmm(rp, self.adj.col, u, gz, rowend=re, col_map=self.smap, **sa)
+                self._spmm_u(rp, self.adj.col, u, gz, rowend=re, col_map=self.smap, **sa)
             sr = self.ch_send[ci]
             if self.gz_full is not None:  # streamed reverse exchange: gated, summed
                 gz.add_(self.gz_full[r0:r1])
