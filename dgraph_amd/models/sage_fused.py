@@ -606,12 +606,13 @@ class FusedSAGE:
         return F32.spmm_f32(rowptr, col, x, out, **kw)
 
     def _spmm_u(self, rowptr, col, u, out=None, **kw):
-        """SpMM reading ``u``, a gradient stored on the support rows S only (through a
-        column map, or an adjacency compacted to S): full-width passes. The operand is
-        ~S/L of a full activation, so one whole-row pass gathers about as many bytes per
-        row window as a 64-column pass over full rows, and the entries (and their column
-        map) are walked once instead of once per pass: column-mapped F=256 at 30 % of
-        rows 48.9 -> 30.2 ms (64- vs 256-column passes, profiles/r04/)."""
+        """Column-mapped SpMM reading ``u``, a gradient stored on the support rows S only:
+        full-width passes. The operand is ~S/L of a full activation, so one whole-row pass
+        gathers about as many bytes per row window as a 64-column pass over full rows, and
+        the entries and their column map are walked once instead of once per pass:
+        column-mapped F=256 at 30 % of rows 48.9 -> 30.2 ms (64- vs 256-column passes),
+        the W=1 step 1959 -> 1867 ms. Over an S-compacted adjacency (``TS``/``HTS``, no map
+        to walk) the tuned narrow passes stay faster (W=8 265.6 vs 271.1 ms)."""
         forced = int(os.environ.get("DGRAPH_FUSED_PASS_COLS", "0"))
         kw.setdefault("pass_cols", min(forced, u.shape[1]) if forced else min(u.shape[1], 256))
         return F32.spmm_f32(rowptr, col, u, out, **kw)
@@ -827,7 +828,7 @@ class FusedSAGE:
             b = k % nb
             hg = self.ring_recv[b]
             if self.HTS is not None:
-                self._spmm_u(self.HTS[0], self.HTS[1], u[:, c0:c1], hg)
+                self._spmm(self.HTS[0], self.HTS[1], u[:, c0:c1], hg)
             else:
                 self._spmm_u(self.haloT.rowptr, self.haloT.col, u[:, c0:c1], hg,
                              col_map=self.smap)
@@ -982,10 +983,10 @@ class FusedSAGE:
         work = None
         if self.sub is not None:
             ht_nz, a2a_sub, stc, stc_rows = self.sub
-            hg = self._spmm_u(ht_nz.rowptr, ht_nz.col, u2)
+            hg = self._spmm(ht_nz.rowptr, ht_nz.col, u2)
             sg, work = a2a_sub(hg, async_op=True)
             self.edges_aggregated += ht_nz.nnz
-        self._spmm_u(self.AT_S.rowptr, self.AT_S.col, u2, dZ)
+        self._spmm(self.AT_S.rowptr, self.AT_S.col, u2, dZ)
         self.edges_aggregated += self.AT_S.nnz
         if work is not None:
             self._mark("exchange_bwd_out")
@@ -1017,7 +1018,7 @@ class FusedSAGE:
                 # the output layer's received halo rows are dead: its buffer sends, the
                 # forward send buffer receives
                 if self.HTS is not None:
-                    hg1 = self._spmm_u(self.HTS[0], self.HTS[1], u, self.halo_buf[-1])
+                    hg1 = self._spmm(self.HTS[0], self.HTS[1], u, self.halo_buf[-1])
                 else:
                     hg1 = self._spmm_u(self.haloT.rowptr, self.haloT.col, u, self.halo_buf[-1],
                                        col_map=self.smap)
@@ -1096,7 +1097,7 @@ class FusedSAGE:
             sa = dict(gate=h1[r0:r1], self_add=v, self_map=self.smap if v is not None else None,
                       self_row0=r0)
             if self.TS is not None:
-                self._spmm_u(self.TS[0][r0:r1 + 1], self.TS[1], u, gz, **sa)
+                self._spmm(self.TS[0][r0:r1 + 1], self.TS[1], u, gz, **sa)
             elif self.itT is not None:
                 self._spmm_u(self.itT.rowptr[r0:r1 + 1], self.itT.col, u, gz,
                              col_map=self.smap, **sa)
