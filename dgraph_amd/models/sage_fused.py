@@ -82,8 +82,11 @@ HALO_STREAM = os.environ.get("DGRAPH_FUSED_HALO_STREAM", "auto")
 # input-layer backward: the transposed aggregation of u (stored on the support rows S only)
 # over an adjacency compacted to the S columns once, with the columns already mapped to S
 # positions (a plain SpMM over ~S/L of the entries), instead of the column-mapped pass over
-# every entry — when the memory plan has room for it (auto), always (on) or never (off)
-COMPACT_T = os.environ.get("DGRAPH_FUSED_COMPACT_T", "auto")
+# every entry — when the memory plan has room for it (auto), always (on) or never (off,
+# the default). Against the column-mapped pass at 64-column passes it cut the W=2/4/8 rank
+# step by 3-5 %; against the column-mapped pass at full width (_spmm_u) it is a tie
+# (W=8 265.6-267.6 vs 267.0 ms, W=2 1062-1068 vs 1065 ms) at a few GB more memory.
+COMPACT_T = os.environ.get("DGRAPH_FUSED_COMPACT_T", "off")
 # (column block, ring buffers) of the streamed plan, in order of preference
 STREAM_SHAPES = ((64, 2), (64, 1), (32, 2), (32, 1))
 # planning rates of the "auto" choice: xGMI per link and direction, fp32 SpMM gather
