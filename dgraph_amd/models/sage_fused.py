@@ -87,6 +87,10 @@ HALO_STREAM = os.environ.get("DGRAPH_FUSED_HALO_STREAM", "auto")
 # step by 3-5 %; against the column-mapped pass at full width (_spmm_u) it is a tie
 # (W=8 265.6-267.6 vs 267.0 ms, W=2 1062-1068 vs 1065 ms) at a few GB more memory.
 COMPACT_T = os.environ.get("DGRAPH_FUSED_COMPACT_T", "off")
+# column-mapped gradient SpMMs run full-width passes while the support S is at most this
+# share of the rows (papers100M 0.28 at W=1 and W=8: full width, step 1865 ms / 266 ms;
+# ogbn-products 0.98: 64-column passes, 71.7 vs 76.1 ms at full width)
+U_FULL_FRAC = float(os.environ.get("DGRAPH_FUSED_U_FULL_FRAC", "0.35"))
 # (column block, ring buffers) of the streamed plan, in order of preference
 STREAM_SHAPES = ((64, 2), (64, 1), (32, 2), (32, 1))
 # planning rates of the "auto" choice: xGMI per link and direction, fp32 SpMM gather
@@ -597,7 +601,7 @@ class FusedSAGE:
                 "halo_stream": ({"column_block": self.cw, "buffers": self.nbuf}
                                 if self.stream else False),
                 "keep_agg0": self.agg0 is not None, "compact_T": self.TS is not None,
-                "compact_halo_T": self.HTS is not None}
+                "compact_halo_T": self.HTS is not None, "support_rows": self.nS}
 
     # ------------------------------------------------------------------ helpers
     def _gemm(self, A1, B1, A2=None, B2=None, **kw):
@@ -617,7 +621,16 @@ class FusedSAGE:
         the W=1 step 1959 -> 1867 ms. Over an S-compacted adjacency (``TS``/``HTS``, no map
         to walk) the tuned narrow passes stay faster (W=8 265.6 vs 271.1 ms)."""
         forced = int(os.environ.get("DGRAPH_FUSED_PASS_COLS", "0"))
-        kw.setdefault("pass_cols", min(forced, u.shape[1]) if forced else min(u.shape[1], 256))
+        w = u.shape[1]
+        if forced:
+            pc = min(forced, w)
+        else:
+            # full width only while u is a small share of the rows: on ogbn-products
+            # (support ~ most rows) full-width passes lose (bwd_l0 21.3 vs 17.0 ms)
+            base = self.pass_for.get(w, 0)
+            frac = self.nS / max(self.L, 1)
+            pc = min(w, 256) if (not base or base >= w or frac <= U_FULL_FRAC) else base
+        kw.setdefault("pass_cols", pc)
         return F32.spmm_f32(rowptr, col, u, out, **kw)
 
     def _agg(self, hin: torch.Tensor, r0: int, r1: int, out: torch.Tensor, part: str = "all",
