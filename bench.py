@@ -50,8 +50,12 @@ os.environ.setdefault("PYTORCH_ALLOC_CONF", "max_split_size_mb:512")
 # stream sharing the compute stream's queue runs IN ORDER with it: the exchange is then
 # serialised with the kernels it should overlap (measured: a W=8 rank's step 355 ms with
 # 4 queues vs 309 ms with 8 or 16, the exposed exchange moving into the compute regions,
-# profiles/r04/). Override with DGRAPH_HW_QUEUES.
-os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("DGRAPH_HW_QUEUES", "8")
+# profiles/r04/). DGRAPH_HW_QUEUES overrides; an operator's GPU_MAX_HW_QUEUES is kept;
+# the effective value is recorded in the JSON line ("hw_queues").
+if os.environ.get("DGRAPH_HW_QUEUES"):
+    os.environ["GPU_MAX_HW_QUEUES"] = os.environ["DGRAPH_HW_QUEUES"]
+else:
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 import torch
 import torch.distributed as dist
@@ -715,8 +719,13 @@ def main():
                               "fp32 storage and compute (exact-f32 MFMA GEMMs, fp32 SpMM "
                               "accumulation), fp32 weights: the reference's precision"),
             },
+            # SURVEY §5.5 definition, L * E_directed / step (the headline value counts the
+            # symmetrised message edges, 2x as many for this undirected graph)
+            "edges_per_s_directed": args.layers * shape.num_directed_edges / (ms / 1000.0),
+            "E_directed": shape.num_directed_edges,
             "edges_aggregated_per_step": e_step,
             "edges_aggregated_per_s": e_step / (ms / 1000.0),
+            "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
             "final_loss": final_loss,
             "val_acc": val_acc,
             "test_acc": test_acc,

@@ -26,6 +26,10 @@ def main():
     ap.add_argument("--rows", type=int, default=1438388)
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--global-frac", type=float, default=0.05)
+    ap.add_argument("--xcd", default="1", help="SpMM XCD-contiguous block remap: 0, 1 or "
+                    "0,1 (A/B in one process)")
+    ap.add_argument("--pass-cols", default="64", help="SpMM pass widths, comma-separated")
+    ap.add_argument("--spmm-only", action="store_true")
     a = ap.parse_args()
     from dgraph_amd import _native
     from dgraph_amd.data.synthetic import SHAPES, build_partition
@@ -56,24 +60,34 @@ def main():
         res[name] = r
         print(name, r, flush=True)
 
-    for F in (128, 256):
-        x = torch.randn(L, F, device=dev)
-        out = torch.empty(L, F, device=dev)
-        timed(f"spmm_f32_F{F}", lambda: F32.spmm_f32(csr.rowptr, csr.col, x, out,
-                                                     row_scale=inv, pass_cols=64),
-              nbytes=csr.nnz * (F * 4 + 4) + L * F * 4)
-        del x, out
-    # column-mapped: u stored on ~30 % of the rows
     g = torch.Generator(device=dev).manual_seed(0)
     S = torch.nonzero(torch.rand(L, generator=g, device=dev) < 0.3).reshape(-1)
     smap = torch.full((L,), -1, dtype=torch.int32, device=dev)
     smap[S] = torch.arange(S.numel(), dtype=torch.int32, device=dev)
-    u = torch.randn(S.numel(), 256, device=dev)
-    out = torch.empty(L, 256, device=dev)
-    for pc in (64, 128, 256):
-        timed(f"spmm_f32_cmap_F256_pc{pc}", lambda pc=pc: F32.spmm_f32(
-            csr.rowptr, csr.col, u, out, col_map=smap, pass_cols=pc))
-    del u, out
+    for xcd in [int(v) for v in a.xcd.split(",")]:
+        _native.ops().set_f32_sched(-1, -1, xcd)
+        sfx = f"_xcd{xcd}"
+        for pcs in a.pass_cols.split(","):
+            pc = int(pcs)
+            for F in (128, 256):
+                x = torch.randn(L, F, device=dev)
+                out = torch.empty(L, F, device=dev)
+                timed(f"spmm_f32_F{F}_pc{pc}{sfx}",
+                      lambda: F32.spmm_f32(csr.rowptr, csr.col, x, out, row_scale=inv,
+                                           pass_cols=pc),
+                      nbytes=csr.nnz * (F * 4 + 4) + L * F * 4)
+                del x, out
+        # column-mapped: u stored on ~30 % of the rows
+        u = torch.randn(S.numel(), 256, device=dev)
+        out = torch.empty(L, 256, device=dev)
+        for pc in (64, 128, 256):
+            timed(f"spmm_f32_cmap_F256_pc{pc}{sfx}", lambda pc=pc: F32.spmm_f32(
+                csr.rowptr, csr.col, u, out, col_map=smap, pass_cols=pc))
+        del u, out
+    _native.ops().set_f32_sched(-1, -1, 1)
+    if a.spmm_only:
+        print(json.dumps(res))
+        return
     M = a.rows
     A1 = torch.randn(M, 256, device=dev)
     A2 = torch.randn(M, 256, device=dev)

@@ -374,16 +374,20 @@ void set_spmm_f32_config_op(int64_t rowgroup, int64_t pass_cols) {
   set_spmm_f32_config(static_cast<int>(rowgroup), static_cast<int>(pass_cols));
 }
 
-void set_f32_sched_op(int64_t spmm_grid, int64_t dynamic) {
+void set_f32_sched_op(int64_t spmm_grid, int64_t dynamic, int64_t spmm_xcd) {
   if (spmm_grid >= 0) set_spmm_f32_grid(static_cast<int>(spmm_grid));
+  if (spmm_xcd >= 0) set_spmm_f32_xcd(static_cast<int>(spmm_xcd));
   if (dynamic >= 0) set_f32_dynamic(dynamic != 0);
 }
+
+void f32_init_op() { DG_HIP_CHECK(work_counters_init()); }
 
 }  // namespace
 }  // namespace dgraph
 
 TORCH_LIBRARY_FRAGMENT(dgraph_amd, m) {
-  m.def("set_f32_sched(int spmm_grid=-1, int dynamic=-1) -> ()", &dgraph::set_f32_sched_op);
+  m.def("set_f32_sched(int spmm_grid=-1, int dynamic=-1, int spmm_xcd=-1) -> ()", &dgraph::set_f32_sched_op);
+  m.def("f32_init() -> ()", &dgraph::f32_init_op);
   m.def("set_spmm_f32_config(int rowgroup, int pass_cols=-1) -> ()",
         &dgraph::set_spmm_f32_config_op);
   m.def("spmm_f32_ex(Tensor rowptr, Tensor col, Tensor? edge_weight, Tensor? col_scale, "

@@ -43,6 +43,9 @@
 #include "kernels.h"
 #include "lds_dma.h"
 
+#include <mutex>
+#include <unordered_map>
+
 namespace dgraph {
 namespace {
 
@@ -299,6 +302,7 @@ __device__ __forceinline__ void gemm_f32_body(
 template <int N, bool HAS_A2, bool RELU, bool HAS_BIAS, bool HAS_CIN, bool HAS_GATE>
 __global__ __launch_bounds__((threads_of<256, N>()), 1) void gemm_f32_kernel(DG_GEMM_F32_ARGS) {
   gemm_f32_body<256, N, HAS_A2, RELU, HAS_BIAS, HAS_CIN, HAS_GATE>(DG_GEMM_F32_PASS);
+  work_counter_release(tile_ctr);
 }
 
 template <int N, bool HAS_A2, bool RELU, bool HAS_BIAS, bool HAS_CIN, bool HAS_GATE>
@@ -391,22 +395,47 @@ inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) =
 bool g_f32_dynamic = true;
 void set_f32_dynamic(bool on) { g_f32_dynamic = on; }
 
+namespace {
+constexpr int kCtrSlots = 1024;      // streams per device
+constexpr int kCtrStride = 16;       // ints per slot (64 B: one slot per cache line)
+int* g_ctr_ring[64] = {nullptr};
+std::mutex g_ctr_mu;
+std::unordered_map<hipStream_t, int> g_ctr_slot[64];
+
+hipError_t ctr_ring(int dev) {
+  if (g_ctr_ring[dev] != nullptr) return hipSuccess;
+  const size_t bytes = static_cast<size_t>(kCtrSlots) * kCtrStride * sizeof(int);
+  hipError_t e = hipMalloc(reinterpret_cast<void**>(&g_ctr_ring[dev]), bytes);
+  if (e != hipSuccess) {
+    g_ctr_ring[dev] = nullptr;
+    return e;
+  }
+  return hipMemset(g_ctr_ring[dev], 0, bytes);  // synchronous: zero before any launch
+}
+}  // namespace
+
+hipError_t work_counters_init() {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+  std::lock_guard<std::mutex> lk(g_ctr_mu);
+  return ctr_ring(dev);
+}
+
 int* work_counter(hipStream_t st) {
-  constexpr int kSlots = 4096;
-  static int* ring[64] = {nullptr};
-  static unsigned next[64] = {0};
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  if (ring[dev] == nullptr) {
-    if (hipMalloc(reinterpret_cast<void**>(&ring[dev]), kSlots * sizeof(int)) != hipSuccess)
-      return nullptr;
-    if (hipMemset(ring[dev], 0, kSlots * sizeof(int)) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(g_ctr_mu);
+  if (ctr_ring(dev) != hipSuccess) return nullptr;
+  auto& m = g_ctr_slot[dev];
+  auto it = m.find(st);
+  if (it == m.end()) {
+    if (static_cast<int>(m.size()) >= kCtrSlots) return nullptr;  // more streams than slots
+    it = m.emplace(st, static_cast<int>(m.size())).first;
   }
-  // consecutive launches use distinct slots (a slot is reused 4096 launches later, long after
-  // its kernel finished); the reset is ordered before the launch on the same stream
-  int* c = ring[dev] + (next[dev]++ % kSlots) * 1;
-  if (hipMemsetAsync(c, 0, sizeof(int), st) != hipSuccess) return nullptr;
-  return c;
+  // zero at every launch boundary of `st`: the previous kernel's last block reset it
+  return g_ctr_ring[dev] + static_cast<size_t>(it->second) * kCtrStride;
 }
 
 bool gemm_f32_supported(int64_t N, int64_t K1, int64_t K2) {

@@ -86,6 +86,7 @@ struct SpmmF32Args {
   const int32_t* self_map = nullptr;
   int64_t self_row0 = 0;
   int pass_cols = 0;
+  int xcd_remap = 0;  // set by the launcher (set_spmm_f32_xcd)
 };
 hipError_t spmm_f32_run(const SpmmF32Args& a, hipStream_t st);
 void set_spmm_f32_pass_cols(int cols);
@@ -93,6 +94,8 @@ void set_spmm_f32_pass_cols(int cols);
 // pass width (0 = default 64); negative arguments leave a setting unchanged
 void set_spmm_f32_config(int rowgroup, int pass_cols);
 void set_spmm_f32_grid(int blocks);   // 0 = uncapped
+// XCD-contiguous row ranges (1, default) or plain in-order blocks (0): see spmm_f32.hip
+void set_spmm_f32_xcd(int on);
 
 // Hub-row splitting (rows whose degree exceeds `cap` are aggregated in three steps):
 //   1. spmm_csr(..., cap): every row sums at most its first `cap` entries;
@@ -243,12 +246,16 @@ hipError_t dual_gemm_bs(const void* A1, int64_t lda1, const void* B1t, int64_t K
 // operands with leading dimensions % 4 == 0. a_rows / o_rows nullable int64 [M].
 // gate (nullable, [*, N] with ldg): v = gate[o(i)][n] > 0 ? v : 0. cin may alias out.
 // Work counters of the dynamically scheduled persistent kernels (gemm_f32, wgrad_f32):
-// a zeroed int32 counter for ONE launch on `st` (a slot of a per-device ring; the reset is
-// an async memset enqueued on `st`, so it is stream-ordered and graph-capturable). Blocks
-// pull tiles / row units from it, so a block that cannot start (its CU held by another
-// stream's kernel, e.g. RCCL's during a halo exchange) costs nothing: the running blocks
-// take its work.
+// the counter pair {work, blocks done} of stream `st` (one slot per stream, allocated once
+// per device; zero at every launch boundary on that stream). Blocks pull tiles / row units
+// from it, so a block that cannot start (its CU held by another stream's kernel, e.g.
+// RCCL's during a halo exchange) costs nothing: the running blocks take its work. The
+// kernel's last block to finish resets the pair (work_counter_release), so no memset is
+// enqueued per launch, a captured HIP graph replays with a zeroed slot every time, and
+// kernels of different streams never share a slot (launches on one stream serialise).
 int* work_counter(hipStream_t st);
+// Allocate the counter slots of the current device now (before any stream capture).
+hipError_t work_counters_init();
 // dynamic (work counter, default) or static (block b: tiles b, b + grid, ...) schedule of
 // the fp32 GEMM and weight-gradient kernels launched from now on
 extern bool g_f32_dynamic;

@@ -30,4 +30,19 @@ __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
+// End of a dynamically scheduled persistent block (work_counter, kernels.h): thread 0
+// counts the block done after its last pull of ctr[0]; the grid's last block resets the
+// pair, so the next launch on the stream (or the next replay of a captured graph) starts
+// from zero. Call once per block, from every thread, after the block's last work pull.
+__device__ __forceinline__ void work_counter_release(int* ctr) {
+  if (ctr == nullptr || threadIdx.x != 0) return;
+  __threadfence();  // this block's pulls of ctr[0] are ordered before its done count
+  const int d = atomicAdd(ctr + 1, 1);
+  if (d == static_cast<int>(gridDim.x) - 1) {
+    __threadfence();
+    atomicExch(ctr, 0);
+    atomicExch(ctr + 1, 0);
+  }
+}
+
 }  // namespace dgraph

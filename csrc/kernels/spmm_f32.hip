@@ -54,7 +54,19 @@ __global__ __launch_bounds__(256) void spmm_f32_rowgroup_kernel(SpmmF32Args a) {
   const int64_t nrows = a.nrows;
   const int F = a.F;
   const int64_t ngroups = (nrows + G - 1) / G;
-  const int64_t q0 = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  // XCD-contiguous rows: blocks are dealt round-robin over the 8 XCDs (b and b + 8 share
+  // one, MI355X_MICROARCH.md "Workgroup dispatch"), so in-order blocks would give every
+  // XCD's L2 every 8th row group and each neighbour row of a local window would be fetched
+  // into all 8 L2s. Remapped, the XCD of blocks b = 8k + x walks the contiguous block range
+  // [x * nb/8, (x + 1) * nb/8) in order: a row's in-window uses all hit one L2. Only for
+  // the unpersisted grid (one row group per wave); the tail past a multiple of 8 keeps its
+  // place. Placement is for speed only: any mapping is correct (a bijection).
+  int64_t blk = blockIdx.x;
+  if (a.xcd_remap) {
+    const int64_t full = static_cast<int64_t>(gridDim.x) & ~int64_t(7);
+    if (blk < full) blk = (blk & 7) * (full >> 3) + (blk >> 3);
+  }
+  const int64_t q0 = (blk * blockDim.x + threadIdx.x) >> 6;
   const int64_t qstep = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
   const int f = l * VEC;  // launcher guarantees F <= LPR * VEC
   const bool active = f < F;
@@ -237,6 +249,7 @@ __global__ __launch_bounds__(256) void spmm_f32_rowgroup_kernel(SpmmF32Args a) {
 // grid-strided, so a capped grid is a persistent one that leaves room on every CU for a
 // kernel of another stream (set_spmm_f32_grid)
 int g_f32_grid_cap = 0;
+int g_f32_xcd = 1;
 
 template <typename IdxT>
 hipError_t launch_f32_rg(const SpmmF32Args& a, hipStream_t st) {
@@ -245,7 +258,12 @@ hipError_t launch_f32_rg(const SpmmF32Args& a, hipStream_t st) {
   const int64_t G = kWave / LPR;
   const int64_t ngroups = (a.nrows + G - 1) / G;
   int64_t blocks = (ngroups + 3) / 4;  // in order: one row group per wave
-  if (g_f32_grid_cap > 0 && blocks > g_f32_grid_cap) blocks = g_f32_grid_cap;
+  SpmmF32Args ka = a;
+  ka.xcd_remap = g_f32_xcd ? 1 : 0;
+  if (g_f32_grid_cap > 0 && blocks > g_f32_grid_cap) {
+    blocks = g_f32_grid_cap;
+    ka.xcd_remap = 0;  // persistent grid-stride: blocks stay interleaved
+  }
   if (blocks > 0x7fffffff) return hipErrorInvalidValue;
   const int wmode = (a.ew != nullptr ? 1 : 0) | (a.col_scale != nullptr ? 2 : 0);
   const bool cmap = a.col_map != nullptr;
@@ -255,7 +273,7 @@ hipError_t launch_f32_rg(const SpmmF32Args& a, hipStream_t st) {
 #define DG_F32_K(LPR_, W_, C_, T_)                                                          \
   if (LPR == LPR_ && wmode == W_ && cmap == C_ && two == T_) {                              \
     hipLaunchKernelGGL((spmm_f32_rowgroup_kernel<IdxT, LPR_, W_, C_, T_>), grid, block, 0, \
-                       st, a);                                                              \
+                       st, ka);                                                             \
     return hipGetLastError();                                                               \
   }
 #define DG_F32(LPR_)                                                                        \
@@ -282,6 +300,8 @@ int g_f32_pass_cols = 64;
 void set_spmm_f32_pass_cols(int cols) { g_f32_pass_cols = cols > 0 ? cols : 64; }
 
 void set_spmm_f32_grid(int blocks) { g_f32_grid_cap = blocks > 0 ? blocks : 0; }
+
+void set_spmm_f32_xcd(int on) { g_f32_xcd = on ? 1 : 0; }
 
 bool spmm_f32_rowgroup_ok(int F, int64_t ldx, int64_t ldo, const void* x, const void* out) {
   auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) % 16) == 0; };

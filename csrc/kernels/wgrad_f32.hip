@@ -19,6 +19,7 @@
 // rows 8 apart, which a (K+4)-float pitch alone maps to the same banks (2-way conflict).
 #include "../common.h"
 #include "kernels.h"
+#include "lds_dma.h"
 
 namespace dgraph {
 namespace {
@@ -48,7 +49,7 @@ template <int P>
 __device__ __forceinline__ int srow(int r) { return r * P + ((r >> 3) & 1) * 16; }
 
 template <int K, int N>
-__global__ __launch_bounds__(kThr, 1) void wgrad_f32_kernel(
+__device__ __forceinline__ void wgrad_f32_body(
     const float* __restrict__ A1, int64_t lda1, int K1, const float* __restrict__ A2,
     int64_t lda2, const int64_t* __restrict__ a1_rows, const float* __restrict__ G,
     int64_t ldg, int64_t M, int64_t rows_per_unit, int units, float* __restrict__ partials,
@@ -218,6 +219,17 @@ __global__ __launch_bounds__(kThr, 1) void wgrad_f32_kernel(
     *p = unit < fresh_from ? *p + csum : csum;
   }
   }  // units
+}
+
+template <int K, int N>
+__global__ __launch_bounds__(kThr, 1) void wgrad_f32_kernel(
+    const float* __restrict__ A1, int64_t lda1, int K1, const float* __restrict__ A2,
+    int64_t lda2, const int64_t* __restrict__ a1_rows, const float* __restrict__ G,
+    int64_t ldg, int64_t M, int64_t rows_per_unit, int units, float* __restrict__ partials,
+    int fresh_from, int* __restrict__ unit_ctr, float* __restrict__ col_partials) {
+  wgrad_f32_body<K, N>(A1, lda1, K1, A2, lda2, a1_rows, G, ldg, M, rows_per_unit, units,
+                       partials, fresh_from, unit_ctr, col_partials);
+  work_counter_release(unit_ctr);
 }
 
 // out[i] = sum of the P slabs' element i, added in slab order (deterministic). Each lane

@@ -271,10 +271,14 @@ class FusedSAGE:
             raise ValueError("FusedSAGE: unsupported model/feature shape")
         dev = x.device
         self.dev = dev
-        if dev.type == "cuda" and os.environ.get("DGRAPH_F32_DYNAMIC") is not None:
+        if dev.type == "cuda":
             from .. import _native
 
-            _native.ops().set_f32_sched(-1, int(os.environ["DGRAPH_F32_DYNAMIC"]))
+            with torch.cuda.device(dev):
+                # the persistent kernels' work-counter slots, before any graph capture
+                _native.ops().f32_init()
+            if os.environ.get("DGRAPH_F32_DYNAMIC") is not None:
+                _native.ops().set_f32_sched(-1, int(os.environ["DGRAPH_F32_DYNAMIC"]))
         self.d0_in = x.shape[1]
         self.d0 = _in_width(self.d0_in, len(model.layers))
         if self.d0 != self.d0_in:

@@ -127,6 +127,15 @@ def gemm_f32(A1: torch.Tensor, B1: torch.Tensor, A2=None, B2=None, *, a_rows=Non
         ops = _native.ops()
         # N beyond one kernel tile (a 512-wide hidden layer): column blocks, A read per block
         blocks = [(0, N)] if N <= 256 else _blocks(N, lambda w: w in (128, 176, 192, 256))
+        if len(blocks) > 1:
+            # one kernel reads its A rows before it overwrites them (tile by tile), but a
+            # later column block would read what an earlier one wrote: an A that shares
+            # memory with out (the in-place boundary-row / streamed-halo GEMM of a wide
+            # hidden layer) is copied once first
+            if _overlaps(A1, out):
+                A1 = A1.clone()
+            if A2 is not None and _overlaps(A2, out):
+                A2 = A2.clone()
         for n0, n1 in blocks:
             full = (n0, n1) == (0, N)
             ops.gemm_f32(A1, B1 if full else B1[:, n0:n1], A2,
@@ -153,6 +162,22 @@ def gemm_f32(A1: torch.Tensor, B1: torch.Tensor, A2=None, B2=None, *, a_rows=Non
         v = v.clamp_min(0)
     out[o] = v.to(out.dtype)
     return out
+
+
+def _span(t: torch.Tensor):
+    """Byte range [lo, hi) a strided tensor's elements occupy."""
+    if t.numel() == 0:
+        return (0, 0)
+    lo = t.data_ptr()
+    hi = lo + (1 + sum((s - 1) * st for s, st in zip(t.shape, t.stride()))) * t.element_size()
+    return (lo, hi)
+
+
+def _overlaps(a: torch.Tensor, b: torch.Tensor) -> bool:
+    if a.untyped_storage().data_ptr() != b.untyped_storage().data_ptr():
+        return False
+    (a0, a1), (b0, b1) = _span(a), _span(b)
+    return a0 < b1 and b0 < a1
 
 
 def _wgrad_n_ok(n: int) -> bool:

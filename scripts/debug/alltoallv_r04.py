@@ -102,21 +102,6 @@ class _EventWork:
         return self.event.query()
 
 
-def _stream_done(t: torch.Tensor):
-    """Completion of work just enqueued on the CURRENT stream (which may be a comm side
-    stream, not the caller's compute stream): an event recorded there, so ``wait()`` orders
-    whichever stream is current at wait time after it. The contract every transport keeps:
-    a returned work's ``wait()`` orders the waiting stream after ALL device work the call
-    enqueued, on any stream (the reference's put was synchronous,
-    DGraph/distributed/Engine.py:67-86, and its halo buffer was consumed only after it
-    returned, haloExchange.py:47-62). Host-only tensors complete at once."""
-    if not t.is_cuda:
-        return _Done()
-    ev = torch.cuda.Event()
-    ev.record(torch.cuda.current_stream(t.device))
-    return _EventWork(ev)
-
-
 _SIDE: dict = {}
 
 
@@ -227,9 +212,7 @@ class AllToAllV:
                 out[:m].copy_(send[:m])
             if self.total_recv > m:
                 out[m:].zero_()
-            # the copy is stream-ordered on the current stream, which is the comm side
-            # stream when called from an overlap schedule: never a no-op wait here
-            return (out, _stream_done(out)) if async_op else out
+            return (out, _Done()) if async_op else out
         from .. import _native
 
         dev = send.device
@@ -300,8 +283,7 @@ class AllToAllV:
         heap.put_rows(send, slot, self.send_splits, self._shm_offsets)
         if self.total_recv:
             out.copy_(slot[: self.total_recv])
-        # host-ordered puts, but the copy-out is enqueued on the current stream
-        return _stream_done(out)
+        return _Done()
 
 
 def torch_alltoallv_with_comm_map(contiguous_send_tensor: torch.Tensor,

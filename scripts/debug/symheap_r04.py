@@ -155,10 +155,7 @@ class SymmetricHeap:
         """Host-level: all prior heap traffic of every rank is complete and visible
         (start-up / tear-down; the data path uses :meth:`barrier_stream`)."""
         if self.local is not None and self.local.is_cuda:
-            # the whole device, not the current stream: heap traffic (a copy-out of a
-            # receive slot) may have been enqueued on the comm side stream or on the
-            # compute stream, depending on the caller
-            torch.cuda.synchronize(self.device)
+            torch.cuda.current_stream(self.device).synchronize()
             self.check()
         if dist.is_initialized() and self.world > 1:
             dist.barrier(group=self.group)

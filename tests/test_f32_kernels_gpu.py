@@ -410,3 +410,176 @@ def test_dense_linear_f32_vs_fp64(M, K, N):
         for a, r in zip(got, ref):
             err = float((a - r).abs().max() / r.abs().max().clamp_min(1e-6))
             assert err < 2e-5, (name, err)
+
+
+# ------------------------------------------- in-place wide GEMM
+@pytest.mark.parametrize("N", [384, 512])
+def test_gemm_f32_column_blocks_in_place(N):
+    """``out is A2`` at N > 256 (the boundary-row store / streamed halo of a 384/512-wide
+    hidden layer: the aggregate rows are overwritten by the layer's output). Column block
+    0 must not feed its results to block 1 as the aggregate."""
+    g = torch.Generator().manual_seed(N + 3)
+    M, K1 = 2000, 256
+    A1 = torch.randn(M, K1, generator=g)
+    agg = torch.randn(M, N, generator=g)
+    B1 = torch.randn(K1, N, generator=g) / K1 ** 0.5
+    B2 = torch.randn(N, N, generator=g) / N ** 0.5
+    bias = torch.randn(N, generator=g)
+    ref = (A1.double() @ B1.double() + agg.double() @ B2.double() + bias.double()).clamp_min(0)
+    buf = agg.to(DEV)
+    F32.gemm_f32(A1.to(DEV), B1.to(DEV), buf, B2.to(DEV), bias=bias.to(DEV), relu=True,
+                 out=buf)
+    torch.testing.assert_close(buf.double().cpu(), ref, atol=2e-4, rtol=1e-5)
+    # a row-chunk view of a larger buffer (the executor's hout[r0:r1])
+    big = torch.zeros(M + 300, N, device=DEV)
+    big[100:100 + M] = agg.to(DEV)
+    view = big[100:100 + M]
+    F32.gemm_f32(A1.to(DEV), B1.to(DEV), view, B2.to(DEV), bias=bias.to(DEV), relu=True,
+                 out=view)
+    torch.testing.assert_close(view.double().cpu(), ref, atol=2e-4, rtol=1e-5)
+    assert float(big[:100].abs().sum()) == 0 and float(big[100 + M:].abs().sum()) == 0
+
+
+# ------------------------------- determinism under CU contention (VERDICT r4, next 2)
+def _contend(cus: int, us: float = 4000.0):
+    """A link_delay kernel holding ``cus`` CUs (one wave each, the whole-CU GEMM blocks
+    cannot start there) on another stream, issued before the kernel under test."""
+    from dgraph_amd import _native
+
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        _native.ops().link_delay(float(us), 0, int(cus))
+    return side
+
+
+def _sched(dynamic: bool):
+    from dgraph_amd import _native
+
+    _native.ops().set_f32_sched(-1, 1 if dynamic else 0)
+
+
+def _gemm_cases():
+    g = torch.Generator().manual_seed(77)
+    cases = []
+    # many tiles, gathered A1 rows, dense A2, scattered output rows, partial last tile
+    M = 256 * 256 * 2 + 777
+    src = torch.randn(M + 5000, 128, generator=g)
+    cases.append(dict(A1=src, B1=torch.randn(128, 256, generator=g) / 11,
+                      A2=torch.randn(M, 128, generator=g), B2=torch.randn(128, 256, generator=g) / 11,
+                      a_rows=torch.randperm(M + 5000, generator=g)[:M],
+                      bias=torch.randn(256, generator=g), relu=True, out_rows=M))
+    # N = 176, single operand, fewer tiles than CUs, partial last tile
+    cases.append(dict(A1=torch.randn(5000, 256, generator=g),
+                      B1=torch.randn(256, 176, generator=g) / 16, A2=None, B2=None,
+                      a_rows=None, bias=None, relu=False, out_rows=5000))
+    return cases
+
+
+@pytest.mark.parametrize("cus", [1, 16, 64])
+def test_gemm_f32_dynamic_under_contention_bitwise(cus):
+    for c in _gemm_cases():
+        d = {k: (v.to(DEV) if isinstance(v, torch.Tensor) else v) for k, v in c.items()}
+
+        def run():
+            out = torch.zeros(d["out_rows"], d["B1"].shape[1], device=DEV)
+            F32.gemm_f32(d["A1"], d["B1"], d["A2"], d["B2"], a_rows=d["a_rows"],
+                         bias=d["bias"], relu=d["relu"], out=out)
+            return out
+
+        try:
+            _sched(False)
+            ref = run()
+            torch.cuda.synchronize()
+            _sched(True)
+            for _ in range(2):
+                _contend(cus)
+                got = run()
+                torch.cuda.synchronize()
+                assert torch.equal(ref, got), cus
+        finally:
+            _sched(True)
+    # in place (out is A2, one tile width): the streamed forward's GEMM
+    g = torch.Generator().manual_seed(5)
+    M = 256 * 300 + 33
+    A1 = torch.randn(M, 256, generator=g).to(DEV)
+    agg = torch.randn(M, 256, generator=g).to(DEV)
+    B1 = (torch.randn(256, 256, generator=g) / 16).to(DEV)
+    B2 = (torch.randn(256, 256, generator=g) / 16).to(DEV)
+    try:
+        _sched(False)
+        ref = agg.clone()
+        F32.gemm_f32(A1, B1, ref, B2, relu=True, out=ref)
+        torch.cuda.synchronize()
+        _sched(True)
+        got = agg.clone()
+        _contend(cus)
+        F32.gemm_f32(A1, B1, got, B2, relu=True, out=got)
+        torch.cuda.synchronize()
+        assert torch.equal(ref, got)
+    finally:
+        _sched(True)
+
+
+@pytest.mark.parametrize("cus", [1, 16, 64])
+@pytest.mark.parametrize("K1,K2,N", [(128, 128, 256), (256, 0, 176)])
+def test_wgrad_f32_dynamic_under_contention_bitwise(cus, K1, K2, N):
+    g = torch.Generator().manual_seed(K1 + N + cus)
+    M1, M2 = 200_003, 4_321  # partial last stages, two accumulated calls
+    src = torch.randn(250_000, K1, generator=g).to(DEV)
+    rows = torch.randperm(250_000, generator=g)[:M1].to(DEV)
+    A2a = torch.randn(M1, K2, generator=g).to(DEV) if K2 else None
+    G1 = torch.randn(M1, N, generator=g).to(DEV)
+    A1b = torch.randn(M2, K1, generator=g).to(DEV)
+    A2b = torch.randn(M2, K2, generator=g).to(DEV) if K2 else None
+    G2 = torch.randn(M2, N, generator=g).to(DEV)
+
+    def run(contend):
+        acc = F32.WgradAcc(K1 + K2, N, DEV, colsum=True)
+        if contend:
+            _contend(cus)
+        acc.add(src, G1, A2a, rows)
+        if contend:
+            _contend(cus)
+        acc.add(A1b, G2, A2b)
+        out = acc.result()
+        col = acc.col_result()
+        torch.cuda.synchronize()
+        return out, col
+
+    try:
+        _sched(False)
+        ref, refc = run(False)
+        _sched(True)
+        got, gotc = run(True)
+        assert torch.equal(ref, got) and torch.equal(refc, gotc)
+    finally:
+        _sched(True)
+
+
+@pytest.mark.parametrize("cus", [1, 16, 64])
+def test_spmm_f32_under_contention_bitwise(cus):
+    """The row-group SpMM (fixed per-row order) with a capped persistent grid and with the
+    default grid, with and without CUs held by another stream: bitwise identical."""
+    from dgraph_amd import _native
+
+    rp, col = _csr(200_000, 150_000, 12, 3, hub=5000)
+    g = torch.Generator().manual_seed(cus)
+    x = torch.randn(150_000, 256, generator=g).to(DEV)
+    rs = torch.rand(200_000, generator=g).to(DEV)
+    refs = {}
+    for pc in (64, 256):  # the uncontended full-grid result of each pass width
+        refs[pc] = F32.spmm_f32(rp, col, x, torch.empty(200_000, 256, device=DEV),
+                                row_scale=rs, pass_cols=pc)
+    torch.cuda.synchronize()
+    try:
+        for grid in (0, 512):
+            _native.ops().set_f32_sched(grid, -1)
+            for pc in (64, 256):
+                _contend(cus)
+                out = torch.empty_like(refs[pc])
+                F32.spmm_f32(rp, col, x, out, row_scale=rs, pass_cols=pc)
+                torch.cuda.synchronize()
+                assert torch.equal(refs[pc], out), (grid, pc)
+    finally:
+        _native.ops().set_f32_sched(0, -1)
