@@ -50,12 +50,16 @@ os.environ.setdefault("PYTORCH_ALLOC_CONF", "max_split_size_mb:512")
 # stream sharing the compute stream's queue runs IN ORDER with it: the exchange is then
 # serialised with the kernels it should overlap (measured: a W=8 rank's step 355 ms with
 # 4 queues vs 309 ms with 8 or 16, the exposed exchange moving into the compute regions,
-# profiles/r04/). DGRAPH_HW_QUEUES overrides; an operator's GPU_MAX_HW_QUEUES is kept;
-# the effective value is recorded in the JSON line ("hw_queues").
+# profiles/r04/). The GPU boxes export GPU_MAX_HW_QUEUES=4 (HIP's default), and with it
+# the comm stream shared the compute stream's queue again in round 5 (a W=8 rehearsal's
+# kernel trace: both streams on one queue, zero overlap, profiles/r05/timeline_*), so a
+# value below 8 is raised to 8; DGRAPH_HW_QUEUES sets it explicitly. The value found and
+# the one used are recorded in the JSON line ("hw_queues").
+_HWQ_FOUND = os.environ.get("GPU_MAX_HW_QUEUES")
 if os.environ.get("DGRAPH_HW_QUEUES"):
     os.environ["GPU_MAX_HW_QUEUES"] = os.environ["DGRAPH_HW_QUEUES"]
-else:
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+elif not (_HWQ_FOUND or "").isdigit() or int(_HWQ_FOUND) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 import torch
 import torch.distributed as dist
@@ -725,7 +729,8 @@ def main():
             "E_directed": shape.num_directed_edges,
             "edges_aggregated_per_step": e_step,
             "edges_aggregated_per_s": e_step / (ms / 1000.0),
-            "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
+            "hw_queues": {"used": os.environ.get("GPU_MAX_HW_QUEUES"),
+                          "found_in_env": _HWQ_FOUND},
             "final_loss": final_loss,
             "val_acc": val_acc,
             "test_acc": test_acc,

@@ -84,7 +84,7 @@ def main():
             timed(f"spmm_f32_cmap_F256_pc{pc}{sfx}", lambda pc=pc: F32.spmm_f32(
                 csr.rowptr, csr.col, u, out, col_map=smap, pass_cols=pc))
         del u, out
-    _native.ops().set_f32_sched(-1, -1, 1)
+    _native.ops().set_f32_sched(-1, -1, 0)
     if a.spmm_only:
         print(json.dumps(res))
         return

@@ -27,5 +27,9 @@ hipError_t heap_wait(const uint64_t* flags, int me, int world, uint64_t epoch,
 
 // hold stream `st` for `us` microseconds of device wall-clock time (rehearsal link model)
 hipError_t link_delay(double us, hipStream_t st, int blocks = 1);
+// copy nbytes src -> dst (16-B aligned) with `blocks` workgroups, `hold` of which stay
+// resident until `us` have passed
+hipError_t link_copy(const void* src, void* dst, int64_t nbytes, double us, hipStream_t st,
+                     int blocks, int hold);
 
 }  // namespace dgraph

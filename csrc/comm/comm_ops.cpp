@@ -284,11 +284,28 @@ void link_delay_op(double us, int64_t device, int64_t blocks) {
                           static_cast<int>(blocks)));
 }
 
+// The rehearsal's modelled transfer: dst <- src (same byte count, contiguous) by `blocks`
+// workgroups that stay resident for at least `us` (comm/alltoallv.py)
+void link_copy_op(const at::Tensor& src, at::Tensor& dst, double us, int64_t blocks,
+                  int64_t hold) {
+  TORCH_CHECK(src.is_cuda() && dst.is_cuda() && src.device() == dst.device(),
+              "link_copy: tensors on one GPU");
+  TORCH_CHECK(src.is_contiguous() && dst.is_contiguous(), "link_copy: contiguous tensors");
+  const int64_t nb = src.numel() * src.element_size();
+  TORCH_CHECK(nb == dst.numel() * dst.element_size(), "link_copy: byte counts differ");
+  c10::DeviceGuard g(src.device());
+  DG_HIP_CHECK(link_copy(src.data_ptr(), dst.data_ptr(), nb, us,
+                         c10::hip::getCurrentHIPStream(src.device().index()).stream(),
+                         static_cast<int>(blocks), static_cast<int>(hold)));
+}
+
 }  // namespace
 }  // namespace dgraph
 
 TORCH_LIBRARY_FRAGMENT(dgraph_amd, m) {
   m.def("link_delay(float us, int device, int blocks=1) -> ()", &dgraph::link_delay_op);
+  m.def("link_copy(Tensor src, Tensor(a!) dst, float us, int blocks, int hold) -> ()",
+        &dgraph::link_copy_op);
   m.def("heap_alloc(int nbytes, int device) -> Tensor", &dgraph::heap_alloc);
   m.def("ipc_get_handle(Tensor heap) -> Tensor", &dgraph::ipc_get_handle);
   m.def("ipc_open_handle(Tensor handle, int device) -> int", &dgraph::ipc_open_handle);

@@ -209,8 +209,8 @@ __global__ __launch_bounds__(64) void link_delay_kernel(uint64_t ticks) {
   while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(32);
 }
 
-hipError_t link_delay(double us, hipStream_t st, int blocks) {
-  if (!(us > 0.0)) return hipSuccess;
+namespace {
+uint64_t us_to_ticks(double us) {
   static int khz = 0;
   if (khz == 0) {
     int dev = 0;
@@ -220,8 +220,56 @@ hipError_t link_delay(double us, hipStream_t st, int blocks) {
       khz = 100000;  // 100 MHz
   }
   const double t = us * 1e-3 * static_cast<double>(khz);
-  const uint64_t ticks = t > 1.8e19 ? ~0ull : static_cast<uint64_t>(t);
+  return t > 1.8e19 ? ~0ull : static_cast<uint64_t>(t);
+}
+
+// The modelled collective as ONE kernel: `blocks` workgroups copy the message (16-B
+// vectors, grid-stride; a byte tail) — the HBM traffic a real transfer puts on both ends —
+// and the first `hold` of them (RCCL moves an all-to-all with one workgroup per channel)
+// then stay resident until `ticks` have passed since they started, so the transfer takes
+// max(copy, link time) and the data moves while the link time runs, as on a real link.
+__global__ __launch_bounds__(256) void link_copy_kernel(const uint8_t* __restrict__ src,
+                                                        uint8_t* __restrict__ dst,
+                                                        int64_t nbytes, uint64_t ticks,
+                                                        int hold) {
+  const uint64_t t0 = wall_clock64();
+  const int64_t nv = nbytes >> 4;
+  const int64_t tid = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int64_t step = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  const uint4* s4 = reinterpret_cast<const uint4*>(src);
+  uint4* d4 = reinterpret_cast<uint4*>(dst);
+  int64_t i = tid;
+  for (; i + 3 * step < nv; i += 4 * step) {  // four 16-B loads in flight per lane
+    const uint4 a = s4[i], b = s4[i + step], c = s4[i + 2 * step], d = s4[i + 3 * step];
+    d4[i] = a;
+    d4[i + step] = b;
+    d4[i + 2 * step] = c;
+    d4[i + 3 * step] = d;
+  }
+  for (; i < nv; i += step) d4[i] = s4[i];
+  for (int64_t j = (nv << 4) + tid; j < nbytes; j += step) dst[j] = src[j];
+  if (threadIdx.x != 0 || static_cast<int>(blockIdx.x) >= hold) return;
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(32);
+}
+}  // namespace
+
+hipError_t link_delay(double us, hipStream_t st, int blocks) {
+  if (!(us > 0.0)) return hipSuccess;
+  const uint64_t ticks = us_to_ticks(us);
   hipLaunchKernelGGL(link_delay_kernel, dim3(blocks > 0 ? blocks : 1), dim3(64), 0, st, ticks);
+  return hipGetLastError();
+}
+
+hipError_t link_copy(const void* src, void* dst, int64_t nbytes, double us, hipStream_t st,
+                     int blocks, int hold) {
+  if (nbytes < 0) return hipErrorInvalidValue;
+  const bool aligned = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) &
+                        15) == 0;
+  if (!aligned) return hipErrorInvalidValue;
+  const uint64_t ticks = us > 0.0 ? us_to_ticks(us) : 0;
+  hipLaunchKernelGGL(link_copy_kernel, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st,
+                     static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), nbytes,
+                     ticks, hold);
   return hipGetLastError();
 }
 

@@ -94,7 +94,7 @@ void set_spmm_f32_pass_cols(int cols);
 // pass width (0 = default 64); negative arguments leave a setting unchanged
 void set_spmm_f32_config(int rowgroup, int pass_cols);
 void set_spmm_f32_grid(int blocks);   // 0 = uncapped
-// XCD-contiguous row ranges (1, default) or plain in-order blocks (0): see spmm_f32.hip
+// XCD-contiguous row ranges (1) or plain in-order blocks (0, default): see spmm_f32.hip
 void set_spmm_f32_xcd(int on);
 
 // Hub-row splitting (rows whose degree exceeds `cap` are aggregated in three steps):

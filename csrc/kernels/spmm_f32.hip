@@ -249,7 +249,7 @@ __global__ __launch_bounds__(256) void spmm_f32_rowgroup_kernel(SpmmF32Args a) {
 // grid-strided, so a capped grid is a persistent one that leaves room on every CU for a
 // kernel of another stream (set_spmm_f32_grid)
 int g_f32_grid_cap = 0;
-int g_f32_xcd = 1;
+int g_f32_xcd = 0;  // measured: no gain (PERFORMANCE.md, round 5)
 
 template <typename IdxT>
 hipError_t launch_f32_rg(const SpmmF32Args& a, hipStream_t st) {

@@ -35,8 +35,8 @@ A2A_IMPL = os.environ.get("DGRAPH_A2A_IMPL", "torch")
 
 # Link model of the LOOPBACK exchange (a W-way plan run by one process: bench.py
 # --rehearse-world). 0 = the copy completes at once (a loopback exposes nothing). > 0: the
-# copy is issued on a side stream behind a device-side wait of
-# latency + max-per-peer-bytes / (GBPS * 1e9) — each peer message rides its own xGMI link,
+# copy is issued on a side stream as one kernel of LOOPBACK_CUS workgroups that takes at
+# least latency + max-per-peer-bytes / (GBPS * 1e9) — each peer message rides its own link,
 # all links concurrently — and the call returns a PENDING work whose wait() is a stream
 # event wait, so the executor's overlap schedule meets a link-length transfer and its
 # exposed-exchange regions measure what a W-GPU run would expose (the reference timed its
@@ -48,6 +48,13 @@ LOOPBACK_LATENCY_US = float(os.environ.get("DGRAPH_LOOPBACK_LATENCY_US", "15"))
 # transfer; a block of another kernel that needs the whole CU (the fp32 GEMM) cannot start
 # there until it ends
 LOOPBACK_CUS = int(os.environ.get("DGRAPH_LOOPBACK_CUS", "16"))
+# workgroups that move the modelled transfer's bytes — its HBM traffic at both ends (a
+# real rank reads what it sends and has what it receives written): enough for a full-rate
+# copy, which leaves the CUs again well within the link time (64 workgroups, ~1/4 of the
+# CUs, copied a W=8 rank's 24 GB column block at ~0.5 TB/s and held those CUs for twice
+# the link time, profiles/r05/); the first LOOPBACK_CUS of them then stay until the link
+# time has passed
+LOOPBACK_COPY_CUS = int(os.environ.get("DGRAPH_LOOPBACK_COPY_CUS", "1024"))
 
 _HEAPS: dict = {}
 
@@ -121,9 +128,15 @@ _SIDE: dict = {}
 
 
 def _side_stream(dev) -> "torch.cuda.Stream":
+    """The communication stream of ``dev``: HIGH priority. Streams map onto a handful of
+    hardware queues, and a stream that lands on the compute stream's queue runs in order
+    with it — no overlap at all (a W=8 rehearsal's kernel trace had both on one queue,
+    profiles/r05/timeline_w8_structureless_shared_queue.txt); high-priority streams sit on
+    queues of their own (scripts/debug/queue_probe.py), and the exchange's kernels are the
+    ones to dispatch first (RCCL's own streams are high priority too)."""
     s = _SIDE.get(dev.index)
     if s is None:
-        s = torch.cuda.Stream(dev)
+        s = torch.cuda.Stream(dev, priority=-1)
         _SIDE[dev.index] = s
     return s
 
@@ -235,10 +248,16 @@ class AllToAllV:
         dev = send.device
         side = _side_stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
+        # the modelled collective is ONE kernel on the comm stream: LOOPBACK_COPY_CUS
+        # workgroups move the rows, LOOPBACK_CUS of them stay resident for at least the link
+        # time (the data moves while the link time runs, as on a real link; one stream, so
+        # no extra hardware queue: csrc/comm/symheap.hip link_copy_kernel)
         with torch.cuda.stream(side):
-            _native.ops().link_delay(float(us), int(dev.index), LOOPBACK_CUS)
             if m:
-                out[:m].copy_(send[:m])
+                _native.ops().link_copy(send[:m].contiguous(), out[:m], float(us),
+                                        max(LOOPBACK_COPY_CUS, LOOPBACK_CUS), LOOPBACK_CUS)
+            else:
+                _native.ops().link_delay(float(us), int(dev.index), LOOPBACK_CUS)
             if self.total_recv > m:
                 out[m:].zero_()
             ev = torch.cuda.Event()

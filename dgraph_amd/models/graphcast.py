@@ -166,6 +166,34 @@ class MeshEdgeBlock(nn.Module):
         h = edge_pre_activation(Y, P, Q, src_map, dst_map, self.mesh_mlp.first_act_name())
         return self.mesh_mlp.tail(h, residual=edge_feats)
 
+    def fused_halo(self, src_local: torch.Tensor, dst_local: torch.Tensor,
+                   edge_feats: torch.Tensor, src_map: IndexMap, dst_map: IndexMap,
+                   halo, side: str) -> torch.Tensor:
+        """:meth:`fused` with one endpoint's rows ``[local | halo]`` where the halo rows are
+        still on the links (``halo``: an :class:`~dgraph_amd.parallel.halo.AsyncHalo`, or
+        None when the edge set has no remote endpoint): the edge GEMM, the other endpoint's
+        projection and the local rows' projection run first, the exchange is waited for
+        only before its rows are projected (``side`` = "src" or "dst": the halo side). The
+        index maps address the projected rows ``[local | halo]`` as before."""
+        if halo is None:
+            return self.fused(src_local, dst_local, edge_feats, src_map, dst_map)
+        Ws, Wd, We, b = self._split_first()
+        Y = linear(edge_feats, We, b)
+        if side == "src":
+            Q = linear(dst_local, Wd)
+            P_loc = linear(src_local, Ws)
+            with region("exchange-wait"):  # exposed exchange time (device)
+                hw = halo.wait()
+            P = torch.cat([P_loc, linear(hw, Ws)], dim=0)
+        else:
+            P = linear(src_local, Ws)
+            Q_loc = linear(dst_local, Wd)
+            with region("exchange-wait"):
+                hw = halo.wait()
+            Q = torch.cat([Q_loc, linear(hw, Wd)], dim=0)
+        h = edge_pre_activation(Y, P, Q, src_map, dst_map, self.mesh_mlp.first_act_name())
+        return self.mesh_mlp.tail(h, residual=edge_feats)
+
     def forward(self, src_node_features, dst_node_features, edge_features, src_indices,
                 dst_indices, src_rank_mapping=None, dst_rank_mapping=None):
         """Reference signature (single process, global indices)."""
@@ -216,11 +244,23 @@ class MeshNodeBlock(nn.Module):
 
 # ----------------------------------------------------------------------------- model
 class _Halo:
-    """Halo-exchanged ``[local | halo]`` rows for an edge set (identity when single)."""
+    """Halo exchange of an edge set's non-aggregating endpoint. ``start(x, es)``: the
+    exchange issued asynchronously (:class:`~dgraph_amd.parallel.halo.AsyncHalo`; None when
+    the set has no remote endpoint), consumed by :meth:`MeshEdgeBlock.fused_halo` after
+    the work that does not need it. ``__call__``: the synchronous ``[local | halo]`` rows
+    (the reference's form, haloExchange.py:137 + DGraphMessagePassing's concatenation)."""
 
     def __init__(self, comm):
         self.comm = comm
         self._ex = None
+
+    def start(self, x: torch.Tensor, es):
+        if es.pattern is None:
+            return None
+        from ..parallel.halo import AsyncHalo
+
+        with region("exchange-issue"):
+            return AsyncHalo.start(self.comm, x, es.pattern)
 
     def __call__(self, x: torch.Tensor, es) -> torch.Tensor:
         if es.pattern is None:
@@ -264,9 +304,9 @@ class GraphCastEncoder(nn.Module):
         self.halo = _Halo(comm)
 
     def forward(self, grid_node_features, mesh_node_features, g2m_edge_features, g2m) -> Tuple:
-        grid_all = self.halo(grid_node_features, g2m)       # senders: grid (local|halo)
-        e = self.edge_mlp.fused(grid_all, mesh_node_features, g2m_edge_features,
-                                g2m.other_map(), g2m.agg_map())
+        grid_h = self.halo.start(grid_node_features, g2m)   # senders: grid (local|halo)
+        e = self.edge_mlp.fused_halo(grid_node_features, mesh_node_features, g2m_edge_features,
+                                     g2m.other_map(), g2m.agg_map(), grid_h, "src")
         n = self.mesh_node_mlp.fused(mesh_node_features, e, g2m.agg_map())
         mesh_node_features = mesh_node_features + n
         grid_node_features = self.grid_node_mlp(grid_node_features, residual=grid_node_features)
@@ -288,8 +328,8 @@ class GraphCastProcessor(nn.Module):
         e, n = m2m_edge_features, mesh_features
         for i, (el, nl) in enumerate(zip(self.edge_processors, self.node_processors)):
             with region(f"processor-{i}"):
-                n_all = self.halo(n, m2m)            # receivers (dst) may be remote
-                e = el.fused(n, n_all, e, m2m.agg_map(), m2m.other_map())
+                n_h = self.halo.start(n, m2m)        # receivers (dst) may be remote
+                e = el.fused_halo(n, n, e, m2m.agg_map(), m2m.other_map(), n_h, "dst")
                 n = nl.fused(n, e, m2m.agg_map())    # aggregate at the source
         return n, e
 
@@ -304,9 +344,10 @@ class GraphCastDecoder(nn.Module):
         self.halo = _Halo(comm)
 
     def forward(self, m2g_edge_features, grid_node_features, mesh_node_features, m2g):
-        mesh_all = self.halo(mesh_node_features, m2g)     # senders: mesh (local|halo)
-        e = self.edge_mlp.fused(mesh_all, grid_node_features, m2g_edge_features,
-                                m2g.other_map(), m2g.agg_map())
+        mesh_h = self.halo.start(mesh_node_features, m2g)  # senders: mesh (local|halo)
+        e = self.edge_mlp.fused_halo(mesh_node_features, grid_node_features,
+                                     m2g_edge_features, m2g.other_map(), m2g.agg_map(),
+                                     mesh_h, "src")
         n = self.node_mlp.fused(grid_node_features, e, m2g.agg_map())
         return grid_node_features + n
 

@@ -75,6 +75,12 @@ KEEP_AGG0 = os.environ.get("DGRAPH_FUSED_KEEP_AGG0", "auto")
 # exchange outlasts the interior rows' work (the store costs a second pass over the boundary
 # rows and a read-modify-write of their aggregates: ~10 ms per layer at W = 8)
 BOUNDARY_STORE = os.environ.get("DGRAPH_FUSED_BOUNDARY_STORE", "auto")
+# keep the last hidden layer's input aggregate on the support rows S from the forward (the
+# forward computes it for every row anyway) instead of re-aggregating the S rows in the
+# backward (and, with streamed halos, re-fetching the halo in column blocks): auto = when
+# the memory plan has room for nS x width floats (always with streamed halos, whose plan
+# already holds that store). Saves a pass over the S rows' entries per step.
+KEEP_AS = os.environ.get("DGRAPH_FUSED_KEEP_AS", "auto")
 # W > 1: hidden-layer halos exchanged and consumed in column blocks ("stream") instead of
 # kept at full width for the whole step — "auto" when the full-width plan does not fit (a
 # structureless graph's halo is nearly every remote vertex), "on" / "off" to force
@@ -392,6 +398,13 @@ class FusedSAGE:
         self.halo_bytes = 4 * (H * self.d0 + (self.nl - 1) * H * self.hid + n_send * self.hid)
         self.stream, self.cw, self.nbuf = False, 0, 0
         other += x_tr
+        # the output-layer backward's sub-plan exchange (halo rows adjacent to the loss rows,
+        # A[T, halo]^T u2 out, owners' rows back): resident buffers in storage that is dead
+        # during that exchange — the last received-halo / send buffers, or the streamed ring
+        self.sub_rows = (0, 0)
+        if self.sub is not None:
+            self.sub_rows = (self.sub[0].rowptr.numel() - 1, self.sub[1].total_recv)
+        sub_bytes = 4 * self.hid * (self.sub_rows[0] + self.sub_rows[1])
         full_ok = dev.type != "cuda" or need_h + self.halo_bytes + other + (1 << 28) <= free
         if graph.send_map is not None and (HALO_STREAM == "on" or
                                            (HALO_STREAM == "auto" and not full_ok)):
@@ -399,12 +412,13 @@ class FusedSAGE:
             # cross in column blocks of cw through a ring of nbuf send/receive buffers, and
             # whole-row aggregates land in stores (the output layer's, the S rows' of the
             # re-fetched h1, the reverse exchange's input-layer gradient)
-            stores = L * max(self.hid, self.d0) * 4 + self.nS * self.hid * 4 + \
-                (L * self.hid * 4 if self.nl == 3 else 0)
+            # (the reverse exchange's input-layer gradient store lives in the output
+            # layer's aggregate store, dead once the forward is done)
+            stores = L * max(self.hid, self.d0) * 4 + self.nS * self.hid * 4
             for cw, nb in STREAM_SHAPES:
                 if self.hid % cw:
                     continue
-                ring = nb * (H + n_send) * cw * 4
+                ring = max(nb * (H + n_send) * cw * 4, sub_bytes)
                 hb = 4 * H * self.d0 + ring + stores
                 if dev.type != "cuda" or need_h + hb + other + (1 << 28) <= free:
                     self.stream, self.cw, self.nbuf, self.halo_bytes = True, cw, nb, hb
@@ -456,6 +470,15 @@ class FusedSAGE:
                 and self.use_store["out"] and free - need_h - other - need_full > margin:
             self.agg_full = torch.empty(L - self.Li, wA, dtype=torch.float32, device=dev)
             other += need_full
+        # the last hidden layer's input aggregate on the S rows kept from the forward (else
+        # re-aggregated in the backward); streamed halos keep it in aS_full (planned above)
+        self.aS_keep = None
+        self.w_lh = self.d0 if self.nl == 2 else self.hid  # width of that layer's input
+        need_as = self.nS * self.w_lh * 4
+        self.keep_as = KEEP_AS == "on" or self.stream or (
+            KEEP_AS == "auto" and free - need_h - other - need_as > margin)
+        if self.keep_as and not self.stream:
+            other += need_as
         # layer 0's input aggregate kept from the forward for the backward (else recomputed)
         self.agg0 = None
         need0 = L * self.d0 * 4
@@ -502,11 +525,36 @@ class FusedSAGE:
             self.send_buf = torch.empty(n_send, self.hid, **f)
             self.halo_buf = [torch.empty(H, self.hid, **f) for _ in range(self.nl - 1)]
         elif self.stream:
-            self.ring_send = [torch.empty(n_send, self.cw, **f) for _ in range(self.nbuf)]
-            self.ring_recv = [torch.empty(H, self.cw, **f) for _ in range(self.nbuf)]
+            # one arena: the ring's send / receive blocks, and (dead while the ring is idle,
+            # in the output-layer backward) the sub-plan exchange's buffers
+            blk_s, blk_r = n_send * self.cw, H * self.cw
+            ring_fl = max(self.nbuf * (blk_s + blk_r), sub_bytes // 4)
+            self.ring_arena = torch.empty(ring_fl, **f)
+            ra = self.ring_arena
+            self.ring_send = [ra[b * blk_s:(b + 1) * blk_s].view(n_send, self.cw)
+                              for b in range(self.nbuf)]
+            o = self.nbuf * blk_s
+            self.ring_recv = [ra[o + b * blk_r:o + (b + 1) * blk_r].view(H, self.cw)
+                              for b in range(self.nbuf)]
             self.agg_full = torch.empty(L, max(self.hid, self.d0), **f)
-            self.aS_full = torch.empty(self.nS, self.hid, **f)
-            self.gz_full = torch.empty(L, self.hid, **f) if self.nl == 3 else None
+            self.aS_full = torch.empty(self.nS, self.w_lh, **f)
+            # the reverse exchange's store: the output layer's aggregate store (dead after
+            # the forward; stream-ordered on the compute stream like every use of both)
+            self.gz_full = self.agg_full.view(-1)[:L * self.hid].view(L, self.hid) \
+                if self.nl == 3 else None
+        self.sub_hg = self.sub_sg = None
+        if self.sub is not None:
+            nh, nr = self.sub_rows
+            if self.stream:
+                self.sub_hg = self.ring_arena[:nh * self.hid].view(nh, self.hid)
+                self.sub_sg = self.ring_arena[nh * self.hid:(nh + nr) * self.hid].view(
+                    nr, self.hid)
+            elif nh <= H and nr <= n_send:
+                self.sub_hg = self.halo_buf[-1][:nh]
+                self.sub_sg = self.send_buf[:nr]
+        if self.keep_as:
+            self.aS_keep = self.aS_full if self.aS_full is not None else \
+                torch.empty(self.nS, self.w_lh, **f)
         if self.store_sep:
             self.dZ = torch.empty(self.nS, self.hid, **f)
             self.u = torch.empty(self.nS, self.hid, **f) if self.nl == 3 else None
@@ -604,7 +652,8 @@ class FusedSAGE:
                 "boundary_store": dict(self.use_store),
                 "halo_stream": ({"column_block": self.cw, "buffers": self.nbuf}
                                 if self.stream else False),
-                "keep_agg0": self.agg0 is not None, "compact_T": self.TS is not None,
+                "keep_agg0": self.agg0 is not None, "keep_aS": self.aS_keep is not None,
+                "compact_T": self.TS is not None,
                 "compact_halo_T": self.HTS is not None, "support_rows": self.nS}
 
     # ------------------------------------------------------------------ helpers
@@ -795,7 +844,7 @@ class FusedSAGE:
             return fn()
 
     def _stream_fwd(self, h: torch.Tensor, out: torch.Tensor, name: str,
-                    rows: Optional[torch.Tensor] = None) -> None:
+                    rows: Optional[torch.Tensor] = None, fill=None) -> None:
         """Streamed halo: ``out[:, c] = mean over in-neighbours of h[:, c]`` for every row
         (or for the adjacency rows ``rows``, output row i <- rows[i]), with h's halo rows
         exchanged in column blocks of ``cw`` through the buffer ring — block k+1 is on the
@@ -818,6 +867,8 @@ class FusedSAGE:
         for k, (c0, c1) in enumerate(blocks):
             if nb > 1 and k + 1 < len(blocks):
                 works[k + 1] = issue(k + 1)
+            if k == 0 and fill is not None:
+                fill()  # independent compute-stream work while block 0 is on the links
             recv, work = works.pop(k)
             self._mark(f"exchange_{name}")
             work.wait()
@@ -833,7 +884,7 @@ class FusedSAGE:
                 works[k + 1] = issue(k + 1)
 
     def _stream_rev(self, u: torch.Tensor, gz: torch.Tensor, gate: torch.Tensor,
-                    name: str) -> None:
+                    name: str, fill=None) -> None:
         """Streamed reverse exchange of B1b: for every column block, the halo rows'
         contributions ``A_halo^T u`` (column-mapped onto S) are sent to their owners and
         summed into ``gz`` (zeroed first; the ReLU gate of layer 0 applied), block k+1's
@@ -859,6 +910,8 @@ class FusedSAGE:
         for k, (c0, c1) in enumerate(blocks):
             if nb > 1 and k + 1 < len(blocks):
                 works[k + 1] = issue(k + 1)
+            if k == 0 and fill is not None:
+                fill()
             sg, work = works.pop(k)
             self._mark(f"exchange_{name}")
             work.wait()
@@ -904,17 +957,31 @@ class FusedSAGE:
             hout = self.h[l]
             bias = b.detach()
 
-            def consume(ci, a, hin=hin, hout=hout, ws=ws, wn=wn, bias=bias):
+            keep_s = self.aS_keep if l == nl - 2 else None
+
+            def consume(ci, a, hin=hin, hout=hout, ws=ws, wn=wn, bias=bias, keep_s=keep_s):
                 r0, r1 = self.chunks[ci]
+                if keep_s is not None:
+                    self._keep_s_rows(ci, a, keep_s)
                 self._gemm(hin[r0:r1], ws, a, wn, bias=bias, relu=True, out=hout[r0:r1])
 
             if self.stream and l > 0:
-                # streamed halo: every row's aggregate into the layer's own output buffer
-                # (column block by column block), then the GEMMs in place, chunk by chunk
-                self._stream_fwd(hin, hout, f"fwd_l{l}")
+                # streamed halo: every row's aggregate into the output layer's store
+                # (column block by column block; free until the output layer), while the
+                # self term h W_self + b runs into the layer's output buffer during the
+                # first block's transfer (the pipeline fill); then per chunk
+                # h_out = relu(agg W_neigh + h_out)
+                agg = self.agg_full[:, :hin.shape[1]]
+                self._stream_fwd(hin, agg, f"fwd_l{l}",
+                                 fill=lambda hin=hin, ws=ws, bias=bias, hout=hout:
+                                 self._gemm(hin, ws, bias=bias, out=hout))
                 for ci, (r0, r1) in enumerate(self.chunks):
                     if r1 > r0:
-                        consume(ci, hout[r0:r1])
+                        a = agg[r0:r1]
+                        if keep_s is not None:
+                            self._keep_s_rows(ci, a, keep_s)
+                        self._gemm(a, wn, cin=hout[r0:r1], beta=1.0, relu=True,
+                                   out=hout[r0:r1])
                 halos.append(None)
             else:
                 # layer l >= 1 can store boundary-row aggregates in its own output buffer
@@ -960,6 +1027,13 @@ class FusedSAGE:
         self._mark("bwd_out")
         return self._backward(P, halos, hl, hl_halo, loss)
 
+    def _keep_s_rows(self, ci, a, keep):
+        """The support rows of chunk ci's aggregate ``a`` into ``keep`` (rows in S order),
+        before the chunk's GEMM consumes (or, in place, overwrites) it."""
+        s0, s1 = self.ch_S[ci]
+        if s1 > s0:
+            K.copy_rows(a, src_idx=self.ch_Sloc[ci], out=keep[s0:s1])
+
     def _out_chunk(self, ci, a, hl, wsp, wnp, bp):
         """Output layer of row chunk ci: logits of every row, the loss rows' cross-entropy
         gradient and output-layer weight gradients, eval hits."""
@@ -1003,8 +1077,8 @@ class FusedSAGE:
         work = None
         if self.sub is not None:
             ht_nz, a2a_sub, stc, stc_rows = self.sub
-            hg = self._spmm(ht_nz.rowptr, ht_nz.col, u2)
-            sg, work = a2a_sub(hg, async_op=True)
+            hg = self._spmm(ht_nz.rowptr, ht_nz.col, u2, self.sub_hg)
+            sg, work = a2a_sub(hg, out=self.sub_sg, async_op=True)
             self.edges_aggregated += ht_nz.nnz
         self._spmm(self.AT_S.rowptr, self.AT_S.col, u2, dZ)
         self.edges_aggregated += self.AT_S.nnz
@@ -1024,6 +1098,36 @@ class FusedSAGE:
         hin_l_halo = halos[lh]
         u = None
         work = None
+        self.acc_hid_s.reset()
+        self.acc_hid_n.reset()
+        halo_l = hin_l_halo if self.adj.mid is not None else None
+        kept = self.aS_keep is not None
+        streamed = self.stream and lh > 0 and not kept
+
+        def s_rows():
+            """The last hidden layer's weight gradients over the S rows."""
+            if streamed:
+                # the S rows' aggregate of h1, its halo rows re-fetched in column blocks
+                self._stream_fwd(hin_l, self.aS_full, f"bwd_l{lh}", rows=self.S)
+            for s0, s1 in self.s_chunks:
+                if s1 <= s0:
+                    continue
+                rows = self.S[s0:s1]
+                if kept:  # from the forward: no second aggregation of the S rows
+                    aS = self.aS_keep[s0:s1]
+                elif streamed:
+                    aS = self.aS_full[s0:s1]
+                else:
+                    aS = self.bufA[:s1 - s0, :hin_l.shape[1]]
+                    kw = dict(x2=halo_l, nsplit=self.L) if halo_l is not None else {}
+                    self._spmm(self.adj.rp, self.adj.col, hin_l, aS, row_ids=rows,
+                               row_scale=self.invdegS[s0:s1], **kw)
+                self.acc_hid_s.add(hin_l, dZ[s0:s1], a1_rows=rows)
+                self.acc_hid_n.add(aS, dZ[s0:s1])
+            if not kept:
+                self.edges_aggregated += self.nnz_S
+
+        pending_s = True
         if nl == 3:
             # u1 = (dZ1 Wn1^T) / deg_S: its transposed aggregation feeds layer 0; the halo
             # part is computed and sent first so the exchange overlaps the S-row work and
@@ -1031,8 +1135,12 @@ class FusedSAGE:
             u = self._gemm(dZ, wn1.detach().t().contiguous(), row_scale=self.invdegS,
                            out=self.u)
             if self.haloT is not None and self.stream:
-                # streamed reverse exchange into the input-layer gradient store
-                self._stream_rev(u, self.gz_full, self.h[0], f"bwd_l{lh}")
+                # streamed reverse exchange into the input-layer gradient store; with the
+                # S-row aggregate kept from the forward, the S-row weight gradients need
+                # nothing from it and fill the pipeline's first transfer
+                self._stream_rev(u, self.gz_full, self.h[0], f"bwd_l{lh}",
+                                 fill=s_rows if kept else None)
+                pending_s = not kept
                 self.edges_aggregated += self.haloT.nnz
             elif self.haloT is not None:
                 # the output layer's received halo rows are dead: its buffer sends, the
@@ -1044,27 +1152,8 @@ class FusedSAGE:
                                        col_map=self.smap)
                 sg1, work = g.a2a_rev(hg1, out=self.send_buf, async_op=True)
                 self.edges_aggregated += self.haloT.nnz
-        self.acc_hid_s.reset()
-        self.acc_hid_n.reset()
-        halo_l = hin_l_halo if self.adj.mid is not None else None
-        streamed = self.stream and lh > 0
-        if streamed:
-            # the S rows' aggregate of h1, its halo rows re-fetched in column blocks
-            self._stream_fwd(hin_l, self.aS_full, f"bwd_l{lh}", rows=self.S)
-        for s0, s1 in self.s_chunks:
-            if s1 <= s0:
-                continue
-            rows = self.S[s0:s1]
-            if streamed:
-                aS = self.aS_full[s0:s1]
-            else:
-                aS = self.bufA[:s1 - s0, :hin_l.shape[1]]
-                kw = dict(x2=halo_l, nsplit=self.L) if halo_l is not None else {}
-                self._spmm(self.adj.rp, self.adj.col, hin_l, aS, row_ids=rows,
-                           row_scale=self.invdegS[s0:s1], **kw)
-            self.acc_hid_s.add(hin_l, dZ[s0:s1], a1_rows=rows)
-            self.acc_hid_n.add(aS, dZ[s0:s1])
-        self.edges_aggregated += self.nnz_S
+        if pending_s:
+            s_rows()
         gw[(lh, 0)] = self.acc_hid_s.result()
         gw[(lh, 1)] = self.acc_hid_n.result()
         gw[(lh, 2)] = self.acc_hid_s.col_result()

@@ -73,6 +73,90 @@ class HaloExchange:
         return HaloExchangeImpl.apply(send, self.comm, comm_pattern)
 
 
+class _Pending:
+    """State shared by the two halves of a split (asynchronous) halo exchange."""
+
+    __slots__ = ("fwd", "rev", "work", "rwork", "grad_send")
+
+    def __init__(self, fwd, rev):
+        self.fwd, self.rev = fwd, rev
+        self.work = self.rwork = self.grad_send = None
+
+
+class _HaloStart(Function):
+    """Forward: the exchange is ISSUED (asynchronous all-to-all-v); the returned receive
+    buffer is pending until :class:`_HaloWait`. Backward: waits for the reverse exchange
+    that ``_HaloWait``'s backward started, and returns its rows as the send gradient."""
+
+    @staticmethod
+    def forward(ctx, send, st: _Pending):
+        recv, st.work = st.fwd(send.contiguous(), async_op=True)
+        ctx.st = st
+        return recv
+
+    @staticmethod
+    def backward(ctx, _grad_pending):
+        st = ctx.st
+        st.rwork.wait()
+        g, st.grad_send, st.rwork = st.grad_send, None, None
+        return g, None
+
+
+class _HaloWait(Function):
+    """Forward: the compute stream waits for the exchange (stream-ordered, no host sync).
+    Backward: ISSUES the reverse exchange of the halo gradient; ``_HaloStart``'s backward
+    waits for it, so the backward work between the two (the local rows' gradients)
+    overlaps it."""
+
+    @staticmethod
+    def forward(ctx, pending, st: _Pending):
+        st.work.wait()
+        st.work = None
+        ctx.st = st
+        return pending.view_as(pending)
+
+    @staticmethod
+    def backward(ctx, grad_halo):
+        st = ctx.st
+        st.grad_send, st.rwork = st.rev(grad_halo.contiguous(), async_op=True)
+        return grad_halo, None
+
+
+class AsyncHalo:
+    """A halo exchange split in two so independent work can run while it is on the links:
+    ``h = AsyncHalo.start(comm, x_local, pattern)`` issues it (pack on the compute stream,
+    all-to-all-v asynchronous), ``h.wait()`` returns the ``[num_halo, F]`` rows (the compute
+    stream waits; no host sync). Autograd-aware in both directions: the reverse exchange is
+    issued when the halo's gradient is complete and waited for only when the send rows'
+    gradient is needed. The reference's exchange was synchronous
+    (DGraph/distributed/haloExchange.py:47-62, Engine.py:67-86); engines without an
+    asynchronous all-to-all-v (mpi / gloo CPU) run the synchronous :class:`HaloExchange`
+    at ``start``."""
+
+    def __init__(self, halo: Optional[torch.Tensor], pending=None, st=None):
+        self._halo, self._pending, self._st = halo, pending, st
+
+    @staticmethod
+    def start(comm, x_local: torch.Tensor, cp: CommunicationPattern) -> "AsyncHalo":
+        engine = getattr(comm, "_engine", None)
+        if engine is None or not hasattr(engine, "alltoallv") or x_local.ndim != 2:
+            return AsyncHalo(HaloExchange(comm)(x_local, cp))
+        a2a = cp._cache.get("a2a")
+        if a2a is None:
+            a2a = engine.alltoallv(cp.send_splits(), cp.recv_splits())
+            cp._cache["a2a"] = a2a
+            cp._cache["a2a_rev"] = a2a.reversed()
+        send = gather(x_local, _send_map(cp, x_local.shape[0]))
+        st = _Pending(a2a, cp._cache["a2a_rev"])
+        return AsyncHalo(None, _HaloStart.apply(send, st), st)
+
+    def wait(self) -> torch.Tensor:
+        if self._halo is None:
+            self._halo = _HaloWait.apply(self._pending, self._st)
+            self._pending = self._st = None
+        return self._halo
+
+
 class DGraphMessagePassing(nn.Module):
     """Halo exchange, then ``layer([x_local; halo], local_edge_list, edge_feats)`` which
     must return rows for local vertices only."""

@@ -182,3 +182,17 @@ def _a2a_body(rank, world):
     used = shmem_heap(None, torch.device("cuda", 0))._cursor
     close_shmem_heaps()
     assert used < (64 << 20)
+
+
+@pytest.mark.parametrize("env", [{"DGRAPH_FUSED_BOUNDARY_STORE": "on"},
+                                 {"DGRAPH_FUSED_HALO_STREAM": "on"}],
+                         ids=["store", "stream"])
+def test_bench_step_hidden512_two_processes(monkeypatch, env):
+    """a 512-wide hidden layer at W=2 on the GPU kernels, through the two
+    in-place aggregate-then-GEMM paths (boundary-row store, streamed halos), whose GEMM
+    runs as column blocks with its aggregate operand aliasing the output."""
+    monkeypatch.setenv("DGRAPH_A2A_IMPL", "shmem")
+    monkeypatch.setenv("DGRAPH_SYMHEAP_BYTES", str(1 << 30))
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    run_ranks(_body, 2, dict(global_frac=0.05, hidden=512), "fp32", timeout=240)

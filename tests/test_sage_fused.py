@@ -15,7 +15,8 @@ from dgraph_amd.parallel.dist_graph import DistGraph
 SCALE = 2e-5  # ~2.2K vertices, ~65K messages
 
 
-def _setup(rank, world, dev="cpu", layers=3, chunk_rows=300, gf=0.3, name="ogbn-papers100M"):
+def _setup(rank, world, dev="cpu", layers=3, chunk_rows=300, gf=0.3, name="ogbn-papers100M",
+           hidden=256):
     # ogbn-products: 100 input features (zero-padded to 128 inside the executor), 47 classes
     shape = SHAPES[name].scaled(SCALE if name == "ogbn-papers100M" else 1e-3)
     part = build_partition(shape, rank, world, dev, global_frac=gf, window=64)
@@ -35,12 +36,12 @@ def _setup(rank, world, dev="cpu", layers=3, chunk_rows=300, gf=0.3, name="ogbn-
     # products, seed 0: a layer-2 pre-activation of 6e-8 (a ReLU tie that summation order
     # flips) — seed 1 keeps every |pre-activation| well above fp32 rounding
     torch.manual_seed(0 if name == "ogbn-papers100M" else 1)
-    model = GraphSAGE(shape.num_features, 256, shape.num_classes, layers).to(dev)
+    model = GraphSAGE(shape.num_features, hidden, shape.num_classes, layers).to(dev)
     return shape, g, x, y, split, tr, ev, int(n_tr), model
 
 
 def _fused_grads(rank, world, layers=3, chunk_rows=300, name="ogbn-papers100M",
-                 schedule="full", dev="cpu", gf=0.3):
+                 schedule="full", dev="cpu", gf=0.3, hidden=256):
     """schedule (W > 1): "full" = forward exchanges overlapped through the whole-layer
     aggregate buffer (output layer) and in place (hidden layers); "inplace" = no whole-layer
     buffer (hidden layers in place, the output layer's exchange waited for up front);
@@ -48,7 +49,7 @@ def _fused_grads(rank, world, layers=3, chunk_rows=300, name="ogbn-papers100M",
     import dgraph_amd.models.sage_fused as sf
 
     shape, g, x, y, split, tr, ev, n_tr, model = _setup(rank, world, dev=dev, layers=layers,
-                                                        name=name, gf=gf)
+                                                        name=name, gf=gf, hidden=hidden)
     sf.OVERLAP_FWD = schedule != "off"
     try:
         ex = FusedSAGE(model, g, x, tr, y[tr], ev, y[ev], split[ev] == SPLIT_VALID, n_tr,
@@ -196,7 +197,8 @@ def test_fused_directed_graph_matches_autograd():
         torch.testing.assert_close(a, b, atol=2e-5, rtol=1e-4)
 
 
-def _interior_first_body(rank, world, ref_path, overlap, store="auto", stream="off"):
+def _interior_first_body(rank, world, ref_path, overlap, store="auto", stream="off",
+                         keep_as="auto", hidden=256):
     """One rank of a W-way partition renumbered interior-first (parallel/reorder.py), the
     fused executor's interior-then-boundary schedule, all-reduced against W=1."""
     import dgraph_amd.models.sage_fused as sf
@@ -204,6 +206,7 @@ def _interior_first_body(rank, world, ref_path, overlap, store="auto", stream="o
 
     sf.OVERLAP_FWD = overlap
     sf.BOUNDARY_STORE = store
+    sf.KEEP_AS = keep_as
     sf.HALO_STREAM = "on" if stream != "off" else "off"
     if stream == "single":  # one ring buffer: exchange and aggregation alternate
         sf.STREAM_SHAPES = ((64, 1),)
@@ -224,10 +227,11 @@ def _interior_first_body(rank, world, ref_path, overlap, store="auto", stream="o
     n_tr = torch.tensor([tr.numel()])
     dist.all_reduce(n_tr)
     torch.manual_seed(0)
-    model = GraphSAGE(shape.num_features, 256, shape.num_classes, 3)
+    model = GraphSAGE(shape.num_features, hidden, shape.num_classes, 3)
     ex = FusedSAGE(model, g, x, tr, y[tr], ev, y[ev], split[ev] == SPLIT_VALID, int(n_tr),
                    chunk_rows=300, release_graph=True)
     assert ex.Li == L_int and ex.nA >= 1
+    assert (ex.aS_keep is not None) == (keep_as != "off" or stream != "off")
     if store != "auto":
         assert ex.use_store == {"hidden": store == "on", "out": store == "on"}
     assert ex.stream == (stream != "off")
@@ -259,6 +263,29 @@ def test_fused_interior_first_matches_w1(ranks, world, overlap, store, stream, t
     p = tmp_path / "ref.pt"
     torch.save({"loss": loss, "grads": grads, "corr": corr}, p)
     ranks(_interior_first_body, world, str(p), overlap, store, stream)
+
+
+@pytest.mark.parametrize("world,store,stream,keep_as", [
+    (2, "on", "off", "off"),   # S rows re-aggregated in the backward (resident halo)
+    (2, "auto", "on", "on"),   # S-row aggregate kept from the streamed forward
+    (4, "off", "off", "on")])
+def test_fused_keep_support_aggregate(ranks, world, store, stream, keep_as, tmp_path):
+    """The last hidden layer's input aggregate on the support rows kept from the forward
+    (or recomputed in the backward): same gradients as W=1."""
+    loss, grads, corr = _fused_grads(0, 1, gf=0.05)
+    p = tmp_path / "ref.pt"
+    torch.save({"loss": loss, "grads": grads, "corr": corr}, p)
+    ranks(_interior_first_body, world, str(p), True, store, stream, keep_as)
+
+
+def test_fused_hidden512_store_stream_matches_w1(ranks, tmp_path):
+    """a 512-wide hidden layer with the boundary-row store and with streamed
+    halos (the in-place aggregate-then-GEMM paths at N > 256) at W=2."""
+    loss, grads, corr = _fused_grads(0, 1, gf=0.05, hidden=512)
+    p = tmp_path / "ref.pt"
+    torch.save({"loss": loss, "grads": grads, "corr": corr}, p)
+    ranks(_interior_first_body, 2, str(p), True, "on", "off", "auto", 512)
+    ranks(_interior_first_body, 2, str(p), True, "auto", "on", "auto", 512)
 
 
 @pytest.mark.parametrize("hidden,feat", [(128, 100), (512, 128), (256, 300)])
