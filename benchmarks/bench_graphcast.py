@@ -55,7 +55,22 @@ def main():
                     help="one processor edge per multimesh edge pair (327 660 at level 6); "
                          "default: the reference's graph, every multimesh edge carried twice "
                          "(655 320, experiments/GraphCast/tests/test_single_graph_data.py)")
+    ap.add_argument("--rehearse-world", type=int, default=0,
+                    help="single process: rank --rehearse-rank of a W-way partition, every "
+                         "halo exchange a loopback (patterns of all ranks built in memory)")
+    ap.add_argument("--rehearse-rank", type=int, default=0)
+    ap.add_argument("--link-gbps", type=float, default=0.0,
+                    help="rehearsal link model: each loopback exchange takes latency + "
+                         "largest per-peer message / GBPS (comm/alltoallv.py)")
+    ap.add_argument("--regions", action="store_true",
+                    help="after the timed steps, one more step with per-region device times "
+                         "(exchange-wait = exposed halo exchange), as the reference's "
+                         "microbenchmark times communication vs processing")
     a = ap.parse_args()
+    if a.link_gbps > 0:
+        import dgraph_amd.comm.alltoallv as _A
+
+        _A.LOOPBACK_LINK_GBPS = a.link_gbps
     if a.channels is None:
         a.channels = 73 if a.channel_config == "reference-73" else 6 * 37 + 5
 
@@ -69,6 +84,8 @@ def main():
 
     comm = Communicator.init_process_group("nccl")
     rank, W = comm.get_rank(), comm.get_world_size()
+    rehearse = a.rehearse_world > 1 and W == 1
+    p_rank, p_world = (a.rehearse_rank, a.rehearse_world) if rehearse else (rank, W)
     dev = torch.device("cuda", torch.cuda.current_device())
     dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     t0 = time.perf_counter()
@@ -78,8 +95,9 @@ def main():
     if a.mesh_vertex_placement:
         from dgraph_amd.data.graphcast_graph import load_mesh_placement
 
-        mesh_part = load_mesh_placement(a.mesh_vertex_placement, g.mesh_xyz.shape[0], W)
-    pg = partition_graphcast_graph(g, rank, W, mesh_part=mesh_part, group=comm.group).to(dev)
+        mesh_part = load_mesh_placement(a.mesh_vertex_placement, g.mesh_xyz.shape[0], p_world)
+    pg = partition_graphcast_graph(g, p_rank, p_world, mesh_part=mesh_part, group=comm.group,
+                                   rehearse=rehearse).to(dev)
     build_s = time.perf_counter() - t0
     cfg = Config()
     cfg.model.hidden_dim = a.hidden
@@ -155,7 +173,27 @@ def main():
                 for e in rows[:80]:
                     f.write(f"{e.self_device_time_total:10.0f} {e.count:5d}  {e.key:36s} "
                             f"{str(e.input_shapes)[:110]}\n")
+        regions = {}
+        if a.regions or rehearse:
+            from dgraph_amd.utils.timing import TimingReport
+
+            TimingReport.reset()
+            TimingReport.init()
+            for _ in range(2):
+                step()
+            # per-step totals of each region over the second step (a region may occur
+            # several times per step: one exchange-wait per halo exchange)
+            for k, lst in TimingReport.resolve().items():
+                vals = [v for v in lst if isinstance(v, float)]
+                regions[k] = round(sum(vals[len(vals) // 2:]), 3)
+            TimingReport.reset()
+        halo_rows = {k: int(es.pattern.num_halo_vertices) if es.pattern is not None else 0
+                     for k, es in (("m2m", pg.m2m), ("g2m", pg.g2m), ("m2g", pg.m2g))}
         result = {"metric": "graphcast_step_ms", "ms_per_step": ms,
+                  "regions_ms": regions, "halo_rows": halo_rows,
+                  "local_grid": int(pg.num_local_grid), "local_mesh": int(pg.num_local_mesh),
+                  **({"rehearsal": {"world": p_world, "rank": p_rank,
+                                    "link_gbps": a.link_gbps}} if rehearse else {}),
                   "channels": a.channels, "channel_config": a.channel_config,
                   "mesh_edges": int(g.m2m[0].size), "duplicate_mesh_edges":
                   not a.dedup_mesh_edges,

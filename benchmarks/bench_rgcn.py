@@ -61,6 +61,11 @@ def parse(argv=None):
                          "master weights, a secondary)")
     ap.add_argument("--path", choices=("auto", "lean", "aggregate-first"), default="auto",
                     help="R-GCN execution path (auto: lean at fp32, aggregate-first under bf16)")
+    ap.add_argument("--link-gbps", type=float, default=0.0,
+                    help="rehearsal link model: every loopback exchange takes latency + "
+                         "largest per-peer message / GBPS (comm/alltoallv.py); the step-time "
+                         "difference to --link-gbps 0 is the exchange time the schedule "
+                         "exposes")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args(argv)
 
@@ -72,6 +77,10 @@ def log(rank, *a):
 
 def main(argv=None):
     args = parse(argv)
+    if args.link_gbps > 0:
+        import dgraph_amd.comm.alltoallv as _A
+
+        _A.LOOPBACK_LINK_GBPS = args.link_gbps
     from dgraph_amd import Communicator
     from dgraph_amd.data.mag import (EDGE_TYPES, HETERO_SHAPES, build_hetero_partition,
                                      hetero_node_data)
@@ -177,10 +186,20 @@ def main(argv=None):
     barrier_sync()
     if dev.type == "cuda":
         torch.cuda.reset_peak_memory_stats()
+    def alloc_stats():
+        if dev.type != "cuda":
+            return {}
+        st = torch.cuda.memory_stats(dev)
+        return {k: int(st.get(k, 0)) for k in ("num_device_alloc", "num_device_free",
+                                                "num_alloc_retries")}
+
+    a0 = alloc_stats()
     t1 = time.perf_counter()
     for _ in range(args.steps):
         l = step()
     barrier_sync()
+    a1 = alloc_stats()
+    alloc_timed = {k: a1[k] - a0[k] for k in a0}
     ms = torch.tensor([(time.perf_counter() - t1) * 1e3 / max(args.steps, 1)],
                       dtype=torch.float64, device=dev)
     if world > 1:
@@ -207,13 +226,16 @@ def main(argv=None):
         "path": "lean" if lean else "aggregate-first",
         "layer0_halo": ("kept" if (not lean or model._keep_static_halo(feats, graph))
                         else "exchanged per step"),
+        "allocator_in_timed_steps": alloc_timed,
     }
     if rehearse:
         rec = {"rehearsal": True, "rank": p_rank, "world": p_world,
                "ms_per_step_compute_loopback": ms_step, "messages_local": E_step,
                "halo_rows": halo_total, "peak_mem_gb": round(peak, 2),
                "final_loss_local": float(lt.item()), "path": rec["path"],
-               "layer0_halo": rec["layer0_halo"],
+               "layer0_halo": rec["layer0_halo"], "link_gbps": args.link_gbps,
+               "allocator_in_timed_steps": alloc_timed,
+               "backend": args.backend,
                "dtype": "bf16" if dtype == torch.bfloat16 else "fp32"}
     if rank == 0:
         print(json.dumps(rec), flush=True)

@@ -15,9 +15,18 @@ Layout:
     dgraph_amd.data      DistributedGraph, preprocessing, partitioners, synthetic graphs
     dgraph_amd.utils     TimingReport, metrics, config, checkpointing
 """
-from .__version__ import __version__
-from .comm.base import BackendEngine, CommunicatorBase
-from .comm.communicator import SUPPORTED_BACKENDS, Communicator
+import os as _os
+
+# ProcessGroupNCCL (RCCL) keeps an asynchronous collective's tensors alive until its
+# work.wait() instead of record_stream-ing them onto its stream: blocks freed with pending
+# uses on another stream cannot be reused until the allocator sees that work finished, so
+# near the HBM limit every exchange allocated fresh memory and the allocator's retries
+# stalled the step (comm/alltoallv.py _EventWork). Read when a process group is created.
+_os.environ.setdefault("TORCH_NCCL_AVOID_RECORD_STREAMS", "1")
+
+from .__version__ import __version__  # noqa: E402
+from .comm.base import BackendEngine, CommunicatorBase  # noqa: E402
+from .comm.communicator import SUPPORTED_BACKENDS, Communicator  # noqa: E402
 
 __all__ = ["Communicator", "CommunicatorBase", "BackendEngine", "SUPPORTED_BACKENDS",
            "__version__"]

@@ -96,13 +96,22 @@ class _Done:
 
 class _EventWork:
     """A pending exchange completed by a stream event: ``wait()`` makes the CURRENT stream
-    wait for it (no host synchronisation)."""
+    wait for it (no host synchronisation). ``keep``: the tensors the exchange's stream still
+    uses, held until ``wait()`` instead of ``record_stream`` — a block freed with a pending
+    use on another stream cannot be reused until the allocator sees that stream's work done,
+    so every exchange of a step allocated fresh memory, and near the HBM limit the
+    allocator's retry (free the whole cache, synchronise) stalled the host for seconds (an
+    R-GCN rehearsal rank: 21 hipMallocs and 2 retries in 2 steps, 2.6 s of idle GPU per step,
+    profiles/r05/). After ``wait()`` the waiting stream is ordered after the exchange, so
+    the blocks are free for its work (the TORCH_NCCL_AVOID_RECORD_STREAMS scheme)."""
 
-    def __init__(self, event):
+    def __init__(self, event, keep=()):
         self.event = event
+        self.keep = keep
 
     def wait(self):
         torch.cuda.current_stream().wait_event(self.event)
+        self.keep = ()
         return None
 
     def is_completed(self):
@@ -262,10 +271,9 @@ class AllToAllV:
                 out[m:].zero_()
             ev = torch.cuda.Event()
             ev.record(side)
-        # the allocator must not hand these blocks out again before the side stream is done
-        send.record_stream(side)
-        out.record_stream(side)
-        work = _EventWork(ev)
+        # held until wait(): the allocator must not hand these blocks out again before the
+        # side stream is done with them
+        work = _EventWork(ev, (send, out))
         if async_op:
             return out, work
         work.wait()
@@ -313,9 +321,7 @@ class AllToAllV:
                     out.copy_(slot[: self.total_recv])
                 ev = torch.cuda.Event()
                 ev.record(side)
-            send.record_stream(side)
-            out.record_stream(side)
-            return _EventWork(ev)
+            return _EventWork(ev, (send, out))
         heap.put_rows(send, slot, self.send_splits, self._shm_offsets)
         if self.total_recv:
             out.copy_(slot[: self.total_recv])

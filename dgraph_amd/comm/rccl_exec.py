@@ -22,11 +22,16 @@ from .. import _native
 
 
 class _EventWork:
-    def __init__(self, event: torch.cuda.Event):
+    """Completion event of an exchange on the executor's stream; the exchange's tensors are
+    held until ``wait()`` (no record_stream: see comm/alltoallv.py _EventWork)."""
+
+    def __init__(self, event: torch.cuda.Event, keep=()):
         self._ev = event
+        self._keep = keep
 
     def wait(self):
         torch.cuda.current_stream().wait_event(self._ev)
+        self._keep = ()
 
     def is_completed(self) -> bool:
         return self._ev.query()
@@ -74,9 +79,7 @@ class RCCLExecutor:
             ops.rccl_alltoallv(self.handle, sends, list(recvs), s, r)
             ev = torch.cuda.Event()
             ev.record(self.stream)
-        for t in list(sends) + list(recvs):
-            t.record_stream(self.stream)
-        return _EventWork(ev)
+        return _EventWork(ev, tuple(sends) + tuple(recvs))
 
     def all_reduce(self, t: torch.Tensor) -> None:
         _native.ops().rccl_allreduce(self.handle, t)

@@ -326,11 +326,19 @@ class DistributedGraphCastGraph:
 
 def _edge_set(agg_g: np.ndarray, other_g: np.ndarray, agg_part: torch.Tensor,
               other_part: torch.Tensor, feats: np.ndarray, rank: int, W: int, group,
-              bipartite: bool) -> EdgeSet:
+              bipartite: bool, rehearse: bool = False) -> EdgeSet:
     el = torch.stack([torch.from_numpy(agg_g), torch.from_numpy(other_g)], 1)
-    cp = build_communication_pattern(el, agg_part, rank, W,
-                                     neighbor_partitioning=other_part if bipartite else None,
-                                     group=group)
+    if rehearse and W > 1:
+        # one rank of a W-way job in one process: every rank's pattern built in memory
+        # (the collectives carried out offline), this rank's kept
+        from ..plan.pattern import build_all_patterns_offline
+
+        cp = build_all_patterns_offline(
+            el, agg_part, W, neighbor_partitioning=other_part if bipartite else None)[rank]
+    else:
+        cp = build_communication_pattern(el, agg_part, rank, W,
+                                         neighbor_partitioning=other_part if bipartite
+                                         else None, group=group)
     mine = (agg_part[el[:, 0]] == rank).numpy()
     lel = cp.local_edge_list
     L_other = int(cp.num_local_neighbor_vertices or cp.num_local_vertices)
@@ -342,11 +350,14 @@ def _edge_set(agg_g: np.ndarray, other_g: np.ndarray, agg_part: torch.Tensor,
 def partition_graphcast_graph(g: GlobalGraphCastGraph, rank: int, world_size: int,
                               grid_part: Optional[torch.Tensor] = None,
                               mesh_part: Optional[torch.Tensor] = None,
-                              group=None, grid_rule: str = "g2m") -> DistributedGraphCastGraph:
+                              group=None, grid_rule: str = "g2m",
+                              rehearse: bool = False) -> DistributedGraphCastGraph:
     """Per-rank view (collective when ``world_size > 1``). Local vertices keep increasing
     global-id order. Given only a mesh placement, the grid placement follows it by
     ``grid_rule``: ``"g2m"`` (the reference's: :func:`grid_placement_from_g2m`) or
-    ``"m2g"`` (:func:`grid_placement_from_mesh`: decoder edges stay rank-local)."""
+    ``"m2g"`` (:func:`grid_placement_from_mesh`: decoder edges stay rank-local).
+    ``rehearse``: no process group — the patterns of all ranks are built in this process
+    and ``rank``'s is kept (a single-GPU rehearsal of one rank of a W-way job)."""
     if mesh_part is not None and grid_part is None:
         if grid_rule not in ("g2m", "m2g"):
             raise ValueError(f"grid_rule {grid_rule!r}: expected 'g2m' or 'm2g'")
@@ -359,13 +370,13 @@ def partition_graphcast_graph(g: GlobalGraphCastGraph, rank: int, world_size: in
     mg_src, mg_dst = g.m2g
     m2m = _edge_set(m_src, m_dst, mesh_part, mesh_part,
                     edge_features(g.mesh_xyz[m_src], g.mesh_xyz[m_dst]), rank, world_size,
-                    group, bipartite=False)
+                    group, bipartite=False, rehearse=rehearse)
     g2m = _edge_set(g_dst, g_src, mesh_part, grid_part,
                     edge_features(g.grid_xyz[g_src], g.mesh_xyz[g_dst]), rank, world_size,
-                    group, bipartite=True)
+                    group, bipartite=True, rehearse=rehearse)
     m2g = _edge_set(mg_dst, mg_src, grid_part, mesh_part,
                     edge_features(g.mesh_xyz[mg_src], g.grid_xyz[mg_dst]), rank, world_size,
-                    group, bipartite=True)
+                    group, bipartite=True, rehearse=rehearse)
     mesh_ids = torch.nonzero(mesh_part == rank).reshape(-1)
     grid_ids = torch.nonzero(grid_part == rank).reshape(-1)
     return DistributedGraphCastGraph(

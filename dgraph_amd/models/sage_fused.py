@@ -98,7 +98,11 @@ COMPACT_T = os.environ.get("DGRAPH_FUSED_COMPACT_T", "off")
 # ogbn-products 0.98: 64-column passes, 71.7 vs 76.1 ms at full width)
 U_FULL_FRAC = float(os.environ.get("DGRAPH_FUSED_U_FULL_FRAC", "0.35"))
 # (column block, ring buffers) of the streamed plan, in order of preference
-STREAM_SHAPES = ((64, 2), (64, 1), (32, 2), (32, 1))
+# (column block, ring buffers) in order of preference: two buffers before wider blocks —
+# with one buffer every block's transfer is exposed (a W=2 structureless rank: 1.1 s of its
+# 3.1 s step), and 32-column passes aggregate at the 64-column rate per byte
+# (profiles/r05/xcd_ab2.log)
+STREAM_SHAPES = ((64, 2), (32, 2), (64, 1), (32, 1))
 # planning rates of the "auto" choice: xGMI per link and direction, fp32 SpMM gather
 # (effective) and fp32 MFMA GEMM rates measured on MI355X (PERFORMANCE.md)
 PLAN_LINK_GBPS = float(os.environ.get("DGRAPH_PLAN_LINK_GBPS", "153"))

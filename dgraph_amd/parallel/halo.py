@@ -96,8 +96,11 @@ class _HaloStart(Function):
 
     @staticmethod
     def backward(ctx, _grad_pending):
+        from ..utils.timing import region
+
         st = ctx.st
-        st.rwork.wait()
+        with region("exchange-wait-bwd"):  # exposed reverse exchange (device time)
+            st.rwork.wait()
         g, st.grad_send, st.rwork = st.grad_send, None, None
         return g, None
 

