@@ -304,6 +304,10 @@ class Job:
             torch.cuda.empty_cache()
         self.inv_n = 1.0 / max(self.n_train, 1)
         self.correct = torch.zeros(2, dtype=torch.long, device=dev)  # val, test
+        # resident after setup (graph, data, activations, workspace): the timed steps'
+        # peak minus this is the step's transient memory
+        self.mem_setup_gb = torch.cuda.memory_allocated(dev) / 1e9 if dev.type == "cuda" \
+            else 0.0
 
     def step(self, restrict_last: bool = False):
         import torch.nn.functional as Fn
@@ -566,6 +570,7 @@ def main():
     test_acc = float(corr[1]) / max(job.n_test, 1)
     halo = job.halo_stats()
     alloc_timed = dict(getattr(job, "alloc_timed", {}))
+    mem_setup = getattr(job, "mem_setup_gb", 0.0)
     regions = region_breakdown(job)
     use_fused = job.use_fused
     schedule = job.fused.schedule if job.fused is not None else {}
@@ -665,6 +670,7 @@ def main():
                           "world": args.rehearse_world,
                           "ms_per_step_compute_loopback": ms, "E_local": E_msg,
                           "halo_rows": halo_total, "peak_mem_gb": round(peak_gb, 2),
+                          "mem_after_setup_gb": round(mem_setup, 2),
                           "dtype": args.dtype, "global_frac": args.global_frac,
                           "halo_recompute": job_recompute,
                           "restrict_last": head_restrict,
@@ -735,6 +741,7 @@ def main():
             "val_acc": val_acc,
             "test_acc": test_acc,
             "peak_mem_gb_rank0": round(peak_gb, 2),
+            "mem_after_setup_gb_rank0": round(mem_setup, 2),
             # hipMalloc/hipFree calls and allocation retries inside the timed steps (0 =
             # steady state served from preplanned buffers and the allocator cache)
             "allocator_in_timed_steps": alloc_timed,

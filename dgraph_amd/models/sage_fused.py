@@ -81,6 +81,9 @@ BOUNDARY_STORE = os.environ.get("DGRAPH_FUSED_BOUNDARY_STORE", "auto")
 # the memory plan has room for nS x width floats (always with streamed halos, whose plan
 # already holds that store). Saves a pass over the S rows' entries per step.
 KEEP_AS = os.environ.get("DGRAPH_FUSED_KEEP_AS", "auto")
+# streamed hidden layers: the self term h W_self + b as a separate GEMM during the first
+# column block's transfer (1), or the dual GEMM after the aggregation, in place (0)
+STREAM_FILL = os.environ.get("DGRAPH_FUSED_STREAM_FILL", "1") != "0"
 # W > 1: hidden-layer halos exchanged and consumed in column blocks ("stream") instead of
 # kept at full width for the whole step — "auto" when the full-width plan does not fit (a
 # structureless graph's halo is nearly every remote vertex), "on" / "off" to force
@@ -969,7 +972,13 @@ class FusedSAGE:
                     self._keep_s_rows(ci, a, keep_s)
                 self._gemm(hin[r0:r1], ws, a, wn, bias=bias, relu=True, out=hout[r0:r1])
 
-            if self.stream and l > 0:
+            if self.stream and l > 0 and not STREAM_FILL:
+                self._stream_fwd(hin, hout, f"fwd_l{l}")
+                for ci, (r0, r1) in enumerate(self.chunks):
+                    if r1 > r0:
+                        consume(ci, hout[r0:r1])
+                halos.append(None)
+            elif self.stream and l > 0:
                 # streamed halo: every row's aggregate into the output layer's store
                 # (column block by column block; free until the output layer), while the
                 # self term h W_self + b runs into the layer's output buffer during the
