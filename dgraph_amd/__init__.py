@@ -24,6 +24,28 @@ import os as _os
 # stalled the step (comm/alltoallv.py _EventWork). Read when a process group is created.
 _os.environ.setdefault("TORCH_NCCL_AVOID_RECORD_STREAMS", "1")
 
+
+def _hw_queues() -> None:
+    """At least 8 hardware queues per process (HIP's default, and the GPU boxes' exported
+    value, is 4): with 4, torch's pool streams share queues with the compute stream, and a
+    comm stream on the compute stream's queue runs in order with it — no overlap
+    (PERFORMANCE.md, round 5). Only before the HIP runtime starts; DGRAPH_HW_QUEUES sets
+    the value explicitly."""
+    import sys
+
+    t = sys.modules.get("torch")
+    if t is not None and t.cuda.is_initialized():
+        return
+    want = _os.environ.get("DGRAPH_HW_QUEUES")
+    cur = _os.environ.get("GPU_MAX_HW_QUEUES", "")
+    if want:
+        _os.environ["GPU_MAX_HW_QUEUES"] = want
+    elif not cur.isdigit() or int(cur) < 8:
+        _os.environ["GPU_MAX_HW_QUEUES"] = "8"
+
+
+_hw_queues()
+
 from .__version__ import __version__  # noqa: E402
 from .comm.base import BackendEngine, CommunicatorBase  # noqa: E402
 from .comm.communicator import SUPPORTED_BACKENDS, Communicator  # noqa: E402

@@ -84,6 +84,9 @@ KEEP_AS = os.environ.get("DGRAPH_FUSED_KEEP_AS", "auto")
 # streamed hidden layers: the self term h W_self + b as a separate GEMM during the first
 # column block's transfer (1), or the dual GEMM after the aggregation, in place (0)
 STREAM_FILL = os.environ.get("DGRAPH_FUSED_STREAM_FILL", "1") != "0"
+# streamed halos: the first column block half as wide as the rest (the pipeline fill, whose
+# transfer nothing but the fill work hides, is half as long)
+STREAM_RAMP = os.environ.get("DGRAPH_FUSED_STREAM_RAMP", "1") != "0"
 # W > 1: hidden-layer halos exchanged and consumed in column blocks ("stream") instead of
 # kept at full width for the whole step — "auto" when the full-width plan does not fit (a
 # structureless graph's halo is nearly every remote vertex), "on" / "off" to force
@@ -493,6 +496,13 @@ class FusedSAGE:
                 KEEP_AGG0 == "on" or free - need_h - other - need0 > margin):
             self.agg0 = torch.empty(L, self.d0, dtype=torch.float32, device=dev)
             other += need0
+        # streamed output layer: its self term h W_self + b for every row, computed during
+        # the first column block's transfer (the pipeline fill), when the plan has room
+        self.zself = None
+        need_z = L * self.Cp * 4
+        if self.stream and STREAM_FILL and free - need_h - other - need_z > margin:
+            self.zself = torch.empty(L, self.Cp, dtype=torch.float32, device=dev)
+            other += need_z
         spare = max(free - need_h - other, 1 << 28)
         per_row = 4 * (wA + wB)  # aggregate + logit/gradient chunk buffers
         cr = chunk_rows or CHUNK_ROWS
@@ -660,6 +670,7 @@ class FusedSAGE:
                 "halo_stream": ({"column_block": self.cw, "buffers": self.nbuf}
                                 if self.stream else False),
                 "keep_agg0": self.agg0 is not None, "keep_aS": self.aS_keep is not None,
+                "output_self_term_fill": self.zself is not None,
                 "compact_T": self.TS is not None,
                 "compact_halo_T": self.HTS is not None, "support_rows": self.nS}
 
@@ -850,6 +861,20 @@ class FusedSAGE:
         with torch.cuda.stream(side):
             return fn()
 
+    def _stream_blocks(self, F: int) -> List[Tuple[int, int]]:
+        """Column blocks of a streamed exchange of width ``F``: ``cw`` wide, the first one
+        ``cw / 2`` (STREAM_RAMP) so the pipeline fill is short."""
+        cw = self.cw
+        if STREAM_RAMP and cw >= 64 and F > cw:
+            return [(0, cw // 2)] + _ranges(cw // 2, F, cw)
+        return _ranges(0, F, cw)
+
+    @staticmethod
+    def _ring(bufs, b: int, w: int) -> torch.Tensor:
+        """Ring buffer ``b`` as a contiguous ``[rows, w]`` block (w <= its width)."""
+        t = bufs[b]
+        return t if t.shape[1] == w else t.view(-1)[:t.shape[0] * w].view(t.shape[0], w)
+
     def _stream_fwd(self, h: torch.Tensor, out: torch.Tensor, name: str,
                     rows: Optional[torch.Tensor] = None, fill=None) -> None:
         """Streamed halo: ``out[:, c] = mean over in-neighbours of h[:, c]`` for every row
@@ -858,16 +883,18 @@ class FusedSAGE:
         links while block k is aggregated (two-source: local and received rows in one
         pass). A block's buffers are reused only after the compute stream consumed them
         (the comm stream waits for it before every pack)."""
-        g, L, cw, nb = self.g, self.L, self.cw, self.nbuf
-        blocks = _ranges(0, h.shape[1], cw)
+        g, L, nb = self.g, self.L, self.nbuf
+        blocks = self._stream_blocks(h.shape[1])
 
         def issue(k):
             c0, c1 = blocks[k]
             b = k % nb
+            snd = self._ring(self.ring_send, b, c1 - c0)
+            rcv = self._ring(self.ring_recv, b, c1 - c0)
 
             def go():
-                K.copy_rows(h[:, c0:c1], src_idx=g.send_map.idx, out=self.ring_send[b])
-                return g.a2a(self.ring_send[b], out=self.ring_recv[b], async_op=True)
+                K.copy_rows(h[:, c0:c1], src_idx=g.send_map.idx, out=snd)
+                return g.a2a(snd, out=rcv, async_op=True)
             return self._on_comm_stream(go)
 
         works = {0: issue(0)}
@@ -896,22 +923,22 @@ class FusedSAGE:
         contributions ``A_halo^T u`` (column-mapped onto S) are sent to their owners and
         summed into ``gz`` (zeroed first; the ReLU gate of layer 0 applied), block k+1's
         contributions computed while block k is on the links."""
-        g, cw, nb = self.g, self.cw, self.nbuf
-        blocks = _ranges(0, u.shape[1], cw)
+        g, nb = self.g, self.nbuf
+        blocks = self._stream_blocks(u.shape[1])
         gz.zero_()
         st = self.send_st
 
         def issue(k):
             c0, c1 = blocks[k]
             b = k % nb
-            hg = self.ring_recv[b]
+            hg = self._ring(self.ring_recv, b, c1 - c0)
+            snd = self._ring(self.ring_send, b, c1 - c0)
             if self.HTS is not None:
                 self._spmm(self.HTS[0], self.HTS[1], u[:, c0:c1], hg)
             else:
                 self._spmm_u(self.haloT.rowptr, self.haloT.col, u[:, c0:c1], hg,
                              col_map=self.smap)
-            return self._on_comm_stream(
-                lambda: g.a2a_rev(hg, out=self.ring_send[b], async_op=True))
+            return self._on_comm_stream(lambda: g.a2a_rev(hg, out=snd, async_op=True))
 
         works = {0: issue(0)}
         for k, (c0, c1) in enumerate(blocks):
@@ -1020,7 +1047,10 @@ class FusedSAGE:
         self.acc_out_n.reset()
         hl = hin
         if self.stream:
-            self._stream_fwd(hl, self.agg_full, "fwd_out")
+            zs = self.zself
+            self._stream_fwd(hl, self.agg_full, "fwd_out",
+                             fill=None if zs is None else
+                             (lambda: self._gemm(hl, wsp, bias=bp, out=zs)))
             for ci, (r0, r1) in enumerate(self.chunks):
                 if r1 > r0:
                     self._out_chunk(ci, self.agg_full[r0:r1, :hid], hl, wsp, wnp, bp)
@@ -1053,7 +1083,10 @@ class FusedSAGE:
         C, Cp = self.C, self.Cp
         r0, r1 = self.chunks[ci]
         n = r1 - r0
-        z = self._gemm(hl[r0:r1], wsp, a, wnp, bias=bp, out=self.bufB[:n, :Cp])
+        if self.stream and self.zself is not None:  # self term from the pipeline fill
+            z = self._gemm(a, wnp, cin=self.zself[r0:r1], beta=1.0, out=self.bufB[:n, :Cp])
+        else:
+            z = self._gemm(hl[r0:r1], wsp, a, wnp, bias=bp, out=self.bufB[:n, :Cp])
         t0, t1 = self.ch_T[ci]
         if t1 > t0:
             # one fused kernel: per-row loss and the scaled softmax gradient rows
