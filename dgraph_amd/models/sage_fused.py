@@ -85,8 +85,14 @@ KEEP_AS = os.environ.get("DGRAPH_FUSED_KEEP_AS", "auto")
 # column block's transfer (1), or the dual GEMM after the aggregation, in place (0)
 STREAM_FILL = os.environ.get("DGRAPH_FUSED_STREAM_FILL", "1") != "0"
 # streamed halos: the first column block half as wide as the rest (the pipeline fill, whose
-# transfer nothing but the fill work hides, is half as long)
-STREAM_RAMP = os.environ.get("DGRAPH_FUSED_STREAM_RAMP", "1") != "0"
+# transfer nothing but the fill work hides, is half as long). Off: the extra column pass
+# costs what it saves (W=8 structureless rank 700.6 ms with, 698.8 without; exposed
+# exchange 15 vs 53 ms, profiles/r05/rehearse_structureless_ramp_zself.jsonl)
+STREAM_RAMP = os.environ.get("DGRAPH_FUSED_STREAM_RAMP", "0") != "0"
+# streamed output layer: its self term as a separate GEMM during the first block's transfer
+# (into an [L, Cp] store, when it fits). Off: the split GEMM's extra store traffic costs
+# what it hides (W=8 structureless fwd_out + its exchange 196 ms with, 191.5 without)
+STREAM_OUT_FILL = os.environ.get("DGRAPH_FUSED_STREAM_OUT_FILL", "0") != "0"
 # W > 1: hidden-layer halos exchanged and consumed in column blocks ("stream") instead of
 # kept at full width for the whole step — "auto" when the full-width plan does not fit (a
 # structureless graph's halo is nearly every remote vertex), "on" / "off" to force
@@ -500,7 +506,7 @@ class FusedSAGE:
         # the first column block's transfer (the pipeline fill), when the plan has room
         self.zself = None
         need_z = L * self.Cp * 4
-        if self.stream and STREAM_FILL and free - need_h - other - need_z > margin:
+        if self.stream and STREAM_OUT_FILL and free - need_h - other - need_z > margin:
             self.zself = torch.empty(L, self.Cp, dtype=torch.float32, device=dev)
             other += need_z
         spare = max(free - need_h - other, 1 << 28)

@@ -78,7 +78,7 @@ def _run(rank, world, args, dtype, steps=3):
 def _body(rank, world, kw, dt):
     torch.cuda.set_device(0)
     dtype = torch.float32 if dt == "fp32" else torch.bfloat16
-    args = _args(dtype=dt, **kw)
+    args = _args(dtype=dt, **{k: v for k, v in kw.items() if k != "stream_fill"})
     ref = _run(0, 1, args, dtype) if rank == 0 else None
     dist.barrier()
     got = _run(rank, world, args, dtype)
@@ -99,9 +99,15 @@ def _body(rank, world, kw, dt):
         # first-step gradients: fp32 rounding only (measured 1e-7 .. 7e-7 relative,
         # profiles/r03/multiproc_w2_vs_w1.log); the W=2 aggregation sums interior and halo
         # parts in another order
+        # (streamed hidden layers run the self term as a separate GEMM during the pipeline
+        # fill: one more fp32 rounding of every pre-activation than the W=1 dual GEMM, which
+        # moves 512-wide hidden-layer gradients by 2-4e-5 relative through the few ReLU
+        # gates it flips — 4e-7 with the fill off, scripts/debug/h512_w2_grads.py; an
+        # aliasing error like ADVICE r4's is O(1))
+        g_tol = 1e-4 if kw.get("stream_fill") else 1e-5
         for a, b in zip(got["grads"], ref["grads"]):
             rel = float((a - b).norm() / b.norm().clamp_min(1e-30))
-            assert rel < 1e-5, f"W={world} gradient differs from W=1 by {rel:.2e} (relative)"
+            assert rel < g_tol, f"W={world} gradient differs from W=1 by {rel:.2e} (relative)"
             assert float((a - b).abs().max()) <= 1e-5 * float(b.abs().max()) + 1e-9
         # after 3 Adam steps: Adam divides by sqrt(v), so a near-zero (cancelling) gradient
         # entry whose fp32 rounding differs moves by up to a whole lr step; everything else
@@ -206,4 +212,7 @@ def test_bench_step_hidden512_two_processes(monkeypatch, env):
     # seed 1: with seed 0 one layer-1 pre-activation sits at a ReLU tie that the W=2
     # summation order flips (the hidden-layer gradients then differ by 2e-4 relative at
     # W=2 vs W=1 whatever the path; seeds 1 and 2: 2-4e-7, scripts/debug/h512_w2_grads.py)
-    run_ranks(_body, 2, dict(global_frac=0.05, hidden=512, seed=1), "fp32", timeout=240)
+    kw = dict(global_frac=0.05, hidden=512, seed=1)
+    if "DGRAPH_FUSED_HALO_STREAM" in env:
+        kw["stream_fill"] = True
+    run_ranks(_body, 2, kw, "fp32", timeout=240)

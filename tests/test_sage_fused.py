@@ -210,6 +210,8 @@ def _interior_first_body(rank, world, ref_path, overlap, store="auto", stream="o
     sf.HALO_STREAM = "on" if stream != "off" else "off"
     if stream == "single":  # one ring buffer: exchange and aggregation alternate
         sf.STREAM_SHAPES = ((64, 1),)
+    if stream == "ramp":  # half-width first block, output-layer self term as the fill
+        sf.STREAM_RAMP = sf.STREAM_OUT_FILL = True
     if stream != "off":  # the input's static halo exchanged in 16-column blocks too
         DistGraph.STATIC_BLOCK_BYTES = 1024
     shape = SHAPES["ogbn-papers100M"].scaled(SCALE)
@@ -237,6 +239,8 @@ def _interior_first_body(rank, world, ref_path, overlap, store="auto", stream="o
     assert ex.stream == (stream != "off")
     if stream == "single":
         assert ex.nbuf == 1
+    if stream == "ramp":
+        assert ex.zself is not None and len(ex._stream_blocks(256)) == 5
     assert g.interior is None  # released: the executor runs on its own adjacency
     loss = ex.step()
     grads = [p.grad.clone() for p in model.parameters()]
@@ -257,7 +261,7 @@ def _interior_first_body(rank, world, ref_path, overlap, store="auto", stream="o
     (4, True, "off", "off"), (2, False, "auto", "off"),
     # streamed halos (column blocks through a buffer ring; the structureless-graph plan)
     (2, True, "auto", "on"), (4, True, "auto", "on"), (8, True, "auto", "on"),
-    (2, True, "auto", "single")])
+    (2, True, "auto", "single"), (2, True, "auto", "ramp")])
 def test_fused_interior_first_matches_w1(ranks, world, overlap, store, stream, tmp_path):
     loss, grads, corr = _fused_grads(0, 1, gf=0.05)
     p = tmp_path / "ref.pt"
