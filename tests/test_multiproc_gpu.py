@@ -108,7 +108,7 @@ def _body(rank, world, kw, dt):
         for a, b in zip(got["grads"], ref["grads"]):
             rel = float((a - b).norm() / b.norm().clamp_min(1e-30))
             assert rel < g_tol, f"W={world} gradient differs from W=1 by {rel:.2e} (relative)"
-            assert float((a - b).abs().max()) <= 1e-5 * float(b.abs().max()) + 1e-9
+            assert float((a - b).abs().max()) <= 10 * g_tol * float(b.abs().max()) + 1e-9
         # after 3 Adam steps: Adam divides by sqrt(v), so a near-zero (cancelling) gradient
         # entry whose fp32 rounding differs moves by up to a whole lr step; everything else
         # must agree to fp32 resolution
