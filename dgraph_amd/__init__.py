@@ -17,12 +17,9 @@ Layout:
 """
 import os as _os
 
-# ProcessGroupNCCL (RCCL) keeps an asynchronous collective's tensors alive until its
-# work.wait() instead of record_stream-ing them onto its stream: blocks freed with pending
-# uses on another stream cannot be reused until the allocator sees that work finished, so
-# near the HBM limit every exchange allocated fresh memory and the allocator's retries
-# stalled the step (comm/alltoallv.py _EventWork). Read when a process group is created.
-_os.environ.setdefault("TORCH_NCCL_AVOID_RECORD_STREAMS", "1")
+# (ProcessGroupNCCL keeps an asynchronous collective's tensors alive until its work.wait()
+# instead of record_stream-ing them — the default of this torch; the library's own
+# transports do the same, comm/alltoallv.py _EventWork.)
 
 
 def _hw_queues() -> None:
