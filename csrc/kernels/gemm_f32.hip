@@ -396,11 +396,14 @@ bool g_f32_dynamic = true;
 void set_f32_dynamic(bool on) { g_f32_dynamic = on; }
 
 namespace {
-constexpr int kCtrSlots = 1024;      // streams per device
+constexpr int kCtrStreams = 1024;    // eager slots: one per stream
+constexpr int kCtrCaptured = 3072;   // one per launch recorded into a HIP graph
+constexpr int kCtrSlots = kCtrStreams + kCtrCaptured;
 constexpr int kCtrStride = 16;       // ints per slot (64 B: one slot per cache line)
 int* g_ctr_ring[64] = {nullptr};
 std::mutex g_ctr_mu;
 std::unordered_map<hipStream_t, int> g_ctr_slot[64];
+int g_ctr_captured[64] = {0};
 
 hipError_t ctr_ring(int dev) {
   if (g_ctr_ring[dev] != nullptr) return hipSuccess;
@@ -426,16 +429,29 @@ hipError_t work_counters_init() {
 int* work_counter(hipStream_t st) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cap) != hipSuccess) return nullptr;
   std::lock_guard<std::mutex> lk(g_ctr_mu);
   if (ctr_ring(dev) != hipSuccess) return nullptr;
-  auto& m = g_ctr_slot[dev];
-  auto it = m.find(st);
-  if (it == m.end()) {
-    if (static_cast<int>(m.size()) >= kCtrSlots) return nullptr;  // more streams than slots
-    it = m.emplace(st, static_cast<int>(m.size())).first;
+  int slot;
+  if (cap == hipStreamCaptureStatusActive) {
+    // a launch recorded into a graph gets a slot of its own, never shared with eager
+    // launches: a replay may run on any stream, concurrently with eager kernels of the
+    // capturing stream (the kernel's last block re-zeroes it for the next replay)
+    if (g_ctr_captured[dev] >= kCtrCaptured) return nullptr;
+    slot = kCtrStreams + g_ctr_captured[dev]++;
+  } else {
+    auto& m = g_ctr_slot[dev];
+    auto it = m.find(st);
+    if (it == m.end()) {
+      if (static_cast<int>(m.size()) >= kCtrStreams) return nullptr;  // more streams than slots
+      it = m.emplace(st, static_cast<int>(m.size())).first;
+    }
+    slot = it->second;
   }
-  // zero at every launch boundary of `st`: the previous kernel's last block reset it
-  return g_ctr_ring[dev] + static_cast<size_t>(it->second) * kCtrStride;
+  // zero at every launch boundary of the slot's stream / graph node: the previous kernel's
+  // last block reset it
+  return g_ctr_ring[dev] + static_cast<size_t>(slot) * kCtrStride;
 }
 
 bool gemm_f32_supported(int64_t N, int64_t K1, int64_t K2) {

@@ -251,8 +251,10 @@ hipError_t dual_gemm_bs(const void* A1, int64_t lda1, const void* B1t, int64_t K
 // from it, so a block that cannot start (its CU held by another stream's kernel, e.g.
 // RCCL's during a halo exchange) costs nothing: the running blocks take its work. The
 // kernel's last block to finish resets the pair (work_counter_release), so no memset is
-// enqueued per launch, a captured HIP graph replays with a zeroed slot every time, and
-// kernels of different streams never share a slot (launches on one stream serialise).
+// enqueued per launch and kernels of different streams never share a slot (launches on
+// one stream serialise). A launch recorded into a HIP graph gets a slot of its own (a
+// replay may run on any stream, next to eager kernels of the capturing stream), zeroed
+// again by its last block for the next replay.
 int* work_counter(hipStream_t st);
 // Allocate the counter slots of the current device now (before any stream capture).
 hipError_t work_counters_init();
