@@ -99,3 +99,43 @@ def test_halo_exchange_single_rank():
     x = torch.randn(V, 3, requires_grad=True)
     h = HaloExchange(Fake())(x, cp)
     assert h.shape == (0, 3)
+
+
+def _async_halo(rank, world):
+    """AsyncHalo (issue, independent work, wait) equals the synchronous HaloExchange,
+    forward and backward (the send rows' gradient arrives through the reverse exchange
+    issued from the halo gradient)."""
+    from dgraph_amd import Communicator
+    from dgraph_amd.parallel.halo import AsyncHalo, HaloExchange
+
+    comm = Communicator.init_process_group("nccl")
+    try:
+        V, E = _graph(seed=3)
+        part = torch.randint(0, world, (V,), generator=torch.Generator().manual_seed(4))
+        cp = build_communication_pattern(E, part, rank, world)
+        L = cp.num_local_vertices
+        g = torch.Generator().manual_seed(10 + rank)
+        x0 = torch.randn(L, 5, generator=g, dtype=torch.float64)
+        wh = torch.randn(cp.num_halo_vertices, 5, generator=g, dtype=torch.float64)
+        res = []
+        for mode in ("sync", "async"):
+            x = x0.clone().requires_grad_()
+            if mode == "sync":
+                halo = HaloExchange(comm)(x, cp)
+            else:
+                h = AsyncHalo.start(comm, x, cp)
+                local_work = (x * 2).sum()  # independent work while the exchange is pending
+                halo = h.wait()
+            loss = (halo * wh).sum() + (x ** 2).sum() + (local_work if mode == "async" else 0)
+            loss.backward()
+            grad = x.grad.clone() - (2.0 if mode == "async" else 0.0)
+            res.append((halo.detach().clone(), grad))
+        assert torch.equal(res[0][0], res[1][0])
+        torch.testing.assert_close(res[1][1], res[0][1])
+    finally:
+        comm.destroy()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_async_halo_matches_sync(ranks, world):
+    ranks(_async_halo, world)
