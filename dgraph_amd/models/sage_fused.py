@@ -414,6 +414,7 @@ class FusedSAGE:
         self.halo_bytes = 4 * (H * self.d0 + (self.nl - 1) * H * self.hid + n_send * self.hid)
         self.stream, self.cw, self.nbuf = False, 0, 0
         other += x_tr
+        w_lh = self.d0 if self.nl == 2 else self.hid  # width of the last hidden layer's input
         # the output-layer backward's sub-plan exchange (halo rows adjacent to the loss rows,
         # A[T, halo]^T u2 out, owners' rows back): resident buffers in storage that is dead
         # during that exchange — the last received-halo / send buffers, or the streamed ring
@@ -430,7 +431,7 @@ class FusedSAGE:
             # re-fetched h1, the reverse exchange's input-layer gradient)
             # (the reverse exchange's input-layer gradient store lives in the output
             # layer's aggregate store, dead once the forward is done)
-            stores = L * max(self.hid, self.d0) * 4 + self.nS * self.hid * 4
+            stores = L * max(self.hid, self.d0) * 4 + self.nS * w_lh * 4
             for cw, nb in STREAM_SHAPES:
                 if self.hid % cw:
                     continue
@@ -489,7 +490,7 @@ class FusedSAGE:
         # the last hidden layer's input aggregate on the S rows kept from the forward (else
         # re-aggregated in the backward); streamed halos keep it in aS_full (planned above)
         self.aS_keep = None
-        self.w_lh = self.d0 if self.nl == 2 else self.hid  # width of that layer's input
+        self.w_lh = w_lh
         need_as = self.nS * self.w_lh * 4
         self.keep_as = KEEP_AS == "on" or self.stream or (
             KEEP_AS == "auto" and free - need_h - other - need_as > margin)
