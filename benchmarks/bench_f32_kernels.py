@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--rows", type=int, default=1438388)
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--global-frac", type=float, default=0.05)
+    ap.add_argument("--window", type=int, default=1 << 14)
     ap.add_argument("--xcd", default="1", help="SpMM XCD-contiguous block remap: 0, 1 or "
                     "0,1 (A/B in one process)")
     ap.add_argument("--pass-cols", default="64", help="SpMM pass widths, comma-separated")
@@ -38,7 +39,7 @@ def main():
     _native.load()
     dev = torch.device("cuda", 0)
     shape = SHAPES["ogbn-papers100M"].scaled(a.scale)
-    p = build_partition(shape, 0, 1, dev, global_frac=a.global_frac)
+    p = build_partition(shape, 0, 1, dev, global_frac=a.global_frac, window=a.window)
     csr = p["csr"]
     L = p["L"]
     inv = csr.inv_degree()
