@@ -111,3 +111,24 @@ def test_rehearsal_delayed_equals_instant_bitwise(stream):
     ex1 = sum(v for k, v in r1.items() if k.startswith("exchange"))
     ex0 = sum(v for k, v in r0.items() if k.startswith("exchange"))
     assert ex1 > ex0 + 1.0, (r0, r1)
+
+
+@pytest.mark.parametrize("nbytes", [16, 4096 + 4, 3 * (1 << 20) + 7])
+def test_link_copy_bytes_and_hold(nbytes):
+    """The link model's transfer kernel copies every byte (16-B vectors and a byte tail)
+    and holds its stream for at least the modelled time."""
+    _native.load()
+    src = torch.randint(0, 255, (nbytes,), dtype=torch.uint8, device=DEV)
+    dst = torch.zeros_like(src)
+    _native.ops().link_copy(src, dst, 0.0, 1024, 16)
+    torch.cuda.synchronize()
+    assert torch.equal(src, dst)
+    dst.zero_()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    _native.ops().link_copy(src, dst, 3000.0, 1024, 16)
+    e.record()
+    torch.cuda.synchronize()
+    assert torch.equal(src, dst)
+    assert s.elapsed_time(e) >= 3.0 * 0.95
