@@ -448,6 +448,64 @@ def timed(job: Job, steps: int, warmup: int, restrict_last: bool, verbose: bool 
     return float(red.item()), float(tot[0].item()), float(tot[1].item())
 
 
+def link_probe(job: "Job", width: int = 64, iters: int = 5) -> dict:
+    """Achieved xGMI bandwidth of this job's own halo exchange (W > 1, every rank, after
+    the timed steps): the plan's all-to-all-v of ``width`` fp32 columns, ``iters`` times
+    back to back between barriers, timed with stream events; per rank the largest
+    per-peer message over the exchange time is the per-link rate its slowest link
+    delivered. Reduced to max / min over ranks. (The rehearsal's link model assumes
+    153 GB/s per link; this is the measured number.)"""
+    g = job.graph
+    a2a = getattr(g, "a2a", None)
+    if job.world <= 1 or a2a is None or job.dev.type != "cuda":
+        return {}
+
+    def view(t, n):  # a contiguous [n, width] block of a resident buffer, if large enough
+        return t.view(-1)[:n * width].view(n, width) if t is not None and \
+            t.is_contiguous() and t.numel() >= n * width else None
+
+    ex = job.fused
+    send = view(getattr(ex, "send_buf", None), a2a.total_send)
+    recv = view((getattr(ex, "halo_buf", None) or [None])[0], a2a.total_recv)
+    ok = 1
+    try:  # (resident exchange buffers of the executor when it has them, else fresh)
+        if send is None:
+            send = torch.empty(a2a.total_send, width, device=job.dev)
+        if recv is None:
+            recv = torch.empty(a2a.total_recv, width, device=job.dev)
+        send.fill_(1.0)
+    except torch.OutOfMemoryError:
+        ok = 0
+    okt = torch.tensor([ok], device=job.dev)
+    dist.all_reduce(okt, op=dist.ReduceOp.MIN)  # every rank probes, or none does
+    if int(okt) == 0:
+        return {"skipped": "no device memory for the probe buffers"}
+    for _ in range(2):
+        a2a(send, out=recv)
+    torch.cuda.synchronize()
+    dist.barrier()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        a2a(send, out=recv)
+    e.record()
+    torch.cuda.synchronize()
+    ms = s.elapsed_time(e) / iters
+    peer = max(max(a2a.send_splits, default=0), max(a2a.recv_splits, default=0)) * width * 4
+    tot = (a2a.total_send + a2a.total_recv) * width * 4
+    v = torch.tensor([ms, peer / (ms * 1e6), tot / (ms * 1e6)], dtype=torch.float64,
+                     device=job.dev)
+    vmax, vmin = v.clone(), v.clone()
+    dist.all_reduce(vmax, op=dist.ReduceOp.MAX)
+    dist.all_reduce(vmin, op=dist.ReduceOp.MIN)
+    del send, recv
+    return {"columns": width, "exchange_ms_max": round(float(vmax[0]), 3),
+            "largest_peer_message_GBps_min_over_ranks": round(float(vmin[1]), 1),
+            "largest_peer_message_GBps_max_over_ranks": round(float(vmax[1]), 1),
+            "rank_send_plus_recv_GBps_min_over_ranks": round(float(vmin[2]), 1),
+            "transport": os.environ.get("DGRAPH_A2A_IMPL", "torch")}
+
+
 def region_breakdown(job: "Job") -> dict:
     """One extra (untimed) step with stream events at the executor's region boundaries:
     per-region device ms on every rank (no barrier or host sync inside the step), reduced
@@ -572,6 +630,7 @@ def main():
     alloc_timed = dict(getattr(job, "alloc_timed", {}))
     mem_setup = getattr(job, "mem_setup_gb", 0.0)
     regions = region_breakdown(job)
+    xgmi = link_probe(job) if (world > 1 and not job.rehearse) else {}
     use_fused = job.use_fused
     schedule = job.fused.schedule if job.fused is not None else {}
     pass_for = {str(k): v for k, v in getattr(job.fused, "pass_for", {}).items()} \
@@ -766,6 +825,7 @@ def main():
             "allocator_in_timed_steps": alloc_timed,
             **({"halo": halo} if halo else {}),
             **({"regions": regions} if regions else {}),
+            **({"xgmi_probe": xgmi} if xgmi else {}),
             **extra,
         }
         print(json.dumps(rec), flush=True)

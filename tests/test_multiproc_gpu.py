@@ -216,3 +216,31 @@ def test_bench_step_hidden512_two_processes(monkeypatch, env):
     if "DGRAPH_FUSED_HALO_STREAM" in env:
         kw["stream_fill"] = True
     run_ranks(_body, 2, kw, "fp32", timeout=240)
+
+
+def _probe_body(rank, world):
+    import bench
+
+    torch.cuda.set_device(0)
+    args = _args(dtype="fp32", global_frac=0.05)
+    comm = types.SimpleNamespace(get_rank=lambda: rank, get_world_size=lambda: world,
+                                 group=None)
+    job = bench.Job(args, comm, torch.device("cuda", 0), args.global_frac, torch.float32)
+    job.step(False)
+    rec = bench.link_probe(job, width=64, iters=3)
+    from dgraph_amd.comm.alltoallv import close_shmem_heaps
+
+    job.free()
+    torch.cuda.synchronize()
+    close_shmem_heaps()
+    assert rec["exchange_ms_max"] > 0, rec
+    assert rec["largest_peer_message_GBps_min_over_ranks"] > 0, rec
+    assert rec["transport"] == "shmem"
+
+
+def test_bench_link_probe_two_processes(monkeypatch):
+    """bench.py's W > 1 link probe (the achieved per-link rate of the job's own halo
+    exchange, reported by the driver's multi-GPU runs) runs collectively and reports."""
+    monkeypatch.setenv("DGRAPH_A2A_IMPL", "shmem")
+    monkeypatch.setenv("DGRAPH_SYMHEAP_BYTES", str(1 << 30))
+    run_ranks(_probe_body, 2, timeout=240)
