@@ -118,8 +118,9 @@ STREAM_SHAPES = ((64, 2), (32, 2), (64, 1), (32, 1))
 # planning rates of the "auto" choice: xGMI per link and direction, fp32 SpMM gather
 # (effective) and fp32 MFMA GEMM rates measured on MI355X (PERFORMANCE.md)
 PLAN_LINK_GBPS = float(os.environ.get("DGRAPH_PLAN_LINK_GBPS", "153"))
-PLAN_SPMM_TBPS = 10.0
-PLAN_GEMM_TFPS = 100.0
+PLAN_SPMM_TBPS = 13.0   # row-group SpMM, 64-column passes, bench graph (PERFORMANCE.md)
+PLAN_GEMM_TFPS = 120.0  # exact-f32 MFMA GEMM, interleaved with aggregations
+PLAN_HBM_TBPS = 5.0     # streaming read-modify-write of a store
 
 
 def _ranges(a: int, b: int, step: int) -> List[Tuple[int, int]]:
@@ -477,16 +478,6 @@ class FusedSAGE:
                 self.HTS = _compact_by_map(self.haloT.rowptr, self.haloT.col, None, self.smap,
                                            Hn)
                 other += hts_bytes
-        # W > 1: a whole-layer aggregate buffer lets the interior part of the OUTPUT layer's
-        # boundary rows run while its halo rows are in flight (hidden layers use their own
-        # output buffer for that)
-        self.use_store = self._plan_store()
-        self.agg_full = None
-        need_full = (L - self.Li) * wA * 4
-        if graph.send_map is not None and OVERLAP_FWD and self.Li < L and not self.stream \
-                and self.use_store["out"] and free - need_h - other - need_full > margin:
-            self.agg_full = torch.empty(L - self.Li, wA, dtype=torch.float32, device=dev)
-            other += need_full
         # the last hidden layer's input aggregate on the S rows kept from the forward (else
         # re-aggregated in the backward); streamed halos keep it in aS_full (planned above)
         self.aS_keep = None
@@ -503,6 +494,17 @@ class FusedSAGE:
                 KEEP_AGG0 == "on" or free - need_h - other - need0 > margin):
             self.agg0 = torch.empty(L, self.d0, dtype=torch.float32, device=dev)
             other += need0
+        # W > 1: a whole-layer aggregate buffer lets the interior part of the OUTPUT layer's
+        # boundary rows run while its halo rows are in flight (hidden layers use their own
+        # output buffer for that). Planned after the kept aggregates: those save whole
+        # aggregation passes, the store only exposed exchange time
+        self.use_store = self._plan_store()
+        self.agg_full = None
+        need_full = (L - self.Li) * wA * 4
+        if graph.send_map is not None and OVERLAP_FWD and self.Li < L and not self.stream \
+                and self.use_store["out"] and free - need_h - other - need_full > margin:
+            self.agg_full = torch.empty(L - self.Li, wA, dtype=torch.float32, device=dev)
+            other += need_full
         # streamed output layer: its self term h W_self + b for every row, computed during
         # the first column block's transfer (the pipeline fill), when the plan has room
         self.zself = None
@@ -780,10 +782,13 @@ class FusedSAGE:
 
     def _plan_store(self) -> dict:
         """Per forward layer (by output width): pre-aggregate the boundary rows' interior
-        part while the exchange is in flight? Only when the modelled exchange (largest
-        per-peer message / PLAN_LINK_GBPS) outlasts the interior rows' work (their SpMM
-        bytes and GEMM flops at the planning rates) — otherwise the interior rows alone
-        hide it and the boundary rows run in one pass after the wait."""
+        part while the exchange is in flight? Only when the exchange the interior rows
+        leave exposed — the modelled transfer (largest per-peer message / PLAN_LINK_GBPS)
+        minus the interior rows' work (SpMM bytes and GEMM flops at the planning rates) —
+        exceeds twice what the store costs (a read-modify-write of every boundary row's
+        aggregate): at W=2 on the bench graph the store cost more than the ~6 ms it hid
+        and its output-layer buffer displaced the kept input aggregate (a 973 ms rank step
+        without, 1022 ms with, profiles/r05/)."""
         g = self.g
         if BOUNDARY_STORE in ("on", "off") or g.send_map is None or self.Li >= self.L:
             return {k: BOUNDARY_STORE == "on" for k in ("hidden", "out")}
@@ -791,11 +796,12 @@ class FusedSAGE:
         peer_rows = max(max(a2a.send_splits, default=0), max(a2a.recv_splits, default=0))
         t_x = peer_rows * self.hid * 4 / (PLAN_LINK_GBPS * 1e9)
         nnz_a = int(self.adj.rp[self.Li]) if self.Li > 0 else 0
+        t_store = 2.0 * (self.L - self.Li) * self.hid * 4 / (PLAN_HBM_TBPS * 1e12)
         out = {}
         for key, n_out in (("hidden", self.hid), ("out", self.Cp)):
             t_a = nnz_a * self.hid * 4 / (PLAN_SPMM_TBPS * 1e12) + \
                 2.0 * self.Li * 2 * self.hid * n_out / (PLAN_GEMM_TFPS * 1e12)
-            out[key] = t_x > 0.8 * t_a
+            out[key] = t_x - t_a > 2.0 * t_store
         return out
 
     def _layer(self, hin: torch.Tensor, halo, consume, width: int, name: str,
