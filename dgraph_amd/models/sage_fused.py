@@ -1261,9 +1261,16 @@ class FusedSAGE:
                 self._mark("bwd_l0")
             # memory-bound: the column-mapped transposed aggregation of u1 (gated by layer
             # 0's ReLU) and the layer-0 input aggregate (kept from the forward or recomputed)
-            gz = self.bufB[:n, :hid]
             sa = dict(gate=h1[r0:r1], self_add=v, self_map=self.smap if v is not None else None,
                       self_row0=r0)
+            if self.gz_full is not None:
+                # streamed reverse exchange (already gated): the aggregation accumulates
+                # into its rows in place (beta = 1; gate(old + new) = old + gate(new) for
+                # a gated old) instead of an elementwise add pass per chunk
+                gz = self.gz_full[r0:r1]
+                sa["beta"] = 1.0
+            else:
+                gz = self.bufB[:n, :hid]
             if self.TS is not None:
                 self._spmm(self.TS[0][r0:r1 + 1], self.TS[1], u, gz, **sa)
             elif self.itT is not None:
@@ -1273,9 +1280,7 @@ class FusedSAGE:
                 rp, re = self.adj.rows(r0, r1, "int")
                 self._spmm_u(rp, self.adj.col, u, gz, rowend=re, col_map=self.smap, **sa)
             sr = self.ch_send[ci]
-            if self.gz_full is not None:  # streamed reverse exchange: gated, summed
-                gz.add_(self.gz_full[r0:r1])
-            elif sg1 is not None and sr is not None:
+            if self.gz_full is None and sg1 is not None and sr is not None:
                 rp_s, rmap, _ = sr
                 self._spmm(rp_s, self.send_st.col, sg1, gz, beta=1.0, row_map=rmap,
                            gate=h1[r0:r1])
