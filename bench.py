@@ -473,7 +473,9 @@ def link_probe(job: "Job", width: int = 64, iters: int = 5) -> dict:
             send = torch.empty(a2a.total_send, width, device=job.dev)
         if recv is None:
             recv = torch.empty(a2a.total_recv, width, device=job.dev)
-        send.fill_(1.0)
+        gen = torch.Generator(device=job.dev)
+        gen.manual_seed(1234 + job.rank)
+        send.uniform_(generator=gen)  # distinct rows: the executor A/B compares them bitwise
     except torch.OutOfMemoryError:
         ok = 0
     okt = torch.tensor([ok], device=job.dev)
@@ -498,12 +500,55 @@ def link_probe(job: "Job", width: int = 64, iters: int = 5) -> dict:
     vmax, vmin = v.clone(), v.clone()
     dist.all_reduce(vmax, op=dist.ReduceOp.MAX)
     dist.all_reduce(vmin, op=dist.ReduceOp.MIN)
+    impl = os.environ.get("DGRAPH_A2A_IMPL", "torch")
+    nat = native_probe(job, a2a, send, recv, iters) \
+        if impl == "torch" and dist.get_backend(a2a.group) == "nccl" else {}
     del send, recv
     return {"columns": width, "exchange_ms_max": round(float(vmax[0]), 3),
             "largest_peer_message_GBps_min_over_ranks": round(float(vmin[1]), 1),
             "largest_peer_message_GBps_max_over_ranks": round(float(vmax[1]), 1),
             "rank_send_plus_recv_GBps_min_over_ranks": round(float(vmin[2]), 1),
-            "transport": os.environ.get("DGRAPH_A2A_IMPL", "torch")}
+            "transport": impl, **({"native_executor": nat} if nat else {})}
+
+
+def native_probe(job: "Job", a2a, send: torch.Tensor, ref: torch.Tensor, iters: int) -> dict:
+    """The same exchange through the native grouped send/recv executor (comm/rccl_exec.py:
+    its own RCCL communicator, host-cached splits, zero-size peers skipped) right after the
+    torch-PG one: bitwise equality of the received rows with ``ref`` (what the torch path
+    received) on every rank, and its exchange time. The executor's communicator is
+    destroyed afterwards (its buffers do not stay resident for the secondaries)."""
+    from dgraph_amd.comm.rccl_exec import RCCLExecutor
+
+    ok = 1
+    try:
+        out = torch.empty_like(ref)
+    except torch.OutOfMemoryError:
+        ok = 0
+    okt = torch.tensor([ok], device=job.dev)
+    dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+    if int(okt) == 0:
+        return {"skipped": "no device memory for a second receive buffer"}
+    ex = RCCLExecutor.for_group(a2a.group)
+    try:
+        for _ in range(2):
+            ex.alltoallv([send], [out], a2a.send_splits, a2a.recv_splits)
+        torch.cuda.synchronize()
+        eq = torch.tensor([1 if torch.equal(out, ref) else 0], device=job.dev)
+        dist.barrier()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(iters):
+            ex.alltoallv([send], [out], a2a.send_splits, a2a.recv_splits)
+        e.record()
+        torch.cuda.synchronize()
+        ms = torch.tensor([s.elapsed_time(e) / iters], dtype=torch.float64, device=job.dev)
+        dist.all_reduce(eq, op=dist.ReduceOp.MIN)
+        dist.all_reduce(ms, op=dist.ReduceOp.MAX)
+    finally:
+        RCCLExecutor.close_all()
+    del out
+    return {"bitwise_equal_to_torch": bool(int(eq) == 1),
+            "exchange_ms_max": round(float(ms), 3)}
 
 
 def region_breakdown(job: "Job") -> dict:

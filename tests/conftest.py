@@ -36,7 +36,7 @@ def _free_port() -> int:
     return p
 
 
-def _worker(rank, world_size, port, fn, args, q):
+def _worker(rank, world_size, port, fn, args, q, backend="gloo"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world_size), LOCAL_RANK=str(rank))
     try:
@@ -44,7 +44,18 @@ def _worker(rank, world_size, port, fn, args, q):
 
         # W ranks share the container's CPUs: one intra-op pool each, sized to fit
         torch.set_num_threads(max(1, (os.cpu_count() or 8) // max(world_size, 1)))
-        dist.init_process_group("gloo", rank=rank, world_size=world_size)
+        if backend == "rccl-one-gpu":
+            # real RCCL with every rank on GPU 0: RCCL refuses two ranks of one host on one
+            # device ("Duplicate GPU"), so each rank names its own host and the ranks
+            # connect over RCCL's socket transport on loopback (host-staged: a correctness
+            # path for the RCCL code, not a bandwidth one)
+            os.environ.update(NCCL_HOSTID=f"dgraph-test-rank{rank}", NCCL_SOCKET_IFNAME="lo",
+                              LOCAL_RANK="0")
+            torch.cuda.set_device(0)
+            dist.init_process_group("nccl", rank=rank, world_size=world_size,
+                                    device_id=torch.device("cuda", 0))
+        else:
+            dist.init_process_group(backend, rank=rank, world_size=world_size)
         torch.manual_seed(0)
         fn(rank, world_size, *args)
         dist.barrier()
@@ -54,13 +65,14 @@ def _worker(rank, world_size, port, fn, args, q):
         q.put((rank, traceback.format_exc()))
 
 
-def run_ranks(fn, world_size: int, *args, timeout: float = 240.0):
-    """Run ``fn(rank, world_size, *args)`` in ``world_size`` gloo processes; re-raise the
-    first failure with its traceback."""
+def run_ranks(fn, world_size: int, *args, timeout: float = 240.0, backend: str = "gloo"):
+    """Run ``fn(rank, world_size, *args)`` in ``world_size`` processes over a ``backend``
+    process group (``"gloo"``, or ``"rccl-one-gpu"``: RCCL with every rank on GPU 0); re-raise
+    the first failure with its traceback."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world_size, port, fn, args, q))
+    procs = [ctx.Process(target=_worker, args=(r, world_size, port, fn, args, q, backend))
              for r in range(world_size)]
     for p in procs:
         p.start()
