@@ -105,6 +105,10 @@ HALO_STREAM = os.environ.get("DGRAPH_FUSED_HALO_STREAM", "auto")
 # step by 3-5 %; against the column-mapped pass at full width (_spmm_u) it is a tie
 # (W=8 265.6-267.6 vs 267.0 ms, W=2 1062-1068 vs 1065 ms) at a few GB more memory.
 COMPACT_T = os.environ.get("DGRAPH_FUSED_COMPACT_T", "off")
+# W > 1: where the halo pack (the gather of the send rows into the send buffer) runs: on the
+# communication stream next to the exchange ("comm"), or on the compute stream just before
+# the exchange is issued ("compute")
+PACK_STREAM = os.environ.get("DGRAPH_FUSED_PACK_STREAM", "comm")
 # column-mapped gradient SpMMs run full-width passes while the support S is at most this
 # share of the rows (papers100M 0.28 at W=1 and W=8: full width, step 1865 ms / 266 ms;
 # ogbn-products 0.98: 64-column passes, 71.7 vs 76.1 ms at full width)
@@ -772,6 +776,10 @@ class FusedSAGE:
         # send rows) overlaps the next layer's interior work instead of preceding it. It
         # reads h (complete: the stream waits for the compute stream) and writes the send
         # buffer, whose previous exchange the compute stream has already waited for
+        if PACK_STREAM == "compute":
+            K.copy_rows(h, src_idx=g.send_map.idx, out=self.send_buf)
+            return self._on_comm_stream(
+                lambda: g.a2a(self.send_buf, out=self.halo_buf[l], async_op=True))
         from ..comm.alltoallv import _side_stream
 
         side = _side_stream(self.dev)
@@ -904,6 +912,10 @@ class FusedSAGE:
             b = k % nb
             snd = self._ring(self.ring_send, b, c1 - c0)
             rcv = self._ring(self.ring_recv, b, c1 - c0)
+
+            if PACK_STREAM == "compute":
+                K.copy_rows(h[:, c0:c1], src_idx=g.send_map.idx, out=snd)
+                return self._on_comm_stream(lambda: g.a2a(snd, out=rcv, async_op=True))
 
             def go():
                 K.copy_rows(h[:, c0:c1], src_idx=g.send_map.idx, out=snd)
