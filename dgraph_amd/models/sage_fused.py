@@ -106,9 +106,13 @@ HALO_STREAM = os.environ.get("DGRAPH_FUSED_HALO_STREAM", "auto")
 # (W=8 265.6-267.6 vs 267.0 ms, W=2 1062-1068 vs 1065 ms) at a few GB more memory.
 COMPACT_T = os.environ.get("DGRAPH_FUSED_COMPACT_T", "off")
 # W > 1: where the halo pack (the gather of the send rows into the send buffer) runs: on the
-# communication stream next to the exchange ("comm"), or on the compute stream just before
-# the exchange is issued ("compute")
-PACK_STREAM = os.environ.get("DGRAPH_FUSED_PACK_STREAM", "comm")
+# compute stream just before the exchange is issued ("compute"), or on the communication
+# stream next to the exchange ("comm"). A pack co-running with the aggregation saturates
+# HBM with the SpMM's loads behind it (the first column pass after it: 13.2 instead of
+# 1.2 ms) and hides nothing: windowed W=8 rank 256.2 (comm) vs 257.1 ms (compute), W=2
+# 976.5 vs 975.7; structureless W=8 682.8 vs 670.6 ms, exposed exchange 59.6 vs 12.5 ms
+# (the streamed blocks' transfers start a pack earlier; profiles/r05/pack_ab.jsonl)
+PACK_STREAM = os.environ.get("DGRAPH_FUSED_PACK_STREAM", "compute")
 # column-mapped gradient SpMMs run full-width passes while the support S is at most this
 # share of the rows (papers100M 0.28 at W=1 and W=8: full width, step 1865 ms / 266 ms;
 # ogbn-products 0.98: 64-column passes, 71.7 vs 76.1 ms at full width)
