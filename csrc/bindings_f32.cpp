@@ -112,8 +112,8 @@ void spmm_f32_ex_op(const at::Tensor& rowptr, const at::Tensor& col,
                 "x2 must be 16-B aligned, as wide as x, row stride % 4 == 0");
     TORCH_CHECK(nsplit >= 0 && nsplit <= x.size(0) && nsplit < (int64_t(1) << 32),
                 "nsplit must be in [0, rows of x]");
-    TORCH_CHECK(!a.col_map && !a.ew && !a.col_scale,
-                "x2 (two sources) is not combined with col_map / edge weights / col_scale");
+    TORCH_CHECK(!a.ew && !a.col_scale,
+                "x2 (two sources) is not combined with edge weights / col_scale");
     a.x2 = p->data_ptr<float>();
     a.ldx2 = p->stride(0);
     a.nsplit = nsplit;

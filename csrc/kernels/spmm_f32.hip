@@ -24,6 +24,8 @@
 //   * two sources (compile-time TWO): column c < nsplit reads x row c, column c >= nsplit
 //     reads x2 row c - nsplit (the received halo rows) — interior and halo of a row in ONE
 //     pass when the halo is resident, instead of an interior pass plus a beta=1 halo pass.
+//     With a col_map the split applies to the mapped index (a support-row gradient and the
+//     received support rows of the halo, one map over local + halo columns).
 // Accumulation fp32 with packed FMAs in a fixed order per row: bitwise deterministic.
 #include "../common.h"
 #include "kernels.h"
@@ -268,7 +270,7 @@ hipError_t launch_f32_rg(const SpmmF32Args& a, hipStream_t st) {
   const int wmode = (a.ew != nullptr ? 1 : 0) | (a.col_scale != nullptr ? 2 : 0);
   const bool cmap = a.col_map != nullptr;
   const bool two = a.x2 != nullptr;
-  if (two && (cmap || wmode != 0)) return hipErrorInvalidValue;  // not instantiated
+  if (two && wmode != 0) return hipErrorInvalidValue;  // not instantiated
   dim3 grid(static_cast<unsigned>(blocks)), block(256);
 #define DG_F32_K(LPR_, W_, C_, T_)                                                          \
   if (LPR == LPR_ && wmode == W_ && cmap == C_ && two == T_) {                              \
@@ -281,7 +283,7 @@ hipError_t launch_f32_rg(const SpmmF32Args& a, hipStream_t st) {
   DG_F32_K(LPR_, 2, false, false) DG_F32_K(LPR_, 3, false, false)                           \
   DG_F32_K(LPR_, 0, true, false) DG_F32_K(LPR_, 1, true, false)                             \
   DG_F32_K(LPR_, 2, true, false) DG_F32_K(LPR_, 3, true, false)                             \
-  DG_F32_K(LPR_, 0, false, true)
+  DG_F32_K(LPR_, 0, false, true) DG_F32_K(LPR_, 0, true, true)
   DG_F32(8)
   DG_F32(16)
   DG_F32(32)

@@ -57,6 +57,7 @@ from typing import List, Optional, Tuple
 
 import torch
 
+from ..comm.alltoallv import AllToAllV
 from ..ops import f32 as F32
 from ..ops import kernels as K
 from ..parallel.dist_graph import DistGraph
@@ -113,6 +114,13 @@ COMPACT_T = os.environ.get("DGRAPH_FUSED_COMPACT_T", "off")
 # 976.5 vs 975.7; structureless W=8 682.8 vs 670.6 ms, exposed exchange 59.6 vs 12.5 ms
 # (the streamed blocks' transfers start a pack earlier; profiles/r05/pack_ab.jsonl)
 PACK_STREAM = os.environ.get("DGRAPH_FUSED_PACK_STREAM", "compute")
+# W > 1, symmetric graph, 3 layers: the halo part of the input layer's backward aggregation
+# A^T u (u = the layer-1 pre-activation gradient, nonzero on the support rows S only) by
+# "pull" — the owners send their S rows of u that are some rank's halo rows (a forward-style
+# exchange restricted to S), each rank aggregates them with its own rows in one two-source
+# pass — or by "push": every rank aggregates the contributions of its rows to EVERY halo row
+# (a transposed pass over H rows) and sends them back to the owners, who add them
+BWD_HALO = os.environ.get("DGRAPH_FUSED_BWD_HALO", "pull")
 # column-mapped gradient SpMMs run full-width passes while the support S is at most this
 # share of the rows (papers100M 0.28 at W=1 and W=8: full width, step 1865 ms / 266 ms;
 # ogbn-products 0.98: 64-column passes, 71.7 vs 76.1 ms at full width)
@@ -367,6 +375,10 @@ class FusedSAGE:
         self.haloT = graph.halo.transpose() if graph.halo is not None else None
         self.send_st = graph.send_map.transpose_csr().compact_rows() \
             if graph.halo is not None else None
+        # (collective: built by every rank before the memory plan can raise)
+        self.pull = self._pull_plan(graph) \
+            if (BWD_HALO == "pull" and self.nl == 3 and graph.symmetric and
+                graph.send_map is not None) else None
         self.nnz_it, self.nnz_h = self.adj.nnz_int, self.adj.nnz_halo
         # entries of the S-row aggregation (B1a), counted on the host once
         self.nnz_S = int((self.adj.rp[S + 1] - self.adj.rp[S]).sum())
@@ -639,6 +651,36 @@ class FusedSAGE:
         self.record = False
         self._events: list = []
         self._tune_passes()
+
+    def _pull_plan(self, g) -> dict:
+        """The "pull" exchange of the input layer's backward (BWD_HALO): which of my send
+        rows are in my S (their u rows travel) and which of my halo rows are in their
+        owner's S (learned once through the forward plan: one exchange of a flag per send
+        row), the sub-plan of the forward all-to-all-v restricted to those rows, the rows of
+        u to pack, and one column map over local + halo columns: local c -> smap[c], halo
+        L + h -> nS + (h's slot in the received rows), -1 where the source is not in S."""
+        dev, a2a = self.dev, g.a2a
+        W = len(a2a.send_splits)
+        sidx = g.send_map.idx.long()
+        fs = self.smap[sidx] >= 0
+        flag = fs.to(torch.float32).unsqueeze(1).expand(-1, 4).contiguous()  # 16-B rows
+        fh = a2a(flag)[:, 0] > 0.5
+        del flag
+        peers = torch.arange(W, device=dev)
+        ps = torch.repeat_interleave(peers, torch.tensor(a2a.send_splits, device=dev),
+                                     output_size=sidx.numel())
+        pr = torch.repeat_interleave(peers, torch.tensor(a2a.recv_splits, device=dev),
+                                     output_size=fh.numel())
+        cs = [int(v) for v in torch.bincount(ps[fs], minlength=W).tolist()]
+        cr = [int(v) for v in torch.bincount(pr[fh], minlength=W).tolist()]
+        del ps, pr
+        n_recv = sum(cr)
+        hm = torch.full((fh.numel(),), -1, dtype=torch.int32, device=dev)
+        hm[fh] = torch.arange(n_recv, dtype=torch.int32, device=dev) + self.nS
+        return {"a2a": AllToAllV(cs, cr, a2a.group),
+                "send_rows": self.smap[sidx[fs]].long().contiguous(),
+                "cmap": torch.cat([self.smap, hm]).contiguous(), "n_send": sum(cs),
+                "n_recv": n_recv}
 
     # ------------------------------------------------------------------ regions
     def _mark(self, name: str):
@@ -1203,13 +1245,24 @@ class FusedSAGE:
                 self.edges_aggregated += self.nnz_S
 
         pending_s = True
+        uh = None
         if nl == 3:
             # u1 = (dZ1 Wn1^T) / deg_S: its transposed aggregation feeds layer 0; the halo
             # part is computed and sent first so the exchange overlaps the S-row work and
             # the interior rows of layer 0 below
             u = self._gemm(dZ, wn1.detach().t().contiguous(), row_scale=self.invdegS,
                            out=self.u)
-            if self.haloT is not None and self.stream:
+            if self.pull is not None and not self.stream:
+                # pull: my S rows of u that are halo rows elsewhere leave now (packed into
+                # the dead forward send buffer; received into the output layer's dead halo
+                # buffer) and land while the S-row work and layer 0's interior rows run
+                pl = self.pull
+                snd = self.send_buf.view(-1)[:pl["n_send"] * hid].view(pl["n_send"], hid)
+                rcv = self.halo_buf[-1].view(-1)[:pl["n_recv"] * hid].view(pl["n_recv"], hid)
+                K.copy_rows(u, src_idx=pl["send_rows"], out=snd)
+                uh, work = self._on_comm_stream(
+                    lambda: pl["a2a"](snd, out=rcv, async_op=True))
+            elif self.haloT is not None and self.stream:
                 # streamed reverse exchange into the input-layer gradient store; with the
                 # S-row aggregate kept from the forward, the S-row weight gradients need
                 # nothing from it and fill the pipeline's first transfer
@@ -1235,8 +1288,9 @@ class FusedSAGE:
         if lh == 0:
             gw[(0, 0)], gw[(0, 1)] = gw[(0, 0)][:self.d0_in], gw[(0, 1)][:self.d0_in]
         if nl == 3:
-            self._input_layer_backward(P, halos, dZ, u, work, sg1 if work is not None else None,
-                                       gw)
+            self._input_layer_backward(P, halos, dZ, u, work,
+                                       sg1 if (work is not None and uh is None) else None,
+                                       gw, uh)
         self._mark("grads")
         # ---------------- gradients into the parameters
         for l, (ws_, wn_, b_) in enumerate(P):
@@ -1251,10 +1305,11 @@ class FusedSAGE:
         self._mark("end")
         return loss
 
-    def _input_layer_backward(self, P, halos, dZ, u, work, sg1, gw):
+    def _input_layer_backward(self, P, halos, dZ, u, work, sg1, gw, uh=None):
         """B1b: dZ0 by row chunks, consumed at once by the input layer's weight gradients.
         Interior chunks (no row receives from the reverse exchange) run before it is
-        waited for."""
+        waited for. ``uh``: the received S rows of u of the "pull" exchange (the boundary
+        chunks aggregate local and halo entries in one pass)."""
         x, dev, hid = self.x, self.dev, self.hid
         ws1 = P[1][0]
         ws1_t = ws1.detach().t().contiguous()
@@ -1287,7 +1342,11 @@ class FusedSAGE:
                 sa["beta"] = 1.0
             else:
                 gz = self.bufB[:n, :hid]
-            if self.TS is not None:
+            if uh is not None and ci >= self.nA:
+                rp, _ = self.adj.rows(r0, r1, "all")
+                self._spmm_u(rp, self.adj.col, u, gz, col_map=self.pull["cmap"], x2=uh,
+                             nsplit=self.nS, **sa)
+            elif self.TS is not None:
                 self._spmm(self.TS[0][r0:r1 + 1], self.TS[1], u, gz, **sa)
             elif self.itT is not None:
                 self._spmm_u(self.itT.rowptr[r0:r1 + 1], self.itT.col, u, gz,
@@ -1315,7 +1374,8 @@ class FusedSAGE:
             self._mark("bwd_l0")
         db0 = self.acc_in.col_result()
         self.edges_aggregated += self.nnz_it + \
-            (self.send_st.nnz if self.send_st is not None else 0) + \
+            (self.nnz_h if uh is not None else
+             self.send_st.nnz if self.send_st is not None else 0) + \
             (0 if self.agg0 is not None else self.nnz_it + self.nnz_h)
         w0 = self.acc_in.result()
         gw[(0, 0)], gw[(0, 1)], gw[(0, 2)] = (w0[:self.d0_in],

@@ -234,6 +234,50 @@ def test_hub_split_odd_width(F, dtype):
     torch.testing.assert_close(out.double().cpu(), ref, **tol)
 
 
+@pytest.mark.parametrize("F,pc", [(256, 256), (256, 64), (128, 128), (64, 64)])
+def test_spmm_f32_col_map_two_sources(F, pc):
+    """The pulled backward halo (models/sage_fused.py BWD_HALO="pull"): one column map over
+    local + halo columns whose mapped index is split between the support-row operand (< nS)
+    and the received halo support rows (>= nS), with beta, gate and the self term, vs the
+    CPU fp64 reference and against the dense definition; bitwise run to run."""
+    L, H, nS, nH = 900, 700, 260, 230
+    rp, col = _csr(L, L + H, 23, 17)
+    g = torch.Generator().manual_seed(F + pc)
+    sk = torch.randperm(L, generator=g)[:nS].sort().values
+    hk = torch.randperm(H, generator=g)[:nH].sort().values
+    cmap = torch.full((L + H,), -1, dtype=torch.int32)
+    cmap[sk] = torch.arange(nS, dtype=torch.int32)
+    cmap[L + hk] = nS + torch.arange(nH, dtype=torch.int32)
+    u = torch.randn(nS, F, generator=g)
+    uh = torch.randn(nH, F, generator=g)
+    v = torch.randn(nS, F, generator=g)
+    gate = torch.randn(L, F, generator=g)
+    base = torch.randn(L, F, generator=g) * (gate > 0)
+    kw = dict(col_map=cmap, x2=uh, nsplit=nS, gate=gate, self_add=v,
+              self_map=cmap[:L].contiguous(), beta=1.0)
+    ref = base.clone()
+    F32.spmm_f32(rp.cpu(), col.cpu(), u, ref, **kw)
+    dkw = {k: (t.to(DEV) if isinstance(t, torch.Tensor) else t) for k, t in kw.items()}
+    out = base.clone().to(DEV)
+    F32.spmm_f32(rp, col, u.to(DEV), out, pass_cols=pc, **dkw)
+    torch.testing.assert_close(out.cpu(), ref, atol=2e-5, rtol=1e-5)
+    out2 = base.clone().to(DEV)
+    F32.spmm_f32(rp, col, u.to(DEV), out2, pass_cols=pc, **dkw)
+    assert torch.equal(out, out2)
+    # dense definition: sum over mapped entries of [u; uh][cmap[c]], + self, gated, + base
+    A = torch.zeros(L, L + H, dtype=torch.float64)
+    r_ids = torch.repeat_interleave(torch.arange(L), (rp[1:] - rp[:-1]).cpu())
+    A.index_put_((r_ids, col.cpu().long()), torch.ones(r_ids.numel(), dtype=torch.float64),
+                 accumulate=True)
+    xf = torch.zeros(L + H, F, dtype=torch.float64)
+    xf[sk] = u.double()
+    xf[L + hk] = uh.double()
+    sv = torch.zeros(L, F, dtype=torch.float64)
+    sv[sk] = v.double()
+    dense = torch.where(gate > 0, A @ xf + sv + base.double(), torch.zeros(1, dtype=torch.float64))
+    torch.testing.assert_close(out.double().cpu(), dense, atol=1e-4, rtol=1e-5)
+
+
 def test_spmm_f32_self_add_gate():
     rp, col = _csr(300, 300, 7, 11)
     g = torch.Generator().manual_seed(2)

@@ -198,7 +198,7 @@ def test_fused_directed_graph_matches_autograd():
 
 
 def _interior_first_body(rank, world, ref_path, overlap, store="auto", stream="off",
-                         keep_as="auto", hidden=256):
+                         keep_as="auto", hidden=256, bwd_halo="pull"):
     """One rank of a W-way partition renumbered interior-first (parallel/reorder.py), the
     fused executor's interior-then-boundary schedule, all-reduced against W=1."""
     import dgraph_amd.models.sage_fused as sf
@@ -207,6 +207,7 @@ def _interior_first_body(rank, world, ref_path, overlap, store="auto", stream="o
     sf.OVERLAP_FWD = overlap
     sf.BOUNDARY_STORE = store
     sf.KEEP_AS = keep_as
+    sf.BWD_HALO = bwd_halo
     sf.HALO_STREAM = "on" if stream != "off" else "off"
     if stream == "single":  # one ring buffer: exchange and aggregation alternate
         sf.STREAM_SHAPES = ((64, 1),)
@@ -237,6 +238,10 @@ def _interior_first_body(rank, world, ref_path, overlap, store="auto", stream="o
     if store != "auto":
         assert ex.use_store == {"hidden": store == "on", "out": store == "on"}
     assert ex.stream == (stream != "off")
+    # the input layer's backward halo: pulled S rows of u (symmetric graph), else pushed
+    assert (ex.pull is not None) == (bwd_halo == "pull")
+    if ex.pull is not None:
+        assert 0 < ex.pull["n_send"] < ex.n_send and ex.pull["n_recv"] < ex.H
     if stream == "single":
         assert ex.nbuf == 1
     if stream == "ramp":
@@ -267,6 +272,16 @@ def test_fused_interior_first_matches_w1(ranks, world, overlap, store, stream, t
     p = tmp_path / "ref.pt"
     torch.save({"loss": loss, "grads": grads, "corr": corr}, p)
     ranks(_interior_first_body, world, str(p), overlap, store, stream)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_fused_bwd_halo_push_matches_w1(ranks, world, tmp_path):
+    """The input layer's backward halo by "push" (contributions to every halo row sent back
+    to the owners, the non-symmetric graphs' path) instead of the default "pull"."""
+    loss, grads, corr = _fused_grads(0, 1, gf=0.05)
+    p = tmp_path / "ref.pt"
+    torch.save({"loss": loss, "grads": grads, "corr": corr}, p)
+    ranks(_interior_first_body, world, str(p), True, "auto", "off", "auto", 256, "push")
 
 
 @pytest.mark.parametrize("world,store,stream,keep_as", [
