@@ -1026,6 +1026,44 @@ class FusedSAGE:
             if nb == 1 and k + 1 < len(blocks):
                 works[k + 1] = issue(k + 1)
 
+    def _stream_pull(self, u: torch.Tensor, v: Optional[torch.Tensor], gz: torch.Tensor,
+                     gate: torch.Tensor, name: str, fill=None) -> None:
+        """Streamed pull of B1b: for every column block, my S rows of u that are halo rows
+        elsewhere are packed and sent (the pull sub-plan), and once block k has landed
+        ``gz[:, c] = gate(sum over the row's local and halo support neighbours of u[:, c]
+        + v[:, c])`` for every row in one column-mapped two-source pass, block k+1 on the
+        links meanwhile."""
+        pl, nb = self.pull, self.nbuf
+        blocks = self._stream_blocks(u.shape[1])
+
+        def rows(bufs, b, n, w):
+            return bufs[b].view(-1)[:n * w].view(n, w)
+
+        def issue(k):
+            c0, c1 = blocks[k]
+            b = k % nb
+            snd = rows(self.ring_send, b, pl["n_send"], c1 - c0)
+            rcv = rows(self.ring_recv, b, pl["n_recv"], c1 - c0)
+            K.copy_rows(u[:, c0:c1], src_idx=pl["send_rows"], out=snd)
+            return self._on_comm_stream(lambda: pl["a2a"](snd, out=rcv, async_op=True))
+
+        works = {0: issue(0)}
+        for k, (c0, c1) in enumerate(blocks):
+            if nb > 1 and k + 1 < len(blocks):
+                works[k + 1] = issue(k + 1)
+            if k == 0 and fill is not None:
+                fill()
+            uh, work = works.pop(k)
+            self._mark(f"exchange_{name}")
+            work.wait()
+            self._mark(name)
+            sa = {} if v is None else dict(self_add=v[:, c0:c1], self_map=self.smap)
+            self._spmm_u(self.adj.rp, self.adj.col, u[:, c0:c1], gz[:, c0:c1],
+                         col_map=pl["cmap"], x2=uh, nsplit=self.nS, gate=gate[:, c0:c1],
+                         pass_cols=c1 - c0, **sa)
+            if nb == 1 and k + 1 < len(blocks):
+                works[k + 1] = issue(k + 1)
+
     def _params(self):
         out = []
         for l in self.model.layers:
@@ -1245,7 +1283,7 @@ class FusedSAGE:
                 self.edges_aggregated += self.nnz_S
 
         pending_s = True
-        uh = None
+        uh, v_pre, full = None, None, False
         if nl == 3:
             # u1 = (dZ1 Wn1^T) / deg_S: its transposed aggregation feeds layer 0; the halo
             # part is computed and sent first so the exchange overlaps the S-row work and
@@ -1262,6 +1300,19 @@ class FusedSAGE:
                 K.copy_rows(u, src_idx=pl["send_rows"], out=snd)
                 uh, work = self._on_comm_stream(
                     lambda: pl["a2a"](snd, out=rcv, async_op=True))
+            elif self.pull is not None:
+                # streamed pull: u's column blocks (my S rows that are halo rows elsewhere)
+                # through the buffer ring, every row of the input-layer gradient aggregated
+                # block by block into its store — local and received rows in one pass, the
+                # support rows' self term and layer 0's ReLU gate in its epilogue; the S-row
+                # weight gradients (aggregate kept from the forward) fill the first transfer
+                ws1_t = P[1][0].detach().t().contiguous()
+                v_pre = self._gemm(dZ, ws1_t, out=self.v_self) \
+                    if self.v_self is not None else None
+                self._stream_pull(u, v_pre, self.gz_full, self.h[0], f"bwd_l{lh}",
+                                  fill=s_rows if kept else None)
+                pending_s = not kept
+                full = True
             elif self.haloT is not None and self.stream:
                 # streamed reverse exchange into the input-layer gradient store; with the
                 # S-row aggregate kept from the forward, the S-row weight gradients need
@@ -1290,7 +1341,7 @@ class FusedSAGE:
         if nl == 3:
             self._input_layer_backward(P, halos, dZ, u, work,
                                        sg1 if (work is not None and uh is None) else None,
-                                       gw, uh)
+                                       gw, uh, full, v_pre)
         self._mark("grads")
         # ---------------- gradients into the parameters
         for l, (ws_, wn_, b_) in enumerate(P):
@@ -1305,11 +1356,14 @@ class FusedSAGE:
         self._mark("end")
         return loss
 
-    def _input_layer_backward(self, P, halos, dZ, u, work, sg1, gw, uh=None):
+    def _input_layer_backward(self, P, halos, dZ, u, work, sg1, gw, uh=None, full=False,
+                              v=None):
         """B1b: dZ0 by row chunks, consumed at once by the input layer's weight gradients.
         Interior chunks (no row receives from the reverse exchange) run before it is
         waited for. ``uh``: the received S rows of u of the "pull" exchange (the boundary
-        chunks aggregate local and halo entries in one pass)."""
+        chunks aggregate local and halo entries in one pass). ``full``: the streamed pull
+        left every row's finished gradient (self term ``v`` and gate applied) in the
+        store."""
         x, dev, hid = self.x, self.dev, self.hid
         ws1 = P[1][0]
         ws1_t = ws1.detach().t().contiguous()
@@ -1319,7 +1373,8 @@ class FusedSAGE:
         x_halo = halos[0] if self.adj.mid is not None else None
         # the support rows' own term dZ1 Ws1^T, once over S (one full-size GEMM instead
         # of a row-scattered one per chunk); added by the aggregation's epilogue
-        v = self._gemm(dZ, ws1_t, out=self.v_self) if self.v_self is not None else None
+        if not full:
+            v = self._gemm(dZ, ws1_t, out=self.v_self) if self.v_self is not None else None
         items = [ci for ci, (r0, r1) in enumerate(self.chunks) if r1 > r0]
         waited = work is None
         for ci in items:
@@ -1334,7 +1389,9 @@ class FusedSAGE:
             # 0's ReLU) and the layer-0 input aggregate (kept from the forward or recomputed)
             sa = dict(gate=h1[r0:r1], self_add=v, self_map=self.smap if v is not None else None,
                       self_row0=r0)
-            if self.gz_full is not None:
+            if full:
+                gz = self.gz_full[r0:r1]
+            elif self.gz_full is not None:
                 # streamed reverse exchange (already gated): the aggregation accumulates
                 # into its rows in place (beta = 1; gate(old + new) = old + gate(new) for
                 # a gated old) instead of an elementwise add pass per chunk
@@ -1342,7 +1399,9 @@ class FusedSAGE:
                 sa["beta"] = 1.0
             else:
                 gz = self.bufB[:n, :hid]
-            if uh is not None and ci >= self.nA:
+            if full:
+                pass
+            elif uh is not None and ci >= self.nA:
                 rp, _ = self.adj.rows(r0, r1, "all")
                 self._spmm_u(rp, self.adj.col, u, gz, col_map=self.pull["cmap"], x2=uh,
                              nsplit=self.nS, **sa)
@@ -1374,7 +1433,7 @@ class FusedSAGE:
             self._mark("bwd_l0")
         db0 = self.acc_in.col_result()
         self.edges_aggregated += self.nnz_it + \
-            (self.nnz_h if uh is not None else
+            (self.nnz_h if (uh is not None or full) else
              self.send_st.nnz if self.send_st is not None else 0) + \
             (0 if self.agg0 is not None else self.nnz_it + self.nnz_h)
         w0 = self.acc_in.result()

@@ -274,14 +274,15 @@ def test_fused_interior_first_matches_w1(ranks, world, overlap, store, stream, t
     ranks(_interior_first_body, world, str(p), overlap, store, stream)
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_fused_bwd_halo_push_matches_w1(ranks, world, tmp_path):
+@pytest.mark.parametrize("world,stream", [(2, "off"), (4, "off"), (2, "on")])
+def test_fused_bwd_halo_push_matches_w1(ranks, world, stream, tmp_path):
     """The input layer's backward halo by "push" (contributions to every halo row sent back
-    to the owners, the non-symmetric graphs' path) instead of the default "pull"."""
+    to the owners, the non-symmetric graphs' path) instead of the default "pull", resident
+    and streamed."""
     loss, grads, corr = _fused_grads(0, 1, gf=0.05)
     p = tmp_path / "ref.pt"
     torch.save({"loss": loss, "grads": grads, "corr": corr}, p)
-    ranks(_interior_first_body, world, str(p), True, "auto", "off", "auto", 256, "push")
+    ranks(_interior_first_body, world, str(p), True, "auto", stream, "auto", 256, "push")
 
 
 @pytest.mark.parametrize("world,store,stream,keep_as", [
