@@ -372,13 +372,15 @@ class FusedSAGE:
         # B1b's transposed interior aggregation: the interior part of the rows themselves
         # when the interior block is symmetric, else its transpose
         self.itT = None if it.symmetric else it.transpose()
-        self.haloT = graph.halo.transpose() if graph.halo is not None else None
-        self.send_st = graph.send_map.transpose_csr().compact_rows() \
-            if graph.halo is not None else None
         # (collective: built by every rank before the memory plan can raise)
         self.pull = self._pull_plan(graph) \
             if (BWD_HALO == "pull" and self.nl == 3 and graph.symmetric and
                 graph.send_map is not None) else None
+        # the push path's transposed halo block and send-row scatter (not built for the
+        # pull: at W=2 on the structureless graph the transposed halo alone is ~7 GB)
+        push = self.pull is None and graph.halo is not None
+        self.haloT = graph.halo.transpose() if push else None
+        self.send_st = graph.send_map.transpose_csr().compact_rows() if push else None
         self.nnz_it, self.nnz_h = self.adj.nnz_int, self.adj.nnz_halo
         # entries of the S-row aggregation (B1a), counted on the host once
         self.nnz_S = int((self.adj.rp[S + 1] - self.adj.rp[S]).sum())
