@@ -44,6 +44,12 @@ def ensure_process_group(backend: Optional[str] = None, **kwargs) -> bool:
     os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
     kw = dict(backend=backend, timeout=kwargs.pop("timeout", _DEFAULT_TIMEOUT))
     if backend == "nccl":
+        if os.environ.get("DGRAPH_RCCL_SHARED_GPU") == "1":
+            # several ranks on one device (a one-GPU test box): RCCL refuses two ranks of
+            # one host on one device, so each rank names its own host and the ranks connect
+            # over RCCL's socket transport on loopback — the RCCL code paths, host-staged
+            os.environ["NCCL_HOSTID"] = f"dgraph-shared-gpu-rank{os.environ.get('RANK', '0')}"
+            os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
         dev = default_device()
         torch.cuda.set_device(dev)
         kw["device_id"] = dev

@@ -114,3 +114,35 @@ def test_bench_link_probe_native_ab_rccl(monkeypatch):
     executor on the same send rows, bitwise equal to it, timed."""
     monkeypatch.setenv("DGRAPH_A2A_IMPL", "torch")
     run_ranks(_probe_body, 2, timeout=240, backend="rccl-one-gpu")
+
+
+def _bench(args, env_extra, timeout=400):
+    import json
+    import os
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, **env_extra)
+    p = subprocess.run([sys.executable, "-u", os.path.join(repo, "bench.py")] + args,
+                       cwd=repo, env=env, capture_output=True, text=True, timeout=timeout)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith('{"metric"')]
+    assert len(lines) == 1, p.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def test_bench_cli_two_ranks_rccl_shared_gpu():
+    """The driver's multi-GPU path end to end on one GPU: ``bench.py --gpus 2`` launches
+    its ranks with torch.distributed.run, both on GPU 0 over real RCCL
+    (DGRAPH_RCCL_SHARED_GPU=1: per-rank NCCL_HOSTID, socket transport); ONE JSON line, the
+    RCCL world of 2, the link probe with the native-executor A/B bitwise equal, and the
+    same loss as the W=1 run of the same (reduced-scale) graph."""
+    common = ["--scale", "0.02", "--steps", "2", "--warmup", "1", "--no-extra"]
+    w1 = _bench(["--gpus", "1"] + common, {})
+    w2 = _bench(["--gpus", "2"] + common, {"DGRAPH_RCCL_SHARED_GPU": "1"})
+    assert w2["n_gpus"] == 2 and w2["config"]["rccl_world_size"] == 2
+    assert w2["config"]["process_group_backend"] == "nccl"
+    assert w2["xgmi_probe"]["native_executor"]["bitwise_equal_to_torch"] is True
+    assert abs(w2["final_loss"] - w1["final_loss"]) <= 1e-4 * abs(w1["final_loss"])
+    assert w2["val_acc"] == w1["val_acc"] and w2["test_acc"] == w1["test_acc"]
