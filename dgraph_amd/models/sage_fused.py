@@ -130,7 +130,9 @@ U_FULL_FRAC = float(os.environ.get("DGRAPH_FUSED_U_FULL_FRAC", "0.35"))
 # with one buffer every block's transfer is exposed (a W=2 structureless rank: 1.1 s of its
 # 3.1 s step), and 32-column passes aggregate at the 64-column rate per byte
 # (profiles/r05/xcd_ab2.log)
-STREAM_SHAPES = ((64, 2), (32, 2), (64, 1), (32, 1))
+STREAM_SHAPES = tuple(
+    tuple(int(v) for v in t.split("x"))
+    for t in os.environ.get("DGRAPH_FUSED_STREAM_SHAPES", "64x2,32x2,64x1,32x1").split(","))
 # planning rates of the "auto" choice: xGMI per link and direction, fp32 SpMM gather
 # (effective) and fp32 MFMA GEMM rates measured on MI355X (PERFORMANCE.md)
 PLAN_LINK_GBPS = float(os.environ.get("DGRAPH_PLAN_LINK_GBPS", "153"))
