@@ -378,6 +378,10 @@ class FusedSAGE:
         self.pull = self._pull_plan(graph) \
             if (BWD_HALO == "pull" and self.nl == 3 and graph.symmetric and
                 graph.send_map is not None) else None
+        # the per-peer link rate the overlap planner assumes: measured on this job's own
+        # exchange (collective), not the xGMI peak
+        self.link_gbps = self._calibrate_link(graph) if graph.send_map is not None \
+            else PLAN_LINK_GBPS
         # the push path's transposed halo block and send-row scatter (not built for the
         # pull: at W=2 on the structureless graph the transposed halo alone is ~7 GB)
         push = self.pull is None and graph.halo is not None
@@ -656,6 +660,39 @@ class FusedSAGE:
         self._events: list = []
         self._tune_passes()
 
+    def _calibrate_link(self, g) -> float:
+        """Per-peer rate of this job's halo all-to-all-v, measured once at setup (every rank
+        of the plan's group calls it): 16 fp32 columns of every send row, twice, timed with
+        stream events; the largest per-peer message over the slowest rank's time. The
+        boundary-store planner (``_plan_store``) then weighs the exposed exchange against the
+        transport this job actually gets (RCCL over xGMI on the node, the link model in a
+        rehearsal) instead of the links' peak. ``DGRAPH_PLAN_LINK_GBPS`` set: that value."""
+        if "DGRAPH_PLAN_LINK_GBPS" in os.environ or self.dev.type != "cuda":
+            return PLAN_LINK_GBPS
+        import torch.distributed as dist
+
+        a2a, w = g.a2a, 16
+        send = torch.zeros(a2a.total_send, w, dtype=torch.float32, device=self.dev)
+        recv = torch.empty(a2a.total_recv, w, dtype=torch.float32, device=self.dev)
+        a2a(send, out=recv)
+        torch.cuda.synchronize(self.dev)
+        peers = g._peers()
+        if peers:
+            dist.barrier(group=a2a.group)
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(2):
+            a2a(send, out=recv)
+        e.record()
+        torch.cuda.synchronize(self.dev)
+        ms = torch.tensor([s.elapsed_time(e) / 2], dtype=torch.float64, device=self.dev)
+        if peers:
+            dist.all_reduce(ms, op=dist.ReduceOp.MAX, group=a2a.group)
+        del send, recv
+        peer = max(max(a2a.send_splits, default=0), max(a2a.recv_splits, default=0)) * w * 4
+        t = float(ms) / 1e3
+        return peer / t / 1e9 if peer > 0 and t > 0 else PLAN_LINK_GBPS
+
     def _pull_plan(self, g) -> dict:
         """The "pull" exchange of the input layer's backward (BWD_HALO): which of my send
         rows are in my S (their u rows travel) and which of my halo rows are in their
@@ -735,7 +772,10 @@ class FusedSAGE:
                 "keep_agg0": self.agg0 is not None, "keep_aS": self.aS_keep is not None,
                 "output_self_term_fill": self.zself is not None,
                 "compact_T": self.TS is not None,
-                "compact_halo_T": self.HTS is not None, "support_rows": self.nS}
+                "compact_halo_T": self.HTS is not None, "support_rows": self.nS,
+                "bwd_halo": "pull" if self.pull is not None else "push",
+                **({"link_gbps_planned": round(self.link_gbps, 1)}
+                   if self.g.send_map is not None else {})}
 
     # ------------------------------------------------------------------ helpers
     def _gemm(self, A1, B1, A2=None, B2=None, **kw):
@@ -852,7 +892,7 @@ class FusedSAGE:
             return {k: BOUNDARY_STORE == "on" for k in ("hidden", "out")}
         a2a = g.a2a
         peer_rows = max(max(a2a.send_splits, default=0), max(a2a.recv_splits, default=0))
-        t_x = peer_rows * self.hid * 4 / (PLAN_LINK_GBPS * 1e9)
+        t_x = peer_rows * self.hid * 4 / (self.link_gbps * 1e9)
         nnz_a = int(self.adj.rp[self.Li]) if self.Li > 0 else 0
         t_store = 2.0 * (self.L - self.Li) * self.hid * 4 / (PLAN_HBM_TBPS * 1e12)
         out = {}

@@ -3,7 +3,8 @@ kernels at fp32: the asynchronous split halo exchange of the encoder / processor
 blocks (parallel/halo.py AsyncHalo: the exchange issued, the edge GEMM and the local
 projections run, the wait before the halo rows' projection; the reverse exchange issued
 from the halo gradient and waited for at the send rows' gradient) on the one-sided
-symmetric-heap transport (RCCL refuses two ranks per device), plus a link-delayed loopback
+symmetric-heap transport and on real RCCL (ranks sharing GPU 0 over RCCL's socket
+transport), plus a link-delayed loopback
 rehearsal of rank 0 of 2 equal to the instant one. Reference: experiments/GraphCast
 (distributed GraphCast with the halo exchange of DGraph/distributed/haloExchange.py).
 """
@@ -72,12 +73,21 @@ def _run(rank, world, out_dir):
         comm.destroy()
 
 
-def test_graphcast_two_processes_one_gpu(monkeypatch, tmp_path):
-    monkeypatch.setenv("DGRAPH_A2A_IMPL", "shmem")
-    monkeypatch.setenv("DGRAPH_SYMHEAP_BYTES", str(1 << 28))
+@pytest.mark.parametrize("transport", ["shmem", "rccl"])
+def test_graphcast_two_processes_one_gpu(monkeypatch, tmp_path, transport):
+    """shmem: the one-sided symmetric-heap transport over a gloo group; rccl: real RCCL
+    (torch ProcessGroupNCCL all-to-all-v, both ranks on GPU 0 over RCCL's socket transport,
+    conftest.run_ranks(backend="rccl-one-gpu"))."""
+    if transport == "shmem":
+        monkeypatch.setenv("DGRAPH_A2A_IMPL", "shmem")
+        monkeypatch.setenv("DGRAPH_SYMHEAP_BYTES", str(1 << 28))
+        backend = "gloo"
+    else:
+        monkeypatch.setenv("DGRAPH_A2A_IMPL", "torch")
+        backend = "rccl-one-gpu"
     d = str(tmp_path)
     run_ranks(_run, 1, d, timeout=240)
-    run_ranks(_run, 2, d, timeout=240)
+    run_ranks(_run, 2, d, timeout=240, backend=backend)
     r1 = torch.load(f"{d}/gc_w1.pt", weights_only=True)
     r2 = torch.load(f"{d}/gc_w2.pt", weights_only=True)
     torch.testing.assert_close(r2["out"], r1["out"], atol=1e-5, rtol=1e-4)
