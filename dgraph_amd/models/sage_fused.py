@@ -121,6 +121,12 @@ PACK_STREAM = os.environ.get("DGRAPH_FUSED_PACK_STREAM", "compute")
 # pass — or by "push": every rank aggregates the contributions of its rows to EVERY halo row
 # (a transposed pass over H rows) and sends them back to the owners, who add them
 BWD_HALO = os.environ.get("DGRAPH_FUSED_BWD_HALO", "pull")
+# W > 1: the output layer projected BEFORE it is aggregated, when its padded width Cp is
+# narrower than the hidden width (mean_N(h) W_neigh = mean_N(h W_neigh)): the logits'
+# neighbour term aggregates and exchanges Cp columns instead of hid (172 -> 176 vs 256 on
+# papers100M). "auto": when the plan has room for the [L, Cp] projection (the W_neigh
+# weight gradient then needs the loss rows' aggregate of h, pulled separately: small)
+PROJECT_FIRST = os.environ.get("DGRAPH_FUSED_PROJECT_FIRST", "auto")
 # column-mapped gradient SpMMs run full-width passes while the support S is at most this
 # share of the rows (papers100M 0.28 at W=1 and W=8: full width, step 1865 ms / 266 ms;
 # ogbn-products 0.98: 64-column passes, 71.7 vs 76.1 ms at full width)
@@ -364,10 +370,14 @@ class FusedSAGE:
         self.AT_S = it_t.select_rows(S)            # rows S (compact), cols T (compact)
         del it_t
         self.sub = None
+        self._sub_pull = None
         if sub is not None:
             ht_nz, a2a_sub, st = sub[0], sub[1], sub[2]
             stc = st.compact_rows()
             self.sub = (ht_nz, a2a_sub, stc, smap[stc.row_map].long().contiguous())
+            # (my halo rows adjacent to a loss row, the rows of mine the peers' loss rows
+            # neighbour: the project-first output layer pulls h over the reversed sub-plan)
+            self._sub_pull = (sub[3], sub[4], a2a_sub)
         # ---- adjacency: interior + halo entries of a row in one array
         it = graph.interior
         self.adj = _Adj(it, graph.halo, L)
@@ -522,6 +532,15 @@ class FusedSAGE:
                 KEEP_AGG0 == "on" or free - need_h - other - need0 > margin):
             self.agg0 = torch.empty(L, self.d0, dtype=torch.float32, device=dev)
             other += need0
+        # W > 1: the output layer's projection [L, Cp] (PROJECT_FIRST), after the kept
+        # aggregates (those save whole aggregation passes)
+        self.pf = None
+        need_pf = L * self.Cp * 4
+        if graph.send_map is not None and PROJECT_FIRST != "off" and self.Cp < self.hid and (
+                PROJECT_FIRST == "on" or free - need_h - other - need_pf > margin):
+            self.pf = torch.empty(L, self.Cp, dtype=torch.float32, device=dev)
+            other += need_pf
+            self._aggT_setup()
         # W > 1: a whole-layer aggregate buffer lets the interior part of the OUTPUT layer's
         # boundary rows run while its halo rows are in flight (hidden layers use their own
         # output buffer for that). Planned after the kept aggregates: those save whole
@@ -537,7 +556,8 @@ class FusedSAGE:
         # the first column block's transfer (the pipeline fill), when the plan has room
         self.zself = None
         need_z = L * self.Cp * 4
-        if self.stream and STREAM_OUT_FILL and free - need_h - other - need_z > margin:
+        if self.stream and STREAM_OUT_FILL and self.pf is None and \
+                free - need_h - other - need_z > margin:
             self.zself = torch.empty(L, self.Cp, dtype=torch.float32, device=dev)
             other += need_z
         spare = max(free - need_h - other, 1 << 28)
@@ -660,6 +680,70 @@ class FusedSAGE:
         self._events: list = []
         self._tune_passes()
 
+    def _aggT_setup(self) -> None:
+        """Project-first output layer: the loss rows' aggregate of the last hidden layer
+        (the operand of the W_neigh weight gradient) from a small CSR of the loss rows whose
+        halo columns point at the rows pulled over the reversed output-layer sub-plan
+        (the owners send the rows their peers' loss rows neighbour)."""
+        dev, L, T = self.dev, self.L, self.T
+        beg, end = self.adj.rp[T], self.adj.rp[T + 1]
+        deg = end - beg
+        nT = T.numel()
+        rp = torch.zeros(nT + 1, dtype=torch.long, device=dev)
+        torch.cumsum(deg, 0, out=rp[1:])
+        nnz = int(rp[-1])
+        pos = torch.repeat_interleave(beg - rp[:-1], deg, output_size=nnz) + \
+            torch.arange(nnz, device=dev)
+        col = self.adj.col[pos].long()
+        del pos
+        self._aggT_pull = None
+        if self._sub_pull is not None:
+            nz, recv_local, a2a_sub = self._sub_pull
+            hm = torch.full((self.H,), -1, dtype=torch.long, device=dev)
+            hm[nz.long()] = torch.arange(nz.numel(), device=dev)
+            hal = col >= L
+            col[hal] = L + hm[col[hal] - L]
+            self._aggT_pull = (a2a_sub.reversed(), recv_local.long().contiguous(),
+                               torch.empty(recv_local.numel(), self.hid,
+                                           dtype=torch.float32, device=dev),
+                               torch.empty(nz.numel(), self.hid, dtype=torch.float32,
+                                           device=dev))
+        if bool((col < 0).any()):
+            raise RuntimeError("FusedSAGE: a loss row neighbours a halo row outside the "
+                               "output-layer sub-plan")
+        self.aggT_rp, self.aggT_col = rp, col.to(torch.int32).contiguous()
+        self.aggT = torch.empty(nT, self.hid, dtype=torch.float32, device=dev)
+
+    def _aggT_issue(self, hl: torch.Tensor):
+        """Send my rows of ``hl`` that the peers' loss rows neighbour (reversed sub-plan);
+        returns the pending exchange or None."""
+        if self._aggT_pull is None:
+            return None
+        a2a, rows, snd, rcv = self._aggT_pull
+        K.copy_rows(hl, src_idx=rows, out=snd)
+        return self._on_comm_stream(lambda: a2a(snd, out=rcv, async_op=True))
+
+    def _aggT_finish(self, hl: torch.Tensor, pending) -> None:
+        """``aggT = mean over the loss rows' neighbours of hl`` (local and pulled rows)."""
+        kw = dict(row_scale=self.invdegT)
+        if pending is not None:
+            rcv, work = pending
+            work.wait()
+            kw.update(x2=rcv, nsplit=self.L)
+        self._spmm(self.aggT_rp, self.aggT_col, hl, self.aggT, **kw)
+
+    def _exchange_pf(self, Pb: torch.Tensor):
+        """The projection's halo rows: packed into the (dead) send buffer, received into the
+        last hidden layer's halo buffer (its rows are never exchanged in this mode)."""
+        g, Cp = self.g, self.Cp
+        snd = self.send_buf.view(-1)[:self.n_send * Cp].view(self.n_send, Cp)
+        rcv = self.halo_buf[-1].view(-1)[:self.H * Cp].view(self.H, Cp)
+        if self.dev.type != "cuda":
+            K.copy_rows(Pb, src_idx=g.send_map.idx, out=snd)
+            return g.a2a(snd, out=rcv, async_op=True)
+        K.copy_rows(Pb, src_idx=g.send_map.idx, out=snd)
+        return self._on_comm_stream(lambda: g.a2a(snd, out=rcv, async_op=True))
+
     def _calibrate_link(self, g) -> float:
         """Per-peer rate of this job's halo all-to-all-v, measured once at setup (every rank
         of the plan's group calls it): 16 fp32 columns of every send row, twice, timed with
@@ -774,6 +858,7 @@ class FusedSAGE:
                 "compact_T": self.TS is not None,
                 "compact_halo_T": self.HTS is not None, "support_rows": self.nS,
                 "bwd_halo": "pull" if self.pull is not None else "push",
+                "output_project_first": self.pf is not None,
                 **({"link_gbps_planned": round(self.link_gbps, 1)}
                    if self.g.send_map is not None else {})}
 
@@ -1186,7 +1271,8 @@ class FusedSAGE:
             self.edges_aggregated += nnz
             hin = hout
             # this layer's halo rows leave now and land while the next layer works
-            hin_halo = None if self.stream else self._exchange(hout, l)
+            hin_halo = None if (self.stream or (self.pf is not None and l == nl - 2)) \
+                else self._exchange(hout, l)
             self._mark(f"fwd_l{l + 1}" if l + 1 < nl - 1 else "fwd_out")
         # ---------------- forward: output layer (all rows), loss and eval on the fly
         ws, wn, b = P[nl - 1]
@@ -1199,7 +1285,31 @@ class FusedSAGE:
         self.acc_out_s.reset()
         self.acc_out_n.reset()
         hl = hin
-        if self.stream:
+        if self.pf is not None:
+            # project first: Pb = h W_neigh (send rows first, so the exchange leaves while
+            # the interior rows are projected), then the logits of every row chunk
+            # z = h W_self + b + mean_N(Pb); the loss rows' aggregate of h (for the W_neigh
+            # weight gradient) from the pulled rows, at the end
+            Pb, Li = self.pf, self.Li
+            tw = self._aggT_issue(hl)
+            self._gemm(hl[Li:], wnp, out=Pb[Li:])
+            out_pf = lambda ci, a: self._out_chunk(ci, a, hl, wsp, wnp, bp, pf=True)  # noqa
+            if self.stream:
+                self._stream_fwd(Pb, self.agg_full[:, :Cp], "fwd_out",
+                                 fill=(lambda: self._gemm(hl[:Li], wnp, out=Pb[:Li]))
+                                 if Li > 0 else None)
+                for ci, (r0, r1) in enumerate(self.chunks):
+                    if r1 > r0:
+                        out_pf(ci, self.agg_full[r0:r1, :Cp])
+                hl_halo = None
+            else:
+                pend = self._exchange_pf(Pb)
+                if Li > 0:
+                    self._gemm(hl[:Li], wnp, out=Pb[:Li])
+                hl_halo = self._layer(Pb, pend, out_pf, Cp, "fwd_out",
+                                      store=self.agg_full if self.use_store["out"] else None)
+            self._aggT_finish(hl, tw)
+        elif self.stream:
             zs = self.zself
             self._stream_fwd(hl, self.agg_full, "fwd_out",
                              fill=None if zs is None else
@@ -1230,13 +1340,16 @@ class FusedSAGE:
         if s1 > s0:
             K.copy_rows(a, src_idx=self.ch_Sloc[ci], out=keep[s0:s1])
 
-    def _out_chunk(self, ci, a, hl, wsp, wnp, bp):
+    def _out_chunk(self, ci, a, hl, wsp, wnp, bp, pf: bool = False):
         """Output layer of row chunk ci: logits of every row, the loss rows' cross-entropy
-        gradient and output-layer weight gradients, eval hits."""
+        gradient and output-layer weight gradients, eval hits. ``pf``: ``a`` is the chunk's
+        aggregate of the projection h W_neigh (project-first), not of h."""
         C, Cp = self.C, self.Cp
         r0, r1 = self.chunks[ci]
         n = r1 - r0
-        if self.stream and self.zself is not None:  # self term from the pipeline fill
+        if pf:
+            z = self._gemm(hl[r0:r1], wsp, bias=bp, cin=a, beta=1.0, out=self.bufB[:n, :Cp])
+        elif self.stream and self.zself is not None:  # self term from the pipeline fill
             z = self._gemm(a, wnp, cin=self.zself[r0:r1], beta=1.0, out=self.bufB[:n, :Cp])
         else:
             z = self._gemm(hl[r0:r1], wsp, a, wnp, bias=bp, out=self.bufB[:n, :Cp])
@@ -1248,7 +1361,8 @@ class FusedSAGE:
             F32.xent_rows(z, tl, self.yT[t0:t1], self.inv_n, dzt, self.row_loss[t0:t1], C)
             # (the self-term weight gradient h[T]^T dz runs once over all loss rows in the
             # backward; the aggregate rows a[T] exist only per chunk)
-            self.acc_out_n.add(a, dzt, a1_rows=tl)
+            if not pf:
+                self.acc_out_n.add(a, dzt, a1_rows=tl)
         e0, e1 = self.ch_E[ci]
         if e1 > e0:
             F32.argmax_hits(z, self.ch_Eloc[ci], self.yE[e0:e1], self.hit[e0:e1], C)
@@ -1263,6 +1377,8 @@ class FusedSAGE:
         del hl_halo, halos[-1]
         gw = {}
         self.acc_out_s.add(hlast, self.dz, a1_rows=self.T)  # one call over every loss row
+        if self.pf is not None:  # project-first: the loss rows' aggregate of h, pulled
+            self.acc_out_n.add(self.aggT, self.dz)
         dws2 = self.acc_out_s.result()[:, :C]
         dwn2 = self.acc_out_n.result()[:, :C]
         gw[(nl - 1, 0)], gw[(nl - 1, 1)] = dws2, dwn2

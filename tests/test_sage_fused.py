@@ -198,7 +198,7 @@ def test_fused_directed_graph_matches_autograd():
 
 
 def _interior_first_body(rank, world, ref_path, overlap, store="auto", stream="off",
-                         keep_as="auto", hidden=256, bwd_halo="pull"):
+                         keep_as="auto", hidden=256, bwd_halo="pull", pf="auto"):
     """One rank of a W-way partition renumbered interior-first (parallel/reorder.py), the
     fused executor's interior-then-boundary schedule, all-reduced against W=1."""
     import dgraph_amd.models.sage_fused as sf
@@ -208,11 +208,13 @@ def _interior_first_body(rank, world, ref_path, overlap, store="auto", stream="o
     sf.BOUNDARY_STORE = store
     sf.KEEP_AS = keep_as
     sf.BWD_HALO = bwd_halo
+    sf.PROJECT_FIRST = pf
     sf.HALO_STREAM = "on" if stream != "off" else "off"
     if stream == "single":  # one ring buffer: exchange and aggregation alternate
         sf.STREAM_SHAPES = ((64, 1),)
     if stream == "ramp":  # half-width first block, output-layer self term as the fill
         sf.STREAM_RAMP = sf.STREAM_OUT_FILL = True
+        sf.PROJECT_FIRST = "off"  # (the self-term fill is the aggregate-first output layer's)
     if stream != "off":  # the input's static halo exchanged in 16-column blocks too
         DistGraph.STATIC_BLOCK_BYTES = 1024
     shape = SHAPES["ogbn-papers100M"].scaled(SCALE)
@@ -238,6 +240,8 @@ def _interior_first_body(rank, world, ref_path, overlap, store="auto", stream="o
     if store != "auto":
         assert ex.use_store == {"hidden": store == "on", "out": store == "on"}
     assert ex.stream == (stream != "off")
+    # the output layer projected before its aggregation (Cp 176 < hidden): on by plan
+    assert (ex.pf is not None) == (stream != "ramp" and pf != "off")
     # the input layer's backward halo: pulled S rows of u (symmetric graph), else pushed
     assert (ex.pull is not None) == (bwd_halo == "pull")
     if ex.pull is not None:
@@ -283,6 +287,17 @@ def test_fused_bwd_halo_push_matches_w1(ranks, world, stream, tmp_path):
     p = tmp_path / "ref.pt"
     torch.save({"loss": loss, "grads": grads, "corr": corr}, p)
     ranks(_interior_first_body, world, str(p), True, "auto", stream, "auto", 256, "push")
+
+
+@pytest.mark.parametrize("world,stream", [(2, "off"), (4, "on")])
+def test_fused_aggregate_first_output_matches_w1(ranks, world, stream, tmp_path):
+    """The output layer aggregated before its projection at W > 1 (PROJECT_FIRST=off, the
+    W=1 order) instead of projected first."""
+    loss, grads, corr = _fused_grads(0, 1, gf=0.05)
+    p = tmp_path / "ref.pt"
+    torch.save({"loss": loss, "grads": grads, "corr": corr}, p)
+    ranks(_interior_first_body, world, str(p), True, "auto", stream, "auto", 256, "pull",
+          "off")
 
 
 @pytest.mark.parametrize("world,store,stream,keep_as", [
