@@ -110,9 +110,8 @@ void spmm_f32_ex_op(const at::Tensor& rowptr, const at::Tensor& col,
     TORCH_CHECK(p->size(1) == x.size(1) && p->stride(0) % 4 == 0 &&
                     reinterpret_cast<uintptr_t>(p->data_ptr()) % 16 == 0,
                 "x2 must be 16-B aligned, as wide as x, row stride % 4 == 0");
-    // (column ids below nsplit read x, the rest x2: the caller's column ranges keep both in
-    // bounds — a row-block pass walks only columns >= nsplit, so nsplit may exceed x's rows)
-    TORCH_CHECK(nsplit >= 0 && nsplit < (int64_t(1) << 31), "nsplit must be in [0, 2^31)");
+    TORCH_CHECK(nsplit >= 0 && nsplit <= x.size(0) && nsplit < (int64_t(1) << 32),
+                "nsplit must be in [0, rows of x]");
     TORCH_CHECK(!a.ew && !a.col_scale,
                 "x2 (two sources) is not combined with edge weights / col_scale");
     a.x2 = p->data_ptr<float>();

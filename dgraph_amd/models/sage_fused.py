@@ -127,12 +127,6 @@ BWD_HALO = os.environ.get("DGRAPH_FUSED_BWD_HALO", "pull")
 # papers100M). "auto": when the plan has room for the [L, Cp] projection (the W_neigh
 # weight gradient then needs the loss rows' aggregate of h, pulled separately: small)
 PROJECT_FIRST = os.environ.get("DGRAPH_FUSED_PROJECT_FIRST", "auto")
-# streamed forward halos by ROW blocks at full width ("on") instead of column blocks: each
-# block carries a quarter of every peer's halo rows whole, so the aggregation gathers whole
-# neighbour rows (the random-row gather rate of full rows vs 64-column segments) — a local
-# pass over every row's interior entries first (the pipeline fill), then one accumulating
-# pass per block over the row's halo entries of that block
-STREAM_ROWS = os.environ.get("DGRAPH_FUSED_STREAM_ROWS", "off")
 # column-mapped gradient SpMMs run full-width passes while the support S is at most this
 # share of the rows (papers100M 0.28 at W=1 and W=8: full width, step 1865 ms / 266 ms;
 # ogbn-products 0.98: 64-column passes, 71.7 vs 76.1 ms at full width)
@@ -480,16 +474,12 @@ class FusedSAGE:
             for cw, nb in STREAM_SHAPES:
                 if self.hid % cw:
                     continue
-                # (+ one row per peer and block of slack: row blocks split every peer's
-                # rows by floor, so a block can exceed its share by a row per peer)
-                ring = max(nb * (H + n_send) * cw * 4 + 8 * nb * self.hid * (len(
-                    graph.a2a.send_splits) + 1), sub_bytes)
+                ring = max(nb * (H + n_send) * cw * 4, sub_bytes)
                 hb = 4 * H * self.d0 + ring + stores
                 if dev.type != "cuda" or need_h + hb + other + (1 << 28) <= free:
                     self.stream, self.cw, self.nbuf, self.halo_bytes = True, cw, nb, hb
                     break
         need_h += self.halo_bytes
-        self.rb = self._rb_setup(graph) if (self.stream and STREAM_ROWS == "on") else None
         if dev.type == "cuda" and need_h + other + (1 << 28) > free:
             # fail here, before any allocation (and after every collective of the setup), so a
             # caller can skip the configuration on every rank alike instead of dying mid-step
@@ -611,19 +601,15 @@ class FusedSAGE:
         elif self.stream:
             # one arena: the ring's send / receive blocks, and (dead while the ring is idle,
             # in the output-layer backward) the sub-plan exchange's buffers
-            slack = self.hid * (len(graph.a2a.send_splits) + 1)
-            blk_s, blk_r = n_send * self.cw + slack, H * self.cw + slack
+            blk_s, blk_r = n_send * self.cw, H * self.cw
             ring_fl = max(self.nbuf * (blk_s + blk_r), sub_bytes // 4)
             self.ring_arena = torch.empty(ring_fl, **f)
             ra = self.ring_arena
-            self.ring_send = [ra[b * blk_s:b * blk_s + n_send * self.cw].view(n_send, self.cw)
+            self.ring_send = [ra[b * blk_s:(b + 1) * blk_s].view(n_send, self.cw)
                               for b in range(self.nbuf)]
             o = self.nbuf * blk_s
-            self.ring_recv = [ra[o + b * blk_r:o + b * blk_r + H * self.cw].view(H, self.cw)
+            self.ring_recv = [ra[o + b * blk_r:o + (b + 1) * blk_r].view(H, self.cw)
                               for b in range(self.nbuf)]
-            # (whole ring slots, for the row-block stream's [rows, width] views)
-            self.ring_slot_s = [ra[b * blk_s:(b + 1) * blk_s] for b in range(self.nbuf)]
-            self.ring_slot_r = [ra[o + b * blk_r:o + (b + 1) * blk_r] for b in range(self.nbuf)]
             self.agg_full = torch.empty(L, max(self.hid, self.d0), **f)
             self.aS_full = torch.empty(self.nS, self.w_lh, **f)
             # the reverse exchange's store: the output layer's aggregate store (dead after
@@ -694,141 +680,6 @@ class FusedSAGE:
         self._events: list = []
         self._tune_passes()
 
-    _RB_STEP = 1 << 26  # halo entries per pass of the row-block renumbering
-
-    def _rb_setup(self, g) -> dict:
-        """Row-block streaming (STREAM_ROWS): split every peer's halo segment into nbk
-        position ranges (floor of the segment length * k / nbk — the sender computes the same
-        split of its send segment, so no exchange is needed), renumber the halo rows
-        block-major (block, peer, position) so block k lands in one contiguous range
-        [hb[k], hb[k+1]), rewrite the adjacency's halo columns to the new numbers with each
-        row's halo entries grouped by block, and record the per-row block boundaries."""
-        dev, L, H = self.dev, self.L, self.H
-        a2a = g.a2a
-        W = len(a2a.send_splits)
-        nbk = max(1, self.hid // self.cw)
-        ss = torch.tensor(a2a.send_splits, dtype=torch.long)
-        rs = torch.tensor(a2a.recv_splits, dtype=torch.long)
-        ks = torch.arange(nbk + 1, dtype=torch.long).unsqueeze(1)
-        tq, rq = ss.unsqueeze(0) * ks // nbk, rs.unsqueeze(0) * ks // nbk  # [nbk + 1, W]
-        so = [0] + torch.cumsum(ss, 0).tolist()
-        ro = [0] + torch.cumsum(rs, 0).tolist()
-        sidx = g.send_map.idx
-        plans, idx, perm, hb = [], [], [], [0]
-        for k in range(nbk):
-            sk = [int(v) for v in (tq[k + 1] - tq[k]).tolist()]
-            rk = [int(v) for v in (rq[k + 1] - rq[k]).tolist()]
-            plans.append(AllToAllV(sk, rk, a2a.group))
-            idx.append(torch.cat([sidx[so[p] + int(tq[k, p]):so[p] + int(tq[k + 1, p])]
-                                  for p in range(W)]).contiguous())
-            perm.append(torch.cat([torch.arange(ro[p] + int(rq[k, p]),
-                                                ro[p] + int(rq[k + 1, p])) for p in range(W)]))
-            hb.append(hb[-1] + sum(rk))
-        perm = torch.cat(perm).to(dev)                 # new halo row -> old
-        inv = torch.empty_like(perm)
-        inv[perm] = torch.arange(H, device=dev)        # old -> new
-        hbt = torch.tensor(hb, dtype=torch.long, device=dev)
-        adj = self.adj
-        mid, rp = adj.mid, adj.rp
-        bpos = torch.empty(nbk + 1, L, dtype=torch.long, device=dev)
-        bpos[0] = mid
-        # row ranges of at most ~2^26 halo entries: bounded temporaries
-        hdeg = rp[1:] - mid
-        hcum = torch.cumsum(hdeg, 0)
-        step = self._RB_STEP
-        r0 = 0
-        while r0 < L:
-            base = int(hcum[r0 - 1]) if r0 > 0 else 0
-            r1 = int(torch.searchsorted(hcum, torch.tensor(base + step, device=dev),
-                                        right=True))
-            r1 = min(L, max(r1, r0 + 1))
-            d = hdeg[r0:r1]
-            n = int(d.sum())
-            if n:
-                rows = torch.repeat_interleave(torch.arange(r1 - r0, device=dev, dtype=torch.int32),
-                                               d, output_size=n)
-                # entry j of the range sits at mid[r] + (j - its row's first j)
-                pos = torch.repeat_interleave(mid[r0:r1] - (hcum[r0:r1] - d - base), d,
-                                              output_size=n) + torch.arange(n, device=dev)
-                cn = inv[adj.col[pos].long() - L]
-                blk = torch.bucketize(cn, hbt[1:-1], right=True).to(torch.int32)
-                key = rows * nbk + blk
-                order = torch.sort(key, stable=True).indices
-                adj.col[pos] = (cn[order] + L).to(torch.int32)
-                cnt = torch.bincount(key.long(), minlength=(r1 - r0) * nbk).view(r1 - r0, nbk)
-                bpos[1:, r0:r1] = mid[r0:r1].unsqueeze(0) + torch.cumsum(cnt, 1).t()
-                del rows, pos, cn, blk, key, order, cnt
-            else:
-                bpos[1:, r0:r1] = mid[r0:r1].unsqueeze(0)
-            r0 = r1
-        if self.pull is not None:  # the pull map's halo part follows the new numbering
-            cm = self.pull["cmap"]
-            cm[L:] = cm[L:][perm]
-        return {"nbk": nbk, "plans": plans, "idx": idx, "hb": hb, "perm": perm, "inv": inv,
-                "bpos": bpos, "xh": None}
-
-    def _rb_static_halo(self, x: torch.Tensor) -> torch.Tensor:
-        """The input's halo rows in the row-block numbering, exchanged once block by block
-        (in column blocks of the static exchange's width) and kept."""
-        rb = self.rb
-        if rb["xh"] is not None and rb["xv"] == x._version:
-            return rb["xh"]
-        F = x.shape[1]
-        cb = self.g.static_halo_block(F, x.element_size())
-        out = torch.empty(self.H, F, dtype=x.dtype, device=x.device)
-        for k, (plan, idx) in enumerate(zip(rb["plans"], rb["idx"])):
-            h0, h1 = rb["hb"][k], rb["hb"][k + 1]
-            for c0 in range(0, F, cb):
-                c1 = min(F, c0 + cb)
-                recv = plan(K.gather_rows(x[:, c0:c1], idx))
-                out[h0:h1, c0:c1] = recv
-        rb["xh"], rb["xv"] = out, x._version
-        return out
-
-    def _stream_fwd_rb(self, h: torch.Tensor, out: torch.Tensor, name: str,
-                       fill=None) -> None:
-        """Row-block streamed halo (STREAM_ROWS): ``out = mean over in-neighbours of h`` for
-        every row, whole rows of h's halo exchanged block by block through the buffer ring;
-        the interior entries of every row are aggregated (full width) while block 0 is on the
-        links, then each block's halo entries accumulate into ``out`` as it lands."""
-        rb, nb, L = self.rb, self.nbuf, self.L
-        F = h.shape[1]
-
-        def issue(k):
-            b = k % nb
-            plan = rb["plans"][k]
-            snd = self.ring_slot_s[b][:plan.total_send * F].view(plan.total_send, F)
-            rcv = self.ring_slot_r[b][:plan.total_recv * F].view(plan.total_recv, F)
-            if PACK_STREAM == "compute":
-                K.copy_rows(h, src_idx=rb["idx"][k], out=snd)
-                return self._on_comm_stream(lambda: plan(snd, out=rcv, async_op=True))
-
-            def go():
-                K.copy_rows(h, src_idx=rb["idx"][k], out=snd)
-                return plan(snd, out=rcv, async_op=True)
-            return self._on_comm_stream(go)
-
-        nbk = rb["nbk"]
-        works = {0: issue(0)}
-        if nb > 1 and nbk > 1:
-            works[1] = issue(1)
-        if fill is not None:
-            fill()
-        # interior entries of every row (no exchange needed)
-        self._spmm(self.adj.rp, self.adj.col, h, out, rowend=self.adj.mid,
-                   row_scale=self.inv_deg)
-        bpos, hb = rb["bpos"], rb["hb"]
-        for k in range(nbk):
-            recv, work = works.pop(k)
-            self._mark(f"exchange_{name}")
-            work.wait()
-            self._mark(name)
-            # block k's halo entries: columns L + hb[k] .. L + hb[k+1], read from the ring
-            self._spmm(bpos[k], self.adj.col, h, out, rowend=bpos[k + 1], x2=recv,
-                       nsplit=L + hb[k], row_scale=self.inv_deg, beta=1.0)
-            if k + nb < nbk:
-                works[k + nb] = issue(k + nb)
-
     def _aggT_setup(self) -> None:
         """Project-first output layer: the loss rows' aggregate of the last hidden layer
         (the operand of the W_neigh weight gradient) from a small CSR of the loss rows whose
@@ -849,8 +700,7 @@ class FusedSAGE:
         if self._sub_pull is not None:
             nz, recv_local, a2a_sub = self._sub_pull
             hm = torch.full((self.H,), -1, dtype=torch.long, device=dev)
-            nzn = nz.long() if self.rb is None else self.rb["inv"][nz.long()]
-            hm[nzn] = torch.arange(nz.numel(), device=dev)
+            hm[nz.long()] = torch.arange(nz.numel(), device=dev)
             hal = col >= L
             col[hal] = L + hm[col[hal] - L]
             self._aggT_pull = (a2a_sub.reversed(), recv_local.long().contiguous(),
@@ -1229,10 +1079,6 @@ class FusedSAGE:
         links while block k is aggregated (two-source: local and received rows in one
         pass). A block's buffers are reused only after the compute stream consumed them
         (the comm stream waits for it before every pack)."""
-        if self.rb is not None:
-            if rows is not None:
-                raise RuntimeError("row-block streaming re-fetches no S rows (kept aggregate)")
-            return self._stream_fwd_rb(h, out, name, fill)
         g, L, nb = self.g, self.L, self.nbuf
         blocks = self._stream_blocks(h.shape[1])
 
@@ -1372,9 +1218,7 @@ class FusedSAGE:
         self._mark("fwd_l0")
         nnz = self.nnz_it + self.nnz_h
         # ---------------- forward: hidden layers
-        hin, hin_halo = x, (None if g.send_map is None else
-                            self._rb_static_halo(x) if self.rb is not None else
-                            g._static_halo(x))
+        hin, hin_halo = x, (g._static_halo(x) if g.send_map is not None else None)
         halos = []
         for l in range(nl - 1):
             ws, wn, b = P[l]

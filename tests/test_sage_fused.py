@@ -215,9 +215,6 @@ def _interior_first_body(rank, world, ref_path, overlap, store="auto", stream="o
     if stream == "ramp":  # half-width first block, output-layer self term as the fill
         sf.STREAM_RAMP = sf.STREAM_OUT_FILL = True
         sf.PROJECT_FIRST = "off"  # (the self-term fill is the aggregate-first output layer's)
-    if stream == "rows":  # whole-row halo blocks (row-block streaming)
-        sf.STREAM_ROWS = "on"
-        sf.FusedSAGE._RB_STEP = 997  # the renumbering in many row ranges
     if stream != "off":  # the input's static halo exchanged in 16-column blocks too
         DistGraph.STATIC_BLOCK_BYTES = 1024
     shape = SHAPES["ogbn-papers100M"].scaled(SCALE)
@@ -253,7 +250,6 @@ def _interior_first_body(rank, world, ref_path, overlap, store="auto", stream="o
         assert ex.nbuf == 1
     if stream == "ramp":
         assert ex.zself is not None and len(ex._stream_blocks(256)) == 5
-    assert (ex.rb is not None) == (stream == "rows")
     assert g.interior is None  # released: the executor runs on its own adjacency
     loss = ex.step()
     grads = [p.grad.clone() for p in model.parameters()]
@@ -274,7 +270,6 @@ def _interior_first_body(rank, world, ref_path, overlap, store="auto", stream="o
     (4, True, "off", "off"), (2, False, "auto", "off"),
     # streamed halos (column blocks through a buffer ring; the structureless-graph plan)
     (2, True, "auto", "on"), (4, True, "auto", "on"), (8, True, "auto", "on"),
-    (2, True, "auto", "rows"), (4, True, "auto", "rows"), (8, True, "auto", "rows"),
     (2, True, "auto", "single"), (2, True, "auto", "ramp")])
 def test_fused_interior_first_matches_w1(ranks, world, overlap, store, stream, tmp_path):
     loss, grads, corr = _fused_grads(0, 1, gf=0.05)
