@@ -114,10 +114,6 @@ COMPACT_T = os.environ.get("DGRAPH_FUSED_COMPACT_T", "off")
 # 976.5 vs 975.7; structureless W=8 682.8 vs 670.6 ms, exposed exchange 59.6 vs 12.5 ms
 # (the streamed blocks' transfers start a pack earlier; profiles/r05/pack_ab.jsonl)
 PACK_STREAM = os.environ.get("DGRAPH_FUSED_PACK_STREAM", "compute")
-# streamed forward halos: each row's interior entries aggregated once at full width while the
-# first column block is on the links ("1"), the column blocks then adding only the halo
-# entries (beta = 1), instead of every block pass walking all of a row's entries ("0")
-STREAM_LOCAL_FIRST = os.environ.get("DGRAPH_FUSED_STREAM_LOCAL_FIRST", "1") != "0"
 # W > 1, symmetric graph, 3 layers: the halo part of the input layer's backward aggregation
 # A^T u (u = the layer-1 pre-activation gradient, nonzero on the support rows S only) by
 # "pull" — the owners send their S rows of u that are some rank's halo rows (a forward-style
@@ -1085,7 +1081,6 @@ class FusedSAGE:
         (the comm stream waits for it before every pack)."""
         g, L, nb = self.g, self.L, self.nbuf
         blocks = self._stream_blocks(h.shape[1])
-        local_first = STREAM_LOCAL_FIRST and rows is None and self.adj.mid is not None
 
         def issue(k):
             c0, c1 = blocks[k]
@@ -1108,20 +1103,11 @@ class FusedSAGE:
                 works[k + 1] = issue(k + 1)
             if k == 0 and fill is not None:
                 fill()  # independent compute-stream work while block 0 is on the links
-            if k == 0 and local_first:
-                # every row's interior entries at full width while block 0 is on the links;
-                # the blocks then add only their halo entries
-                self._spmm(self.adj.rp, self.adj.col, h, out, rowend=self.adj.mid,
-                           row_scale=self.inv_deg)
             recv, work = works.pop(k)
             self._mark(f"exchange_{name}")
             work.wait()
             self._mark(name)
-            if rows is None and local_first:
-                self._spmm(self.adj.mid, self.adj.col, h[:, c0:c1], out[:, c0:c1],
-                           rowend=self.adj.rp[1:], x2=recv, nsplit=L, row_scale=self.inv_deg,
-                           beta=1.0, pass_cols=c1 - c0)
-            elif rows is None:
+            if rows is None:
                 self._spmm(self.adj.rp, self.adj.col, h[:, c0:c1], out[:, c0:c1], x2=recv,
                            nsplit=L, row_scale=self.inv_deg, pass_cols=c1 - c0)
             else:
