@@ -268,13 +268,24 @@ __device__ __forceinline__ void gemm_f32_body(
         if (i < M) {
           const int64_t orow = o_rows ? o_rows[i] : i;
           const float rsc = row_scale ? row_scale[i] : 1.f;
+          // the row's cin / gate operands loaded together before any store: cin may alias
+          // out (in place), so the compiler cannot move a later load above an earlier store
+          // and each load would wait out its own latency. Safe in place: this thread reads
+          // exactly the elements it writes, and no other thread touches them
+          float cv[TN], gv[TN];
+#pragma unroll
+          for (int b = 0; b < TN; ++b) {
+            const int n = bcol_w + b * 16 + li;
+            if constexpr (HAS_CIN) cv[b] = cin[orow * ldc + n];
+            if constexpr (HAS_GATE) gv[b] = gate[orow * ldg + n];
+          }
 #pragma unroll
           for (int b = 0; b < TN; ++b) {
             const int n = bcol_w + b * 16 + li;
             float v = acc[a][b][r] * rsc;
             if constexpr (HAS_BIAS) v += bias[n];
-            if constexpr (HAS_CIN) v = fmaf(beta, cin[orow * ldc + n], v);
-            if constexpr (HAS_GATE) v = gate[orow * ldg + n] > 0.f ? v : 0.f;
+            if constexpr (HAS_CIN) v = fmaf(beta, cv[b], v);
+            if constexpr (HAS_GATE) v = gv[b] > 0.f ? v : 0.f;
             if constexpr (RELU) v = v > 0.f ? v : 0.f;
             out[orow * ldo + n] = v;
           }
