@@ -3,6 +3,9 @@
 // gradient, and the 1-bit keep masks of selected rows. A TORCH_LIBRARY_FRAGMENT of the
 // dgraph_amd library (csrc/bindings.cpp); every launch goes to the current HIP stream and
 // every shape contract is checked here, before a kernel sees a pointer.
+#include <mutex>
+#include <set>
+#include <tuple>
 #include <ATen/ATen.h>
 #include <c10/core/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
@@ -167,7 +170,10 @@ void gemm_f32_op(const at::Tensor& A1, const at::Tensor& B1, const c10::optional
                  const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& cin,
                  double beta, const c10::optional<at::Tensor>& gate,
                  const c10::optional<at::Tensor>& o_rows, bool relu, const at::Tensor& out,
-                 const c10::optional<at::Tensor>& row_scale) {
+                 const c10::optional<at::Tensor>& row_scale,
+                 const c10::optional<at::Tensor>& send_out,
+                 const c10::optional<at::Tensor>& send_ptr,
+                 const c10::optional<at::Tensor>& send_pos) {
   f32_rows(A1, "A1");
   f32_rows(B1, "B1");
   f32_rows(out, "out");
@@ -231,13 +237,57 @@ void gemm_f32_op(const at::Tensor& A1, const at::Tensor& B1, const c10::optional
                 "row_scale must be contiguous float32 [M]");
     rsp = rs->data_ptr<float>();
   }
+  // fused halo pack: row i of this call also lands at send rows send_pos[send_ptr[i] ..
+  // send_ptr[i + 1]) of send_out (positions checked against send_out's rows on the host)
+  GemmSend sd;
+  if (const at::Tensor* so = opt(send_out)) {
+    const at::Tensor *sp = opt(send_ptr), *sq = opt(send_pos);
+    TORCH_CHECK(sp && sq, "gemm_f32: send_out needs send_ptr and send_pos");
+    TORCH_CHECK(!orp, "gemm_f32: send_out is not combined with o_rows");
+    f32_rows(*so, "send_out");
+    same_dev(*so, A1, "send_out");
+    same_dev(*sp, A1, "send_ptr");
+    same_dev(*sq, A1, "send_pos");
+    TORCH_CHECK(so->size(1) == N, "send_out width != N");
+    TORCH_CHECK(sp->scalar_type() == at::kLong && sp->is_contiguous() && sp->numel() == M + 1,
+                "send_ptr must be contiguous int64 [M + 1]");
+    TORCH_CHECK(sq->scalar_type() == at::kInt && sq->is_contiguous(),
+                "send_pos must be contiguous int32");
+    // bounds of the plan (the kernel writes send_out rows send_pos[q] for q in the
+    // send_ptr ranges): a static plan, so checked the first time each (send_ptr, send_pos,
+    // send_out rows) triple is seen — after that no per-call device reduction, which would
+    // synchronise the host with the stream
+    {
+      static std::mutex mu;
+      static std::set<std::tuple<const void*, int64_t, const void*, int64_t, int64_t>> seen;
+      const auto key = std::make_tuple(sp->data_ptr(), sp->numel(), sq->data_ptr(),
+                                       sq->numel(), so->size(0));
+      std::lock_guard<std::mutex> lk(mu);
+      if (!seen.count(key)) {
+        const int64_t q0 = sp->min().item<int64_t>(), q1 = sp->max().item<int64_t>();
+        TORCH_CHECK(q0 >= 0 && q1 <= sq->numel(), "send_ptr outside send_pos");
+        if (sq->numel() > 0) {
+          const int64_t mn = sq->min().item<int32_t>(), mx = sq->max().item<int32_t>();
+          TORCH_CHECK(mn >= 0 && mx < so->size(0), "send_pos outside send_out's rows");
+        }
+        seen.insert(key);
+      }
+    }
+    sd.out = so->data_ptr<float>();
+    sd.ld = so->stride(0);
+    sd.ptr = sp->data_ptr<int64_t>();
+    sd.pos = sq->data_ptr<int32_t>();
+  }
   c10::DeviceGuard g(A1.device());
-  DG_HIP_CHECK(gemm_f32(A1.data_ptr<float>(), A1.stride(0), K1, B1.data_ptr<float>(),
-                        B1.stride(0), a2 ? a2->data_ptr<float>() : nullptr,
-                        a2 ? a2->stride(0) : 0, K2, b2 ? b2->data_ptr<float>() : nullptr,
-                        b2 ? b2->stride(0) : 0, arp, bp, cp, ldc, static_cast<float>(beta), gp,
-                        ldg, orp, rsp, relu, out.data_ptr<float>(), out.stride(0), M, N,
-                        stream_of(A1)));
+  set_gemm_f32_send(sd);
+  const hipError_t err = gemm_f32(
+      A1.data_ptr<float>(), A1.stride(0), K1, B1.data_ptr<float>(), B1.stride(0),
+      a2 ? a2->data_ptr<float>() : nullptr, a2 ? a2->stride(0) : 0, K2,
+      b2 ? b2->data_ptr<float>() : nullptr, b2 ? b2->stride(0) : 0, arp, bp, cp, ldc,
+      static_cast<float>(beta), gp, ldg, orp, rsp, relu, out.data_ptr<float>(), out.stride(0),
+      M, N, stream_of(A1));
+  set_gemm_f32_send(GemmSend{});
+  DG_HIP_CHECK(err);
 }
 
 void wgrad_f32_op(const at::Tensor& A1, const c10::optional<at::Tensor>& A2,
@@ -397,7 +447,8 @@ TORCH_LIBRARY_FRAGMENT(dgraph_amd, m) {
         "Tensor? x2=None, int nsplit=0, int pass_cols=0) -> ()");
   m.def("gemm_f32(Tensor A1, Tensor B1, Tensor? A2, Tensor? B2, Tensor? a_rows, Tensor? bias, "
         "Tensor? cin, float beta, Tensor? gate, Tensor? o_rows, bool relu, Tensor(a!) out, "
-        "Tensor? row_scale=None) -> ()");
+        "Tensor? row_scale=None, Tensor(b!)? send_out=None, Tensor? send_ptr=None, "
+        "Tensor? send_pos=None) -> ()");
   m.def("wgrad_f32(Tensor A1, Tensor? A2, Tensor? a1_rows, Tensor G, Tensor(a!) partials, "
         "int blocks, int fresh_from, Tensor(b!)? col_partials=None) -> ()");
   m.def("wgrad_f32_reduce(Tensor partials, Tensor(a!) out) -> ()");

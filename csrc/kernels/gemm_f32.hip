@@ -99,7 +99,8 @@ __device__ __forceinline__ void gemm_f32_body(
     const float* __restrict__ bias, const float* cin, int64_t ldc, float beta,
     const float* __restrict__ gate, int64_t ldg, const int64_t* __restrict__ o_rows,
     const float* __restrict__ row_scale, float* out, int64_t ldo, int64_t M,
-    int* __restrict__ tile_ctr) {
+    int* __restrict__ tile_ctr, float* __restrict__ send_out, int64_t lds_send,
+    const int64_t* __restrict__ send_ptr, const int32_t* __restrict__ send_pos) {
   constexpr int kBM = BM;
   using C = GCfg<BM, N>;
   using L = GLds<BM, N>;
@@ -279,6 +280,7 @@ __device__ __forceinline__ void gemm_f32_body(
             if constexpr (HAS_CIN) cv[b] = cin[orow * ldc + n];
             if constexpr (HAS_GATE) gv[b] = gate[orow * ldg + n];
           }
+          float vals[TN];
 #pragma unroll
           for (int b = 0; b < TN; ++b) {
             const int n = bcol_w + b * 16 + li;
@@ -288,6 +290,17 @@ __device__ __forceinline__ void gemm_f32_body(
             if constexpr (HAS_GATE) v = gv[b] > 0.f ? v : 0.f;
             if constexpr (RELU) v = v > 0.f ? v : 0.f;
             out[orow * ldo + n] = v;
+            vals[b] = v;
+          }
+          if (send_out != nullptr) {
+            // the halo pack fused into the producer: the row also goes to each of its
+            // positions in the exchange's send buffer (one per peer that needs it)
+            const int64_t p1 = send_ptr[i + 1];
+            for (int64_t q = send_ptr[i]; q < p1; ++q) {
+              float* so = send_out + static_cast<int64_t>(send_pos[q]) * lds_send;
+#pragma unroll
+              for (int b = 0; b < TN; ++b) so[bcol_w + b * 16 + li] = vals[b];
+            }
           }
         }
 #pragma unroll
@@ -305,16 +318,20 @@ __device__ __forceinline__ void gemm_f32_body(
       const float *__restrict__ B2, int64_t ldb2, const int64_t *__restrict__ a_rows,         \
       const float *__restrict__ bias, const float *cin, int64_t ldc, float beta,              \
       const float *__restrict__ gate, int64_t ldg, const int64_t *__restrict__ o_rows,        \
-      const float *__restrict__ row_scale, float *out, int64_t ldo, int64_t M, int *tile_ctr
+      const float *__restrict__ row_scale, float *out, int64_t ldo, int64_t M, int *tile_ctr, \
+      float *send_out, int64_t lds_send, const int64_t *send_ptr, const int32_t *send_pos
 #define DG_GEMM_F32_PASS                                                                       \
   A1, lda1, K1, B1, ldb1, A2, lda2, K2, B2, ldb2, a_rows, bias, cin, ldc, beta, gate, ldg,     \
-      o_rows, row_scale, out, ldo, M, tile_ctr
+      o_rows, row_scale, out, ldo, M, tile_ctr, send_out, lds_send, send_ptr, send_pos
 
 template <int N, bool HAS_A2, bool RELU, bool HAS_BIAS, bool HAS_CIN, bool HAS_GATE>
 __global__ __launch_bounds__((threads_of<256, N>()), 1) void gemm_f32_kernel(DG_GEMM_F32_ARGS) {
   gemm_f32_body<256, N, HAS_A2, RELU, HAS_BIAS, HAS_CIN, HAS_GATE>(DG_GEMM_F32_PASS);
   work_counter_release(tile_ctr);
 }
+
+// the fused halo pack of the next gemm_f32 call (set_gemm_f32_send; host-side, one call)
+GemmSend g_gemm_send;
 
 template <int N, bool HAS_A2, bool RELU, bool HAS_BIAS, bool HAS_CIN, bool HAS_GATE>
 hipError_t launch_gemm_f32(const float* A1, int64_t lda1, int K1, const float* B1, int64_t ldb1,
@@ -349,9 +366,10 @@ hipError_t launch_gemm_f32(const float* A1, int64_t lda1, int K1, const float* B
     ctr = work_counter(st);
     if (ctr == nullptr) return hipErrorOutOfMemory;
   }
+  const GemmSend& sd = g_gemm_send;
   hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(blocks)), dim3((threads_of<256, N>())), lds, st, A1,
                      lda1, K1, B1, ldb1, A2, lda2, K2, B2, ldb2, a_rows, bias, cin, ldc, beta,
-                     gate, ldg, o_rows, rsc, out, ldo, M, ctr);
+                     gate, ldg, o_rows, rsc, out, ldo, M, ctr, sd.out, sd.ld, sd.ptr, sd.pos);
   return hipGetLastError();
 }
 
@@ -405,6 +423,7 @@ inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) =
 
 bool g_f32_dynamic = true;
 void set_f32_dynamic(bool on) { g_f32_dynamic = on; }
+void set_gemm_f32_send(const GemmSend& s) { g_gemm_send = s; }
 
 namespace {
 constexpr int kCtrStreams = 1024;    // eager slots: one per stream

@@ -262,6 +262,16 @@ hipError_t work_counters_init();
 // the fp32 GEMM and weight-gradient kernels launched from now on
 extern bool g_f32_dynamic;
 void set_f32_dynamic(bool on);
+// gemm_f32's fused halo pack: output row i is also stored to send rows
+// send_pos[send_ptr[i] .. send_ptr[i + 1]) of ``out`` (row stride ``ld``) — applies to the
+// next gemm_f32 call only (the binding sets and clears it around that call)
+struct GemmSend {
+  float* out = nullptr;
+  int64_t ld = 0;
+  const int64_t* ptr = nullptr;
+  const int32_t* pos = nullptr;
+};
+void set_gemm_f32_send(const GemmSend& s);
 bool gemm_f32_supported(int64_t N, int64_t K1, int64_t K2);
 hipError_t gemm_f32(const float* A1, int64_t lda1, int64_t K1, const float* B1, int64_t ldb1,
                     const float* A2, int64_t lda2, int64_t K2, const float* B2, int64_t ldb2,

@@ -114,6 +114,9 @@ COMPACT_T = os.environ.get("DGRAPH_FUSED_COMPACT_T", "off")
 # 976.5 vs 975.7; structureless W=8 682.8 vs 670.6 ms, exposed exchange 59.6 vs 12.5 ms
 # (the streamed blocks' transfers start a pack earlier; profiles/r05/pack_ab.jsonl)
 PACK_STREAM = os.environ.get("DGRAPH_FUSED_PACK_STREAM", "compute")
+# W > 1, resident halos: the pack fused into the GEMM that produces the sent rows (its
+# epilogue also stores each row at its send-buffer positions) instead of a gather pass
+FUSED_PACK = os.environ.get("DGRAPH_FUSED_PACK_FUSED", "1") != "0"
 # W > 1, symmetric graph, 3 layers: the halo part of the input layer's backward aggregation
 # A^T u (u = the layer-1 pre-activation gradient, nonzero on the support rows S only) by
 # "pull" — the owners send their S rows of u that are some rank's halo rows (a forward-style
@@ -626,6 +629,8 @@ class FusedSAGE:
             elif nh <= H and nr <= n_send:
                 self.sub_hg = self.halo_buf[-1][:nh]
                 self.sub_sg = self.send_buf[:nr]
+        self.send_plan = self._send_plan(graph) \
+            if (FUSED_PACK and graph.send_map is not None and not self.stream) else None
         if self.keep_as:
             self.aS_keep = self.aS_full if self.aS_full is not None else \
                 torch.empty(self.nS, self.w_lh, **f)
@@ -738,6 +743,8 @@ class FusedSAGE:
         g, Cp = self.g, self.Cp
         snd = self.send_buf.view(-1)[:self.n_send * Cp].view(self.n_send, Cp)
         rcv = self.halo_buf[-1].view(-1)[:self.H * Cp].view(self.H, Cp)
+        if self.send_plan is not None:  # packed by the projection GEMM
+            return self._on_comm_stream(lambda: g.a2a(snd, out=rcv, async_op=True))
         if self.dev.type != "cuda":
             K.copy_rows(Pb, src_idx=g.send_map.idx, out=snd)
             return g.a2a(snd, out=rcv, async_op=True)
@@ -937,13 +944,36 @@ class FusedSAGE:
             return None
         return (csr.rowptr[k0:k1 + 1], (rm[k0:k1] - r0).contiguous(), k1 - k0)
 
+    def _send_plan(self, g):
+        """The fused pack's plan: local row r's positions in the forward send buffer are
+        ``pos[ptr[r]:ptr[r + 1]]`` (a row sent to several peers has several)."""
+        sidx = g.send_map.idx.long()
+        order = torch.argsort(sidx, stable=True)
+        ptr = torch.zeros(self.L + 1, dtype=torch.long, device=self.dev)
+        torch.cumsum(torch.bincount(sidx, minlength=self.L), 0, out=ptr[1:])
+        if int(ptr[-1]) != self.n_send:
+            raise RuntimeError("FusedSAGE: send rows outside the local rows")
+        return ptr, order.to(torch.int32).contiguous()
+
+    def _send_arg(self, r0: int, r1: int, width: int):
+        """``send=`` of the GEMM producing rows [r0, r1) of an exchanged activation (None
+        when no fused pack or no sent row in the range)."""
+        if self.send_plan is None or r1 <= self.Li:
+            return None
+        ptr, pos = self.send_plan
+        snd = self.send_buf.view(-1)[:self.n_send * width].view(self.n_send, width)
+        return snd, ptr[r0:r1 + 1], pos
+
     def _exchange(self, h: torch.Tensor, l: int):
         """Start the halo rows of hidden layer ``l``'s output ``h`` on their way from their
         owners (forward all-to-all-v, asynchronous, resident buffers): ``(recv, work)``, or
-        None at W=1."""
+        None at W=1. With the fused pack the send buffer was filled by h's GEMMs."""
         g = self.g
         if g.send_map is None:
             return None
+        if self.send_plan is not None:
+            return self._on_comm_stream(
+                lambda: g.a2a(self.send_buf, out=self.halo_buf[l], async_op=True))
         if self.dev.type != "cuda":
             K.copy_rows(h, src_idx=g.send_map.idx, out=self.send_buf)
             return g.a2a(self.send_buf, out=self.halo_buf[l], async_op=True)
@@ -1231,11 +1261,17 @@ class FusedSAGE:
 
             keep_s = self.aS_keep if l == nl - 2 else None
 
-            def consume(ci, a, hin=hin, hout=hout, ws=ws, wn=wn, bias=bias, keep_s=keep_s):
+            # (this layer's output is exchanged next unless the projected output layer
+            # exchanges its projection instead)
+            sends = not self.stream and not (self.pf is not None and l == nl - 2)
+
+            def consume(ci, a, hin=hin, hout=hout, ws=ws, wn=wn, bias=bias, keep_s=keep_s,
+                        sends=sends):
                 r0, r1 = self.chunks[ci]
                 if keep_s is not None:
                     self._keep_s_rows(ci, a, keep_s)
-                self._gemm(hin[r0:r1], ws, a, wn, bias=bias, relu=True, out=hout[r0:r1])
+                self._gemm(hin[r0:r1], ws, a, wn, bias=bias, relu=True, out=hout[r0:r1],
+                           send=self._send_arg(r0, r1, hout.shape[1]) if sends else None)
 
             if self.stream and l > 0 and not STREAM_FILL:
                 self._stream_fwd(hin, hout, f"fwd_l{l}")
@@ -1292,7 +1328,8 @@ class FusedSAGE:
             # weight gradient) from the pulled rows, at the end
             Pb, Li = self.pf, self.Li
             tw = self._aggT_issue(hl)
-            self._gemm(hl[Li:], wnp, out=Pb[Li:])
+            self._gemm(hl[Li:], wnp, out=Pb[Li:],
+                       send=None if self.stream else self._send_arg(Li, self.L, Cp))
             out_pf = lambda ci, a: self._out_chunk(ci, a, hl, wsp, wnp, bp, pf=True)  # noqa
             if self.stream:
                 self._stream_fwd(Pb, self.agg_full[:, :Cp], "fwd_out",

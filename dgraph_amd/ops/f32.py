@@ -109,12 +109,17 @@ def gemm_f32_ok(N: int, K1: int, K2: int = 0) -> bool:
 
 def gemm_f32(A1: torch.Tensor, B1: torch.Tensor, A2=None, B2=None, *, a_rows=None, bias=None,
              cin=None, beta: float = 1.0, gate=None, o_rows=None, relu: bool = False,
-             out: Optional[torch.Tensor] = None, row_scale=None) -> torch.Tensor:
+             out: Optional[torch.Tensor] = None, row_scale=None, send=None) -> torch.Tensor:
     """``out[o(i)] = relu?(gate?(rs[i] (A1[a(i)] @ B1 (+ A2[i] @ B2)) + bias +
     beta*cin[o(i)]))`` (csrc/kernels/gemm_f32.hip; B row-major [K, N]); ``gate``: keep
-    where gate > 0; ``row_scale`` (nullable [M]): per input row."""
+    where gate > 0; ``row_scale`` (nullable [M]): per input row. ``send`` = (send_out
+    [rows, N], send_ptr int64 [M + 1], send_pos int32): the halo pack fused into the
+    producer — row i is also stored to send_out rows send_pos[send_ptr[i]:send_ptr[i + 1]]
+    (not with o_rows)."""
     M = a_rows.numel() if a_rows is not None else A1.shape[0]
     N = B1.shape[1]
+    if send is not None and o_rows is not None:
+        raise ValueError("gemm_f32: send is not combined with o_rows")
     if out is None:
         if o_rows is not None:
             raise ValueError("gemm_f32: o_rows needs an explicit out")
@@ -136,6 +141,7 @@ def gemm_f32(A1: torch.Tensor, B1: torch.Tensor, A2=None, B2=None, *, a_rows=Non
                 A1 = A1.clone()
             if A2 is not None and _overlaps(A2, out):
                 A2 = A2.clone()
+        so, sp, sq = send if send is not None else (None, None, None)
         for n0, n1 in blocks:
             full = (n0, n1) == (0, N)
             ops.gemm_f32(A1, B1 if full else B1[:, n0:n1], A2,
@@ -143,7 +149,8 @@ def gemm_f32(A1: torch.Tensor, B1: torch.Tensor, A2=None, B2=None, *, a_rows=Non
                          None if bias is None else bias[n0:n1], None if cin is None else
                          (cin if full else cin[:, n0:n1]), float(beta),
                          None if gate is None else (gate if full else gate[:, n0:n1]), o_rows,
-                         bool(relu), out if full else out[:, n0:n1], rs)
+                         bool(relu), out if full else out[:, n0:n1], rs,
+                         None if so is None else (so if full else so[:, n0:n1]), sp, sq)
         return out
     a = A1.double()[a_rows.long()] if a_rows is not None else A1[:M].double()
     v = a @ B1.double()
@@ -161,6 +168,12 @@ def gemm_f32(A1: torch.Tensor, B1: torch.Tensor, A2=None, B2=None, *, a_rows=Non
     if relu:
         v = v.clamp_min(0)
     out[o] = v.to(out.dtype)
+    if send is not None:
+        so, sp, sq = send
+        sp = sp.long()
+        rows = torch.repeat_interleave(torch.arange(M, device=sp.device), sp[1:] - sp[:-1])
+        q = torch.arange(int(sp[0]), int(sp[-1]), device=sp.device)
+        so[sq.long()[q]] = v[rows].to(so.dtype)
     return out
 
 

@@ -627,3 +627,35 @@ def test_spmm_f32_under_contention_bitwise(cus):
                 assert torch.equal(refs[pc], out), (grid, pc)
     finally:
         _native.ops().set_f32_sched(0, -1)
+
+
+@pytest.mark.parametrize("N", [176, 256, 512])
+def test_gemm_f32_fused_send_rows(N):
+    """The halo pack fused into the producing GEMM (models/sage_fused.py FUSED_PACK): every
+    output row is also stored at its send-buffer positions (0 to 3 per row, rows of a
+    sub-range as the boundary chunks pass them); the send rows equal the output rows
+    bitwise and nothing else of the send buffer is written. N = 512 runs as column blocks."""
+    g = torch.Generator().manual_seed(N)
+    L, M0, M1, K = 1500, 300, 1300, 256
+    x = torch.randn(L, K, generator=g)
+    W = torch.randn(K, N, generator=g) / 16
+    bias = torch.randn(N, generator=g)
+    cnt = torch.randint(0, 4, (L,), generator=g)
+    cnt[:M0] = 0  # (interior rows: sent to nobody)
+    ptr = torch.zeros(L + 1, dtype=torch.long)
+    ptr[1:] = torch.cumsum(cnt, 0)
+    n_send = int(ptr[-1])
+    pos = torch.randperm(n_send, generator=g).to(torch.int32)
+    send = torch.full((n_send + 7, N), -7.0).to(DEV)
+    out = torch.zeros(L, N).to(DEV)
+    F32.gemm_f32(x[M0:M1].to(DEV), W.to(DEV), bias=bias.to(DEV), relu=True,
+                 out=out[M0:M1], send=(send, ptr[M0:M1 + 1].to(DEV), pos.to(DEV)))
+    ref = (x[M0:M1].double() @ W.double() + bias.double()).clamp_min(0)
+    torch.testing.assert_close(out[M0:M1].double().cpu(), ref, atol=1e-4, rtol=1e-5)
+    so, oc = send.cpu(), out.cpu()
+    written = torch.zeros(n_send + 7, dtype=torch.bool)
+    for r in range(M0, M1):
+        for q in range(int(ptr[r]), int(ptr[r + 1])):
+            assert torch.equal(so[int(pos[q])], oc[r]), (r, q)
+            written[int(pos[q])] = True
+    assert bool((so[~written] == -7.0).all())
