@@ -790,7 +790,12 @@ class FusedSAGE:
         owner's S (learned once through the forward plan: one exchange of a flag per send
         row), the sub-plan of the forward all-to-all-v restricted to those rows, the rows of
         u to pack, and one column map over local + halo columns: local c -> smap[c], halo
-        L + h -> nS + (h's slot in the received rows), -1 where the source is not in S."""
+        L + h -> nS + (h's slot in the received rows), -1 where the source is not in S.
+        The reference's halo backward is the push form: the received rows' gradient goes
+        back through the reversed exchange and is scatter-added by the owners
+        (DGraph/distributed/haloExchange.py:67-88); on a symmetric graph pulling the
+        owners' nonzero gradient rows moves ~3.5x fewer bytes and needs no transposed pass
+        over the halo."""
         dev, a2a = self.dev, g.a2a
         W = len(a2a.send_splits)
         sidx = g.send_map.idx.long()
@@ -946,7 +951,9 @@ class FusedSAGE:
 
     def _send_plan(self, g):
         """The fused pack's plan: local row r's positions in the forward send buffer are
-        ``pos[ptr[r]:ptr[r + 1]]`` (a row sent to several peers has several)."""
+        ``pos[ptr[r]:ptr[r + 1]]`` (a row sent to several peers has several). Replaces the
+        gather of the send rows before each all-to-all-v (the reference packs per exchange,
+        DGraph/distributed/haloExchange.py:47-62)."""
         sidx = g.send_map.idx.long()
         order = torch.argsort(sidx, stable=True)
         ptr = torch.zeros(self.L + 1, dtype=torch.long, device=self.dev)
