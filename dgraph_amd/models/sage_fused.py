@@ -631,6 +631,14 @@ class FusedSAGE:
                 self.sub_sg = self.send_buf[:nr]
         self.send_plan = self._send_plan(graph) \
             if (FUSED_PACK and graph.send_map is not None and not self.stream) else None
+        # the same for the pulled backward halo's rows of u (S-compacted rows)
+        self._pull_send = None
+        if self.send_plan is not None and self.pull is not None:
+            rows = self.pull["send_rows"]
+            ptr = torch.zeros(self.nS + 1, dtype=torch.long, device=dev)
+            torch.cumsum(torch.bincount(rows, minlength=self.nS), 0, out=ptr[1:])
+            self._pull_send = (ptr, torch.argsort(rows, stable=True).to(torch.int32)
+                               .contiguous())
         if self.keep_as:
             self.aS_keep = self.aS_full if self.aS_full is not None else \
                 torch.empty(self.nS, self.w_lh, **f)
@@ -1492,16 +1500,22 @@ class FusedSAGE:
             # u1 = (dZ1 Wn1^T) / deg_S: its transposed aggregation feeds layer 0; the halo
             # part is computed and sent first so the exchange overlaps the S-row work and
             # the interior rows of layer 0 below
-            u = self._gemm(dZ, wn1.detach().t().contiguous(), row_scale=self.invdegS,
-                           out=self.u)
-            if self.pull is not None and not self.stream:
-                # pull: my S rows of u that are halo rows elsewhere leave now (packed into
-                # the dead forward send buffer; received into the output layer's dead halo
-                # buffer) and land while the S-row work and layer 0's interior rows run
+            pull_res = self.pull is not None and not self.stream
+            if pull_res:
                 pl = self.pull
                 snd = self.send_buf.view(-1)[:pl["n_send"] * hid].view(pl["n_send"], hid)
                 rcv = self.halo_buf[-1].view(-1)[:pl["n_recv"] * hid].view(pl["n_recv"], hid)
-                K.copy_rows(u, src_idx=pl["send_rows"], out=snd)
+            # (pulled, resident: the pack of u's sent rows fused into u's GEMM)
+            u = self._gemm(dZ, wn1.detach().t().contiguous(), row_scale=self.invdegS,
+                           out=self.u,
+                           send=(snd, *self._pull_send) if (pull_res and self._pull_send)
+                           else None)
+            if pull_res:
+                # pull: my S rows of u that are halo rows elsewhere leave now (packed into
+                # the dead forward send buffer; received into the output layer's dead halo
+                # buffer) and land while the S-row work and layer 0's interior rows run
+                if not self._pull_send:
+                    K.copy_rows(u, src_idx=pl["send_rows"], out=snd)
                 uh, work = self._on_comm_stream(
                     lambda: pl["a2a"](snd, out=rcv, async_op=True))
             elif self.pull is not None:
