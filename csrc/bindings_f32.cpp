@@ -56,7 +56,8 @@ void spmm_f32_ex_op(const at::Tensor& rowptr, const at::Tensor& col,
                     const c10::optional<at::Tensor>& self_add,
                     const c10::optional<at::Tensor>& self_map, int64_t self_row0,
                     const c10::optional<at::Tensor>& rowend,
-                    const c10::optional<at::Tensor>& x2, int64_t nsplit, int64_t pass_cols) {
+                    const c10::optional<at::Tensor>& x2, int64_t nsplit, int64_t pass_cols,
+                    const c10::optional<at::Tensor>& keep_bits) {
   same_dev(rowptr, x, "rowptr");
   same_dev(col, x, "col");
   same_dev(out, x, "out");
@@ -161,6 +162,16 @@ void spmm_f32_ex_op(const at::Tensor& rowptr, const at::Tensor& col,
   a.beta = static_cast<float>(beta);
   a.cap = cap;
   a.pass_cols = static_cast<int>(pass_cols);
+  if (const at::Tensor* kb = opt(keep_bits)) {
+    same_dev(*kb, x, "keep_bits");
+    TORCH_CHECK(kb->scalar_type() == at::kInt && kb->dim() == 2 && kb->stride(1) == 1,
+                "keep_bits must be int32 [rows, words] with unit column stride");
+    TORCH_CHECK(kb->size(1) * 32 >= x.size(1), "keep_bits narrower than the columns");
+    TORCH_CHECK(kb->size(0) >= (rmap ? out.size(0) : nrows),
+                "keep_bits has fewer rows than the output rows");
+    a.keep_bits = reinterpret_cast<const uint32_t*>(kb->data_ptr<int32_t>());
+    a.ld_bits = kb->stride(0);
+  }
   c10::DeviceGuard g(x.device());
   DG_HIP_CHECK(spmm_f32_run(a, stream_of(x)));
 }
@@ -444,7 +455,7 @@ TORCH_LIBRARY_FRAGMENT(dgraph_amd, m) {
         "Tensor? row_scale, Tensor? col_map, Tensor? row_ids, Tensor x, Tensor(a!) out, "
         "float beta=0., int cap=0, Tensor? row_map=None, Tensor? gate=None, "
         "Tensor? self_add=None, Tensor? self_map=None, int self_row0=0, Tensor? rowend=None, "
-        "Tensor? x2=None, int nsplit=0, int pass_cols=0) -> ()");
+        "Tensor? x2=None, int nsplit=0, int pass_cols=0, Tensor? keep_bits=None) -> ()");
   m.def("gemm_f32(Tensor A1, Tensor B1, Tensor? A2, Tensor? B2, Tensor? a_rows, Tensor? bias, "
         "Tensor? cin, float beta, Tensor? gate, Tensor? o_rows, bool relu, Tensor(a!) out, "
         "Tensor? row_scale=None, Tensor(b!)? send_out=None, Tensor? send_ptr=None, "

@@ -87,6 +87,11 @@ struct SpmmF32Args {
   int64_t self_row0 = 0;
   int pass_cols = 0;
   int xcd_remap = 0;  // set by the launcher (set_spmm_f32_xcd)
+  // 1-bit ReLU keep mask of the output rows (bit c of row o: keep column c), applied last;
+  // [out rows, ld_bits] int32 words; bits_col0 = the column of this pass (launcher)
+  const uint32_t* keep_bits = nullptr;
+  int64_t ld_bits = 0;
+  int bits_col0 = 0;
 };
 hipError_t spmm_f32_run(const SpmmF32Args& a, hipStream_t st);
 void set_spmm_f32_pass_cols(int cols);

@@ -242,6 +242,14 @@ __global__ __launch_bounds__(256) void spmm_f32_rowgroup_kernel(SpmmF32Args a) {
         res.z = gv.z > 0.f ? res.z : 0.f;
         res.w = gv.w > 0.f ? res.w : 0.f;
       }
+      if (a.keep_bits) {  // the same from a 1-bit mask (4 columns never straddle a word)
+        const int c = a.bits_col0 + f;
+        const uint32_t w = a.keep_bits[orow * a.ld_bits + (c >> 5)] >> (c & 31);
+        res.x = (w & 1u) ? res.x : 0.f;
+        res.y = (w & 2u) ? res.y : 0.f;
+        res.z = (w & 4u) ? res.z : 0.f;
+        res.w = (w & 8u) ? res.w : 0.f;
+      }
       *reinterpret_cast<float4*>(o) = res;
     }
   }
@@ -334,6 +342,7 @@ hipError_t spmm_f32_run(const SpmmF32Args& args, hipStream_t st) {
     p.out = args.out + c0;
     p.gate = args.gate ? args.gate + c0 : nullptr;
     p.self_add = args.self_add ? args.self_add + c0 : nullptr;
+    p.bits_col0 = args.bits_col0 + c0;
     const hipError_t err = args.it == IType::I32 ? launch_f32_rg<int32_t>(p, st)
                                                  : launch_f32_rg<int64_t>(p, st);
     if (err != hipSuccess) return err;

@@ -1447,16 +1447,22 @@ class FusedSAGE:
             hg = self._spmm(ht_nz.rowptr, ht_nz.col, u2, self.sub_hg)
             sg, work = a2a_sub(hg, out=self.sub_sg, async_op=True)
             self.edges_aggregated += ht_nz.nnz
-        self._spmm(self.AT_S.rowptr, self.AT_S.col, u2, dZ)
+        # the last hidden layer's ReLU derivative applied by each writer of dZ (a 0/1 mask
+        # distributes over the sum): the aggregations in their epilogue from the keep bits,
+        # the loss rows' self term afterwards on those rows only — instead of a pass that
+        # re-reads and re-writes all of dZ
+        self._spmm(self.AT_S.rowptr, self.AT_S.col, u2, dZ, keep_bits=self.bits)
         self.edges_aggregated += self.AT_S.nnz
         if work is not None:
             self._mark("exchange_bwd_out")
             work.wait()
             self._mark("bwd_out")
-            self._spmm(stc.rowptr, stc.col, sg, dZ, beta=1.0, row_map=stc_rows)
+            self._spmm(stc.rowptr, stc.col, sg, dZ, beta=1.0, row_map=stc_rows,
+                       keep_bits=self.bits)
             del sg, hg
         self._gemm(self.dz, ws_t, cin=dZ, o_rows=self.posT, out=dZ)
-        F32.apply_keep_bits(dZ, self.bits)
+        tr = self.posT
+        dZ[tr] = dZ[tr] * F32.unpack_keep_bits(self.bits[tr], hid)
         # ---------------- backward: last hidden layer (index nl-2) weights over S rows
         lh = nl - 2
         self._mark(f"bwd_l{lh}")

@@ -28,7 +28,8 @@ def spmm_f32(rowptr: torch.Tensor, col: torch.Tensor, x: torch.Tensor,
              gate: Optional[torch.Tensor] = None, self_add: Optional[torch.Tensor] = None,
              self_map: Optional[torch.Tensor] = None, self_row0: int = 0,
              pass_cols: int = 0, rowend: Optional[torch.Tensor] = None,
-             x2: Optional[torch.Tensor] = None, nsplit: int = 0) -> torch.Tensor:
+             x2: Optional[torch.Tensor] = None, nsplit: int = 0,
+             keep_bits: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``out[o(i)] = row_scale[o(i)] * sum_j w_j X(m(col_j)) + beta * out[o(i)]`` over the
     entries of CSR row ``r = row_ids[i]`` (all rows when None): ``[rowptr[r], rowptr[r+1])``,
     or ``[rowptr[r], rowend[r])`` when ``rowend`` is given (one run of a row stored in two);
@@ -36,7 +37,9 @@ def spmm_f32(rowptr: torch.Tensor, col: torch.Tensor, x: torch.Tensor,
     with ``x2`` (two sources in one pass) ``x2[c - nsplit]`` for ``c >= nsplit``; ``o =
     row_map`` or identity. ``gate`` (indexed like ``out``): the stored value is kept where
     ``gate > 0`` (a ReLU derivative). ``self_add``: output row o also gets
-    ``self_add[self_map[self_row0 + o]]`` (when >= 0), before the gate. ``pass_cols`` (GPU):
+    ``self_add[self_map[self_row0 + o]]`` (when >= 0), before the gate. ``keep_bits``
+    ([out rows, F/32] int32, as ``row_keep_bits`` writes them): zero column c of output
+    row o unless bit c of its words is set (a 1-bit ReLU derivative). ``pass_cols`` (GPU):
     the column-pass width of this call (0 = the process default, 64): narrow passes keep a
     locality window in the caches, full-width passes make each random row access one long
     read (see FusedSAGE's autotune)."""
@@ -53,7 +56,7 @@ def spmm_f32(rowptr: torch.Tensor, col: torch.Tensor, x: torch.Tensor,
         _native.ops().spmm_f32_ex(rowptr, col, edge_weight, col_scale, row_scale, col_map,
                                   row_ids, x, out, float(beta), 0, row_map, gate, self_add,
                                   self_map, int(self_row0), rowend, x2, int(nsplit),
-                                  int(pass_cols))
+                                  int(pass_cols), keep_bits)
         return out
     # CPU reference (fp64 accumulation)
     rp = rowptr.long()
@@ -98,8 +101,17 @@ def spmm_f32(rowptr: torch.Tensor, col: torch.Tensor, x: torch.Tensor,
         acc = acc + torch.where((m >= 0).unsqueeze(1), add, torch.zeros_like(add))
     if gate is not None:
         acc = torch.where(gate[o][:, :acc.shape[1]] > 0, acc, torch.zeros_like(acc))
+    if keep_bits is not None:
+        acc = torch.where(unpack_keep_bits(keep_bits[o], acc.shape[1]), acc,
+                          torch.zeros_like(acc))
     out[o] = acc.to(out.dtype)
     return out
+
+
+def unpack_keep_bits(words: torch.Tensor, F: int) -> torch.Tensor:
+    """[rows, W] int32 keep words -> [rows, F] bool (bit c of a row's words: column c)."""
+    sh = torch.arange(32, device=words.device, dtype=torch.int32)
+    return (((words.unsqueeze(2) >> sh) & 1) != 0).reshape(words.shape[0], -1)[:, :F]
 
 
 # ------------------------------------------------------------------------------ GEMM

@@ -659,3 +659,28 @@ def test_gemm_f32_fused_send_rows(N):
             assert torch.equal(so[int(pos[q])], oc[r]), (r, q)
             written[int(pos[q])] = True
     assert bool((so[~written] == -7.0).all())
+
+
+@pytest.mark.parametrize("F,pc", [(256, 64), (256, 256), (128, 128)])
+def test_spmm_f32_keep_bits(F, pc):
+    """The 1-bit ReLU mask in the SpMM epilogue (models/sage_fused.py output-layer
+    backward): columns whose keep bit is clear are zeroed, every column pass reading its own
+    bits; with a row map and beta = 1 too. Against the CPU fp64 reference."""
+    rp, col = _csr(700, 500, 13, 5 + F)
+    g = torch.Generator().manual_seed(F + pc)
+    x = torch.randn(500, F, generator=g)
+    h = torch.randn(900, F, generator=g)
+    bits = F32.row_keep_bits(h)  # [900, F/32]
+    rmap = torch.randperm(900, generator=g)[:700]
+    base = torch.randn(900, F, generator=g)
+    for kw in (dict(), dict(row_map=rmap, beta=1.0)):
+        ref = base.clone()
+        F32.spmm_f32(rp.cpu(), col.cpu(), x, ref, keep_bits=bits,
+                     **{k: v for k, v in kw.items()})
+        out = base.clone().to(DEV)
+        F32.spmm_f32(rp, col, x.to(DEV), out, keep_bits=bits.to(DEV), pass_cols=pc,
+                     **{k: (v.to(DEV) if isinstance(v, torch.Tensor) else v)
+                        for k, v in kw.items()})
+        torch.testing.assert_close(out.cpu(), ref, atol=2e-5, rtol=1e-5)
+        o = rmap if "row_map" in kw else torch.arange(700)
+        assert bool((out.cpu()[o][h[o] <= 0] == 0).all())
