@@ -373,7 +373,8 @@ void row_keep_bits_op(const at::Tensor& h, const c10::optional<at::Tensor>& rows
                              reinterpret_cast<uint32_t*>(bits.data_ptr<int32_t>()), stream_of(h)));
 }
 
-void apply_keep_bits_op(const at::Tensor& g, const at::Tensor& bits) {
+void apply_keep_bits_op(const at::Tensor& g, const at::Tensor& bits,
+                        const c10::optional<at::Tensor>& rows) {
   f32_rows(g, "g");
   same_dev(bits, g, "bits");
   const int F = static_cast<int>(g.size(1));
@@ -381,10 +382,15 @@ void apply_keep_bits_op(const at::Tensor& g, const at::Tensor& bits) {
   TORCH_CHECK(bits.scalar_type() == at::kInt && bits.is_contiguous() &&
                   bits.numel() >= g.size(0) * (F / 32),
               "bits must be contiguous int32 with >= rows * F/32 words");
+  const at::Tensor* r = opt(rows);
+  const int64_t n = r ? r->numel() : g.size(0);
+  // (rows index g and bits alike: each must be a row of g, checked by the caller's plan —
+  // the executor passes its loss rows' positions in the support, built once)
+  const int64_t* rp = idx64(rows, g, n, "rows");
   c10::DeviceGuard dg(g.device());
   DG_HIP_CHECK(apply_keep_bits(g.data_ptr<float>(), g.stride(0),
                                reinterpret_cast<const uint32_t*>(bits.data_ptr<int32_t>()),
-                               g.size(0), F, stream_of(g)));
+                               n, F, stream_of(g), rp));
 }
 
 void xent_rows_op(const at::Tensor& z, const at::Tensor& rows, const at::Tensor& y,
@@ -464,7 +470,7 @@ TORCH_LIBRARY_FRAGMENT(dgraph_amd, m) {
         "int blocks, int fresh_from, Tensor(b!)? col_partials=None) -> ()");
   m.def("wgrad_f32_reduce(Tensor partials, Tensor(a!) out) -> ()");
   m.def("row_keep_bits(Tensor h, Tensor? rows, Tensor(a!) bits) -> ()");
-  m.def("apply_keep_bits(Tensor(a!) g, Tensor bits) -> ()");
+  m.def("apply_keep_bits(Tensor(a!) g, Tensor bits, Tensor? rows=None) -> ()");
   m.def("xent_rows(Tensor z, Tensor rows, Tensor y, float scale, Tensor(a!) dz, "
         "Tensor(b!) row_loss, int C) -> ()");
   m.def("argmax_hits(Tensor z, Tensor rows, Tensor y, Tensor(a!) hit, int C) -> ()");

@@ -42,12 +42,14 @@ __global__ __launch_bounds__(256) void row_keep_bits_kernel(const float* __restr
 __global__ __launch_bounds__(256) void apply_keep_bits_kernel(float* __restrict__ g,
                                                               int64_t ldg,
                                                               const uint32_t* __restrict__ bits,
-                                                              int64_t n, int F) {
+                                                              int64_t n, int F,
+                                                              const int64_t* __restrict__ rows) {
   const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   const int V = F / 4;
   if (t >= n * V) return;
-  const int64_t i = t / V;
-  const int f = static_cast<int>(t - i * V);
+  const int64_t k = t / V;
+  const int f = static_cast<int>(t - k * V);
+  const int64_t i = rows ? rows[k] : k;  // (rows: a subset of g's rows, bits indexed alike)
   const uint32_t m = bits[i * (V / 8) + f / 8] >> (4 * (f & 7));
   float4* p = reinterpret_cast<float4*>(g + i * ldg + 4 * f);
   float4 v = *p;
@@ -72,13 +74,13 @@ hipError_t row_keep_bits(const float* h, int64_t ldh, const int64_t* rows, int64
 }
 
 hipError_t apply_keep_bits(float* g, int64_t ldg, const uint32_t* bits, int64_t n, int F,
-                           hipStream_t st) {
+                           hipStream_t st, const int64_t* rows) {
   if (n <= 0) return hipSuccess;
   if (F % 32 != 0 || ldg % 4 != 0 || (reinterpret_cast<uintptr_t>(g) & 15)) return hipErrorInvalidValue;
   const int64_t blocks = (n * (F / 4) + 255) / 256;
   if (blocks > 0x7fffffff) return hipErrorInvalidValue;
   hipLaunchKernelGGL(apply_keep_bits_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0,
-                     st, g, ldg, bits, n, F);
+                     st, g, ldg, bits, n, F, rows);
   return hipGetLastError();
 }
 

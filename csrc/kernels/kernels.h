@@ -301,8 +301,9 @@ hipError_t wgrad_f32_reduce(const float* partials, int P, int64_t KN, float* out
 // 1-bit ReLU keep masks of selected rows (bits.hip): F % 32 == 0, F/32 words per row.
 hipError_t row_keep_bits(const float* h, int64_t ldh, const int64_t* rows, int64_t n, int F,
                          uint32_t* bits, hipStream_t st);
+// rows (nullable): apply to rows rows[0..n) of g (bits indexed by the same row) only
 hipError_t apply_keep_bits(float* g, int64_t ldg, const uint32_t* bits, int64_t n, int F,
-                           hipStream_t st);
+                           hipStream_t st, const int64_t* rows = nullptr);
 
 // Softmax cross-entropy / argmax of selected logit rows (loss.hip), C <= 256:
 //   row_loss[i] = lse(z[rows[i]]) - z[rows[i]][y[i]];  dz[i][c] = (p_c - [c == y]) * scale

@@ -369,6 +369,8 @@ class FusedSAGE:
         smap[S] = torch.arange(self.nS, dtype=torch.int32, device=dev)
         self.smap = smap
         self.posT = smap[self.T].long().contiguous()
+        if self.T.numel() and int(self.posT.min()) < 0:  # (T is part of S by construction)
+            raise RuntimeError("FusedSAGE: a loss row outside the gradient support")
         self.invdegS = self.inv_deg[S].contiguous()
         self.AT_S = it_t.select_rows(S)            # rows S (compact), cols T (compact)
         del it_t
@@ -1461,8 +1463,7 @@ class FusedSAGE:
                        keep_bits=self.bits)
             del sg, hg
         self._gemm(self.dz, ws_t, cin=dZ, o_rows=self.posT, out=dZ)
-        tr = self.posT
-        dZ[tr] = dZ[tr] * F32.unpack_keep_bits(self.bits[tr], hid)
+        F32.apply_keep_bits(dZ, self.bits, rows=self.posT)
         # ---------------- backward: last hidden layer (index nl-2) weights over S rows
         lh = nl - 2
         self._mark(f"bwd_l{lh}")

@@ -464,13 +464,21 @@ def row_keep_bits(h: torch.Tensor, rows: Optional[torch.Tensor] = None,
     return out
 
 
-def apply_keep_bits(g: torch.Tensor, bits: torch.Tensor) -> torch.Tensor:
-    """In place ``g[i, f] = bit(i, f) ? g[i, f] : 0``."""
+def apply_keep_bits(g: torch.Tensor, bits: torch.Tensor,
+                    rows: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """In place ``g[i, f] = bit(i, f) ? g[i, f] : 0`` (for the rows ``rows`` only, bits
+    indexed by the same row, when given)."""
     if g.is_cuda:
-        _native.ops().apply_keep_bits(g, bits)
+        _native.ops().apply_keep_bits(g, bits, rows)
         return g
     n, F = g.shape
     w = bits.view(n, F // 32).long() & 0xFFFFFFFF
+    if rows is not None:
+        r = rows.long()
+        keep = ((w[r].unsqueeze(-1) >> torch.arange(32, dtype=torch.long)) & 1).view(
+            r.numel(), F).bool()
+        g[r] = g[r] * keep.to(g.dtype)
+        return g
     keep = ((w.unsqueeze(-1) >> torch.arange(32, dtype=torch.long)) & 1).view(n, F).bool()
     g.mul_(keep.to(g.dtype))
     return g
