@@ -39,7 +39,7 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 // batch of all LPR rows (all loads of a chunk before its FMAs: -3 %) and against forcing 6 or
 // 8 waves per SIMD (fewer registers, fewer loads in flight: -28 % / -38 %),
 // profiles/r04/spmm_f32_variants_ab.log.
-template <typename IdxT, int LPR, int WMODE, bool CMAP, bool TWO>
+template <typename IdxT, int LPR, int WMODE, bool CMAP, bool TWO, bool KB = false>
 __global__ __launch_bounds__(256) void spmm_f32_rowgroup_kernel(SpmmF32Args a) {
   constexpr int VEC = 4;
   constexpr int G = kWave / LPR;
@@ -242,7 +242,10 @@ __global__ __launch_bounds__(256) void spmm_f32_rowgroup_kernel(SpmmF32Args a) {
         res.z = gv.z > 0.f ? res.z : 0.f;
         res.w = gv.w > 0.f ? res.w : 0.f;
       }
-      if (a.keep_bits) {  // the same from a 1-bit mask (4 columns never straddle a word)
+      // the same from a 1-bit mask (4 columns never straddle a word); compile-time, so the
+      // variants without it keep their register count (the 64-column pass: 94 VGPRs, 5
+      // waves per SIMD; a runtime branch here cost a wave)
+      if constexpr (KB) {
         const int c = a.bits_col0 + f;
         const uint32_t w = a.keep_bits[orow * a.ld_bits + (c >> 5)] >> (c & 31);
         res.x = (w & 1u) ? res.x : 0.f;
@@ -278,7 +281,21 @@ hipError_t launch_f32_rg(const SpmmF32Args& a, hipStream_t st) {
   const int wmode = (a.ew != nullptr ? 1 : 0) | (a.col_scale != nullptr ? 2 : 0);
   const bool cmap = a.col_map != nullptr;
   const bool two = a.x2 != nullptr;
+  const bool kb = a.keep_bits != nullptr;
   if (two && wmode != 0) return hipErrorInvalidValue;  // not instantiated
+  if (kb && (two || cmap || wmode != 0)) return hipErrorInvalidValue;  // not instantiated
+  if (kb) {
+#define DG_F32_KB(LPR_)                                                                      \
+    if (LPR == LPR_) {                                                                       \
+      hipLaunchKernelGGL((spmm_f32_rowgroup_kernel<IdxT, LPR_, 0, false, false, true>), grid, \
+                         block, 0, st, ka);                                                  \
+      return hipGetLastError();                                                              \
+    }
+    dim3 grid(static_cast<unsigned>(blocks)), block(256);
+    DG_F32_KB(8) DG_F32_KB(16) DG_F32_KB(32) DG_F32_KB(64)
+#undef DG_F32_KB
+    return hipErrorInvalidValue;
+  }
   dim3 grid(static_cast<unsigned>(blocks)), block(256);
 #define DG_F32_K(LPR_, W_, C_, T_)                                                          \
   if (LPR == LPR_ && wmode == W_ && cmap == C_ && two == T_) {                              \
