@@ -44,22 +44,10 @@ import time
 # (expandable segments are unsupported on ROCm; forbid splitting huge cached blocks so a
 #  freed 57 GB activation block is never carved up by a 38 GB request)
 os.environ.setdefault("PYTORCH_ALLOC_CONF", "max_split_size_mb:512")
-# hardware queues per process, set before the HIP runtime starts (torch only initialises it
-# on first use). With HIP's default of 4, the streams of one process (default, compute,
-# the communication stream of the halo exchange, ...) share queues round-robin, and a
-# stream sharing the compute stream's queue runs IN ORDER with it: the exchange is then
-# serialised with the kernels it should overlap (measured: a W=8 rank's step 355 ms with
-# 4 queues vs 309 ms with 8 or 16, the exposed exchange moving into the compute regions,
-# profiles/r04/). The GPU boxes export GPU_MAX_HW_QUEUES=4 (HIP's default), and with it
-# the comm stream shared the compute stream's queue again in round 5 (a W=8 rehearsal's
-# kernel trace: both streams on one queue, zero overlap, profiles/r05/timeline_*), so a
-# value below 8 is raised to 8; DGRAPH_HW_QUEUES sets it explicitly. The value found and
-# the one used are recorded in the JSON line ("hw_queues").
+# hardware queues per process: left as the box exports them (HIP's default, 4) — the halo
+# exchange rides a high-priority stream, which gets a queue of its own at any queue budget
+# (comm/alltoallv.py _side_stream); the value in effect is recorded in the JSON line
 _HWQ_FOUND = os.environ.get("GPU_MAX_HW_QUEUES")
-if os.environ.get("DGRAPH_HW_QUEUES"):
-    os.environ["GPU_MAX_HW_QUEUES"] = os.environ["DGRAPH_HW_QUEUES"]
-elif not (_HWQ_FOUND or "").isdigit() or int(_HWQ_FOUND) < 8:
-    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 import torch
 import torch.distributed as dist
@@ -131,6 +119,12 @@ def parse():
                     help="capture the whole step (forward, backward, sync, Adam) into a HIP "
                          "graph after the first eager warmup step and replay it "
                          "(dgraph_amd.utils.graphed; for launch-bound small shapes)")
+    ap.add_argument("--no-shmem-probe", action="store_true",
+                    default=os.environ.get("DGRAPH_BENCH_SHMEM_PROBE", "1") == "0",
+                    help="W > 1: skip the one-sided (symmetric-heap) transport probe that runs "
+                         "as a separate child job after the headline")
+    ap.add_argument("--shmem-probe-timeout", type=float,
+                    default=float(os.environ.get("DGRAPH_BENCH_SHMEM_PROBE_TIMEOUT_S", "240")))
     ap.add_argument("--metrics-jsonl", default=os.environ.get("DGRAPH_METRICS_JSONL", ""),
                     help="append one metrics record per measured phase (rank 0)")
     return ap.parse_args()
@@ -287,7 +281,8 @@ class Job:
                 reserve = int(args.plan_reserve_gb * (1 << 30))
             self.fused = FusedSAGE(self.model, self.graph, self.x, self.train_idx, self.y_train,
                                    self.eval_idx, self.y_eval, self.eval_is_val, self.n_train,
-                                   release_graph=True, reserve_bytes=reserve)
+                                   release_graph=True, reserve_bytes=reserve,
+                                   config=getattr(args, "exec_cfg", None))
         self.steppers = {}
         if getattr(args, "cuda_graph", False) and dev.type == "cuda":
             from dgraph_amd.utils.graphed import GraphedStep, make_capturable
@@ -604,6 +599,80 @@ def region_breakdown(job: "Job") -> dict:
     return out
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def shmem_probe_child(args, rank: int, world: int, splits, dev) -> dict:
+    """The one-sided transport probe (dgraph_amd/comm/shmem_probe.py) over the headline's
+    own halo plan, as a SEPARATE JOB: every rank starts one child process (a fresh
+    interpreter on the same GPU, its own process group on a new port) and waits for it; the
+    ranks themselves are never replaced and run nothing on the GPU meanwhile. A fault, a
+    hang (killed at ``--shmem-probe-timeout``) or an error in any child is recorded as
+    ``{"failed": ...}``; the headline line is printed either way. The children's outcome is
+    gathered over a CPU (gloo) group, which a GPU fault in a child cannot disturb. Returns
+    the merged record on rank 0 ({} elsewhere)."""
+    import subprocess
+    import tempfile
+
+    cpu = dist.new_group(backend="gloo")  # collective: every rank
+    port = [_free_port() if rank == 0 else 0]
+    dist.broadcast_object_list(port, src=0, group=cpu)
+    fd, path = tempfile.mkstemp(prefix=f"dgraph_shmem_plan_r{rank}_", suffix=".json")
+    with os.fdopen(fd, "w") as f:
+        json.dump({"send_splits": splits[0], "recv_splits": splits[1]}, f)
+    env = dict(os.environ, RANK=str(rank), WORLD_SIZE=str(world),
+               LOCAL_RANK=os.environ.get("LOCAL_RANK", str(rank)), MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(port[0]),
+               DGRAPH_PG_TIMEOUT_S=str(int(max(30, args.shmem_probe_timeout * 0.5))))
+    # torchrun's agent store is not the child's rendezvous: rank 0's child hosts its own
+    for k in ("TORCHELASTIC_USE_AGENT_STORE", "TORCHELASTIC_RUN_ID", "GROUP_RANK",
+              "ROLE_RANK", "TORCHELASTIC_RESTART_COUNT", "TORCHELASTIC_MAX_RESTARTS"):
+        env.pop(k, None)
+    if dev.type == "cuda":
+        gc.collect()
+        torch.cuda.synchronize(dev)
+        torch.cuda.empty_cache()  # the headline's cached blocks back for the child
+    cmd = [sys.executable, "-u", "-m", "dgraph_amd.comm.shmem_probe", "--plan", path,
+           "--width", "64", "--iters", "5"]
+    t0 = time.time()
+    rc, out, err = 0, "", ""
+    try:
+        p = subprocess.run(cmd, env=env, cwd=os.path.dirname(os.path.abspath(__file__)),
+                           capture_output=True, text=True, timeout=args.shmem_probe_timeout)
+        rc, out, err = p.returncode, p.stdout, p.stderr
+    except subprocess.TimeoutExpired as e:
+        rc, err = "timeout", (e.stderr or b"").decode(errors="replace") \
+            if isinstance(e.stderr, bytes) else (e.stderr or "")
+    except Exception as e:  # noqa: BLE001 - the probe must not cost the headline
+        rc, err = "spawn-error", repr(e)
+    finally:
+        os.unlink(path)
+    line = next((ln[len("SHMEM_PROBE "):] for ln in out.splitlines()
+                 if ln.startswith("SHMEM_PROBE ")), None)
+    mine = {"rank": rank, "exit": rc, "stderr_tail": (err or "")[-400:] if rc != 0 else ""}
+    allr = [None] * world
+    dist.all_gather_object(allr, mine, group=cpu)
+    dist.destroy_process_group(cpu)
+    if rank != 0:
+        return {}
+    bad = [r for r in allr if r["exit"] != 0]
+    rec = {"child_wall_s": round(time.time() - t0, 1)}
+    if bad or line is None:
+        rec["failed"] = bad or [{"rank": 0, "exit": rc, "stderr_tail": "no SHMEM_PROBE line: "
+                                 + (err or "")[-300:]}]
+        return rec
+    try:
+        rec.update(json.loads(line))
+    except ValueError as e:
+        rec["failed"] = [{"rank": 0, "exit": rc, "stderr_tail": f"bad probe line: {e}"}]
+    return rec
+
+
 def _spawn_ranks(n: int) -> int:
     """Run this script under ``torch.distributed.run`` with ``n`` local ranks (loopback
     rendezvous on a free port) as a CHILD process and return its exit status. Called only
@@ -647,6 +716,8 @@ def main():
     cfg = RunConfig.from_env()  # DGRAPH_<SECTION>_<FIELD> overrides (kernel knobs etc.)
     cfg.model.hidden, cfg.model.num_layers, cfg.model.dtype = args.hidden, args.layers, args.dtype
     cfg.data.dataset, cfg.data.global_frac = args.shape, args.global_frac
+    cfg.data.scale = args.scale
+    args.exec_cfg = cfg.fused  # the fused executor's knobs, resolved once, recorded whole
     comm = Communicator.init_process_group("nccl")
     rank, world = comm.get_rank(), comm.get_world_size()
     dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() \
@@ -662,6 +733,10 @@ def main():
               f"halo_rows_total={job.halo_total} train={job.n_train} val={job.n_val} "
               f"test={job.n_test}")
     head_restrict = args.restrict_last
+    a2a_plan = getattr(job.graph, "a2a", None)
+    # the headline's halo plan (row counts per peer), for the one-sided probe job
+    plan_splits = (list(a2a_plan.send_splits), list(a2a_plan.recv_splits)) \
+        if (a2a_plan is not None and world > 1 and not job.rehearse) else None
     if dev.type == "cuda":
         torch.cuda.reset_peak_memory_stats()
     ms, final_loss, e_step = timed(job, args.steps, args.warmup, head_restrict, args.verbose)
@@ -787,6 +862,9 @@ def main():
     else:
         job.free()
 
+    shm = {}
+    if plan_splits is not None and not args.no_shmem_probe:
+        shm = shmem_probe_child(args, rank, world, plan_splits, dev)
     if args.rehearse_world > 1 and world == 1:
         # not a whole-job number: one rank's compute with a loopback exchange
         print(json.dumps({"rehearsal": True, "rank": args.rehearse_rank,
@@ -858,8 +936,7 @@ def main():
             "E_directed": shape.num_directed_edges,
             "edges_aggregated_per_step": e_step,
             "edges_aggregated_per_s": e_step / (ms / 1000.0),
-            "hw_queues": {"used": os.environ.get("GPU_MAX_HW_QUEUES"),
-                          "found_in_env": _HWQ_FOUND},
+            "hw_queues": _HWQ_FOUND or "runtime default",
             "final_loss": final_loss,
             "val_acc": val_acc,
             "test_acc": test_acc,
@@ -871,6 +948,10 @@ def main():
             **({"halo": halo} if halo else {}),
             **({"regions": regions} if regions else {}),
             **({"xgmi_probe": xgmi} if xgmi else {}),
+            **({"shmem_probe": shm} if shm else {}),
+            # every knob the run resolved (RunConfig: comm / kernels / fused executor / model /
+            # data), so the line alone reproduces the configuration
+            "run_config": cfg.to_dict(),
             **extra,
         }
         print(json.dumps(rec), flush=True)

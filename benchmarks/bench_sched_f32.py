@@ -12,7 +12,6 @@ import os
 import statistics
 import sys
 
-os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("DGRAPH_HW_QUEUES", "8")  # side stream
 import torch  # noqa: E402
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))

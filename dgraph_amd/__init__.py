@@ -15,33 +15,14 @@ Layout:
     dgraph_amd.data      DistributedGraph, preprocessing, partitioners, synthetic graphs
     dgraph_amd.utils     TimingReport, metrics, config, checkpointing
 """
-import os as _os
-
 # (ProcessGroupNCCL keeps an asynchronous collective's tensors alive until its work.wait()
 # instead of record_stream-ing them — the default of this torch; the library's own
 # transports do the same, comm/alltoallv.py _EventWork.)
-
-
-def _hw_queues() -> None:
-    """At least 8 hardware queues per process (HIP's default, and the GPU boxes' exported
-    value, is 4): with 4, torch's pool streams share queues with the compute stream, and a
-    comm stream on the compute stream's queue runs in order with it — no overlap
-    (PERFORMANCE.md, round 5). Only before the HIP runtime starts; DGRAPH_HW_QUEUES sets
-    the value explicitly."""
-    import sys
-
-    t = sys.modules.get("torch")
-    if t is not None and t.cuda.is_initialized():
-        return
-    want = _os.environ.get("DGRAPH_HW_QUEUES")
-    cur = _os.environ.get("GPU_MAX_HW_QUEUES", "")
-    if want:
-        _os.environ["GPU_MAX_HW_QUEUES"] = want
-    elif not cur.isdigit() or int(cur) < 8:
-        _os.environ["GPU_MAX_HW_QUEUES"] = "8"
-
-
-_hw_queues()
+#
+# GPU_MAX_HW_QUEUES is left as the operator set it (the boxes export HIP's default, 4): the
+# halo exchange runs on a HIGH-priority stream (comm/alltoallv.py _side_stream, RCCL's
+# stream in comm/groups.py), which the runtime places on a queue of its own whatever the
+# queue budget (scripts/debug/queue_probe.py), so overlap does not depend on raising it.
 
 from .__version__ import __version__  # noqa: E402
 from .comm.base import BackendEngine, CommunicatorBase  # noqa: E402

@@ -62,42 +62,46 @@ from ..ops import f32 as F32
 from ..ops import kernels as K
 from ..parallel.dist_graph import DistGraph
 from ..parallel.reorder import graph_locality
+from ..utils.config import ExecutorConfig
 
+# Executor knobs: utils/config.py ExecutorConfig, resolved per FusedSAGE (env
+# DGRAPH_FUSED_<FIELD> or an explicit config=). What each one does, and the measurements
+# behind its default:
 # rows per chunk of the row-chunked passes (0 = auto from free memory)
-CHUNK_ROWS = int(os.environ.get("DGRAPH_FUSED_CHUNK_ROWS", "0"))
+#   -> ExecutorConfig.chunk_rows
 # W > 1: overlap each forward halo exchange with work that does not need it
-OVERLAP_FWD = os.environ.get("DGRAPH_FUSED_OVERLAP", "1") != "0"
+#   -> ExecutorConfig.overlap
 # keep layer 0's input aggregate mean_N(x) from the forward for the backward when the
 # memory plan has room for it ("auto"), never ("off"), or require it ("on")
-KEEP_AGG0 = os.environ.get("DGRAPH_FUSED_KEEP_AGG0", "auto")
+#   -> ExecutorConfig.keep_agg0
 # W > 1, a forward layer whose exchange is in flight: after its interior rows, aggregate the
 # interior part of the boundary rows into a store before waiting ("on"), or wait and run the
 # boundary rows in one two-source pass ("off"); "auto" stores only when the modelled
 # exchange outlasts the interior rows' work (the store costs a second pass over the boundary
 # rows and a read-modify-write of their aggregates: ~10 ms per layer at W = 8)
-BOUNDARY_STORE = os.environ.get("DGRAPH_FUSED_BOUNDARY_STORE", "auto")
+#   -> ExecutorConfig.boundary_store
 # keep the last hidden layer's input aggregate on the support rows S from the forward (the
 # forward computes it for every row anyway) instead of re-aggregating the S rows in the
 # backward (and, with streamed halos, re-fetching the halo in column blocks): auto = when
 # the memory plan has room for nS x width floats (always with streamed halos, whose plan
 # already holds that store). Saves a pass over the S rows' entries per step.
-KEEP_AS = os.environ.get("DGRAPH_FUSED_KEEP_AS", "auto")
+#   -> ExecutorConfig.keep_as
 # streamed hidden layers: the self term h W_self + b as a separate GEMM during the first
 # column block's transfer (1), or the dual GEMM after the aggregation, in place (0)
-STREAM_FILL = os.environ.get("DGRAPH_FUSED_STREAM_FILL", "1") != "0"
+#   -> ExecutorConfig.stream_fill
 # streamed halos: the first column block half as wide as the rest (the pipeline fill, whose
 # transfer nothing but the fill work hides, is half as long). Off: the extra column pass
 # costs what it saves (W=8 structureless rank 700.6 ms with, 698.8 without; exposed
 # exchange 15 vs 53 ms, profiles/r05/rehearse_structureless_ramp_zself.jsonl)
-STREAM_RAMP = os.environ.get("DGRAPH_FUSED_STREAM_RAMP", "0") != "0"
+#   -> ExecutorConfig.stream_ramp
 # streamed output layer: its self term as a separate GEMM during the first block's transfer
 # (into an [L, Cp] store, when it fits). Off: the split GEMM's extra store traffic costs
 # what it hides (W=8 structureless fwd_out + its exchange 196 ms with, 191.5 without)
-STREAM_OUT_FILL = os.environ.get("DGRAPH_FUSED_STREAM_OUT_FILL", "0") != "0"
+#   -> ExecutorConfig.stream_out_fill
 # W > 1: hidden-layer halos exchanged and consumed in column blocks ("stream") instead of
 # kept at full width for the whole step — "auto" when the full-width plan does not fit (a
 # structureless graph's halo is nearly every remote vertex), "on" / "off" to force
-HALO_STREAM = os.environ.get("DGRAPH_FUSED_HALO_STREAM", "auto")
+#   -> ExecutorConfig.halo_stream
 # input-layer backward: the transposed aggregation of u (stored on the support rows S only)
 # over an adjacency compacted to the S columns once, with the columns already mapped to S
 # positions (a plain SpMM over ~S/L of the entries), instead of the column-mapped pass over
@@ -105,7 +109,7 @@ HALO_STREAM = os.environ.get("DGRAPH_FUSED_HALO_STREAM", "auto")
 # the default). Against the column-mapped pass at 64-column passes it cut the W=2/4/8 rank
 # step by 3-5 %; against the column-mapped pass at full width (_spmm_u) it is a tie
 # (W=8 265.6-267.6 vs 267.0 ms, W=2 1062-1068 vs 1065 ms) at a few GB more memory.
-COMPACT_T = os.environ.get("DGRAPH_FUSED_COMPACT_T", "off")
+#   -> ExecutorConfig.compact_t
 # W > 1: where the halo pack (the gather of the send rows into the send buffer) runs: on the
 # compute stream just before the exchange is issued ("compute"), or on the communication
 # stream next to the exchange ("comm"). A pack co-running with the aggregation saturates
@@ -113,38 +117,36 @@ COMPACT_T = os.environ.get("DGRAPH_FUSED_COMPACT_T", "off")
 # 1.2 ms) and hides nothing: windowed W=8 rank 256.2 (comm) vs 257.1 ms (compute), W=2
 # 976.5 vs 975.7; structureless W=8 682.8 vs 670.6 ms, exposed exchange 59.6 vs 12.5 ms
 # (the streamed blocks' transfers start a pack earlier; profiles/r05/pack_ab.jsonl)
-PACK_STREAM = os.environ.get("DGRAPH_FUSED_PACK_STREAM", "compute")
+#   -> ExecutorConfig.pack_stream
 # W > 1, resident halos: the pack fused into the GEMM that produces the sent rows (its
 # epilogue also stores each row at its send-buffer positions) instead of a gather pass
-FUSED_PACK = os.environ.get("DGRAPH_FUSED_PACK_FUSED", "1") != "0"
+#   -> ExecutorConfig.pack_fused
 # W > 1, symmetric graph, 3 layers: the halo part of the input layer's backward aggregation
 # A^T u (u = the layer-1 pre-activation gradient, nonzero on the support rows S only) by
 # "pull" — the owners send their S rows of u that are some rank's halo rows (a forward-style
 # exchange restricted to S), each rank aggregates them with its own rows in one two-source
 # pass — or by "push": every rank aggregates the contributions of its rows to EVERY halo row
 # (a transposed pass over H rows) and sends them back to the owners, who add them
-BWD_HALO = os.environ.get("DGRAPH_FUSED_BWD_HALO", "pull")
+#   -> ExecutorConfig.bwd_halo
 # W > 1: the output layer projected BEFORE it is aggregated, when its padded width Cp is
 # narrower than the hidden width (mean_N(h) W_neigh = mean_N(h W_neigh)): the logits'
 # neighbour term aggregates and exchanges Cp columns instead of hid (172 -> 176 vs 256 on
 # papers100M). "auto": when the plan has room for the [L, Cp] projection (the W_neigh
 # weight gradient then needs the loss rows' aggregate of h, pulled separately: small)
-PROJECT_FIRST = os.environ.get("DGRAPH_FUSED_PROJECT_FIRST", "auto")
+#   -> ExecutorConfig.project_first
 # column-mapped gradient SpMMs run full-width passes while the support S is at most this
 # share of the rows (papers100M 0.28 at W=1 and W=8: full width, step 1865 ms / 266 ms;
 # ogbn-products 0.98: 64-column passes, 71.7 vs 76.1 ms at full width)
-U_FULL_FRAC = float(os.environ.get("DGRAPH_FUSED_U_FULL_FRAC", "0.35"))
-# (column block, ring buffers) of the streamed plan, in order of preference
+#   -> ExecutorConfig.u_full_frac
 # (column block, ring buffers) in order of preference: two buffers before wider blocks —
 # with one buffer every block's transfer is exposed (a W=2 structureless rank: 1.1 s of its
 # 3.1 s step), and 32-column passes aggregate at the 64-column rate per byte
 # (profiles/r05/xcd_ab2.log)
-STREAM_SHAPES = tuple(
-    tuple(int(v) for v in t.split("x"))
-    for t in os.environ.get("DGRAPH_FUSED_STREAM_SHAPES", "64x2,32x2,64x1,32x1").split(","))
+#   -> ExecutorConfig.stream_shapes
 # planning rates of the "auto" choice: xGMI per link and direction, fp32 SpMM gather
 # (effective) and fp32 MFMA GEMM rates measured on MI355X (PERFORMANCE.md)
-PLAN_LINK_GBPS = float(os.environ.get("DGRAPH_PLAN_LINK_GBPS", "153"))
+#   -> ExecutorConfig.plan_link_gbps
+PLAN_LINK_GBPS = 153.0  # xGMI per link and direction: the planner's fallback rate
 PLAN_SPMM_TBPS = 13.0   # row-group SpMM, 64-column passes, bench graph (PERFORMANCE.md)
 PLAN_GEMM_TFPS = 120.0  # exact-f32 MFMA GEMM, interleaved with aggregations
 PLAN_HBM_TBPS = 5.0     # streaming read-modify-write of a store
@@ -316,9 +318,12 @@ class FusedSAGE:
     def __init__(self, model, graph: DistGraph, x: torch.Tensor, train_idx: torch.Tensor,
                  y_train: torch.Tensor, eval_idx: torch.Tensor, y_eval: torch.Tensor,
                  eval_is_val: torch.Tensor, n_train: int, chunk_rows: int = 0,
-                 release_graph: bool = False, reserve_bytes: int = 0):
+                 release_graph: bool = False, reserve_bytes: int = 0,
+                 config: Optional[ExecutorConfig] = None):
         if not supported(model, x):
             raise ValueError("FusedSAGE: unsupported model/feature shape")
+        # the schedule knobs, resolved now (environment read at construction, not import)
+        self.cfg = cfg = config if config is not None else ExecutorConfig.from_env()
         dev = x.device
         self.dev = dev
         if dev.type == "cuda":
@@ -391,7 +396,7 @@ class FusedSAGE:
         self.itT = None if it.symmetric else it.transpose()
         # (collective: built by every rank before the memory plan can raise)
         self.pull = self._pull_plan(graph) \
-            if (BWD_HALO == "pull" and self.nl == 3 and graph.symmetric and
+            if (cfg.bwd_halo == "pull" and self.nl == 3 and graph.symmetric and
                 graph.send_map is not None) else None
         # the per-peer link rate the overlap planner assumes: measured on this job's own
         # exchange (collective), not the xGMI peak
@@ -467,8 +472,15 @@ class FusedSAGE:
             self.sub_rows = (self.sub[0].rowptr.numel() - 1, self.sub[1].total_recv)
         sub_bytes = 4 * self.hid * (self.sub_rows[0] + self.sub_rows[1])
         full_ok = dev.type != "cuda" or need_h + self.halo_bytes + other + (1 << 28) <= free
-        if graph.send_map is not None and (HALO_STREAM == "on" or
-                                           (HALO_STREAM == "auto" and not full_ok)):
+        # Choices that change the SEQUENCE of collectives (streamed halos and their shape,
+        # the projected output layer) are agreed over the plan's group: each rank plans from
+        # its own free memory and partition sizes, and one rank choosing differently would
+        # post all-to-all-v calls its peers never match (a hang or corrupted halos)
+        want_stream = graph.send_map is not None and (
+            cfg.halo_stream == "on" or (cfg.halo_stream == "auto" and not full_ok))
+        if graph.send_map is not None:
+            want_stream = bool(self._agree([int(want_stream)], "max")[0])
+        if want_stream:
             # streamed halos: the input's halo stays resident (static), the hidden layers'
             # cross in column blocks of cw through a ring of nbuf send/receive buffers, and
             # whole-row aggregates land in stores (the output layer's, the S rows' of the
@@ -476,18 +488,31 @@ class FusedSAGE:
             # (the reverse exchange's input-layer gradient store lives in the output
             # layer's aggregate store, dead once the forward is done)
             stores = L * max(self.hid, self.d0) * 4 + self.nS * w_lh * 4
-            for cw, nb in STREAM_SHAPES:
-                if self.hid % cw:
-                    continue
+            shapes = cfg.shapes()
+            fit, hbs = [], []
+            for cw, nb in shapes:
                 ring = max(nb * (H + n_send) * cw * 4, sub_bytes)
                 hb = 4 * H * self.d0 + ring + stores
-                if dev.type != "cuda" or need_h + hb + other + (1 << 28) <= free:
+                hbs.append(hb)
+                fit.append(int(self.hid % cw == 0 and (
+                    dev.type != "cuda" or need_h + hb + other + (1 << 28) <= free)))
+            fit = self._agree(fit, "min")  # the first shape EVERY rank has room for
+            for (cw, nb), ok, hb in zip(shapes, fit, hbs):
+                if ok:
                     self.stream, self.cw, self.nbuf, self.halo_bytes = True, cw, nb, hb
                     break
         need_h += self.halo_bytes
-        if dev.type == "cuda" and need_h + other + (1 << 28) > free:
-            # fail here, before any allocation (and after every collective of the setup), so a
-            # caller can skip the configuration on every rank alike instead of dying mid-step
+        fits = dev.type != "cuda" or need_h + other + (1 << 28) <= free
+        if graph.send_map is not None and not bool(self._agree([int(fits)], "min")[0]):
+            # fail here, before any allocation (and after every collective of the setup), on
+            # every rank alike, so a caller can skip the configuration instead of dying
+            # mid-step
+            raise MemoryError(
+                f"FusedSAGE: activations {need_h / 2**30:.1f} GiB (halo rows "
+                f"{self.halo_bytes / 2**30:.1f}) + workspace {other / 2**30:.1f} GiB exceed the "
+                f"{free / 2**30:.1f} GiB free on {dev}" + ("" if not fits else
+                                                        " of another rank of the group"))
+        if not fits:
             raise MemoryError(
                 f"FusedSAGE: activations {need_h / 2**30:.1f} GiB (halo rows "
                 f"{self.halo_bytes / 2**30:.1f}) + workspace {other / 2**30:.1f} GiB exceed the "
@@ -496,7 +521,7 @@ class FusedSAGE:
         # the input-layer backward's S-compacted transposed adjacency (COMPACT_T): built when
         # it leaves at least 1 GB for the chunk arena (it shrinks the arena, not the plan)
         self.TS = None
-        if self.nl == 3 and COMPACT_T != "off":
+        if self.nl == 3 and cfg.compact_t != "off":
             if self.itT is not None:
                 src = (self.itT.rowptr, self.itT.col, None)
             else:
@@ -505,7 +530,7 @@ class FusedSAGE:
                 if L else 0
             ts_bytes = nnz_ts * 4 + (L + 1) * 8
             room = free - need_h - other - (1 << 28)
-            if COMPACT_T == "on" or dev.type != "cuda" or room - ts_bytes >= (1 << 30):
+            if cfg.compact_t == "on" or dev.type != "cuda" or room - ts_bytes >= (1 << 30):
                 self.TS = _compact_by_map(src[0], src[1], src[2], self.smap, L)
                 other += ts_bytes
         # the same for the halo rows' transposed aggregation of u (the reverse exchange's
@@ -516,7 +541,7 @@ class FusedSAGE:
             nnz_h = _compact_by_map(self.haloT.rowptr, self.haloT.col, None, self.smap, Hn,
                                     count_only=True)
             hts_bytes = nnz_h * 4 + (Hn + 1) * 8
-            if COMPACT_T == "on" or dev.type != "cuda" or \
+            if cfg.compact_t == "on" or dev.type != "cuda" or \
                     free - need_h - other - (1 << 28) - hts_bytes >= (1 << 30):
                 self.HTS = _compact_by_map(self.haloT.rowptr, self.haloT.col, None, self.smap,
                                            Hn)
@@ -526,26 +551,27 @@ class FusedSAGE:
         self.aS_keep = None
         self.w_lh = w_lh
         need_as = self.nS * self.w_lh * 4
-        self.keep_as = KEEP_AS == "on" or self.stream or (
-            KEEP_AS == "auto" and free - need_h - other - need_as > margin)
+        self.keep_as = cfg.keep_as == "on" or self.stream or (
+            cfg.keep_as == "auto" and free - need_h - other - need_as > margin)
         if self.keep_as and not self.stream:
             other += need_as
         # layer 0's input aggregate kept from the forward for the backward (else recomputed)
         self.agg0 = None
         need0 = L * self.d0 * 4
-        if self.nl == 3 and KEEP_AGG0 != "off" and (
-                KEEP_AGG0 == "on" or free - need_h - other - need0 > margin):
+        if self.nl == 3 and cfg.keep_agg0 != "off" and (
+                cfg.keep_agg0 == "on" or free - need_h - other - need0 > margin):
             self.agg0 = torch.empty(L, self.d0, dtype=torch.float32, device=dev)
             other += need0
         # W > 1: the output layer's projection [L, Cp] (PROJECT_FIRST), after the kept
         # aggregates (those save whole aggregation passes)
         self.pf = None
         need_pf = L * self.Cp * 4
-        if graph.send_map is not None and PROJECT_FIRST != "off" and self.Cp < self.hid and (
-                PROJECT_FIRST == "on" or free - need_h - other - need_pf > margin):
-            self.pf = torch.empty(L, self.Cp, dtype=torch.float32, device=dev)
-            other += need_pf
-            self._aggT_setup()
+        if graph.send_map is not None and cfg.project_first != "off" and self.Cp < self.hid:
+            want_pf = cfg.project_first == "on" or free - need_h - other - need_pf > margin
+            if bool(self._agree([int(want_pf)], "min")[0]):  # (changes the exchanges)
+                self.pf = torch.empty(L, self.Cp, dtype=torch.float32, device=dev)
+                other += need_pf
+                self._aggT_setup()
         # W > 1: a whole-layer aggregate buffer lets the interior part of the OUTPUT layer's
         # boundary rows run while its halo rows are in flight (hidden layers use their own
         # output buffer for that). Planned after the kept aggregates: those save whole
@@ -553,7 +579,7 @@ class FusedSAGE:
         self.use_store = self._plan_store()
         self.agg_full = None
         need_full = (L - self.Li) * wA * 4
-        if graph.send_map is not None and OVERLAP_FWD and self.Li < L and not self.stream \
+        if graph.send_map is not None and cfg.overlap and self.Li < L and not self.stream \
                 and self.use_store["out"] and free - need_h - other - need_full > margin:
             self.agg_full = torch.empty(L - self.Li, wA, dtype=torch.float32, device=dev)
             other += need_full
@@ -561,13 +587,13 @@ class FusedSAGE:
         # the first column block's transfer (the pipeline fill), when the plan has room
         self.zself = None
         need_z = L * self.Cp * 4
-        if self.stream and STREAM_OUT_FILL and self.pf is None and \
+        if self.stream and cfg.stream_out_fill and self.pf is None and \
                 free - need_h - other - need_z > margin:
             self.zself = torch.empty(L, self.Cp, dtype=torch.float32, device=dev)
             other += need_z
         spare = max(free - need_h - other, 1 << 28)
         per_row = 4 * (wA + wB)  # aggregate + logit/gradient chunk buffers
-        cr = chunk_rows or CHUNK_ROWS
+        cr = chunk_rows or cfg.chunk_rows
         if cr <= 0:
             cr = int(min(max(spare // per_row, 1 << 16), 1 << 21))
         self.cr = max(256, min(int(cr), max(L, 256)))
@@ -632,7 +658,7 @@ class FusedSAGE:
                 self.sub_hg = self.halo_buf[-1][:nh]
                 self.sub_sg = self.send_buf[:nr]
         self.send_plan = self._send_plan(graph) \
-            if (FUSED_PACK and graph.send_map is not None and not self.stream) else None
+            if (cfg.pack_fused and graph.send_map is not None and not self.stream) else None
         # the same for the pulled backward halo's rows of u (S-compacted rows)
         self._pull_send = None
         if self.send_plan is not None and self.pull is not None:
@@ -695,6 +721,24 @@ class FusedSAGE:
         self._events: list = []
         self._tune_passes()
 
+    def _agree(self, vals: List[int], op: str) -> List[int]:
+        """``vals`` reduced elementwise (``"max"`` / ``"min"``) over the plan's group, so
+        every rank takes the same branch; local values without peers (W=1, a rehearsal's
+        loopback plan)."""
+        import torch.distributed as dist
+
+        g = self.g
+        group = g.a2a.group if g.send_map is not None else None
+        if not dist.is_initialized() or g.send_map is None or \
+                dist.get_world_size(group) <= 1:
+            return [int(v) for v in vals]
+        from ..comm.groups import comm_device
+
+        t = torch.tensor([int(v) for v in vals], dtype=torch.long, device=comm_device(group))
+        dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.MIN,
+                        group=group)
+        return [int(v) for v in t.tolist()]
+
     def _aggT_setup(self) -> None:
         """Project-first output layer: the loss rows' aggregate of the last hidden layer
         (the operand of the W_neigh weight gradient) from a small CSR of the loss rows whose
@@ -723,7 +767,8 @@ class FusedSAGE:
                                            dtype=torch.float32, device=dev),
                                torch.empty(nz.numel(), self.hid, dtype=torch.float32,
                                            device=dev))
-        if bool((col < 0).any()):
+        bad = bool((col < 0).any())
+        if bool(self._agree([int(bad)], "max")[0]):  # raised by every rank, or by none
             raise RuntimeError("FusedSAGE: a loss row neighbours a halo row outside the "
                                "output-layer sub-plan")
         self.aggT_rp, self.aggT_col = rp, col.to(torch.int32).contiguous()
@@ -767,8 +812,10 @@ class FusedSAGE:
         stream events; the largest per-peer message over the slowest rank's time. The
         boundary-store planner (``_plan_store``) then weighs the exposed exchange against the
         transport this job actually gets (RCCL over xGMI on the node, the link model in a
-        rehearsal) instead of the links' peak. ``DGRAPH_PLAN_LINK_GBPS`` set: that value."""
-        if "DGRAPH_PLAN_LINK_GBPS" in os.environ or self.dev.type != "cuda":
+        rehearsal) instead of the links' peak. ``cfg.plan_link_gbps`` > 0 (DGRAPH_PLAN_LINK_GBPS): that value."""
+        if self.cfg.plan_link_gbps > 0:
+            return self.cfg.plan_link_gbps
+        if self.dev.type != "cuda":
             return PLAN_LINK_GBPS
         import torch.distributed as dist
 
@@ -901,7 +948,7 @@ class FusedSAGE:
         column-mapped F=256 at 30 % of rows 48.9 -> 30.2 ms (64- vs 256-column passes),
         the W=1 step 1959 -> 1867 ms. Over an S-compacted adjacency (``TS``/``HTS``, no map
         to walk) the tuned narrow passes stay faster (W=8 265.6 vs 271.1 ms)."""
-        forced = int(os.environ.get("DGRAPH_FUSED_PASS_COLS", "0"))
+        forced = self.cfg.pass_cols
         w = u.shape[1]
         if forced:
             pc = min(forced, w)
@@ -910,7 +957,7 @@ class FusedSAGE:
             # (support ~ most rows) full-width passes lose (bwd_l0 21.3 vs 17.0 ms)
             base = self.pass_for.get(w, 0)
             frac = self.nS / max(self.L, 1)
-            pc = min(w, 256) if (not base or base >= w or frac <= U_FULL_FRAC) else base
+            pc = min(w, 256) if (not base or base >= w or frac <= self.cfg.u_full_frac) else base
         kw.setdefault("pass_cols", pc)
         return F32.spmm_f32(rowptr, col, u, out, **kw)
 
@@ -937,7 +984,7 @@ class FusedSAGE:
         interior-first carries it as ``locality_hint``). DGRAPH_FUSED_PASS_COLS forces a
         width."""
         self.pass_for = {}
-        forced = int(os.environ.get("DGRAPH_FUSED_PASS_COLS", "0"))
+        forced = self.cfg.pass_cols
         if forced:
             self.pass_for = {self.d0: min(forced, self.d0), self.hid: min(forced, self.hid)}
             return
@@ -998,7 +1045,7 @@ class FusedSAGE:
         # send rows) overlaps the next layer's interior work instead of preceding it. It
         # reads h (complete: the stream waits for the compute stream) and writes the send
         # buffer, whose previous exchange the compute stream has already waited for
-        if PACK_STREAM == "compute":
+        if self.cfg.pack_stream == "compute":
             K.copy_rows(h, src_idx=g.send_map.idx, out=self.send_buf)
             return self._on_comm_stream(
                 lambda: g.a2a(self.send_buf, out=self.halo_buf[l], async_op=True))
@@ -1020,8 +1067,9 @@ class FusedSAGE:
         and its output-layer buffer displaced the kept input aggregate (a 973 ms rank step
         without, 1022 ms with, profiles/r05/)."""
         g = self.g
-        if BOUNDARY_STORE in ("on", "off") or g.send_map is None or self.Li >= self.L:
-            return {k: BOUNDARY_STORE == "on" for k in ("hidden", "out")}
+        mode = self.cfg.boundary_store
+        if mode in ("on", "off") or g.send_map is None or self.Li >= self.L:
+            return {k: mode == "on" for k in ("hidden", "out")}
         a2a = g.a2a
         peer_rows = max(max(a2a.send_splits, default=0), max(a2a.recv_splits, default=0))
         t_x = peer_rows * self.hid * 4 / (self.link_gbps * 1e9)
@@ -1061,7 +1109,7 @@ class FusedSAGE:
         recv, work = halo
         seg_a = [ci for ci in items if ci < self.nA]
         seg_b = [ci for ci in items if ci >= self.nA]
-        if not OVERLAP_FWD:
+        if not self.cfg.overlap:
             self._mark(f"exchange_{name}")
             work.wait()
             self._mark(name)
@@ -1108,7 +1156,7 @@ class FusedSAGE:
         """Column blocks of a streamed exchange of width ``F``: ``cw`` wide, the first one
         ``cw / 2`` (STREAM_RAMP) so the pipeline fill is short."""
         cw = self.cw
-        if STREAM_RAMP and cw >= 64 and F > cw:
+        if self.cfg.stream_ramp and cw >= 64 and F > cw:
             return [(0, cw // 2)] + _ranges(cw // 2, F, cw)
         return _ranges(0, F, cw)
 
@@ -1135,7 +1183,7 @@ class FusedSAGE:
             snd = self._ring(self.ring_send, b, c1 - c0)
             rcv = self._ring(self.ring_recv, b, c1 - c0)
 
-            if PACK_STREAM == "compute":
+            if self.cfg.pack_stream == "compute":
                 K.copy_rows(h[:, c0:c1], src_idx=g.send_map.idx, out=snd)
                 return self._on_comm_stream(lambda: g.a2a(snd, out=rcv, async_op=True))
 
@@ -1290,7 +1338,7 @@ class FusedSAGE:
                 self._gemm(hin[r0:r1], ws, a, wn, bias=bias, relu=True, out=hout[r0:r1],
                            send=self._send_arg(r0, r1, hout.shape[1]) if sends else None)
 
-            if self.stream and l > 0 and not STREAM_FILL:
+            if self.stream and l > 0 and not self.cfg.stream_fill:
                 self._stream_fwd(hin, hout, f"fwd_l{l}")
                 for ci, (r0, r1) in enumerate(self.chunks):
                     if r1 > r0:

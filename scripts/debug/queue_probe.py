@@ -9,7 +9,8 @@ import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
-os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("PROBE_HWQ", "8")
+if os.environ.get("PROBE_HWQ"):  # opt-in A/B of the queue budget (1..4 on the boxes)
+    os.environ["GPU_MAX_HW_QUEUES"] = str(min(max(int(os.environ["PROBE_HWQ"]), 1), 4))
 
 import torch  # noqa: E402
 

@@ -44,7 +44,18 @@ def _worker(rank, world_size, port, fn, args, q, backend="gloo"):
 
         # W ranks share the container's CPUs: one intra-op pool each, sized to fit
         torch.set_num_threads(max(1, (os.cpu_count() or 8) // max(world_size, 1)))
-        if backend == "rccl-one-gpu":
+        if backend in ("rccl", "gloo-multi-gpu"):
+            # one rank per GPU (the reference's torchrun layout, tests/README.md:1-17):
+            # rank r on cuda:r, RCCL over P2P/xGMI ("rccl") or gloo for the small
+            # collectives with the data on distinct devices ("gloo-multi-gpu": the IPC heap)
+            os.environ.update(DGRAPH_TEST_DEV=str(rank))
+            torch.cuda.set_device(rank)
+            if backend == "rccl":
+                dist.init_process_group("nccl", rank=rank, world_size=world_size,
+                                        device_id=torch.device("cuda", rank))
+            else:
+                dist.init_process_group("gloo", rank=rank, world_size=world_size)
+        elif backend == "rccl-one-gpu":
             # real RCCL with every rank on GPU 0: RCCL refuses two ranks of one host on one
             # device ("Duplicate GPU"), so each rank names its own host and the ranks
             # connect over RCCL's socket transport on loopback (host-staged: a correctness
@@ -67,8 +78,10 @@ def _worker(rank, world_size, port, fn, args, q, backend="gloo"):
 
 def run_ranks(fn, world_size: int, *args, timeout: float = 240.0, backend: str = "gloo"):
     """Run ``fn(rank, world_size, *args)`` in ``world_size`` processes over a ``backend``
-    process group (``"gloo"``, or ``"rccl-one-gpu"``: RCCL with every rank on GPU 0); re-raise
-    the first failure with its traceback."""
+    process group (``"gloo"``; ``"rccl-one-gpu"``: RCCL with every rank on GPU 0; ``"rccl"``:
+    RCCL with rank r on GPU r; ``"gloo-multi-gpu"``: gloo with rank r on GPU r); re-raise
+    the first failure with its traceback. Test bodies take their device from
+    :func:`rank_device`."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -100,3 +113,26 @@ def ranks():
 
 def gpu_available() -> bool:
     return torch.cuda.is_available()
+
+
+def rank_device() -> torch.device:
+    """The GPU of this test rank: cuda:r under the one-rank-per-GPU backends, else cuda:0
+    (ranks sharing the one-GPU box). Also makes it the current device."""
+    dev = torch.device("cuda", int(os.environ.get("DGRAPH_TEST_DEV", "0")))
+    torch.cuda.set_device(dev)
+    return dev
+
+
+def gpu_count() -> int:
+    """Visible GPUs, without initialising the HIP runtime in the pytest process."""
+    try:
+        return torch.cuda.device_count()
+    except Exception:  # noqa: BLE001
+        return 0
+
+
+def needs_gpus(n: int):
+    """Skip (not fail) a test that maps its ranks to ``n`` distinct GPUs on a box with
+    fewer (the 1-GPU box); an 8-GPU node runs it."""
+    return pytest.mark.skipif(gpu_count() < n, reason=f"needs {n} GPUs (one rank per GPU), "
+                                                      f"{gpu_count()} visible")

@@ -31,6 +31,34 @@ def test_bench_cli_w2_spawns_ranks_and_reports_regions(tmp_path):
     assert len(r["bytes_sent_per_rank"]) == 2 and min(r["bytes_sent_per_rank"]) > 0
     assert any(k.startswith("exchange") for k in r["ms_max_over_ranks"])
     assert "structureless" in d  # measured or explicitly skipped, never a crash
+    # the one-sided probe ran as a separate child job over the headline's plan (gloo here:
+    # the torch exchange only, the heap needs device memory)
+    sp = d["shmem_probe"]
+    assert "failed" not in sp, sp
+    assert sp["world"] == 2 and sp["torch_pg"]["exchange_ms_max"] > 0
+    assert sp["rows_sent_max"] > 0 and sp["shmem"].startswith("unavailable")
+    # the resolved configuration, whole
+    assert d["run_config"]["fused"]["halo_stream"] in ("auto", "on", "off")
+    assert d["run_config"]["model"]["dtype"] == "fp32"
+
+
+def test_bench_cli_shmem_probe_failure_keeps_headline(tmp_path):
+    """A probe child that dies (rank 1 aborts, as after a GPU fault) costs the probe only:
+    the headline JSON line is printed with ``shmem_probe.failed`` naming the rank."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["DGRAPH_SHMEM_PROBE_FAULT"] = "abort1"
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--scale", "2e-5",
+           "--steps", "1", "--warmup", "1", "--window", "64", "--no-extra",
+           "--shmem-probe-timeout", "90"]
+    p = subprocess.run(cmd, cwd=tmp_path, env=env, capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["value"] > 0 and d["n_gpus"] == 2
+    failed = d["shmem_probe"]["failed"]
+    assert any(f["rank"] == 1 and f["exit"] not in (0, None) for f in failed), failed
 
 
 def test_bench_cli_refuses_mismatched_world(tmp_path):

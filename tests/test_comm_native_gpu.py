@@ -9,19 +9,20 @@ on one device, so the executor is tested at world size 1 (self send/recv).
 import pytest
 import torch
 
-from conftest import run_ranks
+from conftest import rank_device, run_ranks
 
 pytestmark = pytest.mark.gpu
 
 
-def _heap_body(rank, world):
+def _heap_body(rank, world, expect_mode=None):
     import torch.distributed as dist
 
     from dgraph_amd.comm.symheap import NVSHMEMP2P, SymmetricHeap
 
-    torch.cuda.set_device(0)
-    dev = torch.device("cuda", 0)
+    dev = rank_device()
     heap = SymmetricHeap(1 << 22, group=None, device=dev)
+    if expect_mode is not None:  # distinct GPUs: device-side completion (no host sync)
+        assert heap.device_completion == (expect_mode == "device"), expect_mode
     assert len(heap.peer_ptrs) == world and heap.owns(heap.local)
     # ---- remote gather: per-rank row counts differ (symmetric slot sized to the max)
     F = 40
@@ -204,8 +205,7 @@ def _engine_no_leak_body(rank, world):
 
     from dgraph_amd.comm.shmem_engine import ROCSHMEMBackendEngine
 
-    torch.cuda.set_device(0)
-    dev = torch.device("cuda", 0)
+    dev = rank_device()
     eng = ROCSHMEMBackendEngine()
     h = eng.heap()
     assert h is not None

@@ -59,10 +59,9 @@ def _rehearsal_step(gbps, steps=2, stream="off"):
     from dgraph_amd.parallel.dist_graph import DistGraph
     from dgraph_amd.parallel.reorder import interior_first
 
-    import dgraph_amd.models.sage_fused as sf
+    from dgraph_amd.utils.config import ExecutorConfig
 
     A.LOOPBACK_LINK_GBPS = gbps
-    sf.HALO_STREAM = stream
     try:
         shape = SHAPES["ogbn-papers100M"].scaled(2e-4)
         part = build_partition(shape, 0, 2, DEV, global_frac=0.05, window=256, rehearse=True)
@@ -80,7 +79,8 @@ def _rehearsal_step(gbps, steps=2, stream="off"):
         torch.manual_seed(0)
         model = GraphSAGE(shape.num_features, 256, shape.num_classes, 3).to(DEV)
         ex = FusedSAGE(model, g, x, tr, y[tr], ev, y[ev], split[ev] == SPLIT_VALID,
-                       tr.numel(), chunk_rows=512, release_graph=True)
+                       tr.numel(), chunk_rows=512, release_graph=True,
+                       config=ExecutorConfig(halo_stream=stream))
         assert ex.nA >= 1 and ex.stream == (stream == "on")
         losses = []
         for _ in range(steps):
@@ -95,7 +95,6 @@ def _rehearsal_step(gbps, steps=2, stream="off"):
         return torch.stack(losses), grads, ex.correct.clone(), reg
     finally:
         A.LOOPBACK_LINK_GBPS = 0.0
-        sf.HALO_STREAM = "auto"
 
 
 @pytest.mark.parametrize("stream", ["off", "on"])

@@ -21,7 +21,7 @@ import pytest
 import torch
 import torch.distributed as dist
 
-from conftest import run_ranks
+from conftest import rank_device, run_ranks
 
 pytestmark = pytest.mark.gpu
 
@@ -41,7 +41,7 @@ def _run(rank, world, args, dtype, steps=3):
 
     comm = types.SimpleNamespace(get_rank=lambda: rank, get_world_size=lambda: world,
                                  group=None)
-    dev = torch.device("cuda", 0)
+    dev = rank_device()
     job = bench.Job(args, comm, dev, args.global_frac, dtype)
     if args.halo_recompute == "on" and world > 1:
         assert job.recompute, "halo recomputation was not enabled"
@@ -76,7 +76,7 @@ def _run(rank, world, args, dtype, steps=3):
 
 
 def _body(rank, world, kw, dt):
-    torch.cuda.set_device(0)
+    rank_device()
     dtype = torch.float32 if dt == "fp32" else torch.bfloat16
     args = _args(dtype=dt, **{k: v for k, v in kw.items() if k != "stream_fill"})
     ref = _run(0, 1, args, dtype) if rank == 0 else None
@@ -164,8 +164,8 @@ def test_alltoallv_shmem_processes(monkeypatch, world):
     run_ranks(_a2a_body, world, timeout=120)
 
 
-def _a2a_body(rank, world):
-    torch.cuda.set_device(0)
+def _a2a_body(rank, world, expect_mode=None):
+    dev = rank_device()
     from dgraph_amd.comm.alltoallv import AllToAllV, close_shmem_heaps, shmem_heap
 
     g = torch.Generator().manual_seed(7)
@@ -183,7 +183,7 @@ def _a2a_body(rank, world):
                     torch.arange(F, dtype=torch.float32) * 0
                 v[:, 0] = j
                 rows.append(v)
-            send = torch.cat(rows).to(dt).cuda()
+            send = torch.cat(rows).to(dt).to(dev)
             out = a2a(send)
             torch.cuda.synchronize()
             off = 0
@@ -193,7 +193,11 @@ def _a2a_body(rank, world):
                 exp[:, 0] = torch.arange(recv_s[q], dtype=torch.float32)
                 assert torch.equal(blk, exp.to(dt).float()), (rank, q, it, F)
                 off += recv_s[q]
-    used = shmem_heap(None, torch.device("cuda", 0))._cursor
+    heap = shmem_heap(None, dev)
+    if expect_mode is not None:
+        assert heap.device_completion == (expect_mode == "device"), expect_mode
+        heap.check()
+    used = heap._cursor
     close_shmem_heaps()
     assert used < (64 << 20)
 
@@ -221,11 +225,11 @@ def test_bench_step_hidden512_two_processes(monkeypatch, env):
 def _probe_body(rank, world):
     import bench
 
-    torch.cuda.set_device(0)
+    dev = rank_device()
     args = _args(dtype="fp32", global_frac=0.05)
     comm = types.SimpleNamespace(get_rank=lambda: rank, get_world_size=lambda: world,
                                  group=None)
-    job = bench.Job(args, comm, torch.device("cuda", 0), args.global_frac, torch.float32)
+    job = bench.Job(args, comm, dev, args.global_frac, torch.float32)
     job.step(False)
     rec = bench.link_probe(job, width=64, iters=3)
     from dgraph_amd.comm.alltoallv import close_shmem_heaps

@@ -15,7 +15,7 @@ tests/test_NCCLCommPlan.py (W>1 against replicated ground truth).
 import pytest
 import torch
 
-from conftest import run_ranks
+from conftest import rank_device, run_ranks
 
 pytestmark = pytest.mark.gpu
 
@@ -32,7 +32,7 @@ def _a2a_body(rank, world):
     send_s = [int(v) for v in splits[rank]]
     recv_s = [int(splits[q][rank]) for q in range(world)]
     a2a = A.AllToAllV(send_s, recv_s)
-    dev = torch.device("cuda", 0)
+    dev = rank_device()
     for it in range(2):
         for F, dt in ((64, torch.float32), (200, torch.bfloat16)):
             send = torch.cat([torch.full((n, F), float(rank * 1000 + p * 100 + it))
@@ -96,7 +96,7 @@ def _probe_body(rank, world):
     args = T._args(dtype="fp32", global_frac=0.05)
     comm = types.SimpleNamespace(get_rank=lambda: rank, get_world_size=lambda: world,
                                  group=None)
-    job = bench.Job(args, comm, torch.device("cuda", 0), args.global_frac, torch.float32)
+    job = bench.Job(args, comm, rank_device(), args.global_frac, torch.float32)
     job.step(False)
     rec = bench.link_probe(job, width=64, iters=2)
     job.free()

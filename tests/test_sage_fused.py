@@ -41,25 +41,22 @@ def _setup(rank, world, dev="cpu", layers=3, chunk_rows=300, gf=0.3, name="ogbn-
 
 
 def _fused_grads(rank, world, layers=3, chunk_rows=300, name="ogbn-papers100M",
-                 schedule="full", dev="cpu", gf=0.3, hidden=256):
+                 schedule="full", dev="cpu", gf=0.3, hidden=256, **knobs):
     """schedule (W > 1): "full" = forward exchanges overlapped through the whole-layer
     aggregate buffer (output layer) and in place (hidden layers); "inplace" = no whole-layer
     buffer (hidden layers in place, the output layer's exchange waited for up front);
     "off" = every exchange waited for up front."""
-    import dgraph_amd.models.sage_fused as sf
+    from dgraph_amd.utils.config import ExecutorConfig
 
     shape, g, x, y, split, tr, ev, n_tr, model = _setup(rank, world, dev=dev, layers=layers,
                                                         name=name, gf=gf, hidden=hidden)
-    sf.OVERLAP_FWD = schedule != "off"
-    try:
-        ex = FusedSAGE(model, g, x, tr, y[tr], ev, y[ev], split[ev] == SPLIT_VALID, n_tr,
-                       chunk_rows=chunk_rows)
-        if schedule == "inplace":
-            ex.agg_full = None
-        if world > 1:
-            assert (ex.agg_full is not None) == (schedule == "full")
-    finally:
-        sf.OVERLAP_FWD = True
+    cfg = ExecutorConfig(overlap=schedule != "off", **knobs)
+    ex = FusedSAGE(model, g, x, tr, y[tr], ev, y[ev], split[ev] == SPLIT_VALID, n_tr,
+                   chunk_rows=chunk_rows, config=cfg)
+    if schedule == "inplace":
+        ex.agg_full = None
+    if world > 1:
+        assert (ex.agg_full is not None) == (schedule == "full")
     loss = ex.step()
     grads = [p.grad.clone() for p in model.parameters()]
     return loss, grads, ex.correct.clone()
@@ -69,16 +66,10 @@ def _fused_grads(rank, world, layers=3, chunk_rows=300, name="ogbn-papers100M",
 def test_compact_transposed_adjacency_matches_column_map(ranks, world, tmp_path):
     """The input-layer backward over the S-compacted transposed adjacency (COMPACT_T) and
     over the column-mapped full adjacency give the same step."""
-    import dgraph_amd.models.sage_fused as sf
-
     if world == 1:
         res = {}
         for mode in ("on", "off"):
-            sf.COMPACT_T = mode
-            try:
-                res[mode] = _fused_grads(0, 1)
-            finally:
-                sf.COMPACT_T = "auto"
+            res[mode] = _fused_grads(0, 1, compact_t=mode)
         (l1, g1, c1), (l2, g2, c2) = res["on"], res["off"]
         torch.testing.assert_close(l1, l2)
         for a, b in zip(g1, g2):
@@ -91,16 +82,12 @@ def test_compact_transposed_adjacency_matches_column_map(ranks, world, tmp_path)
 def _compact_body(rank, world, path):
     import torch.distributed as dist
 
-    import dgraph_amd.models.sage_fused as sf
-
     out = {}
     for mode in ("on", "off"):
-        sf.COMPACT_T = mode
-        loss, grads, corr = _fused_grads(rank, world, schedule="off")
+        loss, grads, corr = _fused_grads(rank, world, schedule="off", compact_t=mode)
         for t in grads:
             dist.all_reduce(t)
         out[mode] = (loss, grads)
-    sf.COMPACT_T = "auto"
     for a, b in zip(out["on"][1], out["off"][1]):
         torch.testing.assert_close(a, b, atol=1e-6, rtol=1e-5)
 
@@ -128,9 +115,6 @@ def test_fused_matches_stack_w1(layers, name):
 
 
 def _dist_body(rank, world, ref_path, schedule="full"):
-    import dgraph_amd.models.sage_fused as sf
-
-    sf.OVERLAP_FWD = schedule != "off"
     loss, grads, corr = _fused_grads(rank, world, schedule=schedule)
     for t in grads:
         dist.all_reduce(t)
@@ -201,20 +185,17 @@ def _interior_first_body(rank, world, ref_path, overlap, store="auto", stream="o
                          keep_as="auto", hidden=256, bwd_halo="pull", pf="auto"):
     """One rank of a W-way partition renumbered interior-first (parallel/reorder.py), the
     fused executor's interior-then-boundary schedule, all-reduced against W=1."""
-    import dgraph_amd.models.sage_fused as sf
     from dgraph_amd.parallel.reorder import interior_first
+    from dgraph_amd.utils.config import ExecutorConfig
 
-    sf.OVERLAP_FWD = overlap
-    sf.BOUNDARY_STORE = store
-    sf.KEEP_AS = keep_as
-    sf.BWD_HALO = bwd_halo
-    sf.PROJECT_FIRST = pf
-    sf.HALO_STREAM = "on" if stream != "off" else "off"
+    cfg = ExecutorConfig(overlap=overlap, boundary_store=store, keep_as=keep_as,
+                         bwd_halo=bwd_halo, project_first=pf,
+                         halo_stream="on" if stream != "off" else "off")
     if stream == "single":  # one ring buffer: exchange and aggregation alternate
-        sf.STREAM_SHAPES = ((64, 1),)
+        cfg.stream_shapes = "64x1"
     if stream == "ramp":  # half-width first block, output-layer self term as the fill
-        sf.STREAM_RAMP = sf.STREAM_OUT_FILL = True
-        sf.PROJECT_FIRST = "off"  # (the self-term fill is the aggregate-first output layer's)
+        cfg.stream_ramp = cfg.stream_out_fill = True
+        cfg.project_first = "off"  # (the self-term fill is the aggregate-first output layer's)
     if stream != "off":  # the input's static halo exchanged in 16-column blocks too
         DistGraph.STATIC_BLOCK_BYTES = 1024
     shape = SHAPES["ogbn-papers100M"].scaled(SCALE)
@@ -234,7 +215,7 @@ def _interior_first_body(rank, world, ref_path, overlap, store="auto", stream="o
     torch.manual_seed(0)
     model = GraphSAGE(shape.num_features, hidden, shape.num_classes, 3)
     ex = FusedSAGE(model, g, x, tr, y[tr], ev, y[ev], split[ev] == SPLIT_VALID, int(n_tr),
-                   chunk_rows=300, release_graph=True)
+                   chunk_rows=300, release_graph=True, config=cfg)
     assert ex.Li == L_int and ex.nA >= 1
     assert (ex.aS_keep is not None) == (keep_as != "off" or stream != "off")
     if store != "auto":
@@ -359,3 +340,34 @@ def test_fused_widths_match_stack(hidden, feat):
     torch.testing.assert_close(res[1][0], res[0][0], atol=1e-5, rtol=1e-5)
     for a, b in zip(res[1][1], res[0][1]):
         torch.testing.assert_close(a, b, atol=2e-5, rtol=1e-4)
+
+
+def test_executor_config_resolved_at_construction(monkeypatch):
+    """The schedule knobs are read when an executor is BUILT (they were module
+    globals frozen at import): an environment change after import changes the next
+    executor's schedule, and an explicit config wins over the environment."""
+    from dgraph_amd.utils.config import ExecutorConfig, RunConfig
+
+    shape, g, x, y, split, tr, ev, n_tr, model = _setup(0, 1)
+
+    def build(**kw):
+        return FusedSAGE(model, g, x, tr, y[tr], ev, y[ev], split[ev] == SPLIT_VALID, n_tr,
+                         chunk_rows=300, **kw)
+
+    monkeypatch.setenv("DGRAPH_FUSED_KEEP_AGG0", "off")
+    a = build()
+    assert a.cfg.keep_agg0 == "off" and a.schedule["keep_agg0"] is False
+    monkeypatch.setenv("DGRAPH_FUSED_KEEP_AGG0", "on")
+    b = build()
+    assert b.schedule["keep_agg0"] is True
+    c = build(config=ExecutorConfig(keep_agg0="off"))
+    assert c.schedule["keep_agg0"] is False
+    # the same knobs through the run config (bench.py records cfg.to_dict() whole)
+    monkeypatch.setenv("DGRAPH_FUSED_HALO_STREAM", "on")
+    monkeypatch.setenv("DGRAPH_PLAN_LINK_GBPS", "75")
+    rc = RunConfig.from_env()
+    assert rc.fused.halo_stream == "on" and rc.fused.plan_link_gbps == 75.0
+    assert rc.to_dict()["fused"]["keep_agg0"] == "on"
+    assert rc.model.dtype == "fp32"
+    with pytest.raises(ValueError):
+        ExecutorConfig(halo_stream="sometimes")
