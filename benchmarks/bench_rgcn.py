@@ -66,6 +66,11 @@ def parse(argv=None):
                          "largest per-peer message / GBPS (comm/alltoallv.py); the step-time "
                          "difference to --link-gbps 0 is the exchange time the schedule "
                          "exposes")
+    ap.add_argument("--model", choices=("rgcn", "rgat"), default="rgcn",
+                    help="rgat: the reference's OGB-LSC model (experiments/OGB-LSC/RGAT.py) on "
+                         "its lean fp32 path (fused relation attention, ops/gat.py)")
+    ap.add_argument("--heads", type=int, default=4,
+                    help="RGAT attention heads (the reference config's 4)")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args(argv)
 
@@ -150,17 +155,27 @@ def main(argv=None):
               f"messages/step={E_step} halo_rows={halo_total} train={n_train}")
 
     torch.manual_seed(args.seed)
-    model = CommAwareRGCN(shape.num_features, args.hidden, shape.num_classes, len(EDGE_TYPES),
-                          args.layers, dropout=args.dropout, comm=comm,
-                          bn_group=comm.group).to(dev)
-    if args.path != "auto":
-        model.lean = args.path == "lean"
+    if args.model == "rgat":
+        from dgraph_amd.models.rgat import CommAwareRGAT
+
+        if dtype != torch.float32:
+            raise SystemExit("[bench_rgcn] --model rgat runs the lean fp32 path only")
+        model = CommAwareRGAT(shape.num_features, shape.num_classes, args.hidden,
+                              len(EDGE_TYPES), args.layers, args.heads, comm=comm,
+                              dropout=args.dropout, bn_group=comm.group).to(dev)
+    else:
+        model = CommAwareRGCN(shape.num_features, args.hidden, shape.num_classes,
+                              len(EDGE_TYPES), args.layers, dropout=args.dropout, comm=comm,
+                              bn_group=comm.group).to(dev)
+        if args.path != "auto":
+            model.lean = args.path == "lean"
     opt = torch.optim.Adam(model.parameters(), lr=args.lr, fused=dev.type == "cuda")
     sync = GradSync(model.parameters(), group=comm.group) if world > 1 else None
     inv_n = 1.0 / max(n_train, 1)
     use_amp = dev.type == "cuda" and dtype == torch.bfloat16
 
-    lean = model.lean if model.lean is not None else (dtype == torch.float32)
+    lean = True if args.model == "rgat" else (
+        model.lean if model.lean is not None else (dtype == torch.float32))
 
     def step():
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=use_amp):
@@ -217,19 +232,23 @@ def main(argv=None):
         "data": (f"synthetic {shape.name}-shaped hetero graph (nodes={list(shape.num_nodes)}, "
                  f"global_frac={args.global_frac}, window={args.window}), random features/"
                  f"labels, random-init weights"),
-        "config": {"model": f"R-GCN {args.layers}-layer hidden {args.hidden}",
+        "config": {"model": (f"RGAT {args.layers}-layer hidden {args.hidden} heads "
+                             f"{args.heads}" if args.model == "rgat" else
+                             f"R-GCN {args.layers}-layer hidden {args.hidden}"),
                    "backend": args.backend, "messages_per_step": E_step,
                    "halo_rows_total": halo_total, "train_papers": n_train,
                    "parallelism": f"graph-partition{p_world}" + (" (rehearsal)" if rehearse
                                                                   else "")},
         "final_loss": float(lt.item()), "peak_mem_gb_rank0": round(peak, 2),
         "path": "lean" if lean else "aggregate-first",
-        "layer0_halo": ("kept" if (not lean or model._keep_static_halo(feats, graph))
+        "layer0_halo": ("kept" if (args.model == "rgat" or not lean or
+                                   model._keep_static_halo(feats, graph))
                         else "exchanged per step"),
         "allocator_in_timed_steps": alloc_timed,
     }
     if rehearse:
-        rec = {"rehearsal": True, "rank": p_rank, "world": p_world,
+        rec = {"rehearsal": True, "model": rec["config"]["model"], "rank": p_rank,
+               "world": p_world,
                "ms_per_step_compute_loopback": ms_step, "messages_local": E_step,
                "halo_rows": halo_total, "peak_mem_gb": round(peak, 2),
                "final_loss_local": float(lt.item()), "path": rec["path"],

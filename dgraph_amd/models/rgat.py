@@ -21,16 +21,29 @@ index-based (G1 COO) forwards are kept for API parity.
 
 ``CommAwareRGAT`` runs ALL relations of every layer (the reference broke out after the
 first relation, RGAT.py:357-358; ``relations="first"`` restores that behaviour).
+
+Lean fp32 path (``CommAwareRGAT.forward(xs, HeteroGraph)``, :meth:`CommAwareRGAT.
+_forward_hetero_lean`): the R-GCN treatment (models/rgcn.py) — transform-first with the
+exact-f32 MFMA linears, ONE :func:`~dgraph_amd.ops.act_linear.act_linears` call per source
+type builds ``act(BN(pre))`` transiently and runs every GEMM that reads it (the skip and
+all residual transforms of its destination relations folded into ONE weight, each
+relation's ``W_r``, and each relation's destination-score projection
+``V_r = a_dst W_r`` so ``h_i`` is never formed); each relation's attention is the fused
+kernel of ``ops/gat.py`` added in place into its destination's pre-activation, with its halo
+rows exchanged by one all-to-all-v (layer 0: the kept halo feature rows are transformed
+locally, no exchange) and read as a second source (no ``torch.cat``); BN / ReLU / dropout are
+recomputed in backward instead of stored.
 """
 from __future__ import annotations
 
-from typing import List, Optional
+from typing import Dict, List, Optional
 
 import torch
 import torch.distributed as dist
 import torch.nn as nn
 
 from ..ops.aggregate import aggregate, edge_softmax
+from ..ops.act_linear import act_linears
 from ..ops.edge_mlp import edge_pre_activation
 from .norm import DistributedBatchNorm1D
 
@@ -205,7 +218,13 @@ class CommAwareRGAT(nn.Module):
             nn.Linear(hidden_channels, out_channels),
         )
 
-    def forward(self, xs: List[torch.Tensor], edge_types, graphs) -> torch.Tensor:
+    def forward(self, xs, edge_types, graphs=None) -> torch.Tensor:
+        """``forward(xs, edge_types, graphs)`` over per-relation RelationGraphs (API of the
+        reference), or ``forward(xs, HeteroGraph)`` — the lean fp32 path."""
+        from .rgcn import HeteroGraph
+
+        if isinstance(edge_types, HeteroGraph):
+            return self._forward_hetero_lean(xs, edge_types)
         assert len(edge_types) == len(graphs)
         outs = list(xs)
         for i in range(self.num_layers):
@@ -220,3 +239,111 @@ class CommAwareRGAT(nn.Module):
                 t = torch.relu(self.bn_layers[i](t))
                 outs.append(nn.functional.dropout(t, self.dropout, self.training))
         return self.mlp(outs[0])
+
+    # ------------------------------------------------------------------ lean fp32 path
+    @staticmethod
+    def _att_vectors(conv: CommAwareGAT):
+        """(a_dst, a_src) as [heads, D] (per-head blocks of ``project_message``)."""
+        H, C = conv.heads, conv.out_channels
+        D = C // H
+        W = conv.project_message.weight
+        a_dst = torch.stack([W[k, k * D:(k + 1) * D] for k in range(H)])
+        a_src = torch.stack([W[k, C + k * D:C + (k + 1) * D] for k in range(H)])
+        return a_dst, a_src
+
+    def _patterns(self, g) -> Dict[int, "object"]:
+        from ..ops.gat import GatPattern
+
+        pats = g.extra.get("gat_patterns")
+        if pats is None:
+            pats = {}
+            for s, sg in g.sources.items():
+                for rid in sg.ranges:
+                    pats[rid] = GatPattern.merged(sg.part("interior", rid),
+                                                  sg.part("halo", rid) if sg.halo is not None
+                                                  else None, sg.Ls)
+            g.extra["gat_patterns"] = pats
+        return pats
+
+    def _forward_hetero_lean(self, xs: Dict[int, torch.Tensor], g) -> torch.Tensor:
+        """Transform-first at every layer, activations recomputed in backward:
+
+            pre_t^l = x W_t'^T + b_t' + sum_{r: s->t} att_r(z_r = h_s W_r^T, sd_r = h_t V_r^T)
+
+        with ``W_t' = skip_l + sum_{r->t} res_net_r`` and ``b_t' = skip bias + sum_{r->t}
+        bias_r`` (one GEMM instead of 1 + |relations into t|: the skip and residual
+        transforms read the same input), ``V_r[k] = a_dst[k] W_r[head k rows]`` and ``att_r``
+        the fused relation attention (ops/gat.py) added in place into ``pre_t``."""
+        from ..ops.gat import gat_relation_into
+        from .rgcn import layer_plan
+
+        ets = g.edge_types
+        avail = [r for s in g.sources.values() for r in s.ranges]
+        need, rels = layer_plan(ets, self.num_layers, 0, avail)
+        pats = self._patterns(g)
+        pre: Dict[int, torch.Tensor] = {}
+        for l in range(self.num_layers):
+            convs = self.layers[l]
+            by_src: Dict[int, List[int]] = {}
+            by_dst: Dict[int, List[int]] = {}
+            for r in rels[l]:
+                by_src.setdefault(ets[r][0], []).append(r)
+                by_dst.setdefault(ets[r][1], []).append(r)
+            new: Dict[int, torch.Tensor] = {}
+            sds: Dict[int, torch.Tensor] = {}
+            work = []
+            for s in sorted(set(need[l]) | set(by_src)):
+                rs_src = by_src.get(s, [])
+                rs_dst = by_dst.get(s, []) if s in need[l] else []
+                skip = s in need[l]
+                Ws, bias = [], None
+                if skip:
+                    W = self.skip_layers[l].weight
+                    b = self.skip_layers[l].bias
+                    for r in rs_dst:
+                        W = W + convs[r].res_net.weight
+                        if convs[r].bias is not None:
+                            b = b + convs[r].bias
+                    Ws.append(W)
+                    bias = b
+                Ws += [convs[r].conv1.weight for r in rs_src]
+                vs = []
+                for r in rs_dst:
+                    c = convs[r]
+                    a_dst, _ = self._att_vectors(c)
+                    Hh, D = a_dst.shape
+                    vs.append(torch.einsum("kd,kdc->kc", a_dst,
+                                           c.conv1.weight.view(Hh, D, -1)))
+                Ws += vs
+                inp = xs[s] if l == 0 else pre[s]
+                bn = self.bn_layers[l - 1] if l else None
+                outs = act_linears(inp, Ws, bias, bn=bn, relu=l > 0,
+                                   dropout=self.dropout if l else 0.0)
+                k = 0
+                if skip:
+                    new[s] = outs[0]
+                    k = 1
+                zs = outs[k:k + len(rs_src)]
+                for r, o in zip(rs_dst, outs[k + len(rs_src):]):
+                    sds[r] = o + convs[r].project_message.bias
+                zh = [None] * len(rs_src)
+                if l == 0:
+                    # read-only features: halo rows fetched once, transformed here
+                    xh = g.sources[s].static_halo(xs[s])
+                    if xh is not None:
+                        zh = act_linears(xh, [convs[r].conv1.weight for r in rs_src])
+                work += [(s, r, z, h) for r, z, h in zip(rs_src, zs, zh)]
+            while work:  # each relation's transformed rows released after its attention
+                s, r, z, zh = work.pop(0)
+                d = ets[r][1]
+                _, a_src = self._att_vectors(convs[r])
+                sg = g.sources[s]
+                new[d] = gat_relation_into(z, sds.pop(r), a_src, new[d], pats[r],
+                                           sg=sg if zh is None else None, zh_static=zh)
+                del z, zh
+            pre = new
+        lin1, bn, _, drop, lin2 = self.mlp
+        p1 = act_linears(pre[0], [lin1.weight], lin1.bias, bn=self.bn_layers[-1], relu=True,
+                         dropout=self.dropout)[0]
+        return act_linears(p1, [lin2.weight], lin2.bias, bn=bn, relu=True,
+                           dropout=drop.p)[0]
