@@ -241,8 +241,8 @@ def main(argv=None):
                                                                   else "")},
         "final_loss": float(lt.item()), "peak_mem_gb_rank0": round(peak, 2),
         "path": "lean" if lean else "aggregate-first",
-        "layer0_halo": ("kept" if (args.model == "rgat" or not lean or
-                                   model._keep_static_halo(feats, graph))
+        "layer0_halo": ("kept" if (not lean or
+                                   CommAwareRGCN._keep_static_halo(model, feats, graph))
                         else "exchanged per step"),
         "allocator_in_timed_steps": alloc_timed,
     }

@@ -217,6 +217,9 @@ class CommAwareRGAT(nn.Module):
             nn.Dropout(dropout),
             nn.Linear(hidden_channels, out_channels),
         )
+        self.static_halo: Optional[bool] = None  # lean path; None: by memory (R-GCN's rule)
+
+    STATIC_HALO_FRAC = 0.08
 
     def forward(self, xs, edge_types, graphs=None) -> torch.Tensor:
         """``forward(xs, edge_types, graphs)`` over per-relation RelationGraphs (API of the
@@ -281,6 +284,14 @@ class CommAwareRGAT(nn.Module):
         avail = [r for s in g.sources.values() for r in s.ranges]
         need, rels = layer_plan(ets, self.num_layers, 0, avail)
         pats = self._patterns(g)
+        from .rgcn import CommAwareRGCN
+
+        # layer 0's feature halo rows kept (fetched once, transformed locally every step)
+        # unless they would take more than STATIC_HALO_FRAC of the device; then each
+        # relation's transformed halo rows are exchanged per step like a hidden layer's
+        # (256 instead of 768 columns, nothing resident: a W=8 MAG240M rank's feature halo
+        # is ~48 GB)
+        keep_halo = CommAwareRGCN._keep_static_halo(self, xs, g)
         pre: Dict[int, torch.Tensor] = {}
         for l in range(self.num_layers):
             convs = self.layers[l]
@@ -327,7 +338,7 @@ class CommAwareRGAT(nn.Module):
                 for r, o in zip(rs_dst, outs[k + len(rs_src):]):
                     sds[r] = o + convs[r].project_message.bias
                 zh = [None] * len(rs_src)
-                if l == 0:
+                if l == 0 and keep_halo:
                     # read-only features: halo rows fetched once, transformed here
                     xh = g.sources[s].static_halo(xs[s])
                     if xh is not None:

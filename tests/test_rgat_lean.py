@@ -112,7 +112,7 @@ def test_gat_relation_op_gradcheck():
     assert torch.autograd.gradcheck(f, (z, sd, a, base), eps=1e-6, atol=1e-6)
 
 
-def _train(rank, world, steps, out, heads):
+def _train(rank, world, steps, out, heads, static_halo=None):
     import torch.distributed as dist
 
     from dgraph_amd.parallel.grad_sync import GradSync
@@ -126,8 +126,7 @@ def _train(rank, world, steps, out, heads):
     if world > 1:
         dist.all_reduce(n)
     m = _model(24, 16, 2, heads)
-    for bn in list(m.bn_layers) + [m.mlp[1]]:
-        bn.group = None  # the default group: synchronised statistics over the W ranks
+    m.static_halo = static_halo
     opt = torch.optim.Adam(m.parameters(), lr=1e-2)
     sync = GradSync(m.parameters())
     losses = []
@@ -146,10 +145,13 @@ def _train(rank, world, steps, out, heads):
         torch.save(torch.tensor(losses), out)
 
 
-@pytest.mark.parametrize("world,heads", [(2, 4), (3, 1), (8, 2)])
-def test_rgat_lean_distributed_matches_single_rank(ranks, tmp_path, world, heads):
+@pytest.mark.parametrize("world,heads,static_halo", [(2, 4, None), (3, 1, None), (8, 2, None),
+                                                    (2, 4, False), (3, 2, False)])
+def test_rgat_lean_distributed_matches_single_rank(ranks, tmp_path, world, heads, static_halo):
+    """(``static_halo=False``: layer 0 exchanges each relation's transformed halo rows per
+    step and returns their gradient, instead of transforming kept feature halo rows.)"""
     _train(0, 1, 3, tmp_path / "w1.pt", heads)
-    ranks(_train, world, 3, str(tmp_path / "wn.pt"), heads)
+    ranks(_train, world, 3, str(tmp_path / "wn.pt"), heads, static_halo)
     a = torch.load(tmp_path / "w1.pt", weights_only=True)
     b = torch.load(tmp_path / "wn.pt", weights_only=True)
     torch.testing.assert_close(a, b, atol=2e-5, rtol=2e-5)
