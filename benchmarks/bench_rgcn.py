@@ -131,8 +131,9 @@ def main(argv=None):
             sg.heap = heap
     feats, y, train = hetero_node_data(shape, p_rank, part["offsets"], dev, seed=args.seed,
                                        dtype=dtype, alloc=alloc)
-    for sg in graph.sources.values():
-        sg.prepare_backward()
+    if args.model != "rgat":  # (RGAT's patterns carry their own transposes, ops/gat.py)
+        for sg in graph.sources.values():
+            sg.prepare_backward()
     train_idx = torch.nonzero(train, as_tuple=True)[0]
     y_train = y[train_idx]
     del y, train

@@ -218,6 +218,7 @@ class CommAwareRGAT(nn.Module):
             nn.Linear(hidden_channels, out_channels),
         )
         self.static_halo: Optional[bool] = None  # lean path; None: by memory (R-GCN's rule)
+        self.remake_layer0 = True  # lean path: layer-0 z rebuilt in backward, not saved
 
     STATIC_HALO_FRAC = 0.08
 
@@ -338,19 +339,26 @@ class CommAwareRGAT(nn.Module):
                 for r, o in zip(rs_dst, outs[k + len(rs_src):]):
                     sds[r] = o + convs[r].project_message.bias
                 zh = [None] * len(rs_src)
+                xh = None
                 if l == 0 and keep_halo:
                     # read-only features: halo rows fetched once, transformed here
                     xh = g.sources[s].static_halo(xs[s])
                     if xh is not None:
                         zh = act_linears(xh, [convs[r].conv1.weight for r in rs_src])
-                work += [(s, r, z, h) for r, z, h in zip(rs_src, zs, zh)]
+                # layer 0: z = x W_r^T is rebuilt in backward from the resident features
+                # rather than kept (saves [rows, hidden] per relation: 47 GB on one GPU's
+                # 1/8 MAG240M share)
+                rem = [((xs[s], convs[r].conv1.weight) + ((xh,) if xh is not None else ()))
+                       if (l == 0 and self.remake_layer0) else None for r in rs_src]
+                work += [(s, r, z, h, q) for r, z, h, q in zip(rs_src, zs, zh, rem)]
             while work:  # each relation's transformed rows released after its attention
-                s, r, z, zh = work.pop(0)
+                s, r, z, zh, rem = work.pop(0)
                 d = ets[r][1]
                 _, a_src = self._att_vectors(convs[r])
                 sg = g.sources[s]
                 new[d] = gat_relation_into(z, sds.pop(r), a_src, new[d], pats[r],
-                                           sg=sg if zh is None else None, zh_static=zh)
+                                           sg=sg if zh is None else None, zh_static=zh,
+                                           remake=rem)
                 del z, zh
             pre = new
         lin1, bn, _, drop, lin2 = self.mlp

@@ -111,8 +111,10 @@ def _reference(z, zh, sd, a_src, pat: GatPattern):
 
 class _GatRelFn(Function):
     @staticmethod
-    def forward(ctx, z, zh_static, sd, a_src, into, pat: GatPattern, sg, heads: int):
+    def forward(ctx, z, zh_static, sd, a_src, into, pat: GatPattern, sg, heads: int,
+                remake=None):
         Hh = int(heads)
+        ctx.remake = remake
         exchange = zh_static is None and sg is not None and sg.halo is not None
         ctx.pat, ctx.sg, ctx.exchange, ctx.heads = pat, sg, exchange, Hh
         ctx.static = zh_static is not None
@@ -148,7 +150,12 @@ class _GatRelFn(Function):
         l = torch.empty_like(m)
         _native.ops().gat_fwd_f32(pat.rowptr, pat.col, z, zh, pat.nsplit, ss, ssh,
                                   sd.contiguous(), into, 1.0, m, l, Hh, SLOPE)
-        ctx.save_for_backward(z, zh, ss, ssh, sd, m, l, a_src)
+        # remake = (x, W[, xh]): z (and a static zh) are x W^T — rebuilt bitwise in backward
+        # by the same GEMM instead of being kept (x: the resident input features)
+        keep_z = z if remake is None else None
+        keep_zh = zh if (remake is None or len(remake) < 3 or zh_static is None) else None
+        ctx.zh_remade = keep_zh is None and zh is not None
+        ctx.save_for_backward(keep_z, keep_zh, ss, ssh, sd, m, l, a_src)
         ctx.mark_dirty(into)
         return into
 
@@ -172,8 +179,16 @@ class _GatRelFn(Function):
                 K.spmm(st.rowptr, st.col, back, gz, beta=1.0)
                 gzh = None
             return (gz, gzh.to(z_dt) if (gzh is not None and ctx.static) else None,
-                    gsd.to(z_dt), ga.to(z_dt), g, None, None, None)
+                    gsd.to(z_dt), ga.to(z_dt), g, None, None, None, None)
         z, zh, ss, ssh, sd, m, l, a_src = ctx.saved_tensors
+        if ctx.remake is not None:
+            from . import f32 as F32
+
+            x, W = ctx.remake[0], ctx.remake[1]
+            if z is None:
+                z = F32.linear_fwd(x, W)
+            if ctx.zh_remade:
+                zh = F32.linear_fwd(ctx.remake[2], W)
         pat, Hh = ctx.pat, ctx.heads
         ops = _native.ops()
         g = g.contiguous()
@@ -205,19 +220,25 @@ class _GatRelFn(Function):
                 st = sg.send_map.transpose_csr()
                 K.spmm(st.rowptr, st.col, back, gz, beta=1.0)
                 gzh = None
-        return (gz, gzh if ctx.static else None, gsd, ga.contiguous(), g, None, None, None)
+        return (gz, gzh if ctx.static else None, gsd, ga.contiguous(), g, None, None, None,
+                None)
 
 
 def gat_relation_into(z: torch.Tensor, sd: torch.Tensor, a_src: torch.Tensor,
                       into: torch.Tensor, pat: GatPattern, sg=None,
-                      zh_static: Optional[torch.Tensor] = None) -> torch.Tensor:
+                      zh_static: Optional[torch.Tensor] = None, remake=None) -> torch.Tensor:
     """``into += attention(z [, halo rows], sd, a_src)`` over ``pat`` (autograd; returns the
     updated ``into``). ``a_src``: [heads, D]. Halo rows: ``zh_static`` when given, else
-    exchanged through ``sg`` (a :class:`~dgraph_amd.parallel.hetero_graph.SourceGraph`)."""
+    exchanged through ``sg`` (a :class:`~dgraph_amd.parallel.hetero_graph.SourceGraph`).
+    ``remake = (x, W[, xh])`` (GPU): ``z = x W^T`` (and ``zh_static = xh W^T``) are
+    recomputed in backward by the same exact-f32 GEMM instead of being saved — the layer-0
+    memory diet (x: resident features)."""
     heads = a_src.shape[0]
     if z.is_cuda and z.dtype == torch.float32:
         C = z.shape[1]
         if C not in (64, 128, 256) or C % heads or (C // 4) // heads < 2:
             raise ValueError(f"gat_relation_into: unsupported width {C} / heads {heads}")
+    if remake is not None and not z.is_cuda:
+        remake = None  # (the CPU oracle keeps its own fp64 graph)
     return _GatRelFn.apply(z.contiguous(), zh_static, sd, a_src.contiguous(), into, pat, sg,
-                           int(heads))
+                           int(heads), remake)
