@@ -145,8 +145,12 @@ class CommAwareGAT(nn.Module):
 
     # ------------------------------------------------------------------ reference paths
     def _process_messages(self, h, h_j):
-        scores = self.leaky_relu(self.project_message(torch.cat([h, h_j], dim=-1)))
-        return torch.exp(scores)
+        """``exp(leaky_relu(a . [h_i || h_j] + c))`` per head (the reference's unnormalised
+        numerator, RGAT.py:146-156), with the same per-head score blocks as the fast path
+        (identical to the reference's ``Linear(2C, 1)`` at one head)."""
+        s = self._head_scores(h, 0) + self._head_scores(h_j, 1) + \
+            self.project_message.bias.to(h.dtype)
+        return torch.exp(self.leaky_relu(s))
 
     def _calc_attention_messages(self, neighbor_features, numerator, denominator):
         alpha = numerator / (denominator + 1e-16)
@@ -155,7 +159,15 @@ class CommAwareGAT(nn.Module):
         return (nf * alpha.unsqueeze(-1)).reshape(neighbor_features.shape)
 
     def _forward_comm_plan(self, x, comm_plan, x_j=None):
-        """G2 plan path (RGAT.py:171-201): per-edge tensors through plan gathers."""
+        """G2 plan path (RGAT.py:171-201), with its five collectives per relation-layer
+        (two gathers, scatter + gather of the denominator, scatter of the messages) cut to
+        TWO: one grouped all-to-all-v carries both endpoint gathers
+        (:func:`~dgraph_amd.parallel.plan_ops.plan_gather_grouped`), and one scatter carries
+        ``[num * h_j | num]`` so every destination divides its own message sum by its own
+        denominator — ``sum_j num_ij h_j / (den_i + 1e-16)`` is the reference's
+        ``sum_j (num_ij / (den_i + 1e-16)) h_j``. Backward: the adjoints, two more."""
+        from ..parallel.plan_ops import plan_gather_grouped, plan_scatter
+
         h = self.conv1(x)
         src_plan = comm_plan.source_graph_plan
         if self.hetero:
@@ -163,12 +175,14 @@ class CommAwareGAT(nn.Module):
             dst_plan = comm_plan.dest_graph_plan
         else:
             h_j, dst_plan = h, src_plan
-        h_i = self.comm.gather(h, comm_plan=dst_plan)
-        h_j = self.comm.gather(h_j, comm_plan=src_plan)
-        num = self._process_messages(h_i, h_j)
-        den = self.comm.gather(self.comm.scatter(num, comm_plan=dst_plan), comm_plan=dst_plan)
-        out = self.comm.scatter(self._calc_attention_messages(h_j, num, den),
-                                comm_plan=dst_plan)
+        group = getattr(self.comm, "group", None) if self.comm is not None else None
+        h_i, h_j = plan_gather_grouped([h, h_j], [dst_plan, src_plan], group)
+        num = self._process_messages(h_i, h_j)  # [E, heads]
+        C, H = self.out_channels, self.heads
+        msg = (h_j.view(-1, H, C // H) * num.unsqueeze(-1).to(h_j.dtype)).reshape(-1, C)
+        agg = plan_scatter(torch.cat([msg, num.to(msg.dtype)], dim=1), dst_plan, group)
+        den = agg[:, C:] + 1e-16
+        out = (agg[:, :C].view(-1, H, C // H) / den.unsqueeze(-1)).reshape(-1, C)
         return self._apply_res_and_bias(out, x)
 
     def _forward_coo(self, x, edge_index, rank_mapping, x_j=None, src_gather_cache=None,

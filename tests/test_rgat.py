@@ -177,3 +177,55 @@ def test_rgat_distributed_equivalence(ranks, tmp_path):
         torch.testing.assert_close(rw["out"], r1["out"])
         torch.testing.assert_close(rw["loss"], r1["loss"])
         torch.testing.assert_close(rw["gnorm"], r1["gnorm"])
+
+
+def _g2_body(rank, world, heads):
+    """The G2 (edge-conditioned plan) path of CommAwareGAT on W gloo ranks: every rank
+    holds a round-robin share of the edges; its destination rows' output and the
+    all-reduced parameter gradients equal the dense single-process layer."""
+    import types
+
+    import torch.distributed as dist
+
+    from dgraph_amd.plan.nccl_plan import COO_to_NCCLEdgeConditionedCommPlan
+
+    Ns, Nd, E, Cin, C = 23, 17, 90, 6, 8
+    g = torch.Generator().manual_seed(4)
+    edges = torch.stack([torch.randint(0, Ns, (E,), generator=g),
+                         torch.randint(0, Nd, (E,), generator=g)])
+    edges = torch.unique(edges, dim=1)
+    xs = torch.randn(Ns, Cin, generator=g, dtype=torch.float64)
+    xd = torch.randn(Nd, Cin, generator=g, dtype=torch.float64)
+    so = torch.tensor([Ns * r // world for r in range(world + 1)])
+    do = torch.tensor([Nd * r // world for r in range(world + 1)])
+    mine = torch.nonzero(torch.arange(edges.shape[1]) % world == rank).squeeze(1)
+    plan = COO_to_NCCLEdgeConditionedCommPlan(rank, world, edges[0], edges[1], mine, so, do)
+    torch.manual_seed(0)
+    layer = CommAwareGAT(Cin, C, comm=types.SimpleNamespace(group=None), heads=heads,
+                         residual=True, hetero=True).double()
+    with torch.no_grad():
+        layer.bias.normal_()
+        layer.project_message.weight.normal_(0, 0.5)
+    from dgraph_amd.comm.alltoallv import CommStats
+
+    d0, d1 = int(do[rank]), int(do[rank + 1])
+    CommStats.reset()
+    out = layer(xd[d0:d1], plan, x_j=xs[int(so[rank]):int(so[rank + 1])])
+    assert CommStats.calls == 2, CommStats.calls  # grouped gather + one scatter (ref: 5)
+    w = torch.randn(Nd, C, generator=torch.Generator().manual_seed(9), dtype=torch.float64)
+    (out * w[d0:d1]).sum().backward()
+    assert CommStats.calls == 4, CommStats.calls  # their two adjoints
+    got = [p.grad.clone() for p in layer.parameters()]
+    for t in got:
+        dist.all_reduce(t)
+    layer.zero_grad()
+    ref = _dense_gat(layer, xd, xs, edges)
+    torch.testing.assert_close(out, ref[d0:d1])
+    (ref * w).sum().backward()
+    for a, p in zip(got, layer.parameters()):
+        torch.testing.assert_close(a, p.grad)
+
+
+@pytest.mark.parametrize("world,heads", [(1, 1), (2, 2), (3, 1)])
+def test_gat_g2_plan_path_two_exchanges(ranks, world, heads):
+    ranks(_g2_body, world, heads)
