@@ -3,7 +3,9 @@
 // gradient, and the 1-bit keep masks of selected rows. A TORCH_LIBRARY_FRAGMENT of the
 // dgraph_amd library (csrc/bindings.cpp); every launch goes to the current HIP stream and
 // every shape contract is checked here, before a kernel sees a pointer.
+#include <algorithm>
 #include <mutex>
+#include <vector>
 #include <set>
 #include <tuple>
 #include <ATen/ATen.h>
@@ -265,23 +267,47 @@ void gemm_f32_op(const at::Tensor& A1, const at::Tensor& B1, const c10::optional
     TORCH_CHECK(sq->scalar_type() == at::kInt && sq->is_contiguous(),
                 "send_pos must be contiguous int32");
     // bounds of the plan (the kernel writes send_out rows send_pos[q] for q in the
-    // send_ptr ranges): a static plan, so checked the first time each (send_ptr, send_pos,
-    // send_out rows) triple is seen — after that no per-call device reduction, which would
-    // synchronise the host with the stream
+    // send_ptr ranges): a static plan, so checked the first time each plan is seen — after
+    // that no per-call device reduction, which would synchronise the host with the stream.
+    // A plan is identified by its index tensors' STORAGE (weak references: a freed plan's
+    // entry expires, so new tensors reusing its address are checked again), view offsets,
+    // sizes and version counters (an in-place rewrite is checked again), and send_out's rows.
     {
+      struct Seen {
+        c10::weak_intrusive_ptr<c10::StorageImpl> sp, sq;
+        int64_t sp_off, sp_n, sq_off, sq_n, rows;
+        uint32_t sp_ver, sq_ver;
+      };
       static std::mutex mu;
-      static std::set<std::tuple<const void*, int64_t, const void*, int64_t, int64_t>> seen;
-      const auto key = std::make_tuple(sp->data_ptr(), sp->numel(), sq->data_ptr(),
-                                       sq->numel(), so->size(0));
+      static std::vector<Seen> seen;
       std::lock_guard<std::mutex> lk(mu);
-      if (!seen.count(key)) {
+      seen.erase(std::remove_if(seen.begin(), seen.end(),
+                                [](const Seen& e) { return e.sp.expired() || e.sq.expired(); }),
+                 seen.end());
+      const c10::StorageImpl* spi = sp->storage().unsafeGetStorageImpl();
+      const c10::StorageImpl* sqi = sq->storage().unsafeGetStorageImpl();
+      const uint32_t spv = sp->_version(), sqv = sq->_version();
+      bool hit = false;
+      for (const Seen& e : seen) {
+        if (e.sp.lock().get() == spi && e.sq.lock().get() == sqi &&
+            e.sp_off == sp->storage_offset() && e.sp_n == sp->numel() &&
+            e.sq_off == sq->storage_offset() && e.sq_n == sq->numel() && e.rows == so->size(0) &&
+            e.sp_ver == spv && e.sq_ver == sqv) {
+          hit = true;
+          break;
+        }
+      }
+      if (!hit) {
         const int64_t q0 = sp->min().item<int64_t>(), q1 = sp->max().item<int64_t>();
         TORCH_CHECK(q0 >= 0 && q1 <= sq->numel(), "send_ptr outside send_pos");
         if (sq->numel() > 0) {
           const int64_t mn = sq->min().item<int32_t>(), mx = sq->max().item<int32_t>();
           TORCH_CHECK(mn >= 0 && mx < so->size(0), "send_pos outside send_out's rows");
         }
-        seen.insert(key);
+        seen.push_back(Seen{sp->storage().getWeakStorageImpl(),
+                            sq->storage().getWeakStorageImpl(), sp->storage_offset(),
+                            sp->numel(), sq->storage_offset(), sq->numel(), so->size(0), spv,
+                            sqv});
       }
     }
     sd.out = so->data_ptr<float>();

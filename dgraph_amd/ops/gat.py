@@ -152,8 +152,10 @@ class _GatRelFn(Function):
                                   sd.contiguous(), into, 1.0, m, l, Hh, SLOPE)
         # remake = (x, W[, xh]): z (and a static zh) are x W^T — rebuilt bitwise in backward
         # by the same GEMM instead of being kept (x: the resident input features)
+        # (an exchanged zh is received again in backward from the owners' rebuilt z)
         keep_z = z if remake is None else None
-        keep_zh = zh if (remake is None or len(remake) < 3 or zh_static is None) else None
+        keep_zh = zh if (remake is None or (zh_static is not None and len(remake) < 3)) \
+            else None
         ctx.zh_remade = keep_zh is None and zh is not None
         ctx.save_for_backward(keep_z, keep_zh, ss, ssh, sd, m, l, a_src)
         ctx.mark_dirty(into)
@@ -188,7 +190,10 @@ class _GatRelFn(Function):
             if z is None:
                 z = F32.linear_fwd(x, W)
             if ctx.zh_remade:
-                zh = F32.linear_fwd(ctx.remake[2], W)
+                if ctx.exchange:  # every rank rebuilds its z here: the same rows again
+                    zh = ctx.sg.a2a(K.gather_rows(z, ctx.sg.send_map.idx))
+                else:
+                    zh = F32.linear_fwd(ctx.remake[2], W)
         pat, Hh = ctx.pat, ctx.heads
         ops = _native.ops()
         g = g.contiguous()

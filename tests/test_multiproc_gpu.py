@@ -203,8 +203,10 @@ def _a2a_body(rank, world, expect_mode=None):
 
 
 @pytest.mark.parametrize("env", [{"DGRAPH_FUSED_BOUNDARY_STORE": "on"},
-                                 {"DGRAPH_FUSED_HALO_STREAM": "on"}],
-                         ids=["store", "stream"])
+                                 {"DGRAPH_FUSED_HALO_STREAM": "on"},
+                                 {"DGRAPH_FUSED_HALO_STREAM": "on",
+                                  "DGRAPH_FUSED_STREAM_FILL": "0"}],
+                         ids=["store", "stream", "stream-nofill"])
 def test_bench_step_hidden512_two_processes(monkeypatch, env):
     """a 512-wide hidden layer at W=2 on the GPU kernels, through the two
     in-place aggregate-then-GEMM paths (boundary-row store, streamed halos), whose GEMM
@@ -217,7 +219,9 @@ def test_bench_step_hidden512_two_processes(monkeypatch, env):
     # summation order flips (the hidden-layer gradients then differ by 2e-4 relative at
     # W=2 vs W=1 whatever the path; seeds 1 and 2: 2-4e-7, scripts/debug/h512_w2_grads.py)
     kw = dict(global_frac=0.05, hidden=512, seed=1)
-    if "DGRAPH_FUSED_HALO_STREAM" in env:
+    if "DGRAPH_FUSED_HALO_STREAM" in env and env.get("DGRAPH_FUSED_STREAM_FILL") != "0":
+        # (the fill's one extra fp32 rounding: the looser gate; with the fill off the same
+        # streamed in-place column-block path is held to the tight 1e-5 gate)
         kw["stream_fill"] = True
     run_ranks(_body, 2, kw, "fp32", timeout=240)
 

@@ -112,20 +112,30 @@ def test_gat_relation_op_gradcheck():
     assert torch.autograd.gradcheck(f, (z, sd, a, base), eps=1e-6, atol=1e-6)
 
 
-def _train(rank, world, steps, out, heads, static_halo=None):
+def _train(rank, world, steps, out, heads, static_halo=None, dev="cpu", width=24, hid=16):
     import torch.distributed as dist
 
     from dgraph_amd.parallel.grad_sync import GradSync
 
+    if dev != "cpu":
+        from conftest import rank_device
+
+        dev = rank_device()
+    # graph and data generated on the CPU (device RNG streams differ), then moved
     part = build_hetero_partition(SHAPE, rank, world, "cpu", global_frac=0.3, window=64)
+    part = {k: v for k, v in part.items()}
+    part["sources"] = {s: {k: (v.to(dev) if hasattr(v, "to") else v) for k, v in d.items()}
+                       for s, d in part["sources"].items()}
     g = HeteroGraph.from_partition(part, EDGE_TYPES, rank=rank)
     feats, y, tr = hetero_node_data(SHAPE, rank, part["offsets"], "cpu", dtype=torch.float32)
-    feats = {t: v[:, :24].contiguous() for t, v in feats.items()}
+    feats = {t: v[:, :width].contiguous().to(dev) for t, v in feats.items()}
+    y, tr = y.to(dev), tr.to(dev)
     idx = torch.nonzero(tr).squeeze(1)
-    n = torch.tensor([idx.numel()])
+    n = torch.tensor([idx.numel()], device=dev if dist.is_initialized() and
+                     dist.get_backend() == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(n)
-    m = _model(24, 16, 2, heads)
+    m = _model(width, hid, 2, heads).to(dev)
     m.static_halo = static_halo
     opt = torch.optim.Adam(m.parameters(), lr=1e-2)
     sync = GradSync(m.parameters())
@@ -137,12 +147,17 @@ def _train(rank, world, steps, out, heads, static_halo=None):
         sync.all_reduce()
         opt.step()
         opt.zero_grad()
-        lt = loss.detach().clone()
+        lt = loss.detach().clone().to(n.device)
         if world > 1:
             dist.all_reduce(lt)
         losses.append(float(lt))
     if rank == 0:
         torch.save(torch.tensor(losses), out)
+    if dev != "cpu":
+        from dgraph_amd.comm.alltoallv import close_shmem_heaps
+
+        torch.cuda.synchronize()
+        close_shmem_heaps()
 
 
 @pytest.mark.parametrize("world,heads,static_halo", [(2, 4, None), (3, 1, None), (8, 2, None),
@@ -154,6 +169,25 @@ def test_rgat_lean_distributed_matches_single_rank(ranks, tmp_path, world, heads
     ranks(_train, world, 3, str(tmp_path / "wn.pt"), heads, static_halo)
     a = torch.load(tmp_path / "w1.pt", weights_only=True)
     b = torch.load(tmp_path / "wn.pt", weights_only=True)
+    torch.testing.assert_close(a, b, atol=2e-5, rtol=2e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("static_halo", [None, False])
+def test_rgat_lean_two_processes_one_gpu(monkeypatch, tmp_path, static_halo):
+    """W=2 on the GPU kernels (two processes sharing the GPU, halo exchanges on the IPC
+    heap): layer 0 with the kept feature halo or with exchanged transformed halo rows —
+    rebuilt in backward (remake: z recomputed by the same GEMM, its halo rows received
+    again) — follows the W=1 losses of the same GPU model."""
+    from conftest import run_ranks
+
+    monkeypatch.setenv("DGRAPH_A2A_IMPL", "shmem")
+    monkeypatch.setenv("DGRAPH_SYMHEAP_BYTES", str(256 << 20))
+    _train(0, 1, 3, tmp_path / "w1.pt", 4, None, "cuda", 64, 64)
+    run_ranks(_train, 2, 3, str(tmp_path / "w2.pt"), 4, static_halo, "cuda", 64, 64,
+              timeout=240)
+    a = torch.load(tmp_path / "w1.pt", weights_only=True)
+    b = torch.load(tmp_path / "w2.pt", weights_only=True)
     torch.testing.assert_close(a, b, atol=2e-5, rtol=2e-5)
 
 
