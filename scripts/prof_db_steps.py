@@ -18,11 +18,16 @@ def main():
     ap.add_argument("--skip-last", type=int, default=0,
                     help="ignore this many trailing steps (e.g. region-timing steps)")
     ap.add_argument("--top", type=int, default=30)
+    ap.add_argument("--total-steps", type=int, default=0,
+                    help="steps the traced program ran (warmup + timed + extra): markers per "
+                         "step = markers / this (an optimizer may launch several per step)")
     a = ap.parse_args()
     cur = sqlite3.connect(a.db).cursor()
     rows = cur.execute("select name, start, end, duration, stream_id from kernels "
                        "order by start").fetchall()
     ends = [r[2] for r in rows if a.marker in r[0]]
+    k = max(1, round(len(ends) / a.total_steps)) if a.total_steps else 1
+    ends = ends[k - 1::k]  # the last marker of every step
     if a.skip_last:
         ends = ends[:-a.skip_last]
     ends = ends[-(a.steps + 1):]
