@@ -35,12 +35,17 @@ void rows_f32(const at::Tensor& t, const at::Tensor& ref, int64_t min_rows, int6
               " must be 16-B aligned with a row stride divisible by 4");
 }
 
+// per-head score / statistics arrays: [rows, heads] with unit column stride and the row
+// stride `lds` shared by every such array of a call (heads for whole rows; a one-head column
+// pass hands in column slices of [rows, H] arrays, row stride H)
 void scores(const at::Tensor& t, const at::Tensor& ref, int64_t min_rows, int64_t heads,
-            const char* name) {
+            int64_t lds, const char* name) {
   TORCH_CHECK(t.is_cuda() && t.device() == ref.device() && t.scalar_type() == at::kFloat &&
-                  t.is_contiguous() && t.dim() == 2 && t.size(1) == heads &&
-                  t.size(0) >= min_rows,
-              "gat: ", name, " must be contiguous float32 [>= ", min_rows, ", ", heads, "]");
+                  t.dim() == 2 && t.size(1) == heads && t.size(0) >= min_rows &&
+                  (t.size(1) == 1 || t.stride(1) == 1) && t.stride(0) == lds && lds >= heads,
+              "gat: ", name, " must be float32 [>= ", min_rows, ", ", heads,
+              "] with unit column stride and row stride ", lds, ", got ", t.sizes(), " / ",
+              t.strides());
 }
 
 IType pattern(const at::Tensor& rowptr, const at::Tensor& col, const at::Tensor& ref) {
@@ -66,6 +71,7 @@ void gat_fwd_op(const at::Tensor& rowptr, const at::Tensor& col, const at::Tenso
   const int C = static_cast<int>(x.size(1));
   TORCH_CHECK(gat_f32_shape_ok(C, static_cast<int>(heads)), "gat: unsupported width ", C,
               " / heads ", heads, " (C in 64/128/256, >= 2 lanes per head)");
+  const int64_t lds = ss.stride(0);
   rows_f32(x, x, 1, C, "x");
   const at::Tensor* p2 = opt_t(x2);
   const at::Tensor* q2 = opt_t(ss2);
@@ -73,16 +79,16 @@ void gat_fwd_op(const at::Tensor& rowptr, const at::Tensor& col, const at::Tenso
   TORCH_CHECK(nsplit >= 0 && nsplit < (int64_t(1) << 32), "gat: bad nsplit");
   if (p2) {
     rows_f32(*p2, x, 0, C, "x2");
-    scores(*q2, x, p2->size(0), heads, "ss2");
+    scores(*q2, x, p2->size(0), heads, lds, "ss2");
     TORCH_CHECK(x.size(0) >= nsplit, "gat: x has fewer rows than nsplit");
   }
-  scores(ss, x, p2 ? nsplit : x.size(0), heads, "ss");
-  scores(sd, x, R, heads, "sd");
+  scores(ss, x, p2 ? nsplit : x.size(0), heads, lds, "ss");
+  scores(sd, x, R, heads, lds, "sd");
   rows_f32(out, x, R, C, "out");
-  scores(stat_m, x, R, heads, "stat_m");
-  scores(stat_l, x, R, heads, "stat_l");
+  scores(stat_m, x, R, heads, lds, "stat_m");
+  scores(stat_l, x, R, heads, lds, "stat_l");
   DG_HIP_CHECK(gat_fwd_f32(it, rowptr.data_ptr<int64_t>(), col.data_ptr(), R, C,
-                           static_cast<int>(heads), static_cast<float>(slope),
+                           static_cast<int>(heads), lds, static_cast<float>(slope),
                            x.data_ptr<float>(), x.stride(0), p2 ? p2->data_ptr<float>() : nullptr,
                            p2 ? p2->stride(0) : 0, p2 ? nsplit : 0, ss.data_ptr<float>(),
                            q2 ? q2->data_ptr<float>() : nullptr, sd.data_ptr<float>(),
@@ -101,6 +107,7 @@ void gat_bwd_dst_op(const at::Tensor& rowptr, const at::Tensor& col, const at::T
   const int64_t R = rowptr.numel() - 1;
   const int C = static_cast<int>(x.size(1));
   TORCH_CHECK(gat_f32_shape_ok(C, static_cast<int>(heads)), "gat: unsupported width / heads");
+  const int64_t lds = ss.stride(0);
   rows_f32(x, x, 1, C, "x");
   const at::Tensor* p2 = opt_t(x2);
   const at::Tensor* q2 = opt_t(ss2);
@@ -108,18 +115,18 @@ void gat_bwd_dst_op(const at::Tensor& rowptr, const at::Tensor& col, const at::T
   TORCH_CHECK(nsplit >= 0 && nsplit < (int64_t(1) << 32), "gat: bad nsplit");
   if (p2) {
     rows_f32(*p2, x, 0, C, "x2");
-    scores(*q2, x, p2->size(0), heads, "ss2");
+    scores(*q2, x, p2->size(0), heads, lds, "ss2");
     TORCH_CHECK(x.size(0) >= nsplit, "gat: x has fewer rows than nsplit");
   }
-  scores(ss, x, p2 ? nsplit : x.size(0), heads, "ss");
-  scores(sd, x, std::max<int64_t>(R, 1), heads, "sd");
-  scores(stat_m, x, std::max<int64_t>(R, 1), heads, "stat_m");
-  scores(stat_l, x, std::max<int64_t>(R, 1), heads, "stat_l");
+  scores(ss, x, p2 ? nsplit : x.size(0), heads, lds, "ss");
+  scores(sd, x, std::max<int64_t>(R, 1), heads, lds, "sd");
+  scores(stat_m, x, std::max<int64_t>(R, 1), heads, lds, "stat_m");
+  scores(stat_l, x, std::max<int64_t>(R, 1), heads, lds, "stat_l");
   rows_f32(g, x, std::max<int64_t>(R, 1), C, "g");
-  scores(c_out, x, R, heads, "c_out");
-  scores(gsd_out, x, R, heads, "gsd_out");
+  scores(c_out, x, R, heads, lds, "c_out");
+  scores(gsd_out, x, R, heads, lds, "gsd_out");
   DG_HIP_CHECK(gat_bwd_dst_f32(it, rowptr.data_ptr<int64_t>(), col.data_ptr(), R, C,
-                               static_cast<int>(heads), static_cast<float>(slope),
+                               static_cast<int>(heads), lds, static_cast<float>(slope),
                                x.data_ptr<float>(), x.stride(0),
                                p2 ? p2->data_ptr<float>() : nullptr, p2 ? p2->stride(0) : 0,
                                p2 ? nsplit : 0, ss.data_ptr<float>(),
@@ -140,23 +147,24 @@ void gat_bwd_src_op(const at::Tensor& rowptr, const at::Tensor& col, const at::T
   const int64_t R = rowptr.numel() - 1;
   const int C = static_cast<int>(g.size(1));
   TORCH_CHECK(gat_f32_shape_ok(C, static_cast<int>(heads)), "gat: unsupported width / heads");
+  const int64_t lds = ss_row.stride(0);
   const int64_t nd = std::max<int64_t>(g.size(0), 1);
   rows_f32(g, g, 1, C, "g");
   rows_f32(z, g, std::max<int64_t>(R, 1), C, "z");
-  scores(ss_row, g, std::max<int64_t>(R, 1), heads, "ss_row");
-  scores(sd, g, nd, heads, "sd");
-  scores(m_dst, g, nd, heads, "m_dst");
-  scores(l_dst, g, nd, heads, "l_dst");
-  scores(c_dst, g, nd, heads, "c_dst");
+  scores(ss_row, g, std::max<int64_t>(R, 1), heads, lds, "ss_row");
+  scores(sd, g, nd, heads, lds, "sd");
+  scores(m_dst, g, nd, heads, lds, "m_dst");
+  scores(l_dst, g, nd, heads, lds, "l_dst");
+  scores(c_dst, g, nd, heads, lds, "c_dst");
   TORCH_CHECK(a_src.is_cuda() && a_src.device() == g.device() &&
                   a_src.scalar_type() == at::kFloat && a_src.is_contiguous() &&
                   a_src.numel() == C && al16(a_src.data_ptr()),
               "gat: a_src must be contiguous float32 [C], 16-B aligned");
   rows_f32(gz, g, R, C, "gz");
   const at::Tensor* pg = opt_t(gss);
-  if (pg) scores(*pg, g, R, heads, "gss");
+  if (pg) scores(*pg, g, R, heads, lds, "gss");
   DG_HIP_CHECK(gat_bwd_src_f32(it, rowptr.data_ptr<int64_t>(), col.data_ptr(), R, C,
-                               static_cast<int>(heads), static_cast<float>(slope),
+                               static_cast<int>(heads), lds, static_cast<float>(slope),
                                g.data_ptr<float>(), g.stride(0), z.data_ptr<float>(),
                                z.stride(0), ss_row.data_ptr<float>(), sd.data_ptr<float>(),
                                m_dst.data_ptr<float>(), l_dst.data_ptr<float>(),

@@ -41,6 +41,9 @@ struct GatArgs {
   int64_t nrows;
   int C;            // feature width (= 4 * LPR)
   float slope;      // leaky-ReLU negative slope
+  int64_t lds;      // row stride (floats) of every per-head score / statistics array:
+                    // heads for whole-row calls; the caller's heads for a one-head column
+                    // pass over a slice of wider rows
   // operands
   const float* x;   // rows gathered (z for fwd / bwd_dst, g for bwd_src)
   int64_t ldx;
@@ -125,7 +128,7 @@ __global__ __launch_bounds__(256) void gat_fwd_kernel(GatArgs a) {
   const int64_t qstep = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
   const uint32_t ns = static_cast<uint32_t>(a.nsplit);
   auto ssp = [&](int64_t c) -> const float* {
-    return (a.ss2 && c >= ns) ? a.ss2 + (c - ns) * HH : a.ss + c * HH;
+    return (a.ss2 && c >= ns) ? a.ss2 + (c - ns) * a.lds : a.ss + c * a.lds;
   };
   auto xrow = [&](int64_t c) -> const float* {
     return (a.x2 && c >= ns) ? a.x2 + (c - ns) * a.ldx2 + f : a.x + c * a.ldx + f;
@@ -138,7 +141,7 @@ __global__ __launch_bounds__(256) void gat_fwd_kernel(GatArgs a) {
     const int maxdeg = group_imax<LPR>(deg);
     float sd[HH];
 #pragma unroll
-    for (int k = 0; k < HH; ++k) sd[k] = has_row ? a.sd[r * HH + k] : 0.f;
+    for (int k = 0; k < HH; ++k) sd[k] = has_row ? a.sd[r * a.lds + k] : 0.f;
     // pass A: per-head max, then sum of exp, lane-parallel over the row's edges
     float m[HH], lsum[HH];
 #pragma unroll
@@ -205,8 +208,8 @@ __global__ __launch_bounds__(256) void gat_fwd_kernel(GatArgs a) {
     }
     *reinterpret_cast<float4*>(o) = acc;
     if (l % LH == 0) {
-      a.stat_m[r * HH + hk] = my_m;
-      a.stat_l[r * HH + hk] = my_inv;  // 1 / sum (0 for an isolated row)
+      a.stat_m[r * a.lds + hk] = my_m;
+      a.stat_l[r * a.lds + hk] = my_inv;  // 1 / sum (0 for an isolated row)
     }
   }
 }
@@ -224,7 +227,7 @@ __global__ __launch_bounds__(256) void gat_bwd_dst_kernel(GatArgs a) {
   const int64_t qstep = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
   const uint32_t ns = static_cast<uint32_t>(a.nsplit);
   auto ssp = [&](int64_t c) -> const float* {
-    return (a.ss2 && c >= ns) ? a.ss2 + (c - ns) * HH : a.ss + c * HH;
+    return (a.ss2 && c >= ns) ? a.ss2 + (c - ns) * a.lds : a.ss + c * a.lds;
   };
   auto xrow = [&](int64_t c) -> const float* {
     return (a.x2 && c >= ns) ? a.x2 + (c - ns) * a.ldx2 + f : a.x + c * a.ldx + f;
@@ -237,9 +240,9 @@ __global__ __launch_bounds__(256) void gat_bwd_dst_kernel(GatArgs a) {
     const int deg = has_row ? static_cast<int>(a.rowptr[r + 1] - s) : 0;
     const int maxdeg = group_imax<LPR>(deg);
     const float4 gv = *reinterpret_cast<const float4*>(a.g + rr * a.ldg + f);
-    const float my_sd = a.sd[rr * HH + hk];
-    const float my_m = a.stat_m[rr * HH + hk];
-    const float my_inv = a.stat_l[rr * HH + hk];
+    const float my_sd = a.sd[rr * a.lds + hk];
+    const float my_m = a.stat_m[rr * a.lds + hk];
+    const float my_inv = a.stat_l[rr * a.lds + hk];
     float cacc = 0.f, aacc = 0.f, bacc = 0.f;
     for (int k0 = 0; k0 < maxdeg; k0 += LPR) {
       const int kk = k0 + l;
@@ -272,8 +275,8 @@ __global__ __launch_bounds__(256) void gat_bwd_dst_kernel(GatArgs a) {
       }
     }
     if (has_row && l % LH == 0) {
-      a.c_out[r * HH + hk] = cacc;
-      a.gsd_out[r * HH + hk] = aacc - cacc * bacc;
+      a.c_out[r * a.lds + hk] = cacc;
+      a.gsd_out[r * a.lds + hk] = aacc - cacc * bacc;
     }
   }
 }
@@ -298,7 +301,7 @@ __global__ __launch_bounds__(256) void gat_bwd_src_kernel(GatArgs a) {
     const int deg = has_row ? static_cast<int>(a.rowptr[r + 1] - s) : 0;
     const int maxdeg = group_imax<LPR>(deg);
     const float4 zv = *reinterpret_cast<const float4*>(a.z + rr * a.ldz + f);
-    const float my_ss = a.ss_row[rr * HH + hk];
+    const float my_ss = a.ss_row[rr * a.lds + hk];
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     float gss = 0.f;
     for (int k0 = 0; k0 < maxdeg; k0 += LPR) {
@@ -315,10 +318,10 @@ __global__ __launch_bounds__(256) void gat_bwd_src_kernel(GatArgs a) {
           ok[u] = j < LPR && k0 + j < deg;
           const int64_t ii = ok[u] ? i : 0;
           v[u] = *reinterpret_cast<const float4*>(a.x + ii * a.ldx + f);
-          e[u] = a.sd[ii * HH + hk] + my_ss;
-          m[u] = a.m_dst[ii * HH + hk];
-          il[u] = a.l_dst[ii * HH + hk];
-          c[u] = a.c_dst[ii * HH + hk];
+          e[u] = a.sd[ii * a.lds + hk] + my_ss;
+          m[u] = a.m_dst[ii * a.lds + hk];
+          il[u] = a.l_dst[ii * a.lds + hk];
+          c[u] = a.c_dst[ii * a.lds + hk];
         }
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
@@ -344,7 +347,7 @@ __global__ __launch_bounds__(256) void gat_bwd_src_kernel(GatArgs a) {
     acc.z = fmaf(gss, av.z, acc.z);
     acc.w = fmaf(gss, av.w, acc.w);
     *reinterpret_cast<float4*>(a.gz + r * a.ldgz + f) = acc;
-    if (a.gss && l % LH == 0) a.gss[r * HH + hk] = gss;
+    if (a.gss && l % LH == 0) a.gss[r * a.lds + hk] = gss;
   }
 }
 
@@ -396,7 +399,7 @@ bool gat_f32_shape_ok(int C, int heads) {
 }
 
 hipError_t gat_fwd_f32(IType it, const int64_t* rowptr, const void* col, int64_t nrows, int C,
-                       int heads, float slope, const float* x, int64_t ldx, const float* x2,
+                       int heads, int64_t lds, float slope, const float* x, int64_t ldx, const float* x2,
                        int64_t ldx2, int64_t nsplit, const float* ss, const float* ss2,
                        const float* sd, float* out, int64_t ldo, float beta, float* stat_m,
                        float* stat_l, hipStream_t st) {
@@ -405,6 +408,7 @@ hipError_t gat_fwd_f32(IType it, const int64_t* rowptr, const void* col, int64_t
   a.col = col;
   a.nrows = nrows;
   a.C = C;
+  a.lds = lds;
   a.slope = slope;
   a.x = x;
   a.ldx = ldx;
@@ -423,7 +427,7 @@ hipError_t gat_fwd_f32(IType it, const int64_t* rowptr, const void* col, int64_t
 }
 
 hipError_t gat_bwd_dst_f32(IType it, const int64_t* rowptr, const void* col, int64_t nrows,
-                           int C, int heads, float slope, const float* x, int64_t ldx,
+                           int C, int heads, int64_t lds, float slope, const float* x, int64_t ldx,
                            const float* x2, int64_t ldx2, int64_t nsplit, const float* ss,
                            const float* ss2, const float* sd, const float* stat_m,
                            const float* stat_l, const float* g, int64_t ldg, float* c_out,
@@ -433,6 +437,7 @@ hipError_t gat_bwd_dst_f32(IType it, const int64_t* rowptr, const void* col, int
   a.col = col;
   a.nrows = nrows;
   a.C = C;
+  a.lds = lds;
   a.slope = slope;
   a.x = x;
   a.ldx = ldx;
@@ -452,7 +457,7 @@ hipError_t gat_bwd_dst_f32(IType it, const int64_t* rowptr, const void* col, int
 }
 
 hipError_t gat_bwd_src_f32(IType it, const int64_t* rowptr, const void* col, int64_t nrows,
-                           int C, int heads, float slope, const float* g, int64_t ldg,
+                           int C, int heads, int64_t lds, float slope, const float* g, int64_t ldg,
                            const float* z, int64_t ldz, const float* ss_row, const float* sd,
                            const float* m_dst, const float* l_dst, const float* c_dst,
                            const float* a_src, float* gz, int64_t ldgz, float* gss,
@@ -462,6 +467,7 @@ hipError_t gat_bwd_src_f32(IType it, const int64_t* rowptr, const void* col, int
   a.col = col;
   a.nrows = nrows;
   a.C = C;
+  a.lds = lds;
   a.slope = slope;
   a.x = g;
   a.ldx = ldg;

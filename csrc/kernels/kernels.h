@@ -325,18 +325,18 @@ int get_dual_gemm_variant();
 // dL/dss). Two sources: columns >= nsplit read x2 / ss2.
 bool gat_f32_shape_ok(int C, int heads);
 hipError_t gat_fwd_f32(IType it, const int64_t* rowptr, const void* col, int64_t nrows, int C,
-                       int heads, float slope, const float* x, int64_t ldx, const float* x2,
+                       int heads, int64_t lds, float slope, const float* x, int64_t ldx, const float* x2,
                        int64_t ldx2, int64_t nsplit, const float* ss, const float* ss2,
                        const float* sd, float* out, int64_t ldo, float beta, float* stat_m,
                        float* stat_l, hipStream_t st);
 hipError_t gat_bwd_dst_f32(IType it, const int64_t* rowptr, const void* col, int64_t nrows,
-                           int C, int heads, float slope, const float* x, int64_t ldx,
+                           int C, int heads, int64_t lds, float slope, const float* x, int64_t ldx,
                            const float* x2, int64_t ldx2, int64_t nsplit, const float* ss,
                            const float* ss2, const float* sd, const float* stat_m,
                            const float* stat_l, const float* g, int64_t ldg, float* c_out,
                            float* gsd_out, hipStream_t st);
 hipError_t gat_bwd_src_f32(IType it, const int64_t* rowptr, const void* col, int64_t nrows,
-                           int C, int heads, float slope, const float* g, int64_t ldg,
+                           int C, int heads, int64_t lds, float slope, const float* g, int64_t ldg,
                            const float* z, int64_t ldz, const float* ss_row, const float* sd,
                            const float* m_dst, const float* l_dst, const float* c_dst,
                            const float* a_src, float* gz, int64_t ldgz, float* gss,

@@ -33,6 +33,22 @@ from . import kernels as K
 from .csr import CSR
 
 SLOPE = 0.2
+# GPU: one kernel pass per head over that head's columns (D = C / heads of 64/128/256) instead
+# of whole rows — the SpMM's narrow-pass idea (kernels/spmm_f32.hip): each pass gathers
+# D-column slices of the neighbour rows, whose locality window the L2 / Infinity Cache holds
+# 4x longer than whole 1 KB rows at C = 256; the per-row softmax statistics are per head
+# anyway. DGRAPH_GAT_HEAD_PASSES=0: whole rows, all heads per kernel.
+import os as _os
+
+HEAD_PASSES = _os.environ.get("DGRAPH_GAT_HEAD_PASSES", "1") != "0"
+
+
+def _passes(C: int, Hh: int):
+    """[(column slice, head slice)] of the kernel calls of one op, and the heads per call."""
+    D = C // Hh
+    if HEAD_PASSES and Hh > 1 and D in (64, 128, 256):
+        return [(slice(k * D, (k + 1) * D), slice(k, k + 1)) for k in range(Hh)], 1
+    return [(slice(None), slice(None))], Hh
 
 
 class GatPattern:
@@ -148,8 +164,14 @@ class _GatRelFn(Function):
         R = pat.R
         m = torch.empty(R, Hh, dtype=torch.float32, device=z.device)
         l = torch.empty_like(m)
-        _native.ops().gat_fwd_f32(pat.rowptr, pat.col, z, zh, pat.nsplit, ss, ssh,
-                                  sd.contiguous(), into, 1.0, m, l, Hh, SLOPE)
+        sdc = sd.contiguous()
+        passes, hp = _passes(z.shape[1], Hh)
+        for cs, hs in passes:
+            _native.ops().gat_fwd_f32(pat.rowptr, pat.col, z[:, cs],
+                                      None if zh is None else zh[:, cs], pat.nsplit,
+                                      ss[:, hs], None if ssh is None else ssh[:, hs],
+                                      sdc[:, hs], into[:, cs], 1.0, m[:, hs], l[:, hs], hp,
+                                      SLOPE)
         # remake = (x, W[, xh]): z (and a static zh) are x W^T — rebuilt bitwise in backward
         # by the same GEMM instead of being kept (x: the resident input features)
         # (an exchanged zh is received again in backward from the owners' rebuilt z)
@@ -201,21 +223,29 @@ class _GatRelFn(Function):
         c = torch.empty(R, Hh, dtype=torch.float32, device=g.device)
         gsd = torch.empty_like(c)
         sdc = sd.contiguous()
-        ops.gat_bwd_dst_f32(pat.rowptr, pat.col, z, zh, pat.nsplit, ss, ssh, sdc, m, l, g, c,
-                            gsd, Hh, SLOPE)
+        passes, hp = _passes(z.shape[1], Hh)
+        for cs, hs in passes:
+            ops.gat_bwd_dst_f32(pat.rowptr, pat.col, z[:, cs],
+                                None if zh is None else zh[:, cs], pat.nsplit, ss[:, hs],
+                                None if ssh is None else ssh[:, hs], sdc[:, hs], m[:, hs],
+                                l[:, hs], g[:, cs], c[:, hs], gsd[:, hs], hp, SLOPE)
         a_flat = a_src.reshape(-1).contiguous()
         gz = torch.empty_like(z)
         gss = torch.empty(Ls, Hh, dtype=torch.float32, device=g.device)
-        ops.gat_bwd_src_f32(pat.t_rowptr[:Ls + 1], pat.t_col, g, z, ss, sdc, m, l, c, a_flat,
-                            gz, gss, Hh, SLOPE)
+        for cs, hs in passes:
+            ops.gat_bwd_src_f32(pat.t_rowptr[:Ls + 1], pat.t_col, g[:, cs], z[:, cs],
+                                ss[:, hs], sdc[:, hs], m[:, hs], l[:, hs], c[:, hs],
+                                a_flat[cs], gz[:, cs], gss[:, hs], hp, SLOPE)
         Hh_, D = a_src.shape
         ga = (gss.t() @ z).view(Hh, Hh, D).diagonal(dim1=0, dim2=1).t()
         gzh = None
         if zh is not None:
             gzh = torch.empty_like(zh)
             gssh = torch.empty(zh.shape[0], Hh, dtype=torch.float32, device=g.device)
-            ops.gat_bwd_src_f32(pat.t_rowptr[Ls:], pat.t_col, g, zh, ssh, sdc, m, l, c,
-                                a_flat, gzh, gssh, Hh, SLOPE)
+            for cs, hs in passes:
+                ops.gat_bwd_src_f32(pat.t_rowptr[Ls:], pat.t_col, g[:, cs], zh[:, cs],
+                                    ssh[:, hs], sdc[:, hs], m[:, hs], l[:, hs], c[:, hs],
+                                    a_flat[cs], gzh[:, cs], gssh[:, hs], hp, SLOPE)
             ga = ga + (gssh.t() @ zh).view(Hh, Hh, D).diagonal(dim1=0, dim2=1).t()
             if ctx.exchange:
                 # the halo rows' gradient back to their owners, summed there in a fixed order

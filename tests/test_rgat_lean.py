@@ -192,7 +192,7 @@ def test_rgat_lean_two_processes_one_gpu(monkeypatch, tmp_path, static_halo):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("width,heads", [(64, 1), (128, 4), (256, 4), (256, 8)])
+@pytest.mark.parametrize("width,heads", [(64, 1), (128, 4), (128, 2), (256, 4), (256, 8)])
 def test_rgat_lean_gpu_matches_fp64_cpu(width, heads):
     """The fused attention kernels (csrc/kernels/gat_f32.hip) and the exact-f32 MFMA linears
     against the same model run on the CPU in fp64 attention; then bitwise run to run."""
@@ -225,3 +225,38 @@ def test_rgat_lean_gpu_matches_fp64_cpu(width, heads):
         a = res["cuda"][1][n]
         rel = float((a - b).norm() / b.norm().clamp_min(1e-4))
         assert rel < 1e-3, (n, rel)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("C,heads", [(256, 4), (128, 2), (256, 2)])
+def test_gat_head_passes_match_whole_rows(monkeypatch, C, heads):
+    """One kernel pass per head over its column slice (ops/gat.py HEAD_PASSES) against one
+    pass over whole rows: same forward and gradients to fp32 rounding (the per-head softmax
+    sums are grouped differently), two sources (a halo part) included."""
+    import dgraph_amd.ops.gat as G
+    from dgraph_amd.ops.csr import CSR
+
+    torch.manual_seed(3)
+    R, N, H, E = 3000, 2500, 700, 60000
+    rows = torch.randint(0, R, (E,))
+    cols = torch.randint(0, N + H, (E,))
+    csr = CSR.from_coo(rows, cols, R, N + H)
+    dev = torch.device("cuda")
+    pat = G.GatPattern(csr.rowptr.to(dev), csr.col.to(dev), N, H)
+    z0 = torch.randn(N, C, device=dev)
+    zh = torch.randn(H, C, device=dev)
+    sd0 = torch.randn(R, heads, device=dev)
+    a0 = torch.randn(heads, C // heads, device=dev) * 0.3
+    base = torch.randn(R, C, device=dev)
+    w = torch.randn(R, C, device=dev)
+    res = {}
+    for hp in (True, False):
+        monkeypatch.setattr(G, "HEAD_PASSES", hp)
+        z = z0.clone().requires_grad_()
+        sd = sd0.clone().requires_grad_()
+        a = a0.clone().requires_grad_()
+        out = G.gat_relation_into(z, sd, a, base.clone(), pat, zh_static=zh)
+        (out * w).sum().backward()
+        res[hp] = (out.detach(), z.grad, sd.grad, a.grad)
+    for x, y in zip(res[True], res[False]):
+        torch.testing.assert_close(x, y, rtol=2e-5, atol=2e-5)
