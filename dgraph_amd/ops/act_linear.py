@@ -39,6 +39,12 @@ def _wgrad(g: torch.Tensor, y: torch.Tensor, W: torch.Tensor, bias: bool = False
     return dW, (K.col_sum(g) if g.is_cuda else g.sum(0))
 
 
+def _tiled(y: torch.Tensor, W: torch.Tensor) -> bool:
+    """Does ``F32.linear_fwd(y, W)`` run on the MFMA kernel (else the library GEMM)?"""
+    N, K = W.shape
+    return F32._on(y) and K % 32 == 0 and F32.tileable(N)
+
+
 class _ActLinearsFn(Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, bias, bn, relu: bool, drop_p: float, *Ws):
@@ -50,7 +56,23 @@ class _ActLinearsFn(Function):
             bn._update_running(st.N, st.mean, var)
         else:
             y = x
-        outs = [F32.linear_fwd(y, W, bias if i == 0 else None) for i, W in enumerate(Ws)]
+        # narrow outputs (widths the MFMA kernels do not tile, e.g. RGAT's per-head
+        # destination scores) as ONE library GEMM over their stacked weights: the input is
+        # read once for all of them, not once each
+        narrow = [i for i, W in enumerate(Ws) if (i > 0 or bias is None) and
+                  not _tiled(y, W)]
+        outs = [None] * len(Ws)
+        if len(narrow) > 1:
+            Wn = torch.cat([Ws[i] for i in narrow]).to(y.dtype)
+            zn = y @ Wn.t()
+            o = 0
+            for i in narrow:
+                n = Ws[i].shape[0]
+                outs[i] = zn[:, o:o + n]
+                o += n
+        for i, W in enumerate(Ws):
+            if outs[i] is None:
+                outs[i] = F32.linear_fwd(y, W, bias if i == 0 else None)
         del y
         ctx.st = st
         ctx.has_bias = bias is not None
@@ -73,8 +95,24 @@ class _ActLinearsFn(Function):
         dWs = []
         db = None
         want_b = ctx.has_bias and ctx.needs_input_grad[3] and gs_c[0] is not None
+        # narrow weight gradients (no MFMA tiling) as ONE library GEMM over their stacked
+        # output gradients: the activation is read once for all of them
+        narrow = [i for i, (g, W) in enumerate(zip(gs_c, Ws)) if g is not None and
+                  not (i == 0 and want_b) and not F32.wgrad_tiled(g, y, W)]
+        done = {}
+        if len(narrow) > 1:
+            gn = torch.cat([gs_c[i] for i in narrow], 1)
+            adt = torch.float64 if gn.dtype == torch.float64 else torch.float32
+            dWn = gn.t().to(adt) @ y.to(adt)
+            o = 0
+            for i in narrow:
+                n = Ws[i].shape[0]
+                done[i] = dWn[o:o + n].to(Ws[i].dtype)
+                o += n
         for i, (g, W) in enumerate(zip(gs_c, Ws)):
-            if g is None:
+            if i in done:
+                dWs.append(done[i])
+            elif g is None:
                 dWs.append(None)
             elif i == 0 and want_b:
                 dW, db = _wgrad(g, y, W, bias=True)

@@ -416,20 +416,47 @@ def linear_fwd(x: torch.Tensor, W: torch.Tensor, b: Optional[torch.Tensor] = Non
 
 def linear_dgrad(gs, Ws) -> torch.Tensor:
     """``sum_i g_i W_i`` (two terms per kernel call, the running sum chained through
-    ``cin``)."""
+    ``cin``). Narrow terms (an output width that is not a multiple of 32, e.g. the per-head
+    attention scores of RGAT's destination projection) are packed side by side into ONE
+    zero-padded 32-wide term of the same chain, instead of sending the whole sum to the
+    library GEMM."""
     K = Ws[0].shape[1]
     gs = [g if g.stride(-1) == 1 else g.contiguous() for g in gs]
-    if _on(*gs) and all(g.shape[1] % 32 == 0 for g in gs) and tileable(K):
+    if _on(*gs) and tileable(K):
+        big = [(g, W) for g, W in zip(gs, Ws) if g.shape[1] % 32 == 0]
+        small = [(g, W) for g, W in zip(gs, Ws) if g.shape[1] % 32 != 0]
+        if small:
+            n = sum(g.shape[1] for g, _ in small)
+            npad = _pad32(n)
+            gcat = gs[0].new_zeros(gs[0].shape[0], npad)
+            Wcat = Ws[0].new_zeros(npad, K)
+            off = 0
+            for g, W in small:
+                w = g.shape[1]
+                gcat[:, off:off + w] = g
+                Wcat[off:off + w] = W.to(Wcat.dtype)
+                off += w
+            big.append((gcat, Wcat))
         out = None
-        for k in range(0, len(gs), 2):
-            two = k + 1 < len(gs)
-            out = gemm_f32(gs[k], Ws[k].contiguous(), gs[k + 1] if two else None,
-                           Ws[k + 1].contiguous() if two else None, cin=out, out=out)
+        for k in range(0, len(big), 2):
+            two = k + 1 < len(big)
+            out = gemm_f32(big[k][0], big[k][1].contiguous(), big[k + 1][0] if two else None,
+                           big[k + 1][1].contiguous() if two else None, cin=out, out=out)
         return out
     out = gs[0] @ Ws[0].to(gs[0].dtype)
     for g, W in zip(gs[1:], Ws[1:]):
         out = out + g @ W.to(g.dtype)
     return out
+
+
+def _pad32(n: int) -> int:
+    return (n + 31) // 32 * 32
+
+
+def wgrad_tiled(g: torch.Tensor, x: torch.Tensor, W: torch.Tensor) -> bool:
+    """Does :func:`linear_wgrad` run the MFMA accumulator for this shape (else None)?"""
+    N, K = W.shape
+    return _on(g, x) and wgrad_ok(K, N)
 
 
 def linear_wgrad(g: torch.Tensor, x: torch.Tensor, W: torch.Tensor, bias: bool = False):

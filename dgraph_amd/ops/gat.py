@@ -33,14 +33,17 @@ from . import kernels as K
 from .csr import CSR
 
 SLOPE = 0.2
-# GPU: one kernel pass per head over that head's columns (D = C / heads of 64/128/256) instead
-# of whole rows — the SpMM's narrow-pass idea (kernels/spmm_f32.hip): each pass gathers
-# D-column slices of the neighbour rows, whose locality window the L2 / Infinity Cache holds
-# 4x longer than whole 1 KB rows at C = 256; the per-row softmax statistics are per head
-# anyway. DGRAPH_GAT_HEAD_PASSES=0: whole rows, all heads per kernel.
+# GPU: one kernel pass per head over that head's columns (D = C / heads of 64/128/256)
+# instead of whole rows — the SpMM's narrow-pass idea (kernels/spmm_f32.hip: a D-column
+# slice of the neighbour rows keeps its locality window in the L2 / Infinity Cache longer).
+# Measured on the 1/8 MAG240M RGAT step (4 heads, C = 256): the three attention kernels take
+# 660 ms per step with head passes against 510 ms with whole rows (the per-pass softmax
+# statistics, index reads and 4-rows-per-wave degree imbalance cost more than the locality
+# gains; profiles/r06/rgat_eighth_kernels_per_step*.txt), so whole rows are the default;
+# DGRAPH_GAT_HEAD_PASSES=1 selects the passes.
 import os as _os
 
-HEAD_PASSES = _os.environ.get("DGRAPH_GAT_HEAD_PASSES", "1") != "0"
+HEAD_PASSES = _os.environ.get("DGRAPH_GAT_HEAD_PASSES", "0") == "1"
 
 
 def _passes(C: int, Hh: int):
