@@ -45,11 +45,19 @@ DType dtype_of(const at::Tensor& t) {
 }
 
 // ------------------------------------------------------------------ symmetric heap
-at::Tensor heap_alloc(int64_t nbytes, int64_t device) {
+// fine = true: fine-grained device memory (hipDeviceMallocFinegrained): peers' writes over
+// xGMI are coherent for this GPU's readers at any time, not only at kernel boundaries
+// after a system-scope acquire — the heap's alternative when coarse-grained IPC memory
+// turns out not to be (the one-sided probe of bench.py measures both)
+at::Tensor heap_alloc(int64_t nbytes, int64_t device, bool fine) {
   TORCH_CHECK(nbytes > 0, "heap_alloc: nbytes must be positive");
   c10::DeviceGuard g(c10::Device(c10::kCUDA, static_cast<c10::DeviceIndex>(device)));
   void* p = nullptr;
-  DG_HIP_CHECK(hipMalloc(&p, static_cast<size_t>(nbytes)));
+  if (fine)
+    DG_HIP_CHECK(hipExtMallocWithFlags(&p, static_cast<size_t>(nbytes),
+                                       hipDeviceMallocFinegrained));
+  else
+    DG_HIP_CHECK(hipMalloc(&p, static_cast<size_t>(nbytes)));
   DG_HIP_CHECK(hipMemset(p, 0, static_cast<size_t>(nbytes)));
   auto opts = at::TensorOptions().dtype(at::kByte).device(c10::kCUDA, device);
   return at::from_blob(
@@ -306,7 +314,7 @@ TORCH_LIBRARY_FRAGMENT(dgraph_amd, m) {
   m.def("link_delay(float us, int device, int blocks=1) -> ()", &dgraph::link_delay_op);
   m.def("link_copy(Tensor src, Tensor(a!) dst, float us, int blocks, int hold) -> ()",
         &dgraph::link_copy_op);
-  m.def("heap_alloc(int nbytes, int device) -> Tensor", &dgraph::heap_alloc);
+  m.def("heap_alloc(int nbytes, int device, bool fine=False) -> Tensor", &dgraph::heap_alloc);
   m.def("ipc_get_handle(Tensor heap) -> Tensor", &dgraph::ipc_get_handle);
   m.def("ipc_open_handle(Tensor handle, int device) -> int", &dgraph::ipc_open_handle);
   m.def("ipc_close(int ptr) -> ()", &dgraph::ipc_close);

@@ -109,11 +109,38 @@ def run(send_splits, recv_splits, width: int = 64, iters: int = 5) -> dict:
     rmax, smax = rec["rows_recv_max"], rec["rows_sent_max"]
     need = (max(rmax, 1) + max(smax, 1)) * width * 4 + (4 << 20)
     SymmetricHeap.DEFAULT_BYTES = max(need, 16 << 20)
-    from .alltoallv import close_shmem_heaps, shmem_heap
+    # both heap memory kinds: coarse-grained hipMalloc (the default) and fine-grained device
+    # memory (DGRAPH_SYMHEAP_FINE=1), whose cross-GPU coherence does not rest on kernel
+    # boundaries — the first multi-GPU run shows which one the transport may rely on
+    for fine in (False, True):
+        sub = _heap_variant(rec if not fine else rec.setdefault("fine_grained", {}), fine,
+                            send, ref, ss, rs, width, iters, dev, peer_bytes, world)
+        if sub is not None:
+            rec["fine_grained" if fine else "heap_error"] = sub
+    return rec
 
-    heap = shmem_heap(None, dev)
+
+def _heap_variant(rec, fine, send, ref, ss, rs, width, iters, dev, peer_bytes, world):
+    """Probe put_rows / remote_gather on one heap kind into ``rec``; returns an error record
+    when the heap cannot be created (on every rank alike: the creation is collective)."""
+    from .alltoallv import AllToAllV, close_shmem_heaps, shmem_heap
+
+    old = os.environ.get("DGRAPH_SYMHEAP_FINE")
+    os.environ["DGRAPH_SYMHEAP_FINE"] = "1" if fine else "0"
+    try:
+        heap = shmem_heap(None, dev)
+    except Exception as e:  # noqa: BLE001 - recorded; a heap kind the runtime refuses
+        return {"error": repr(e)[:300]}
+    finally:
+        if old is None:
+            os.environ.pop("DGRAPH_SYMHEAP_FINE", None)
+        else:
+            os.environ["DGRAPH_SYMHEAP_FINE"] = old
+    rank = dist.get_rank()
+    n_recv = sum(rs)
     rec["mode"] = "device" if heap.device_completion else "host"
     rec["heap_bytes"] = heap.nbytes
+    rec["heap_memory"] = "fine-grained" if fine else "coarse-grained"
     plan = AllToAllV(ss, rs)
     out = torch.empty_like(ref)
 
@@ -164,7 +191,7 @@ def run(send_splits, recv_splits, width: int = 64, iters: int = 5) -> dict:
     probe("remote_gather", get)
     torch.cuda.synchronize(dev)
     close_shmem_heaps()
-    return rec
+    return None
 
 
 def main(argv=None) -> int:

@@ -87,7 +87,10 @@ class SymmetricHeap:
         ops = _native.ops()
         sizes = _allgather_obj(int(nbytes), group)
         self.nbytes = (max(sizes) + _ALIGN - 1) // _ALIGN * _ALIGN
-        self.local = ops.heap_alloc(self.nbytes, dev.index)
+        # DGRAPH_SYMHEAP_FINE=1: fine-grained device memory (see csrc/comm/comm_ops.cpp
+        # heap_alloc); default coarse-grained hipMalloc
+        self.fine = os.environ.get("DGRAPH_SYMHEAP_FINE", "0") == "1"
+        self.local = ops.heap_alloc(self.nbytes, dev.index, self.fine)
         handle = ops.ipc_get_handle(self.local)
         handles = _allgather_obj(bytes(handle.numpy().tobytes()), group)
         self._opened = []
