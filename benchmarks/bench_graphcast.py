@@ -55,6 +55,9 @@ def main():
                     help="one processor edge per multimesh edge pair (327 660 at level 6); "
                          "default: the reference's graph, every multimesh edge carried twice "
                          "(655 320, experiments/GraphCast/tests/test_single_graph_data.py)")
+    ap.add_argument("--partition", default="latitude", choices=["latitude", "aligned"],
+                    help="latitude: equal grid-row bands, mesh by latitude quantiles; aligned: "
+                         "one set of cost-balanced latitude cuts for grid and mesh (small halos)")
     ap.add_argument("--rehearse-world", type=int, default=0,
                     help="single process: rank --rehearse-rank of a W-way partition, every "
                          "halo exchange a loopback (patterns of all ranks built in memory)")
@@ -97,7 +100,7 @@ def main():
 
         mesh_part = load_mesh_placement(a.mesh_vertex_placement, g.mesh_xyz.shape[0], p_world)
     pg = partition_graphcast_graph(g, p_rank, p_world, mesh_part=mesh_part, group=comm.group,
-                                   rehearse=rehearse).to(dev)
+                                   rehearse=rehearse, partition=a.partition).to(dev)
     build_s = time.perf_counter() - t0
     cfg = Config()
     cfg.model.hidden_dim = a.hidden
@@ -195,6 +198,7 @@ def main():
                   **({"rehearsal": {"world": p_world, "rank": p_rank,
                                     "link_gbps": a.link_gbps}} if rehearse else {}),
                   "channels": a.channels, "channel_config": a.channel_config,
+                  "partition": a.partition if not a.mesh_vertex_placement else "placement file",
                   "mesh_edges": int(g.m2m[0].size), "duplicate_mesh_edges":
                   not a.dedup_mesh_edges,
                   "launch": "HIP graph replay" if a.cuda_graph else "eager",

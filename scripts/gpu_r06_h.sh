@@ -20,3 +20,7 @@ timeout -k 10 900 python -u bench.py > $O/bench_default_h.json 2> $O/bench_defau
 rc=$?; echo "== bench rc=$rc"; python3 -c "
 import json;d=json.loads(open('$O/bench_default_h.json').read().splitlines()[-1])
 print(d['ms_per_step'], d['value'], d['peak_mem_gb_rank0'], d.get('structureless',{}).get('ms_per_step'), d.get('bf16_stack',{}).get('ms_per_step'))"
+timeout -k 10 400 env DGRAPH_RCCL_SHARED_GPU=1 python -u bench.py --gpus 2 --scale 0.02 --steps 2 \
+  --warmup 1 --no-extra > $O/bench_w2_shared_h.json 2> $O/bench_w2_shared_h.err
+rc=$?; echo "== w2 shared rc=$rc"
+python3 -c "import json;d=json.loads(open('$O/bench_w2_shared_h.json').read().splitlines()[-1]);print(json.dumps(d['shmem_probe']))" | cut -c1-1500

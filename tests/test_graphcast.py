@@ -101,7 +101,7 @@ def _small_cfg():
     return cfg
 
 
-def _gc_dist(rank, world, out_dir, placement=None):
+def _gc_dist(rank, world, out_dir, placement=None, partition="latitude"):
     import torch.distributed as dist
 
     from dgraph_amd import Communicator
@@ -116,7 +116,8 @@ def _gc_dist(rank, world, out_dir, placement=None):
             from dgraph_amd.data.graphcast_graph import load_mesh_placement
 
             mesh_part = load_mesh_placement(placement, g.mesh_xyz.shape[0], world)
-        pg = partition_graphcast_graph(g, rank, world, mesh_part=mesh_part, group=comm.group)
+        pg = partition_graphcast_graph(g, rank, world, mesh_part=mesh_part, group=comm.group,
+                                       partition=partition)
         if mesh_part is not None:
             assert torch.equal(pg.mesh_global_ids.sort().values,
                                torch.nonzero(mesh_part == rank).reshape(-1))
@@ -138,7 +139,8 @@ def _gc_dist(rank, world, out_dir, placement=None):
         gn = torch.stack([p.grad.norm() if p.grad is not None else torch.zeros((), dtype=torch.float64)
                           for p in model.parameters()])
         if rank == 0:
-            tag = "p" if placement is not None else ""
+            tag = ("p" if placement is not None else "") + ("a" if partition == "aligned"
+                                                            else "")
             torch.save({"out": full, "loss": gl, "gn": gn}, f"{out_dir}/gc_w{world}{tag}.pt")
     finally:
         comm.destroy()
@@ -220,3 +222,49 @@ def _rehearse_cmp(rank, world):
 
 def test_graphcast_rehearsal_partition_matches(ranks):
     ranks(_rehearse_cmp, 3)
+
+
+def test_aligned_partition_small_halos_balanced():
+    """Grid rows and mesh vertices cut at the same latitudes (data/graphcast_graph.py
+    aligned_latitude_partition): on the reference's level-6 graph at W=8 every grid2mesh
+    halo is a few grid rows (the equal-row latitude partition's polar ranks: ~110K), and the
+    modelled per-rank work is within 2 % of the mean (latitude partition: +11 %)."""
+    import numpy as np
+
+    from dgraph_amd.data.graphcast_graph import (COST_WEIGHTS, aligned_latitude_partition,
+                                                 latitude_partition)
+
+    g = build_global_graph(6, (721, 1440), duplicate_mesh_edges=True)
+    W = 8
+    res = {}
+    for name, fn in (("latitude", latitude_partition), ("aligned", aligned_latitude_partition)):
+        gp, mp = fn(g, W)
+        gp, mp = gp.numpy(), mp.numpy()
+        assert gp.shape == (721 * 1440,) and mp.shape == (g.mesh_xyz.shape[0],)
+        assert gp.min() == 0 and gp.max() == W - 1 and mp.min() == 0 and mp.max() == W - 1
+        gs, gd = g.g2m
+        mgs, mgd = g.m2g
+        ms, md = g.m2m
+        cost, halo = [], []
+        for r in range(W):
+            e = mp[gd] == r  # grid2mesh edges aggregated on r
+            halo.append(np.unique(gs[e][gp[gs[e]] != r]).size)
+            cost.append(COST_WEIGHTS["grid"] * (gp == r).sum() +
+                        COST_WEIGHTS["mesh"] * (mp == r).sum() +
+                        COST_WEIGHTS["g2m"] * e.sum() +
+                        COST_WEIGHTS["m2g"] * (gp[mgd] == r).sum() +
+                        COST_WEIGHTS["m2m"] * (mp[ms] == r).sum())
+        res[name] = (max(halo), max(cost) / np.mean(cost))
+    assert res["latitude"][0] > 100_000 and res["latitude"][1] > 1.10
+    assert res["aligned"][0] < 5_000 and res["aligned"][1] < 1.02, res
+
+
+def test_graphcast_aligned_partition_matches_w1(ranks, tmp_path):
+    d = str(tmp_path)
+    ranks(_gc_dist, 1, d)
+    ranks(_gc_dist, 3, d, None, "aligned")
+    r1 = torch.load(f"{d}/gc_w1.pt", weights_only=True)
+    ra = torch.load(f"{d}/gc_w3a.pt", weights_only=True)
+    torch.testing.assert_close(ra["out"], r1["out"])
+    torch.testing.assert_close(ra["loss"], r1["loss"])
+    torch.testing.assert_close(ra["gn"], r1["gn"])
