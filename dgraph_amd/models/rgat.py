@@ -232,7 +232,10 @@ class CommAwareRGAT(nn.Module):
             nn.Linear(hidden_channels, out_channels),
         )
         self.static_halo: Optional[bool] = None  # lean path; None: by memory (R-GCN's rule)
-        self.remake_layer0 = True  # lean path: layer-0 z rebuilt in backward, not saved
+        # lean path: layer-0 z rebuilt in backward instead of saved — None (auto): when the
+        # graph has halos (W > 1: their exchanged rows add to the step's memory; one GPU's
+        # 1/8 MAG240M share fits without, 1542 vs 1666 ms per step with)
+        self.remake_layer0: Optional[bool] = None
 
     STATIC_HALO_FRAC = 0.08
 
@@ -307,6 +310,8 @@ class CommAwareRGAT(nn.Module):
         # (256 instead of 768 columns, nothing resident: a W=8 MAG240M rank's feature halo
         # is ~48 GB)
         keep_halo = CommAwareRGCN._keep_static_halo(self, xs, g)
+        remake0 = self.remake_layer0 if self.remake_layer0 is not None else any(
+            sg.halo is not None for sg in g.sources.values())
         pre: Dict[int, torch.Tensor] = {}
         for l in range(self.num_layers):
             convs = self.layers[l]
@@ -363,7 +368,7 @@ class CommAwareRGAT(nn.Module):
                 # rather than kept (saves [rows, hidden] per relation: 47 GB on one GPU's
                 # 1/8 MAG240M share)
                 rem = [((xs[s], convs[r].conv1.weight) + ((xh,) if xh is not None else ()))
-                       if (l == 0 and self.remake_layer0) else None for r in rs_src]
+                       if (l == 0 and remake0) else None for r in rs_src]
                 work += [(s, r, z, h, q) for r, z, h, q in zip(rs_src, zs, zh, rem)]
             while work:  # each relation's transformed rows released after its attention
                 s, r, z, zh, rem = work.pop(0)

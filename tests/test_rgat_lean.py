@@ -209,6 +209,7 @@ def test_rgat_lean_gpu_matches_fp64_cpu(width, heads):
         feats = {t: v[:, :width].to(dev).contiguous() for t, v in feats_cpu.items()}
         y, tr = y_cpu.to(dev), tr_cpu.to(dev)
         m = _model(width, width, 2, heads).to(dev)
+        m.remake_layer0 = True  # (the W>1 default: layer-0 z rebuilt in backward)
         out = m(feats, g)
         F.cross_entropy(out[tr], y[tr]).backward()
         got = (out.detach().cpu(), {n: p.grad.cpu() for n, p in m.named_parameters()
