@@ -21,4 +21,5 @@ for r in 0 1 2 3 4 5 6 7; do
 done
 run w8r0_aligned_g153_eager --partition aligned --rehearse-world 8 --rehearse-rank 0 --link-gbps 153
 run w8r3_latitude_g153_graph --rehearse-world 8 --rehearse-rank 3 --link-gbps 153 --cuda-graph
-bash scripts/gpu_suite.sh
+bash scripts/gpu_suite.sh; rc=$?; case $rc in 124|134|137|139) exit $rc;; esac
+bash scripts/gpu_r06_j.sh
