@@ -204,13 +204,13 @@ def latitude_partition(g: GlobalGraphCastGraph, world_size: int
     return grid_part, mesh_part
 
 
-# Work of one rank in units of one 128-wide MLP over one row: every grid point runs ~4 node
-# MLPs (embedder, encoder grid MLP, decoder node MLP, final), every mesh vertex ~6
-# (embedder, encoder node MLP, 4 processor node MLPs), every grid2mesh / mesh2grid edge one
-# edge MLP, every multimesh edge 4 (one per processor layer). Edges count at the rank that
-# aggregates them (grid2mesh: the mesh destination; mesh2grid: the grid destination;
-# multimesh: the source).
-COST_WEIGHTS = {"grid": 4.0, "mesh": 6.0, "g2m": 1.0, "m2g": 1.0, "m2m": 4.0}
+# Work of one rank, per item counted at the rank that aggregates it (grid2mesh edges: the
+# mesh destination; mesh2grid: the grid destination; multimesh: the source). Relative
+# weights fitted to the per-rank step times of W=8 rehearsals (round 6: 5 aligned ranks and
+# 2 latitude ranks, `profiles/r06/gc/`): a grid point (embedder, encoder grid MLP, decoder
+# node MLP, final MLP, plus its 3 mesh2grid edges) costs ~2.5x a multimesh edge (4
+# processor layers), a grid2mesh edge ~0.08x; mesh vertices (6 node MLPs) are few.
+COST_WEIGHTS = {"grid": 8.0, "mesh": 6.0, "g2m": 0.33, "m2g": 1.0, "m2m": 4.0}
 
 
 def aligned_latitude_partition(g: GlobalGraphCastGraph, world_size: int,

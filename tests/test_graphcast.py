@@ -228,7 +228,7 @@ def test_aligned_partition_small_halos_balanced():
     """Grid rows and mesh vertices cut at the same latitudes (data/graphcast_graph.py
     aligned_latitude_partition): on the reference's level-6 graph at W=8 every grid2mesh
     halo is a few grid rows (the equal-row latitude partition's polar ranks: ~110K), and the
-    modelled per-rank work is within 2 % of the mean (latitude partition: +11 %)."""
+    modelled per-rank work is within 2 % of the mean (latitude partition: +3.7 %)."""
     import numpy as np
 
     from dgraph_amd.data.graphcast_graph import (COST_WEIGHTS, aligned_latitude_partition,
@@ -255,7 +255,7 @@ def test_aligned_partition_small_halos_balanced():
                         COST_WEIGHTS["m2g"] * (gp[mgd] == r).sum() +
                         COST_WEIGHTS["m2m"] * (mp[ms] == r).sum())
         res[name] = (max(halo), max(cost) / np.mean(cost))
-    assert res["latitude"][0] > 100_000 and res["latitude"][1] > 1.10
+    assert res["latitude"][0] > 100_000 and res["latitude"][1] > 1.03
     assert res["aligned"][0] < 5_000 and res["aligned"][1] < 1.02, res
 
 
