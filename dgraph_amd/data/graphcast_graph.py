@@ -210,7 +210,7 @@ def latitude_partition(g: GlobalGraphCastGraph, world_size: int
 # 2 latitude ranks, `profiles/r06/gc/`): a grid point (embedder, encoder grid MLP, decoder
 # node MLP, final MLP, plus its 3 mesh2grid edges) costs ~2.5x a multimesh edge (4
 # processor layers), a grid2mesh edge ~0.08x; mesh vertices (6 node MLPs) are few.
-COST_WEIGHTS = {"grid": 8.0, "mesh": 6.0, "g2m": 0.33, "m2g": 1.0, "m2m": 4.0}
+COST_WEIGHTS = {"grid": 20.0, "mesh": 6.0, "g2m": 2.0, "m2g": 1.0, "m2m": 4.0}
 
 
 def aligned_latitude_partition(g: GlobalGraphCastGraph, world_size: int,

@@ -719,6 +719,7 @@ class FusedSAGE:
         self.correct = torch.zeros(2, dtype=torch.long, device=dev)
         self.record = False
         self._events: list = []
+        self._packs: dict = {}  # send-row packs in source order (_pack)
         self._tune_passes()
 
     def _agree(self, vals: List[int], op: str) -> List[int]:
@@ -801,9 +802,9 @@ class FusedSAGE:
         if self.send_plan is not None:  # packed by the projection GEMM
             return self._on_comm_stream(lambda: g.a2a(snd, out=rcv, async_op=True))
         if self.dev.type != "cuda":
-            K.copy_rows(Pb, src_idx=g.send_map.idx, out=snd)
+            self._pack(Pb, "send", snd)
             return g.a2a(snd, out=rcv, async_op=True)
-        K.copy_rows(Pb, src_idx=g.send_map.idx, out=snd)
+        self._pack(Pb, "send", snd)
         return self._on_comm_stream(lambda: g.a2a(snd, out=rcv, async_op=True))
 
     def _calibrate_link(self, g) -> float:
@@ -1028,6 +1029,23 @@ class FusedSAGE:
         snd = self.send_buf.view(-1)[:self.n_send * width].view(self.n_send, width)
         return snd, ptr[r0:r1 + 1], pos
 
+    def _pack(self, x: torch.Tensor, which: str, out: torch.Tensor) -> None:
+        """``out[i] = x[src[i]]`` for the send rows of the forward plan (``which`` =
+        "send") or of the pulled backward halo ("pull"), issued in SOURCE-row order: a row
+        sent to k peers is read k times back to back (the repeats hit the cache) instead of
+        k times far apart, and written to its k send-buffer positions. Each pack of a
+        structureless W=8 rank read ~3.5x its unique rows from HBM (the pack was 78 ms of a
+        565 ms step, profiles/r06/structureless_w8_rank_kernels_per_step.txt)."""
+        p = self._packs.get(which)
+        if p is None:
+            src = (self.g.send_map.idx if which == "send" else self.pull["send_rows"]).long()
+            order = torch.argsort(src, stable=True)
+            idt = torch.int32 if max(src.numel(), int(src.max()) + 1 if src.numel() else 0) \
+                < 2 ** 31 else torch.long
+            p = (src[order].to(idt).contiguous(), order.to(idt).contiguous())
+            self._packs[which] = p
+        K.copy_rows(x, src_idx=p[0], dst_idx=p[1], out=out)
+
     def _exchange(self, h: torch.Tensor, l: int):
         """Start the halo rows of hidden layer ``l``'s output ``h`` on their way from their
         owners (forward all-to-all-v, asynchronous, resident buffers): ``(recv, work)``, or
@@ -1039,14 +1057,14 @@ class FusedSAGE:
             return self._on_comm_stream(
                 lambda: g.a2a(self.send_buf, out=self.halo_buf[l], async_op=True))
         if self.dev.type != "cuda":
-            K.copy_rows(h, src_idx=g.send_map.idx, out=self.send_buf)
+            self._pack(h, "send", self.send_buf)
             return g.a2a(self.send_buf, out=self.halo_buf[l], async_op=True)
         # pack and send on the communication stream: the pack (a streaming gather of the
         # send rows) overlaps the next layer's interior work instead of preceding it. It
         # reads h (complete: the stream waits for the compute stream) and writes the send
         # buffer, whose previous exchange the compute stream has already waited for
         if self.cfg.pack_stream == "compute":
-            K.copy_rows(h, src_idx=g.send_map.idx, out=self.send_buf)
+            self._pack(h, "send", self.send_buf)
             return self._on_comm_stream(
                 lambda: g.a2a(self.send_buf, out=self.halo_buf[l], async_op=True))
         from ..comm.alltoallv import _side_stream
@@ -1054,7 +1072,7 @@ class FusedSAGE:
         side = _side_stream(self.dev)
         side.wait_stream(torch.cuda.current_stream(self.dev))
         with torch.cuda.stream(side):
-            K.copy_rows(h, src_idx=g.send_map.idx, out=self.send_buf)
+            self._pack(h, "send", self.send_buf)
             return g.a2a(self.send_buf, out=self.halo_buf[l], async_op=True)
 
     def _plan_store(self) -> dict:
@@ -1184,11 +1202,11 @@ class FusedSAGE:
             rcv = self._ring(self.ring_recv, b, c1 - c0)
 
             if self.cfg.pack_stream == "compute":
-                K.copy_rows(h[:, c0:c1], src_idx=g.send_map.idx, out=snd)
+                self._pack(h[:, c0:c1], "send", snd)
                 return self._on_comm_stream(lambda: g.a2a(snd, out=rcv, async_op=True))
 
             def go():
-                K.copy_rows(h[:, c0:c1], src_idx=g.send_map.idx, out=snd)
+                self._pack(h[:, c0:c1], "send", snd)
                 return g.a2a(snd, out=rcv, async_op=True)
             return self._on_comm_stream(go)
 
@@ -1268,7 +1286,7 @@ class FusedSAGE:
             b = k % nb
             snd = rows(self.ring_send, b, pl["n_send"], c1 - c0)
             rcv = rows(self.ring_recv, b, pl["n_recv"], c1 - c0)
-            K.copy_rows(u[:, c0:c1], src_idx=pl["send_rows"], out=snd)
+            self._pack(u[:, c0:c1], "pull", snd)
             return self._on_comm_stream(lambda: pl["a2a"](snd, out=rcv, async_op=True))
 
         works = {0: issue(0)}
@@ -1570,7 +1588,7 @@ class FusedSAGE:
                 # the dead forward send buffer; received into the output layer's dead halo
                 # buffer) and land while the S-row work and layer 0's interior rows run
                 if not self._pull_send:
-                    K.copy_rows(u, src_idx=pl["send_rows"], out=snd)
+                    self._pack(u, "pull", snd)
                 uh, work = self._on_comm_stream(
                     lambda: pl["a2a"](snd, out=rcv, async_op=True))
             elif self.pull is not None:
