@@ -91,7 +91,7 @@ class _GatherFn(Function):
     @staticmethod
     def backward(ctx, g):
         t = ctx.imap.transpose_csr()
-        gx = K.spmm(t.rowptr, t.col, g.contiguous())
+        gx = K.spmm(t.rowptr, t.col, g.contiguous(), split=ctx.imap.transpose_split())
         return gx, None
 
 
@@ -100,7 +100,7 @@ class _ScatterSumFn(Function):
     def forward(ctx, x, imap: IndexMap):
         ctx.imap = imap
         t = imap.transpose_csr()
-        return K.spmm(t.rowptr, t.col, x.contiguous())
+        return K.spmm(t.rowptr, t.col, x.contiguous(), split=imap.transpose_split())
 
     @staticmethod
     def backward(ctx, g):

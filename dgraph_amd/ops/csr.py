@@ -285,3 +285,14 @@ class IndexMap:
             slots = torch.arange(n, device=self.idx.device)
             self._t = CSR.from_coo(self.idx.long(), slots, self.num_src, n, keep_perm=False)
         return self._t
+
+    # Hub cap of the transposed segment sums. GraphCast's maps are the case it is for: a
+    # polar mesh vertex receives 3,753 grid2mesh edges and feeds 6,157 mesh2grid edges
+    # (means 40 and 76); unsplit, the one wave holding that row outlasts the rest of a W=8
+    # rank's kernel.
+    HUB_CAP = 256
+
+    def transpose_split(self) -> Optional[HubSplit]:
+        """:meth:`CSR.hub_split` of :meth:`transpose_csr` at :data:`HUB_CAP` (None when no
+        source row has more slots), for ``K.spmm(..., split=...)``."""
+        return self.transpose_csr().hub_split(self.HUB_CAP)

@@ -86,10 +86,10 @@ class _EdgePreActFn(Function):
         dP = dQ = None
         if a["P"] is not None and ctx.needs_input_grad[1]:
             t = ctx.src_map.transpose_csr()
-            dP = K.spmm(t.rowptr, t.col, d)
+            dP = K.spmm(t.rowptr, t.col, d, split=ctx.src_map.transpose_split())
         if a["Q"] is not None and ctx.needs_input_grad[2]:
             t = ctx.dst_map.transpose_csr()
-            dQ = K.spmm(t.rowptr, t.col, d)
+            dQ = K.spmm(t.rowptr, t.col, d, split=ctx.dst_map.transpose_split())
         return dY, dP, dQ, None, None, None
 
 

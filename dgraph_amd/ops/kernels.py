@@ -83,7 +83,8 @@ def spmm(
     else:
         _ref.spmm(rowptr, col, x, out, edge_weight, col_scale, row_scale, heads, beta, cap)
     if split is not None:
-        part = torch.empty(split.num_segments, F, dtype=torch.float32, device=x.device)
+        pdt = torch.float64 if x.dtype == torch.float64 else torch.float32
+        part = torch.empty(split.num_segments, F, dtype=pdt, device=x.device)
         _ref.spmm_hub_partials(split.seg_beg, split.seg_end, col, x, part, edge_weight,
                                col_scale)
         _ref.spmm_hub_reduce(part, split.hub_seg_ptr, split.hub_rows, out, row_scale)

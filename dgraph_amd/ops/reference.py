@@ -59,7 +59,9 @@ def spmm(
 
 
 def spmm_hub_partials(seg_beg, seg_end, col, x, partials, edge_weight=None, col_scale=None):
-    """fp32 sums of the hub-tail segments ``col[seg_beg[i]:seg_end[i]]`` (cf. kernels.h)."""
+    """fp32 sums of the hub-tail segments ``col[seg_beg[i]:seg_end[i]]`` (cf. kernels.h;
+    fp64 for fp64 inputs, so gradcheck sees the split path at full precision)."""
+    cdt = torch.float64 if x.dtype == torch.float64 else torch.float32
     lens = seg_end - seg_beg
     S = seg_beg.numel()
     if S == 0:
@@ -69,13 +71,13 @@ def spmm_hub_partials(seg_beg, seg_end, col, x, partials, edge_weight=None, col_
     torch.cumsum(lens, 0, out=off[1:])
     pos = seg_beg[seg] + (torch.arange(seg.numel(), device=col.device) - off[:-1][seg])
     c = col.long()[pos]
-    vals = x.float()[c]
-    w = torch.ones(pos.numel(), device=col.device)
+    vals = x.to(cdt)[c]
+    w = torch.ones(pos.numel(), dtype=cdt, device=col.device)
     if edge_weight is not None:
-        w = w * edge_weight.reshape(-1).float()[pos]
+        w = w * edge_weight.reshape(-1).to(cdt)[pos]
     if col_scale is not None:
-        w = w * col_scale.float()[c]
-    acc = torch.zeros(S, x.shape[1], device=x.device)
+        w = w * col_scale.to(cdt)[c]
+    acc = torch.zeros(S, x.shape[1], dtype=cdt, device=x.device)
     acc.index_add_(0, seg, vals * w.unsqueeze(1))
     partials[:S].copy_(acc)
     return partials
@@ -87,12 +89,13 @@ def spmm_hub_reduce(partials, hub_seg_ptr, hub_rows, out, row_scale=None):
     if nh == 0:
         return out
     cnt = hub_seg_ptr[1:] - hub_seg_ptr[:-1]
+    cdt = torch.float64 if out.dtype == torch.float64 else torch.float32
     owner = torch.repeat_interleave(torch.arange(nh, device=out.device), cnt)
-    acc = torch.zeros(nh, out.shape[1], device=out.device)
-    acc.index_add_(0, owner, partials[: owner.numel()].float())
+    acc = torch.zeros(nh, out.shape[1], dtype=cdt, device=out.device)
+    acc.index_add_(0, owner, partials[: owner.numel()].to(cdt))
     if row_scale is not None:
-        acc = acc * row_scale.float()[hub_rows].unsqueeze(1)
-    out[hub_rows] = (out[hub_rows].float() + acc).to(out.dtype)
+        acc = acc * row_scale.to(cdt)[hub_rows].unsqueeze(1)
+    out[hub_rows] = (out[hub_rows].to(cdt) + acc).to(out.dtype)
     return out
 
 
