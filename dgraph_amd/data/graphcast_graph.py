@@ -206,11 +206,12 @@ def latitude_partition(g: GlobalGraphCastGraph, world_size: int
 
 # Work of one rank, per item counted at the rank that aggregates it (grid2mesh edges: the
 # mesh destination; mesh2grid: the grid destination; multimesh: the source). Relative
-# weights fitted to the per-rank step times of W=8 rehearsals (round 6: 5 aligned ranks and
-# 2 latitude ranks, `profiles/r06/gc/`): a grid point (embedder, encoder grid MLP, decoder
-# node MLP, final MLP, plus its 3 mesh2grid edges) costs ~2.5x a multimesh edge (4
-# processor layers), a grid2mesh edge ~0.08x; mesh vertices (6 node MLPs) are few.
-COST_WEIGHTS = {"grid": 20.0, "mesh": 6.0, "g2m": 2.0, "m2g": 1.0, "m2m": 4.0}
+# weights fitted to the per-rank step times of W=8 rehearsals (round 6, `profiles/r06/gc/`,
+# after the hub-row split removed the polar ranks' one-row stragglers): a rank step is
+# ~10 ms of size-independent cost plus ~4.9e-5 ms per grid point (embedder, encoder grid
+# MLP, decoder, final MLP, its 3 mesh2grid edges and ~1.6 grid2mesh edges) and ~1.4e-5 ms
+# per multimesh edge (4 processor layers): a grid point weighs ~3.5 multimesh edges.
+COST_WEIGHTS = {"grid": 10.0, "mesh": 6.0, "g2m": 1.0, "m2g": 1.0, "m2m": 4.0}
 
 
 def aligned_latitude_partition(g: GlobalGraphCastGraph, world_size: int,
