@@ -58,6 +58,8 @@ def main():
     ap.add_argument("--partition", default="latitude", choices=["latitude", "aligned"],
                     help="latitude: equal grid-row bands, mesh by latitude quantiles; aligned: "
                          "one set of cost-balanced latitude cuts for grid and mesh (small halos)")
+    ap.add_argument("--wgrad-stream", type=int, default=1, choices=[0, 1],
+                    help="1: weight gradients on a side stream (ops.dense.deferred_wgrad)")
     ap.add_argument("--rehearse-world", type=int, default=0,
                     help="single process: rank --rehearse-rank of a W-way partition, every "
                          "halo exchange a loopback (patterns of all ranks built in memory)")
@@ -81,6 +83,7 @@ def main():
 
     from dgraph_amd import Communicator
     from dgraph_amd.data.graphcast_graph import build_global_graph, partition_graphcast_graph
+    from dgraph_amd.ops.dense import deferred_wgrad
     from dgraph_amd.data.weather import SyntheticWeatherDataset
     from dgraph_amd.models.graphcast import Config, DGraphCast, MeshEdgeBlock
     from dgraph_amd.parallel.grad_sync import GradSync
@@ -133,7 +136,8 @@ def main():
             model.zero_grad(set_to_none=True)
             out = model(x, pg)
             loss = ((out.float() - y.float()) ** 2).mean()
-            loss.backward()
+            with deferred_wgrad(bool(a.wgrad_stream)):
+                loss.backward()
             gs.all_reduce()
             if masters is not None:
                 masters.step()
@@ -202,6 +206,7 @@ def main():
                   "mesh_edges": int(g.m2m[0].size), "duplicate_mesh_edges":
                   not a.dedup_mesh_edges,
                   "launch": "HIP graph replay" if a.cuda_graph else "eager",
+                  "wgrad_stream": bool(a.wgrad_stream),
                   "precision": "bf16 compute, fp32 master weights" if masters is not None
                   else "fp32",
                   "edge_updates_per_s": edges / (ms / 1e3), "loss": float(loss),

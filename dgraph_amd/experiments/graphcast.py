@@ -30,6 +30,7 @@ from ..data.graphcast_graph import (build_global_graph, load_mesh_placement,
                                    partition_graphcast_graph)
 from ..data.weather import SyntheticWeatherDataset
 from ..models.graphcast import Config, DGraphCast
+from ..ops.dense import deferred_wgrad
 from ..parallel.grad_sync import GradSync
 from ..utils.master_weights import MasterWeights
 from ..utils.metrics import print_on_rank_zero
@@ -113,7 +114,8 @@ class GraphCastTrainer:
         self.optimizer.zero_grad(set_to_none=True)
         out = self.model(x, self.graph)
         loss = ((out.float() - y.float()) ** 2).sum() / self.n_global
-        loss.backward()
+        with deferred_wgrad():  # weight gradients off the backward's critical path
+            loss.backward()
         # sum over the graph group = this replica's gradient; mean over replicas
         self.sync.all_reduce()
         if self.num_replicas > 1:

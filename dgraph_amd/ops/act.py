@@ -21,7 +21,8 @@ import torch.nn.functional as Fn
 
 from .. import _native
 from . import f32 as F32
-from .dense import (_auto_rows_per_chunk, _native_linear_sum_ok, dual_gemm, dual_gemm_shape_ok,
+from .dense import (_DEFER, _auto_rows_per_chunk, _native_linear_sum_ok, _wgrad_chunk,
+                    defer_param_grads, dual_gemm, dual_gemm_shape_ok,
                     wgrad)
 
 ACTS = {"identity": 0, "silu": 1, "relu": 2}
@@ -109,6 +110,8 @@ class _LinearActFn(torch.autograd.Function):
             (dz,) = torch.autograd.grad(yy, zz, dy)
             db = dz.to(torch.float64 if dz.dtype == torch.float64 else torch.float32).sum(0)
         grads: List[Optional[torch.Tensor]] = []
+        wi = [i for i in range(len(Ws)) if ctx.needs_input_grad[3 + 2 * i]]
+        deferred = dz.is_cuda and _DEFER.active and bool(wi)
         for i, (x, W) in enumerate(zip(xs, Ws)):
             dx = dW = None
             if ctx.needs_input_grad[2 + 2 * i]:
@@ -116,7 +119,7 @@ class _LinearActFn(torch.autograd.Function):
                     dx = dual_gemm(dz, W.to(dz.dtype).t().contiguous())
                 else:
                     dx = F32.linear_dgrad([dz], [W])
-            if ctx.needs_input_grad[3 + 2 * i]:
+            if ctx.needs_input_grad[3 + 2 * i] and not deferred:
                 dW = F32.linear_wgrad(dz, x, W)  # fp32: split-M MFMA accumulator
                 if dW is None and dz.is_cuda:
                     L = dz.shape[0]
@@ -127,6 +130,19 @@ class _LinearActFn(torch.autograd.Function):
                     dW = dz.t().to(adt) @ x.to(adt)
                 dW = dW.to(W.dtype)
             grads += [dx, dW]
+        if deferred:
+            def comp():
+                out = []
+                for i in wi:
+                    r = F32.linear_wgrad(dz, xs[i], Ws[i])
+                    out.append(r if r is not None else
+                               wgrad(dz, xs[i].contiguous(), _wgrad_chunk(dz.shape[0])))
+                return out
+
+            if not defer_param_grads([Ws[i] for i in wi], comp,
+                                     keep_alive=(dz, *[xs[i] for i in wi])):
+                for i, r in zip(wi, comp()):  # not deferrable: the normal path
+                    grads[2 * i + 1] = r.to(Ws[i].dtype)
         dbo = db.to(ctx.bdt) if ctx.has_b and ctx.needs_input_grad[0] else None
         return (dbo, None, *grads)
 

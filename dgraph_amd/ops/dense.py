@@ -6,8 +6,13 @@
   and run as one batched GEMM (split-K over the batch), then the fp32 partial products
   are summed (deterministic, fixed order).
 * :func:`col_sum_f32` — bias gradient via the native column-sum kernel.
+* :func:`deferred_wgrad` — weight gradients of the library's linears computed on a side
+  stream, off the backward's critical path.
 """
 from __future__ import annotations
+
+import contextlib
+from typing import Callable, Optional, Sequence
 
 import torch
 
@@ -48,6 +53,98 @@ def _partials(dev: torch.device, n: int) -> torch.Tensor:
 def release_workspace() -> None:
     """Free the resident split-K workspaces (e.g. before a memory-hungry phase)."""
     _PARTIALS.clear()
+
+
+# ------------------------------------------------------------- deferred weight gradients
+class _Deferral:  # process-wide: the autograd engine runs GPU backward on its own thread
+    active = False
+    calls = 0  # backward calls whose parameter gradients went to the side stream
+
+
+_DEFER = _Deferral()
+_SIDE: dict = {}
+
+
+def _side_stream(dev: torch.device) -> torch.cuda.Stream:
+    s = _SIDE.get(dev.index)
+    if s is None:
+        s = _SIDE[dev.index] = torch.cuda.Stream(dev)
+    return s
+
+
+@contextlib.contextmanager
+def deferred_wgrad(enabled: bool = True):
+    """Inside the block, the backward of :func:`linear`, :func:`linear_sum` and
+    ``ops.act.linear_act`` computes each weight (and bias) gradient on ONE side stream
+    and adds it into the parameter's ``.grad`` there, while the data-gradient chain goes
+    on on the current stream; leaving the block joins the side stream into the current
+    one, so the gradients are complete for what follows (gradient sync, optimizer).
+
+    For steps of many small kernels (GraphCast's MLPs at 10^5 rows per rank, where one
+    GEMM fills a fraction of the 256 CUs) the weight gradients then run in the data
+    chain's idle CUs instead of after each of its kernels. The order of the adds into one
+    ``.grad`` is the backward's issue order, so results are bitwise reproducible. Every
+    use of a parameter in the step must go through these ops (a parameter whose gradient
+    also arrives through autograd's own accumulation would be added to from two streams);
+    parameters reached through another view than a plain slice of a contiguous leaf keep
+    the normal path. Capturable (the side stream forks from and joins the capturing
+    stream)."""
+    if not enabled or not torch.cuda.is_available():
+        yield
+        return
+    prev = _DEFER.active
+    _DEFER.active = True
+    cur = torch.cuda.current_stream()
+    try:
+        yield
+    finally:
+        _DEFER.active = prev
+        s = _SIDE.get(cur.device.index)
+        if s is not None:
+            cur.wait_stream(s)
+
+
+def _leaf_target(p: torch.Tensor):
+    """(leaf parameter, view of its ``.grad`` that ``p``'s gradient adds into) or None."""
+    if not p.requires_grad:
+        return None
+    if p.is_leaf:
+        return (p, None) if p.is_contiguous() else None
+    b = p._base
+    if b is None or not b.is_leaf or not b.requires_grad or not b.is_contiguous():
+        return None
+    return b, (p.size(), p.stride(), p.storage_offset() - b.storage_offset())
+
+
+def defer_param_grads(params: Sequence[torch.Tensor], compute: Callable[[], Sequence],
+                      keep_alive: Sequence[torch.Tensor] = ()) -> bool:
+    """Under :func:`deferred_wgrad`: run ``compute()`` (returning one gradient per entry
+    of ``params``) on the side stream and add each into its parameter's ``.grad``;
+    returns True (the caller then returns None for those inputs). False, with nothing
+    run, when deferral is off or a parameter is not a plain leaf / slice of one.
+    ``keep_alive``: tensors ``compute`` reads (their memory is held for the side stream)."""
+    if not _DEFER.active or not params or not params[0].is_cuda:
+        return False
+    targets = [_leaf_target(p) for p in params]
+    if any(t is None for t in targets):
+        return False
+    cur = torch.cuda.current_stream()
+    side = _side_stream(params[0].device)
+    dsts = []
+    for leaf, view in targets:
+        if leaf.grad is None:
+            leaf.grad = torch.zeros_like(leaf)  # on the current stream, before the fork
+        g = leaf.grad
+        dsts.append(g if view is None else g.as_strided(view[0], view[1],
+                                                       g.storage_offset() + view[2]))
+    _DEFER.calls += 1
+    side.wait_stream(cur)
+    for t in keep_alive:
+        t.record_stream(side)
+    with torch.cuda.stream(side):
+        for d, o in zip(dsts, compute()):
+            d.add_(o.to(d.dtype))
+    return True
 
 
 def _bmm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
@@ -104,6 +201,10 @@ def col_sum_f32(g: torch.Tensor) -> torch.Tensor:
     return K.col_sum(g)
 
 
+def _wgrad_chunk(L: int) -> int:
+    return 0 if L >= 1 << 23 else _auto_rows_per_chunk(L)
+
+
 def _auto_rows_per_chunk(L: int) -> int:
     """Chunk so the batched wgrad has >= ~128 independent output tiles (256 CUs), but
     keeps chunks >= 4096 rows."""
@@ -122,6 +223,7 @@ class _LinearFn(torch.autograd.Function):
     def forward(ctx, x, W, b):
         ctx.save_for_backward(x, W)
         ctx.has_b = b is not None
+        ctx.b = b  # the parameter itself (deferred_wgrad adds into its .grad)
         if x.dim() == 2:  # fp32 on the GPU: the exact-f32 MFMA GEMM, bias fused
             return F32.linear_fwd(x, W, b)
         return torch.nn.functional.linear(x, W, b)
@@ -136,6 +238,18 @@ class _LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = F32.linear_dgrad([g2], [W]).reshape(x.shape)
         want_b = ctx.has_b and ctx.needs_input_grad[2]
+        if ctx.needs_input_grad[1] and g2.is_cuda and _DEFER.active:
+            ps = [W, ctx.b] if want_b else [W]
+
+            def comp():
+                r = F32.linear_wgrad(g2, x2, W, bias=want_b)
+                if r is None:
+                    r = wgrad(g2, x2.contiguous(), _wgrad_chunk(g2.shape[0]))
+                    r = (r, col_sum_f32(g2)) if want_b else r
+                return r if isinstance(r, tuple) else (r,)
+
+            if defer_param_grads(ps, comp, keep_alive=(g2, x2)):
+                return dx, None, None
         if ctx.needs_input_grad[1]:
             # fp32: split-M MFMA accumulator (and the bias gradient from the same pass)
             dW = F32.linear_wgrad(g2, x2, W, bias=want_b)
@@ -147,8 +261,7 @@ class _LinearFn(torch.autograd.Function):
                 # >= 8M rows (R-GCN relation linears): the 2^14-row split-K default
                 # (1/8 MAG240M step 378 -> 357 ms); fewer rows (GraphCast, 1-2M): >= 4096
                 # rows x <= 128 chunks (50.5 -> 46.4 ms)
-                L2 = g2.shape[0]
-                dW = wgrad(g2, x2.contiguous(), 0 if L2 >= 1 << 23 else _auto_rows_per_chunk(L2))
+                dW = wgrad(g2, x2.contiguous(), _wgrad_chunk(g2.shape[0]))
             elif dW is None:
                 dW = g2.t().to(torch.float64 if g2.dtype == torch.float64 else torch.float32) @ \
                     x2.to(torch.float64 if g2.dtype == torch.float64 else torch.float32)
@@ -258,6 +371,8 @@ class _LinearSumFn(torch.autograd.Function):
         xs, Ws = flat[0::2], flat[1::2]
         g = g.contiguous()
         grads = []
+        wi = [i for i in range(len(Ws)) if ctx.needs_input_grad[3 + 2 * i]]
+        deferred = g.is_cuda and _DEFER.active and bool(wi)
         for i, (x, W) in enumerate(zip(xs, Ws)):
             dx = dW = None
             if ctx.needs_input_grad[2 + 2 * i]:
@@ -265,7 +380,7 @@ class _LinearSumFn(torch.autograd.Function):
                     dx = dual_gemm(g, W.to(g.dtype).t().contiguous())
                 else:
                     dx = F32.linear_dgrad([g], [W])
-            if ctx.needs_input_grad[3 + 2 * i]:
+            if ctx.needs_input_grad[3 + 2 * i] and not deferred:
                 dW = F32.linear_wgrad(g, x, W)  # fp32: split-M MFMA accumulator
                 if dW is None and g.is_cuda:
                     L = g.shape[0]
@@ -276,6 +391,23 @@ class _LinearSumFn(torch.autograd.Function):
                 dW = dW.to(W.dtype)
             grads += [dx, dW]
         db = None
+        if deferred:
+            ps = [Ws[i] for i in wi]
+
+            def comp():
+                out = []
+                for i in wi:
+                    r = F32.linear_wgrad(g, xs[i], Ws[i])
+                    out.append(r if r is not None else
+                               wgrad(g, xs[i].contiguous(), _wgrad_chunk(g.shape[0])))
+                return out
+
+            if not defer_param_grads(ps, comp, keep_alive=(g, *[xs[i] for i in wi])):
+                for i in wi:  # not deferrable (a parameter behind another view)
+                    r = F32.linear_wgrad(g, xs[i], Ws[i])
+                    r = r if r is not None else wgrad(g, xs[i].contiguous(),
+                                                      _wgrad_chunk(g.shape[0]))
+                    grads[2 * i + 1] = r.to(Ws[i].dtype)
         if ctx.has_b and ctx.needs_input_grad[0]:
             db = col_sum_f32(g) if g.is_cuda else \
                 g.to(torch.float64 if g.dtype == torch.float64 else torch.float32).sum(0)

@@ -6,7 +6,7 @@ cd "$R" && mkdir -p gpurun_out/r06/gc
 O=gpurun_out/r06/gc
 for r in ${RANKS:-0 1 2 3 4 5 6 7}; do
   timeout -k 10 300 python -u benchmarks/bench_graphcast.py --mode step --steps 20 --warmup 3 \
-    --partition aligned --rehearse-world 8 --rehearse-rank $r --link-gbps 153 --cuda-graph \
+    --partition aligned --rehearse-world 8 --rehearse-rank $r --link-gbps 153 --cuda-graph ${EXTRA:-} \
     > $O/w8r${r}_aligned${TAG:-2}_g153_graph.log 2>&1
   rc=$?
   grep '^{' $O/w8r${r}_aligned${TAG:-2}_g153_graph.log | python3 -c "

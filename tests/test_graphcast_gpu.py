@@ -140,3 +140,45 @@ def test_graphcast_rehearsal_link_delay_bitwise():
     assert torch.equal(res[0][0], res[1][0])
     for a, b in zip(res[0][1], res[1][1]):
         assert torch.equal(a, b)
+
+
+def test_graphcast_deferred_wgrad_bitwise():
+    """Weight gradients on the side stream (ops.dense.deferred_wgrad): the same gradients,
+    bit for bit, as the inline backward, eagerly and inside a captured HIP graph, and every
+    parameter gets one."""
+    from dgraph_amd.data.graphcast_graph import build_global_graph, partition_graphcast_graph
+    from dgraph_amd.data.weather import SyntheticWeatherDataset
+    from dgraph_amd.models.graphcast import DGraphCast
+    from dgraph_amd.ops import dense
+    from dgraph_amd.utils.graphed import GraphedStep
+
+    dev = torch.device("cuda", 0)
+    g = build_global_graph(4, (91, 180))
+    pg = partition_graphcast_graph(g, 0, 1).to(dev)
+    ds = SyntheticWeatherDataset(pg, num_channels=5, num_samples_per_year=3)
+    x, y = (t.to(dev) for t in ds[0])
+    torch.manual_seed(0)
+    model = DGraphCast(_cfg(), None).to(dev)
+
+    def step(defer):
+        model.zero_grad(set_to_none=True)
+        loss = ((model(x, pg) - y) ** 2).mean()
+        with dense.deferred_wgrad(defer):
+            loss.backward()
+        return loss
+
+    step(False)
+    ref = [p.grad.clone() for p in model.parameters()]
+    c0 = dense._DEFER.calls
+    step(True)
+    assert dense._DEFER.calls > c0, "no gradient went to the side stream"
+    got = [p.grad.clone() for p in model.parameters()]
+    for (n, _), a, b in zip(model.named_parameters(), got, ref):
+        assert torch.equal(a, b), n
+    run = GraphedStep(lambda: step(True), warmup=1)
+    for _ in range(3):
+        run()
+    torch.cuda.synchronize()
+    assert run.captured
+    for (n, p), b in zip(model.named_parameters(), ref):
+        assert torch.equal(p.grad, b), n
