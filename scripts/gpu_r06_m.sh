@@ -4,7 +4,7 @@
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 cd "$R" && mkdir -p gpurun_out/r06/gc
 O=gpurun_out/r06/gc
-timeout -k 10 400 python -u -m pytest tests/test_hub_split.py tests/test_graphcast.py tests/test_graphcast_gpu.py -m gpu -q \
+timeout -k 10 400 python -u -m pytest tests/test_indexmap_hub_split.py tests/test_graphcast.py tests/test_graphcast_gpu.py -m gpu -q \
   --timeout 120 --timeout-method thread -p no:cacheprovider > $O/hub_tests.log 2>&1
 rc=$?; echo "== pytest rc=$rc"; tail -3 $O/hub_tests.log
 case $rc in 0) ;; *) exit $rc;; esac

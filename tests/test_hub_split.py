@@ -1,84 +1,99 @@
-"""Hub-row split of the transposed segment sums (``IndexMap.transpose_split``): scatter_sum,
-the gather adjoint and the edge pre-activation's endpoint gradients give the unsplit result
-when a few source rows own most slots (GraphCast's polar mesh vertices)."""
+"""Hub-row splitting of the CSR SpMM (csrc/kernels/spmm.hip: degree-capped main pass +
+hub-tail segment partials + fixed-order reduction) equals the unsplit aggregation, against
+an fp64 reference, on a power-law graph (a few rows with 10^3-10^4 neighbours)."""
 import pytest
 import torch
-import torch.nn.functional as F
 
 from dgraph_amd.ops import kernels as K
-from dgraph_amd.ops.aggregate import gather, scatter_sum
-from dgraph_amd.ops.csr import IndexMap
-from dgraph_amd.ops.edge_mlp import edge_pre_activation
+from dgraph_amd.ops.csr import CSR
 
 
-def _skewed(n_rows, n_slots, seed=0):
+def _powerlaw_csr(n=3000, nnz=60000, seed=0, device="cpu"):
     g = torch.Generator().manual_seed(seed)
-    idx = torch.randint(0, n_rows, (n_slots,), generator=g)
-    idx[: n_slots // 3] = 0  # one hub row with a third of the slots
-    idx[n_slots // 3: n_slots // 2] = n_rows - 1
-    return idx[torch.randperm(n_slots, generator=g)]
+    u = torch.rand(nnz, generator=g)
+    rows = (u ** 3 * n).long().clamp(max=n - 1)  # heavy skew: row 0 gets ~n^(1/3) share
+    rows = rows[rows % 7 != 3]  # and some empty rows (row compaction)
+    nnz = rows.numel()
+    cols = torch.randint(0, n, (nnz,), generator=g)
+    return CSR.from_coo(rows, cols, n, n).to(device)
 
 
-def test_transpose_split_finds_hubs(monkeypatch):
-    monkeypatch.setattr(IndexMap, "HUB_CAP", 8)
-    im = IndexMap(_skewed(10, 90), 10)
-    s = im.transpose_split()
-    assert s is not None and set(s.hub_rows.tolist()) >= {0, 9}
-    monkeypatch.setattr(IndexMap, "HUB_CAP", 1000)
-    assert IndexMap(_skewed(10, 90), 10).transpose_split() is None
+def _dense_ref(csr, x, ew=None, cs=None, rs=None, beta=0.0, out0=None):
+    rows = csr.row_ids()
+    c = csr.col.long()
+    w = torch.ones(c.numel(), dtype=torch.float64)
+    if ew is not None:
+        w = w * ew.double().cpu()
+    if cs is not None:
+        w = w * cs.double().cpu()[c.cpu()]
+    acc = torch.zeros(csr.num_rows, x.shape[1], dtype=torch.float64)
+    acc.index_add_(0, rows.cpu(), x.double().cpu()[c.cpu()] * w.unsqueeze(1))
+    if rs is not None:
+        acc = acc * rs.double().cpu().unsqueeze(1)
+    if beta:
+        acc = acc + beta * out0.double().cpu()
+    return acc
 
 
-def test_scatter_gather_split_gradcheck(monkeypatch):
-    monkeypatch.setattr(IndexMap, "HUB_CAP", 4)
-    idx = _skewed(7, 60, seed=1)
-    im = IndexMap(idx, 7)
-    e = torch.randn(60, 3, dtype=torch.float64, requires_grad=True)
-    torch.testing.assert_close(scatter_sum(e, im),
-                               torch.zeros(7, 3, dtype=torch.float64).index_add_(0, idx, e))
-    assert torch.autograd.gradcheck(lambda t: scatter_sum(t, im), (e,))
-    x = torch.randn(7, 3, dtype=torch.float64, requires_grad=True)
-    assert torch.autograd.gradcheck(lambda t: gather(t, im), (x,))
+def test_split_metadata_covers_every_entry_once():
+    csr = _powerlaw_csr()
+    cap = 64
+    sp = csr.hub_split(cap)
+    deg = csr.degree()
+    assert sp is not None and torch.equal(sp.hub_rows, torch.nonzero(deg > cap).reshape(-1))
+    assert bool(((sp.seg_end - sp.seg_beg) <= cap).all())
+    assert bool(((sp.seg_end - sp.seg_beg) > 0).all())
+    # tails: entries [rowptr[r] + cap, rowptr[r+1]) of every hub row, tiled exactly
+    for h in range(sp.hub_rows.numel()):
+        r = int(sp.hub_rows[h])
+        a, b = int(sp.hub_seg_ptr[h]), int(sp.hub_seg_ptr[h + 1])
+        assert int(sp.seg_beg[a]) == int(csr.rowptr[r]) + cap
+        assert int(sp.seg_end[b - 1]) == int(csr.rowptr[r + 1])
+        assert torch.equal(sp.seg_beg[a + 1:b], sp.seg_end[a:b - 1])
+    assert csr.hub_split(cap) is sp  # cached
+    assert csr.hub_split(10 ** 9) is None
 
 
-def test_edge_pre_activation_split_gradcheck(monkeypatch):
-    monkeypatch.setattr(IndexMap, "HUB_CAP", 4)
-    Vs, Vd, E, H = 6, 5, 50, 3
-    src, dst = _skewed(Vs, E, seed=2), _skewed(Vd, E, seed=3)
-    Y = torch.randn(E, H, dtype=torch.float64, requires_grad=True)
-    P = torch.randn(Vs, H, dtype=torch.float64, requires_grad=True)
-    Q = torch.randn(Vd, H, dtype=torch.float64, requires_grad=True)
-    sm, dm = IndexMap(src, Vs), IndexMap(dst, Vd)
-    fn = lambda y, p, q: edge_pre_activation(y, p, q, sm, dm, "silu")  # noqa: E731
-    torch.testing.assert_close(fn(Y, P, Q), F.silu(Y + P[src] + Q[dst]))
-    assert torch.autograd.gradcheck(fn, (Y, P, Q))
+def _check(device, dtype, cap, weighted, beta, F, compact=False):
+    csr = _powerlaw_csr(device=device)
+    g = torch.Generator().manual_seed(cap + F)
+    x = torch.randn(csr.num_cols, F, generator=g).to(device=device, dtype=dtype)
+    ew = torch.rand(csr.nnz, generator=g).to(device) if weighted else None
+    cs = (torch.rand(csr.num_cols, generator=g) + 0.5).to(device) if weighted else None
+    rs = csr.inv_degree()
+    out0 = torch.randn(csr.num_rows, F, generator=g).to(device=device, dtype=dtype)
+    out = out0.clone()
+    if compact:
+        # row-compacted CSR (empty rows skipped): the empty rows keep beta * out0
+        cc = csr.compact_rows()
+        assert cc.num_rows < csr.num_rows and cc.col is csr.col
+        K.spmm(cc.rowptr, cc.col, x, out, edge_weight=ew, col_scale=cs, row_scale=rs,
+               beta=beta, split=cc.hub_split(cap), row_map=cc.row_map)
+    else:
+        K.spmm(csr.rowptr, csr.col, x, out, edge_weight=ew, col_scale=cs, row_scale=rs,
+               beta=beta, split=csr.hub_split(cap))
+    ref = _dense_ref(csr, x, ew, cs, rs, beta, out0)
+    if compact and beta == 0.0:
+        empty = (csr.degree() == 0).cpu()
+        ref[empty] = out0.double().cpu()[empty]
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    torch.testing.assert_close(out.double().cpu(), ref, atol=tol, rtol=tol)
+
+
+@pytest.mark.parametrize("cap", [16, 64, 1000])
+@pytest.mark.parametrize("weighted", [False, True])
+@pytest.mark.parametrize("beta", [0.0, 1.0])
+@pytest.mark.parametrize("compact", [False, True])
+def test_split_spmm_cpu(cap, weighted, beta, compact):
+    _check("cpu", torch.float32, cap, weighted, beta, 24, compact)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("Fdim", [64, 128])
-def test_scatter_sum_hub_split_gpu(Fdim):
-    """Native path at GraphCast's skew (a 6,000-slot row among ~76-slot rows, 128
-    features): equal to an fp64 reference, bitwise run to run, and to the unsplit pass."""
-    from dgraph_amd import _native
-
-    assert _native.load(), "native library missing"
-    dev = torch.device("cuda", 0)
-    g = torch.Generator().manual_seed(5)
-    R, per = 40_000, 76
-    idx = torch.randint(0, R, (R * per,), generator=g)
-    idx[:6000] = 17
-    idx[6000:9753] = R - 3
-    im = IndexMap(idx.to(dev), R)
-    assert im.transpose_split() is not None
-    e = torch.randn(idx.numel(), Fdim, generator=g)
-    ed = e.to(dev)
-    outs = [scatter_sum(ed, im) for _ in range(3)]
-    assert all(torch.equal(outs[0], o) for o in outs[1:])
-    ref = torch.zeros(R, Fdim, dtype=torch.float64).index_add_(0, idx, e.double())
-    torch.testing.assert_close(outs[0].double().cpu(), ref, atol=2e-4, rtol=1e-4)
-    t = im.transpose_csr()
-    plain = K.spmm(t.rowptr, t.col, ed)
-    torch.testing.assert_close(outs[0], plain, atol=2e-4, rtol=1e-5)
-    # the adjoint (gather backward) through the same split
-    x = torch.randn(R, Fdim, device=dev, requires_grad=True)
-    gather(x, im).backward(ed)
-    torch.testing.assert_close(x.grad, outs[0], atol=0, rtol=0)
+@pytest.mark.parametrize("cap", [16, 256])
+@pytest.mark.parametrize("weighted", [False, True])
+@pytest.mark.parametrize("beta", [0.0, 1.0])
+@pytest.mark.parametrize("dtype,F", [(torch.bfloat16, 128), (torch.bfloat16, 256),
+                                     (torch.bfloat16, 40), (torch.float32, 64)])
+@pytest.mark.parametrize("compact", [False, True])
+def test_split_spmm_gpu(cap, weighted, beta, dtype, F, compact):
+    _check("cuda", dtype, cap, weighted, beta, F, compact)
