@@ -301,6 +301,27 @@ class _Adj:
         return self.rp.numel() * 8 + self.mid.numel() * 8 + self.col.numel() * 4
 
 
+class _Budget:
+    """The setup's device-memory plan (``FusedSAGE._plan_memory``): ``free`` bytes,
+    ``need_h`` (activations and halo rows), ``other`` (workspaces and every buffer chosen so
+    far), the ``margin`` an optional buffer must leave, the chunk arena's row widths
+    (``wA`` aggregate, ``wB`` logit / gradient) and the sub-plan exchange's bytes."""
+
+    def __init__(self, free: int, need_h: int, other: int, margin: int, wA: int, wB: int):
+        self.free, self.need_h, self.other, self.margin = free, need_h, other, margin
+        self.wA, self.wB = wA, wB
+        self.sub_bytes = 0
+
+    def room(self) -> int:
+        """Bytes not yet planned."""
+        return self.free - self.need_h - self.other
+
+    def describe(self, halo_bytes: int, dev) -> str:
+        return (f"FusedSAGE: activations {self.need_h / 2**30:.1f} GiB (halo rows "
+                f"{halo_bytes / 2**30:.1f}) + workspace {self.other / 2**30:.1f} GiB exceed the "
+                f"{self.free / 2**30:.1f} GiB free on {dev}")
+
+
 class FusedSAGE:
     """The fp32 training step of a 2- or 3-layer :class:`~dgraph_amd.models.sage.GraphSAGE`
     (mean aggregator, ReLU between layers, no dropout) over a :class:`DistGraph`.
@@ -323,7 +344,7 @@ class FusedSAGE:
         if not supported(model, x):
             raise ValueError("FusedSAGE: unsupported model/feature shape")
         # the schedule knobs, resolved now (environment read at construction, not import)
-        self.cfg = cfg = config if config is not None else ExecutorConfig.from_env()
+        self.cfg = config if config is not None else ExecutorConfig.from_env()
         dev = x.device
         self.dev = dev
         if dev.type == "cuda":
@@ -343,8 +364,7 @@ class FusedSAGE:
             xp[:, :self.d0_in] = x
             x = xp
         self.model, self.g, self.x = model, graph, x.contiguous()
-        L, H = graph.L, graph.H
-        self.L, self.H = L, H
+        self.L, self.H = graph.L, graph.H
         self.nl = len(model.layers)
         self.hid = model.layers[0].out_dim
         self.C = model.layers[-1].out_dim
@@ -354,7 +374,29 @@ class FusedSAGE:
         self.Cg = _width_at_least(_pad_to(self.C, 32) if self.C > 128 else self.C,
                                   (128, 176, 192, 256))
         self.inv_n = 1.0 / max(int(n_train), 1)
-        # ---- loss / eval rows, sorted (chunk ranges are searchsorted)
+        # setup phases: rows, adjacency (collective parts included), the memory plan (every
+        # schedule choice, agreed over the plan's group), the row chunks, the buffers
+        self._setup_rows(graph, train_idx, y_train, eval_idx, y_eval, eval_is_val)
+        self._setup_adjacency(graph, release_graph)
+        b = self._plan_memory(graph, reserve_bytes)
+        self._plan_chunks(chunk_rows, b)
+        self._allocate(graph, b)
+        self.row_loss = torch.zeros(self.T.numel(), dtype=torch.float32, device=dev)
+        self.hit = torch.zeros(self.E.numel(), dtype=torch.uint8, device=dev)
+        self.E_val_l = self.E_val.long()
+        self.correct = torch.zeros(2, dtype=torch.long, device=dev)
+        self.record = False
+        self._events: list = []
+        self._packs: dict = {}  # send-row packs in source order (_pack)
+        self._tune_passes()
+
+    # ------------------------------------------------------------------ setup phases
+    def _setup_rows(self, graph: DistGraph, train_idx, y_train, eval_idx, y_eval,
+                    eval_is_val) -> None:
+        """Loss / eval rows (sorted: chunk ranges are searchsorted) and the gradient support
+        S (rows where dZ of the last hidden layer can be nonzero), with the output-layer
+        backward's sub-plan when remote loss rows reach this rank."""
+        dev, L = self.dev, self.L
         t, tp = torch.sort(train_idx.long())
         self.T, self.yT = t.contiguous(), y_train[tp].contiguous()
         e, ep = torch.sort(eval_idx.long())
@@ -362,7 +404,6 @@ class FusedSAGE:
         self.E_val = eval_is_val[ep].contiguous()
         self.inv_deg = graph.inv_deg
         self.invdegT = self.inv_deg[self.T].contiguous()
-        # ---- gradient support S (rows where dZ of the last hidden layer can be nonzero)
         it_t, _, sub = graph._restricted(self.T)  # A[T, :L]^T (rows L, cols |T|), sub-plan
         parts = [self.T, it_t.compact_rows().row_map.long()]
         if sub is not None:
@@ -388,13 +429,17 @@ class FusedSAGE:
             # (my halo rows adjacent to a loss row, the rows of mine the peers' loss rows
             # neighbour: the project-first output layer pulls h over the reversed sub-plan)
             self._sub_pull = (sub[3], sub[4], a2a_sub)
-        # ---- adjacency: interior + halo entries of a row in one array
+
+    def _setup_adjacency(self, graph: DistGraph, release_graph: bool) -> None:
+        """The one-array adjacency (interior + halo entries of a row), its transposed
+        blocks, the pulled backward halo's plan and the link calibration (both collective,
+        built by every rank before the memory plan can raise), and the interior prefix."""
+        cfg, dev, L = self.cfg, self.dev, self.L
         it = graph.interior
         self.adj = _Adj(it, graph.halo, L)
         # B1b's transposed interior aggregation: the interior part of the rows themselves
         # when the interior block is symmetric, else its transpose
         self.itT = None if it.symmetric else it.transpose()
-        # (collective: built by every rank before the memory plan can raise)
         self.pull = self._pull_plan(graph) \
             if (cfg.bwd_halo == "pull" and self.nl == 3 and graph.symmetric and
                 graph.send_map is not None) else None
@@ -409,7 +454,7 @@ class FusedSAGE:
         self.send_st = graph.send_map.transpose_csr().compact_rows() if push else None
         self.nnz_it, self.nnz_h = self.adj.nnz_int, self.adj.nnz_halo
         # entries of the S-row aggregation (B1a), counted on the host once
-        self.nnz_S = int((self.adj.rp[S + 1] - self.adj.rp[S]).sum())
+        self.nnz_S = int((self.adj.rp[self.S + 1] - self.adj.rp[self.S]).sum())
         # ---- interior prefix: rows [0, Li) have no halo entry and are sent to nobody
         bnd = self.adj.halo_degree() > 0
         if graph.send_map is not None and graph.send_map.idx.numel():
@@ -423,8 +468,16 @@ class FusedSAGE:
         if release_graph:
             graph.release_csr()
             del it
-        # ---- memory plan (the planning above left cached temporaries: return them first,
-        # and count what the caching allocator still holds unused as free)
+
+    def _plan_memory(self, graph: DistGraph, reserve_bytes: int) -> "_Budget":
+        """Every schedule choice, from the device's free memory: streamed halos and their
+        shape, the kept aggregates, the projected output layer, the boundary stores, the
+        pipeline-fill self term. Choices that change the sequence of collectives are agreed
+        over the plan's group; a plan that does not fit raises MemoryError on every rank
+        alike, before any allocation."""
+        cfg, dev, L, H = self.cfg, self.dev, self.L, self.H
+        # (the planning above left cached temporaries: return them first, and count what
+        # the caching allocator still holds unused as free)
         if dev.type == "cuda":
             torch.cuda.empty_cache()
             free = torch.cuda.mem_get_info(dev)[0] + \
@@ -450,7 +503,8 @@ class FusedSAGE:
         other = 4 * nT * self.Cg + 4 * slab_floats * ncu * F32.WgradAcc.UNITS_PER_CU + \
             (3 << 29) + \
             (4 * nT * self.hid if self.u_sep else 0)
-        wA, wB = max(self.hid, self.d0), max(self.Cp, self.hid)
+        b = _Budget(free, need_h, other, 16 << 30 if dev.type == "cuda" else 0,
+                    wA=max(self.hid, self.d0), wB=max(self.Cp, self.hid))
         # W > 1: the received halo rows live through the step — the input's (exchanged once,
         # kept), every hidden layer's (the backward reads them) — and each exchange's send
         # rows while it is in flight: planned here, not discovered by the allocator
@@ -462,16 +516,18 @@ class FusedSAGE:
             if graph.send_map is not None else 0
         self.halo_bytes = 4 * (H * self.d0 + (self.nl - 1) * H * self.hid + n_send * self.hid)
         self.stream, self.cw, self.nbuf = False, 0, 0
-        other += x_tr
+        b.other += x_tr
         w_lh = self.d0 if self.nl == 2 else self.hid  # width of the last hidden layer's input
+        self.w_lh = w_lh
         # the output-layer backward's sub-plan exchange (halo rows adjacent to the loss rows,
         # A[T, halo]^T u2 out, owners' rows back): resident buffers in storage that is dead
         # during that exchange — the last received-halo / send buffers, or the streamed ring
         self.sub_rows = (0, 0)
         if self.sub is not None:
             self.sub_rows = (self.sub[0].rowptr.numel() - 1, self.sub[1].total_recv)
-        sub_bytes = 4 * self.hid * (self.sub_rows[0] + self.sub_rows[1])
-        full_ok = dev.type != "cuda" or need_h + self.halo_bytes + other + (1 << 28) <= free
+        b.sub_bytes = 4 * self.hid * (self.sub_rows[0] + self.sub_rows[1])
+        full_ok = dev.type != "cuda" or \
+            b.need_h + self.halo_bytes + b.other + (1 << 28) <= b.free
         # Choices that change the SEQUENCE of collectives (streamed halos and their shape,
         # the projected output layer) are agreed over the plan's group: each rank plans from
         # its own free memory and partition sizes, and one rank choosing differently would
@@ -491,35 +547,78 @@ class FusedSAGE:
             shapes = cfg.shapes()
             fit, hbs = [], []
             for cw, nb in shapes:
-                ring = max(nb * (H + n_send) * cw * 4, sub_bytes)
+                ring = max(nb * (H + n_send) * cw * 4, b.sub_bytes)
                 hb = 4 * H * self.d0 + ring + stores
                 hbs.append(hb)
                 fit.append(int(self.hid % cw == 0 and (
-                    dev.type != "cuda" or need_h + hb + other + (1 << 28) <= free)))
+                    dev.type != "cuda" or b.need_h + hb + b.other + (1 << 28) <= b.free)))
             fit = self._agree(fit, "min")  # the first shape EVERY rank has room for
             for (cw, nb), ok, hb in zip(shapes, fit, hbs):
                 if ok:
                     self.stream, self.cw, self.nbuf, self.halo_bytes = True, cw, nb, hb
                     break
-        need_h += self.halo_bytes
-        fits = dev.type != "cuda" or need_h + other + (1 << 28) <= free
+        b.need_h += self.halo_bytes
+        fits = dev.type != "cuda" or b.need_h + b.other + (1 << 28) <= b.free
         if graph.send_map is not None and not bool(self._agree([int(fits)], "min")[0]):
             # fail here, before any allocation (and after every collective of the setup), on
             # every rank alike, so a caller can skip the configuration instead of dying
             # mid-step
-            raise MemoryError(
-                f"FusedSAGE: activations {need_h / 2**30:.1f} GiB (halo rows "
-                f"{self.halo_bytes / 2**30:.1f}) + workspace {other / 2**30:.1f} GiB exceed the "
-                f"{free / 2**30:.1f} GiB free on {dev}" + ("" if not fits else
-                                                        " of another rank of the group"))
+            raise MemoryError(b.describe(self.halo_bytes, dev) +
+                              ("" if not fits else " of another rank of the group"))
         if not fits:
-            raise MemoryError(
-                f"FusedSAGE: activations {need_h / 2**30:.1f} GiB (halo rows "
-                f"{self.halo_bytes / 2**30:.1f}) + workspace {other / 2**30:.1f} GiB exceed the "
-                f"{free / 2**30:.1f} GiB free on {dev}")
-        margin = 16 << 30 if dev.type == "cuda" else 0
-        # the input-layer backward's S-compacted transposed adjacency (COMPACT_T): built when
-        # it leaves at least 1 GB for the chunk arena (it shrinks the arena, not the plan)
+            raise MemoryError(b.describe(self.halo_bytes, dev))
+        self._plan_compact_t(b)
+        # the last hidden layer's input aggregate on the S rows kept from the forward (else
+        # re-aggregated in the backward); streamed halos keep it in aS_full (planned above)
+        self.aS_keep = None
+        need_as = self.nS * self.w_lh * 4
+        self.keep_as = cfg.keep_as == "on" or self.stream or (
+            cfg.keep_as == "auto" and b.room() - need_as > b.margin)
+        if self.keep_as and not self.stream:
+            b.other += need_as
+        # layer 0's input aggregate kept from the forward for the backward (else recomputed)
+        self.agg0 = None
+        need0 = L * self.d0 * 4
+        if self.nl == 3 and cfg.keep_agg0 != "off" and (
+                cfg.keep_agg0 == "on" or b.room() - need0 > b.margin):
+            self.agg0 = torch.empty(L, self.d0, dtype=torch.float32, device=dev)
+            b.other += need0
+        # W > 1: the output layer's projection [L, Cp] (PROJECT_FIRST), after the kept
+        # aggregates (those save whole aggregation passes)
+        self.pf = None
+        need_pf = L * self.Cp * 4
+        if graph.send_map is not None and cfg.project_first != "off" and self.Cp < self.hid:
+            want_pf = cfg.project_first == "on" or b.room() - need_pf > b.margin
+            if bool(self._agree([int(want_pf)], "min")[0]):  # (changes the exchanges)
+                self.pf = torch.empty(L, self.Cp, dtype=torch.float32, device=dev)
+                b.other += need_pf
+                self._aggT_setup()
+        # W > 1: a whole-layer aggregate buffer lets the interior part of the OUTPUT layer's
+        # boundary rows run while its halo rows are in flight (hidden layers use their own
+        # output buffer for that). Planned after the kept aggregates: those save whole
+        # aggregation passes, the store only exposed exchange time
+        self.use_store = self._plan_store()
+        self.agg_full = None
+        need_full = (L - self.Li) * b.wA * 4
+        if graph.send_map is not None and cfg.overlap and self.Li < L and not self.stream \
+                and self.use_store["out"] and b.room() - need_full > b.margin:
+            self.agg_full = torch.empty(L - self.Li, b.wA, dtype=torch.float32, device=dev)
+            b.other += need_full
+        # streamed output layer: its self term h W_self + b for every row, computed during
+        # the first column block's transfer (the pipeline fill), when the plan has room
+        self.zself = None
+        need_z = L * self.Cp * 4
+        if self.stream and cfg.stream_out_fill and self.pf is None and \
+                b.room() - need_z > b.margin:
+            self.zself = torch.empty(L, self.Cp, dtype=torch.float32, device=dev)
+            b.other += need_z
+        return b
+
+    def _plan_compact_t(self, b: "_Budget") -> None:
+        """The input-layer backward's S-compacted transposed adjacencies (COMPACT_T): built
+        when they leave at least 1 GB for the chunk arena (they shrink the arena, not the
+        plan)."""
+        cfg, dev, L = self.cfg, self.dev, self.L
         self.TS = None
         if self.nl == 3 and cfg.compact_t != "off":
             if self.itT is not None:
@@ -529,10 +628,10 @@ class FusedSAGE:
             nnz_ts = _compact_by_map(src[0], src[1], src[2], self.smap, L, count_only=True) \
                 if L else 0
             ts_bytes = nnz_ts * 4 + (L + 1) * 8
-            room = free - need_h - other - (1 << 28)
-            if cfg.compact_t == "on" or dev.type != "cuda" or room - ts_bytes >= (1 << 30):
+            if cfg.compact_t == "on" or dev.type != "cuda" or \
+                    b.room() - (1 << 28) - ts_bytes >= (1 << 30):
                 self.TS = _compact_by_map(src[0], src[1], src[2], self.smap, L)
-                other += ts_bytes
+                b.other += ts_bytes
         # the same for the halo rows' transposed aggregation of u (the reverse exchange's
         # payload, computed before the S-row work so the exchange overlaps it)
         self.HTS = None
@@ -542,62 +641,21 @@ class FusedSAGE:
                                     count_only=True)
             hts_bytes = nnz_h * 4 + (Hn + 1) * 8
             if cfg.compact_t == "on" or dev.type != "cuda" or \
-                    free - need_h - other - (1 << 28) - hts_bytes >= (1 << 30):
+                    b.room() - (1 << 28) - hts_bytes >= (1 << 30):
                 self.HTS = _compact_by_map(self.haloT.rowptr, self.haloT.col, None, self.smap,
                                            Hn)
-                other += hts_bytes
-        # the last hidden layer's input aggregate on the S rows kept from the forward (else
-        # re-aggregated in the backward); streamed halos keep it in aS_full (planned above)
-        self.aS_keep = None
-        self.w_lh = w_lh
-        need_as = self.nS * self.w_lh * 4
-        self.keep_as = cfg.keep_as == "on" or self.stream or (
-            cfg.keep_as == "auto" and free - need_h - other - need_as > margin)
-        if self.keep_as and not self.stream:
-            other += need_as
-        # layer 0's input aggregate kept from the forward for the backward (else recomputed)
-        self.agg0 = None
-        need0 = L * self.d0 * 4
-        if self.nl == 3 and cfg.keep_agg0 != "off" and (
-                cfg.keep_agg0 == "on" or free - need_h - other - need0 > margin):
-            self.agg0 = torch.empty(L, self.d0, dtype=torch.float32, device=dev)
-            other += need0
-        # W > 1: the output layer's projection [L, Cp] (PROJECT_FIRST), after the kept
-        # aggregates (those save whole aggregation passes)
-        self.pf = None
-        need_pf = L * self.Cp * 4
-        if graph.send_map is not None and cfg.project_first != "off" and self.Cp < self.hid:
-            want_pf = cfg.project_first == "on" or free - need_h - other - need_pf > margin
-            if bool(self._agree([int(want_pf)], "min")[0]):  # (changes the exchanges)
-                self.pf = torch.empty(L, self.Cp, dtype=torch.float32, device=dev)
-                other += need_pf
-                self._aggT_setup()
-        # W > 1: a whole-layer aggregate buffer lets the interior part of the OUTPUT layer's
-        # boundary rows run while its halo rows are in flight (hidden layers use their own
-        # output buffer for that). Planned after the kept aggregates: those save whole
-        # aggregation passes, the store only exposed exchange time
-        self.use_store = self._plan_store()
-        self.agg_full = None
-        need_full = (L - self.Li) * wA * 4
-        if graph.send_map is not None and cfg.overlap and self.Li < L and not self.stream \
-                and self.use_store["out"] and free - need_h - other - need_full > margin:
-            self.agg_full = torch.empty(L - self.Li, wA, dtype=torch.float32, device=dev)
-            other += need_full
-        # streamed output layer: its self term h W_self + b for every row, computed during
-        # the first column block's transfer (the pipeline fill), when the plan has room
-        self.zself = None
-        need_z = L * self.Cp * 4
-        if self.stream and cfg.stream_out_fill and self.pf is None and \
-                free - need_h - other - need_z > margin:
-            self.zself = torch.empty(L, self.Cp, dtype=torch.float32, device=dev)
-            other += need_z
-        spare = max(free - need_h - other, 1 << 28)
-        per_row = 4 * (wA + wB)  # aggregate + logit/gradient chunk buffers
-        cr = chunk_rows or cfg.chunk_rows
+                b.other += hts_bytes
+
+    def _plan_chunks(self, chunk_rows: int, b: "_Budget") -> None:
+        """Row chunks sized from what the plan left (never straddling the interior /
+        boundary split), with each chunk's loss / eval / support row ranges."""
+        L = self.L
+        spare = max(b.room(), 1 << 28)
+        per_row = 4 * (b.wA + b.wB)  # aggregate + logit/gradient chunk buffers
+        cr = chunk_rows or self.cfg.chunk_rows
         if cr <= 0:
             cr = int(min(max(spare // per_row, 1 << 16), 1 << 21))
         self.cr = max(256, min(int(cr), max(L, 256)))
-        # chunks never straddle the interior / boundary split
         self.chunks = _ranges(0, self.Li, self.cr) + _ranges(self.Li, L, self.cr)
         if not self.chunks:
             self.chunks = [(0, 0)]
@@ -607,14 +665,19 @@ class FusedSAGE:
         self.ch_T = [(ss(self.T, r0), ss(self.T, r1)) for r0, r1 in self.chunks]
         self.ch_E = [(ss(self.E, r0), ss(self.E, r1)) for r0, r1 in self.chunks]
         self.ch_S = [(ss(self.S, r0), ss(self.S, r1)) for r0, r1 in self.chunks]
-        self.ch_Tloc = [(self.T[a:b] - r0).contiguous()
-                        for (r0, _), (a, b) in zip(self.chunks, self.ch_T)]
-        self.ch_Eloc = [(self.E[a:b] - r0).contiguous()
-                        for (r0, _), (a, b) in zip(self.chunks, self.ch_E)]
-        self.ch_Sloc = [(self.S[a:b] - r0).contiguous()
-                        for (r0, _), (a, b) in zip(self.chunks, self.ch_S)]
+        self.ch_Tloc = [(self.T[a:b_] - r0).contiguous()
+                        for (r0, _), (a, b_) in zip(self.chunks, self.ch_T)]
+        self.ch_Eloc = [(self.E[a:b_] - r0).contiguous()
+                        for (r0, _), (a, b_) in zip(self.chunks, self.ch_E)]
+        self.ch_Sloc = [(self.S[a:b_] - r0).contiguous()
+                        for (r0, _), (a, b_) in zip(self.chunks, self.ch_S)]
         self.ch_send = [self._csr_range(self.send_st, r0, r1) for r0, r1 in self.chunks]
-        # ---- persistent buffers (allocated once: no allocation in the steady state)
+
+    def _allocate(self, graph: DistGraph, b: "_Budget") -> None:
+        """The persistent buffers the plan counted (allocated once: no allocation in the
+        steady state)."""
+        cfg, dev, L, H = self.cfg, self.dev, self.L, self.H
+        n_send, nT = self.n_send, self.T.numel()
         f = dict(dtype=torch.float32, device=dev)
         self.h = [torch.empty(L, self.hid, **f) for _ in range(self.nl - 1)]
         # W > 1: the exchange buffers, resident — an exchange's buffers are in use on the
@@ -633,14 +696,14 @@ class FusedSAGE:
             # one arena: the ring's send / receive blocks, and (dead while the ring is idle,
             # in the output-layer backward) the sub-plan exchange's buffers
             blk_s, blk_r = n_send * self.cw, H * self.cw
-            ring_fl = max(self.nbuf * (blk_s + blk_r), sub_bytes // 4)
+            ring_fl = max(self.nbuf * (blk_s + blk_r), b.sub_bytes // 4)
             self.ring_arena = torch.empty(ring_fl, **f)
             ra = self.ring_arena
-            self.ring_send = [ra[b * blk_s:(b + 1) * blk_s].view(n_send, self.cw)
-                              for b in range(self.nbuf)]
+            self.ring_send = [ra[i * blk_s:(i + 1) * blk_s].view(n_send, self.cw)
+                              for i in range(self.nbuf)]
             o = self.nbuf * blk_s
-            self.ring_recv = [ra[o + b * blk_r:o + (b + 1) * blk_r].view(H, self.cw)
-                              for b in range(self.nbuf)]
+            self.ring_recv = [ra[o + i * blk_r:o + (i + 1) * blk_r].view(H, self.cw)
+                              for i in range(self.nbuf)]
             self.agg_full = torch.empty(L, max(self.hid, self.d0), **f)
             self.aS_full = torch.empty(self.nS, self.w_lh, **f)
             # the reverse exchange's store: the output layer's aggregate store (dead after
@@ -681,13 +744,14 @@ class FusedSAGE:
         # ONE chunk arena: the aggregate and the logit / gradient chunk buffers during the
         # row-chunked passes, and the last hidden layer's keep bits (output-layer backward
         # only, when no chunk buffer is live)
+        wA, wB = b.wA, b.wB
         bits_words = self.nS * (self.hid // 32)
         arena_fl = max(self.cr * (wA + wB), bits_words)
         self.arena = torch.empty(arena_fl, **f)
         self.bufA = self.arena[:self.cr * wA].view(self.cr, wA)
         self.bufB = self.arena[self.cr * wA:self.cr * (wA + wB)].view(self.cr, wB)
         self.bits = self.arena[:bits_words].view(torch.int32).view(self.nS, self.hid // 32)
-        self.dz = torch.zeros(self.T.numel(), self.Cg, **f)  # output-layer gradient rows
+        self.dz = torch.zeros(nT, self.Cg, **f)  # output-layer gradient rows
         # the output layer's projected gradient rows (B2 only): the last hidden buffer's tail,
         # past dZ and u, is free by then
         if self.u_sep:
@@ -701,7 +765,7 @@ class FusedSAGE:
             if not self.store_sep and n_used + self.nS * self.hid <= L * self.hid:
                 self.v_self = self.h[-1].view(-1)[n_used:n_used + self.nS * self.hid].view(
                     self.nS, self.hid)
-            elif dev.type != "cuda" or free - need_h > (4 * self.nS * self.hid + (8 << 30)):
+            elif dev.type != "cuda" or b.free - b.need_h > (4 * self.nS * self.hid + (8 << 30)):
                 self.v_self = torch.empty(self.nS, self.hid, **f)
             # else: no room — the self term runs as a row-scattered GEMM per chunk
         self.acc_out_s = F32.WgradAcc(self.hid, self.Cg, dev)
@@ -713,14 +777,6 @@ class FusedSAGE:
         self.acc_hid_n = F32.WgradAcc(kh, self.hid, dev)
         self.acc_in = F32.WgradAcc(2 * self.d0, self.hid, dev, colsum=True) \
             if self.nl == 3 else None
-        self.row_loss = torch.zeros(nT, **f)
-        self.hit = torch.zeros(self.E.numel(), dtype=torch.uint8, device=dev)
-        self.E_val_l = self.E_val.long()
-        self.correct = torch.zeros(2, dtype=torch.long, device=dev)
-        self.record = False
-        self._events: list = []
-        self._packs: dict = {}  # send-row packs in source order (_pack)
-        self._tune_passes()
 
     def _agree(self, vals: List[int], op: str) -> List[int]:
         """``vals`` reduced elementwise (``"max"`` / ``"min"``) over the plan's group, so
