@@ -124,7 +124,7 @@ def parse():
                     help="W > 1: skip the one-sided (symmetric-heap) transport probe that runs "
                          "as a separate child job after the headline")
     ap.add_argument("--shmem-probe-timeout", type=float,
-                    default=float(os.environ.get("DGRAPH_BENCH_SHMEM_PROBE_TIMEOUT_S", "240")))
+                    default=float(os.environ.get("DGRAPH_BENCH_SHMEM_PROBE_TIMEOUT_S", "150")))
     ap.add_argument("--metrics-jsonl", default=os.environ.get("DGRAPH_METRICS_JSONL", ""),
                     help="append one metrics record per measured phase (rank 0)")
     return ap.parse_args()
