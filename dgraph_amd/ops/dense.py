@@ -108,11 +108,12 @@ def _leaf_target(p: torch.Tensor):
     """(leaf parameter, view of its ``.grad`` that ``p``'s gradient adds into) or None."""
     if not p.requires_grad:
         return None
-    if p.is_leaf:
-        return (p, None) if p.is_contiguous() else None
-    b = p._base
-    if b is None or not b.is_leaf or not b.requires_grad or not b.is_contiguous():
-        return None
+    b = p if p.is_leaf else p._base
+    if b is None or not b.is_leaf or not b.requires_grad or not b.is_contiguous() or (
+            b.grad is not None and not b.grad.is_contiguous()):
+        return None  # (a view's strides address the grad only when both are contiguous)
+    if b is p:
+        return p, None
     return b, (p.size(), p.stride(), p.storage_offset() - b.storage_offset())
 
 
