@@ -311,6 +311,12 @@ class _Budget:
         self.free, self.need_h, self.other, self.margin = free, need_h, other, margin
         self.wA, self.wB = wA, wB
         self.sub_bytes = 0
+        self.decisions: list = []
+
+    def note(self, what: str, nbytes: int, taken: bool) -> None:
+        """Record one plan choice with the room it was decided against (schedule())."""
+        self.decisions.append({"what": what, "gb": round(nbytes / 2**30, 2),
+                               "room_gb": round(self.room() / 2**30, 2), "taken": bool(taken)})
 
     def room(self) -> int:
         """Bytes not yet planned."""
@@ -554,9 +560,9 @@ class FusedSAGE:
                     dev.type != "cuda" or b.need_h + hb + b.other + (1 << 28) <= b.free)))
             fit = self._agree(fit, "min")  # the first shape EVERY rank has room for
             for (cw, nb), ok, hb in zip(shapes, fit, hbs):
-                if ok:
+                b.note(f"halo_stream_{cw}x{nb}", hb, ok and not self.stream)
+                if ok and not self.stream:
                     self.stream, self.cw, self.nbuf, self.halo_bytes = True, cw, nb, hb
-                    break
         b.need_h += self.halo_bytes
         fits = dev.type != "cuda" or b.need_h + b.other + (1 << 28) <= b.free
         if graph.send_map is not None and not bool(self._agree([int(fits)], "min")[0]):
@@ -574,22 +580,27 @@ class FusedSAGE:
         need_as = self.nS * self.w_lh * 4
         self.keep_as = cfg.keep_as == "on" or self.stream or (
             cfg.keep_as == "auto" and b.room() - need_as > b.margin)
+        b.note("keep_aS", 0 if self.stream else need_as, self.keep_as)
         if self.keep_as and not self.stream:
             b.other += need_as
         # layer 0's input aggregate kept from the forward for the backward (else recomputed)
         self.agg0 = None
         need0 = L * self.d0 * 4
-        if self.nl == 3 and cfg.keep_agg0 != "off" and (
-                cfg.keep_agg0 == "on" or b.room() - need0 > b.margin):
-            self.agg0 = torch.empty(L, self.d0, dtype=torch.float32, device=dev)
-            b.other += need0
+        if self.nl == 3 and cfg.keep_agg0 != "off":
+            take = cfg.keep_agg0 == "on" or b.room() - need0 > b.margin
+            b.note("keep_agg0", need0, take)
+            if take:
+                self.agg0 = torch.empty(L, self.d0, dtype=torch.float32, device=dev)
+                b.other += need0
         # W > 1: the output layer's projection [L, Cp] (PROJECT_FIRST), after the kept
         # aggregates (those save whole aggregation passes)
         self.pf = None
         need_pf = L * self.Cp * 4
         if graph.send_map is not None and cfg.project_first != "off" and self.Cp < self.hid:
             want_pf = cfg.project_first == "on" or b.room() - need_pf > b.margin
-            if bool(self._agree([int(want_pf)], "min")[0]):  # (changes the exchanges)
+            want_pf = bool(self._agree([int(want_pf)], "min")[0])  # (changes the exchanges)
+            b.note("project_first", need_pf, want_pf)
+            if want_pf:
                 self.pf = torch.empty(L, self.Cp, dtype=torch.float32, device=dev)
                 b.other += need_pf
                 self._aggT_setup()
@@ -601,17 +612,22 @@ class FusedSAGE:
         self.agg_full = None
         need_full = (L - self.Li) * b.wA * 4
         if graph.send_map is not None and cfg.overlap and self.Li < L and not self.stream \
-                and self.use_store["out"] and b.room() - need_full > b.margin:
-            self.agg_full = torch.empty(L - self.Li, b.wA, dtype=torch.float32, device=dev)
-            b.other += need_full
+                and self.use_store["out"]:
+            take = b.room() - need_full > b.margin
+            b.note("output_store", need_full, take)
+            if take:
+                self.agg_full = torch.empty(L - self.Li, b.wA, dtype=torch.float32, device=dev)
+                b.other += need_full
         # streamed output layer: its self term h W_self + b for every row, computed during
         # the first column block's transfer (the pipeline fill), when the plan has room
         self.zself = None
         need_z = L * self.Cp * 4
-        if self.stream and cfg.stream_out_fill and self.pf is None and \
-                b.room() - need_z > b.margin:
-            self.zself = torch.empty(L, self.Cp, dtype=torch.float32, device=dev)
-            b.other += need_z
+        if self.stream and cfg.stream_out_fill and self.pf is None:
+            take = b.room() - need_z > b.margin
+            b.note("output_self_term_fill", need_z, take)
+            if take:
+                self.zself = torch.empty(L, self.Cp, dtype=torch.float32, device=dev)
+                b.other += need_z
         return b
 
     def _plan_compact_t(self, b: "_Budget") -> None:
@@ -628,8 +644,10 @@ class FusedSAGE:
             nnz_ts = _compact_by_map(src[0], src[1], src[2], self.smap, L, count_only=True) \
                 if L else 0
             ts_bytes = nnz_ts * 4 + (L + 1) * 8
-            if cfg.compact_t == "on" or dev.type != "cuda" or \
-                    b.room() - (1 << 28) - ts_bytes >= (1 << 30):
+            take = cfg.compact_t == "on" or dev.type != "cuda" or \
+                b.room() - (1 << 28) - ts_bytes >= (1 << 30)
+            b.note("compact_T", ts_bytes, take)
+            if take:
                 self.TS = _compact_by_map(src[0], src[1], src[2], self.smap, L)
                 b.other += ts_bytes
         # the same for the halo rows' transposed aggregation of u (the reverse exchange's
@@ -640,8 +658,10 @@ class FusedSAGE:
             nnz_h = _compact_by_map(self.haloT.rowptr, self.haloT.col, None, self.smap, Hn,
                                     count_only=True)
             hts_bytes = nnz_h * 4 + (Hn + 1) * 8
-            if cfg.compact_t == "on" or dev.type != "cuda" or \
-                    b.room() - (1 << 28) - hts_bytes >= (1 << 30):
+            take = cfg.compact_t == "on" or dev.type != "cuda" or \
+                b.room() - (1 << 28) - hts_bytes >= (1 << 30)
+            b.note("compact_halo_T", hts_bytes, take)
+            if take:
                 self.HTS = _compact_by_map(self.haloT.rowptr, self.haloT.col, None, self.smap,
                                            Hn)
                 b.other += hts_bytes
@@ -656,6 +676,8 @@ class FusedSAGE:
         if cr <= 0:
             cr = int(min(max(spare // per_row, 1 << 16), 1 << 21))
         self.cr = max(256, min(int(cr), max(L, 256)))
+        b.note("chunk_arena", self.cr * per_row, True)
+        self.memory_plan = b.decisions
         self.chunks = _ranges(0, self.Li, self.cr) + _ranges(self.Li, L, self.cr)
         if not self.chunks:
             self.chunks = [(0, 0)]
@@ -985,6 +1007,7 @@ class FusedSAGE:
                 "compact_halo_T": self.HTS is not None, "support_rows": self.nS,
                 "bwd_halo": "pull" if self.pull is not None else "push",
                 "output_project_first": self.pf is not None,
+                "memory_plan": list(self.memory_plan),
                 **({"link_gbps_planned": round(self.link_gbps, 1)}
                    if self.g.send_map is not None else {})}
 
