@@ -574,6 +574,7 @@ class FusedSAGE:
         if not fits:
             raise MemoryError(b.describe(self.halo_bytes, dev))
         self._plan_compact_t(b)
+        self._plan_compact_pull(b)
         # the last hidden layer's input aggregate on the S rows kept from the forward (else
         # re-aggregated in the backward); streamed halos keep it in aS_full (planned above)
         self.aS_keep = None
@@ -665,6 +666,27 @@ class FusedSAGE:
                 self.HTS = _compact_by_map(self.haloT.rowptr, self.haloT.col, None, self.smap,
                                            Hn)
                 b.other += hts_bytes
+
+    def _plan_compact_pull(self, b: "_Budget") -> None:
+        """The pulled backward halo's adjacency with its column map applied once (``PT``):
+        only the entries whose neighbour is a support row (mine, or a peer's pulled in), with
+        the mapped column (support index, or ``nS`` + pulled row) stored in place of the
+        original. Without it every pass of B1b walks ALL entries and looks each column up
+        in the map (a random 4-byte read per entry per column block): the structureless
+        W=2 rank spent 58 ms per 32-column block there, for ~26 % of the entries used."""
+        cfg, dev, L = self.cfg, self.dev, self.L
+        self.PT = None
+        if self.pull is None or cfg.compact_t == "off" or not L:
+            return
+        nnz = _compact_by_map(self.adj.rp, self.adj.col, None, self.pull["cmap"], L,
+                              count_only=True)
+        nbytes = nnz * 4 + (L + 1) * 8
+        take = cfg.compact_t == "on" or dev.type != "cuda" or \
+            b.room() - (1 << 28) - nbytes >= (1 << 30)
+        b.note("compact_pull", nbytes, take)
+        if take:
+            self.PT = _compact_by_map(self.adj.rp, self.adj.col, None, self.pull["cmap"], L)
+            b.other += nbytes
 
     def _plan_chunks(self, chunk_rows: int, b: "_Budget") -> None:
         """Row chunks sized from what the plan left (never straddling the interior /
@@ -1004,7 +1026,8 @@ class FusedSAGE:
                 "keep_agg0": self.agg0 is not None, "keep_aS": self.aS_keep is not None,
                 "output_self_term_fill": self.zself is not None,
                 "compact_T": self.TS is not None,
-                "compact_halo_T": self.HTS is not None, "support_rows": self.nS,
+                "compact_halo_T": self.HTS is not None, "compact_pull": self.PT is not None,
+                "support_rows": self.nS,
                 "bwd_halo": "pull" if self.pull is not None else "push",
                 "output_project_first": self.pf is not None,
                 "memory_plan": list(self.memory_plan),
@@ -1379,9 +1402,13 @@ class FusedSAGE:
             work.wait()
             self._mark(name)
             sa = {} if v is None else dict(self_add=v[:, c0:c1], self_map=self.smap)
-            self._spmm_u(self.adj.rp, self.adj.col, u[:, c0:c1], gz[:, c0:c1],
-                         col_map=pl["cmap"], x2=uh, nsplit=self.nS, gate=gate[:, c0:c1],
-                         pass_cols=c1 - c0, **sa)
+            if self.PT is not None:
+                self._spmm(self.PT[0], self.PT[1], u[:, c0:c1], gz[:, c0:c1], x2=uh,
+                           nsplit=self.nS, gate=gate[:, c0:c1], pass_cols=c1 - c0, **sa)
+            else:
+                self._spmm_u(self.adj.rp, self.adj.col, u[:, c0:c1], gz[:, c0:c1],
+                             col_map=pl["cmap"], x2=uh, nsplit=self.nS, gate=gate[:, c0:c1],
+                             pass_cols=c1 - c0, **sa)
             if nb == 1 and k + 1 < len(blocks):
                 works[k + 1] = issue(k + 1)
 
@@ -1771,6 +1798,9 @@ class FusedSAGE:
                 gz = self.bufB[:n, :hid]
             if full:
                 pass
+            elif uh is not None and ci >= self.nA and self.PT is not None:
+                self._spmm(self.PT[0][r0:r1 + 1], self.PT[1], u, gz, x2=uh, nsplit=self.nS,
+                           **sa)
             elif uh is not None and ci >= self.nA:
                 rp, _ = self.adj.rows(r0, r1, "all")
                 self._spmm_u(rp, self.adj.col, u, gz, col_map=self.pull["cmap"], x2=uh,
