@@ -671,17 +671,20 @@ class FusedSAGE:
         """The pulled backward halo's adjacency with its column map applied once (``PT``):
         only the entries whose neighbour is a support row (mine, or a peer's pulled in), with
         the mapped column (support index, or ``nS`` + pulled row) stored in place of the
-        original. Without it every pass of B1b walks ALL entries and looks each column up
-        in the map (a random 4-byte read per entry per column block): the structureless
-        W=2 rank spent 58 ms per 32-column block there, for ~26 % of the entries used."""
+        original. Streamed halos pull u in column blocks, and without it every block's pass
+        of B1b walks ALL entries and looks each column up in the map (a random 4-byte read
+        per entry per block): the structureless W=2 rank spent 58 ms per 32-column block
+        there, for ~26 % of the entries used. A resident pull walks the map once, in one
+        full-width pass (``_spmm_u``), so "auto" builds it for streamed halos only."""
         cfg, dev, L = self.cfg, self.dev, self.L
         self.PT = None
-        if self.pull is None or cfg.compact_t == "off" or not L:
+        if self.pull is None or cfg.compact_pull == "off" or not L or (
+                cfg.compact_pull == "auto" and not self.stream):
             return
         nnz = _compact_by_map(self.adj.rp, self.adj.col, None, self.pull["cmap"], L,
                               count_only=True)
         nbytes = nnz * 4 + (L + 1) * 8
-        take = cfg.compact_t == "on" or dev.type != "cuda" or \
+        take = cfg.compact_pull == "on" or dev.type != "cuda" or \
             b.room() - (1 << 28) - nbytes >= (1 << 30)
         b.note("compact_pull", nbytes, take)
         if take:

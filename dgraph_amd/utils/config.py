@@ -82,6 +82,7 @@ class ExecutorConfig:
     stream_out_fill: bool = False   # streamed output layer: self term as the pipeline fill
     halo_stream: str = "auto"       # hidden halos in column blocks: auto | on | off
     compact_t: str = "off"          # S-compacted transposed adjacency: auto | on | off
+    compact_pull: str = "auto"      # pulled halo's adjacency, map applied (auto: streamed)
     pack_stream: str = "compute"    # halo pack on the compute or the comm stream
     pack_fused: bool = True         # halo pack fused into the producing GEMM's epilogue
     bwd_halo: str = "pull"          # input-layer backward halo: pull | push
@@ -97,6 +98,7 @@ class ExecutorConfig:
                          ("keep_as", ("auto", "on", "off")),
                          ("halo_stream", ("auto", "on", "off")),
                          ("compact_t", ("auto", "on", "off")),
+                         ("compact_pull", ("auto", "on", "off")),
                          ("pack_stream", ("compute", "comm")),
                          ("bwd_halo", ("pull", "push")),
                          ("project_first", ("auto", "on", "off"))):

@@ -227,6 +227,8 @@ def _interior_first_body(rank, world, ref_path, overlap, store="auto", stream="o
     assert (ex.pull is not None) == (bwd_halo == "pull")
     if ex.pull is not None:
         assert 0 < ex.pull["n_send"] < ex.n_send and ex.pull["n_recv"] < ex.H
+    # streamed pulls run B1b over the compacted, pre-mapped adjacency (compact_pull=auto)
+    assert (ex.PT is not None) == (ex.stream and ex.pull is not None)
     if stream == "single":
         assert ex.nbuf == 1
     if stream == "ramp":
