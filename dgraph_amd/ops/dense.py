@@ -133,6 +133,9 @@ def defer_param_grads(params: Sequence[torch.Tensor], compute: Callable[[], Sequ
     side = _side_stream(params[0].device)
     dsts = []
     for leaf, view in targets:
+        if leaf.grad is None and view is None:
+            dsts.append(leaf)  # the gradient itself becomes .grad (no zero fill + add)
+            continue
         if leaf.grad is None:
             leaf.grad = torch.zeros_like(leaf)  # on the current stream, before the fork
         g = leaf.grad
@@ -143,8 +146,13 @@ def defer_param_grads(params: Sequence[torch.Tensor], compute: Callable[[], Sequ
     for t in keep_alive:
         t.record_stream(side)
     with torch.cuda.stream(side):
-        for d, o in zip(dsts, compute()):
-            d.add_(o.to(d.dtype))
+        for d, o, p in zip(dsts, compute(), params):
+            if d is p:
+                o = o.to(p.dtype).contiguous()
+                o.record_stream(cur)  # read (and freed) on the current stream after the join
+                p.grad = o
+            else:
+                d.add_(o.to(d.dtype))
     return True
 
 
