@@ -373,3 +373,20 @@ def test_executor_config_resolved_at_construction(monkeypatch):
     assert rc.model.dtype == "fp32"
     with pytest.raises(ValueError):
         ExecutorConfig(halo_stream="sometimes")
+
+
+def test_memory_plan_recorded():
+    """The setup's memory plan lists each optional buffer with its bytes, the room it was
+    decided against and whether it was taken; the recorded choices are the executor's."""
+    shape, g, x, y, split, tr, ev, n_tr, model = _setup(0, 1)
+    ex = FusedSAGE(model, g, x, tr, y[tr], ev, y[ev], split[ev] == SPLIT_VALID, n_tr,
+                   chunk_rows=300)
+    plan = ex.schedule["memory_plan"]
+    by = {m["what"]: m for m in plan}
+    assert {"keep_aS", "keep_agg0", "chunk_arena"} <= set(by)
+    assert by["keep_agg0"]["taken"] == (ex.agg0 is not None)
+    assert by["keep_aS"]["taken"] == (ex.aS_keep is not None)
+    assert by["chunk_arena"]["gb"] >= 0 and all(m["room_gb"] >= 0 for m in plan)
+    # room only shrinks as buffers are taken
+    rooms = [m["room_gb"] for m in plan]
+    assert rooms == sorted(rooms, reverse=True)
