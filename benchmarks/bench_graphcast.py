@@ -58,6 +58,8 @@ def main():
     ap.add_argument("--partition", default="latitude", choices=["latitude", "aligned"],
                     help="latitude: equal grid-row bands, mesh by latitude quantiles; aligned: "
                          "one set of cost-balanced latitude cuts for grid and mesh (small halos)")
+    ap.add_argument("--branch-streams", type=int, default=1, choices=[0, 1],
+                    help="1: independent parts of the step on a second stream")
     ap.add_argument("--wgrad-stream", type=int, default=1, choices=[0, 1],
                     help="1: weight gradients on a side stream (ops.dense.deferred_wgrad)")
     ap.add_argument("--rehearse-world", type=int, default=0,
@@ -121,6 +123,7 @@ def main():
         ds = SyntheticWeatherDataset(pg, a.channels, 3)
         x, y = (t.to(dev, dt) for t in ds[0])
         model = DGraphCast(cfg, comm).to(dev, dt)
+        model.branch_streams = bool(a.branch_streams)
         gs = GradSync(model.parameters())
         if dt == torch.float32:
             opt = torch.optim.Adam(model.parameters(), lr=1e-4, fused=True)
@@ -207,6 +210,7 @@ def main():
                   not a.dedup_mesh_edges,
                   "launch": "HIP graph replay" if a.cuda_graph else "eager",
                   "wgrad_stream": bool(a.wgrad_stream),
+                  "branch_streams": bool(a.branch_streams),
                   "precision": "bf16 compute, fp32 master weights" if masters is not None
                   else "fp32",
                   "edge_updates_per_s": edges / (ms / 1e3), "loss": float(loss),

@@ -294,6 +294,48 @@ class GraphCastEmbedder(nn.Module):
                 self.mesh2grid_edge_embedder(mesh2grid_edge_features))
 
 
+class _Branch:
+    """A second stream for independent parts of the step (forked from and joined into the
+    current stream; autograd runs each op's backward on its forward's stream, so the
+    backwards overlap too, and a HIP-graph capture records the fork and join)."""
+
+    def __init__(self, device: torch.device):
+        self.stream = torch.cuda.Stream(device)
+
+
+class _on_branch:
+    """``with _on_branch(branch, x) as br: y = f(x)`` runs ``f`` on the branch stream (after
+    everything already issued on the current one); ``br.join(y)`` makes the current stream
+    wait for it and returns ``y``. Without a branch both are no-ops."""
+
+    def __init__(self, branch: Optional[_Branch], ref: torch.Tensor, reads=()):
+        self.branch = branch if branch is not None and ref.is_cuda else None
+        self.reads = reads
+        self._ctx = None
+
+    def __enter__(self):
+        if self.branch is not None:
+            self.cur = torch.cuda.current_stream()
+            self.branch.stream.wait_stream(self.cur)
+            for t in self.reads:  # current-stream tensors the branch reads
+                t.record_stream(self.branch.stream)
+            self._ctx = torch.cuda.stream(self.branch.stream)
+            self._ctx.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        if self._ctx is not None:
+            self._ctx.__exit__(*exc)
+        return False
+
+    def join(self, *ts):
+        if self.branch is not None:
+            self.cur.wait_stream(self.branch.stream)
+            for t in ts:
+                t.record_stream(self.cur)  # allocated on the branch, used on the current
+        return ts[0] if len(ts) == 1 else ts
+
+
 class GraphCastEncoder(nn.Module):
     def __init__(self, cfg, comm=None, *args, **kwargs):
         super().__init__()
@@ -303,14 +345,18 @@ class GraphCastEncoder(nn.Module):
         self.grid_node_mlp = MeshGraphMLP(H, H)
         self.halo = _Halo(comm)
 
-    def forward(self, grid_node_features, mesh_node_features, g2m_edge_features, g2m) -> Tuple:
+    def forward(self, grid_node_features, mesh_node_features, g2m_edge_features, g2m,
+                branch: Optional["_Branch"] = None) -> Tuple:
         grid_h = self.halo.start(grid_node_features, g2m)   # senders: grid (local|halo)
+        # the grid node update does not depend on the grid2mesh edges: on the branch stream
+        # it runs next to the edge block and the mesh node update (and so do their backwards)
+        with _on_branch(branch, grid_node_features, reads=(grid_node_features,)) as br:
+            grid_out = self.grid_node_mlp(grid_node_features, residual=grid_node_features)
         e = self.edge_mlp.fused_halo(grid_node_features, mesh_node_features, g2m_edge_features,
                                      g2m.other_map(), g2m.agg_map(), grid_h, "src")
         n = self.mesh_node_mlp.fused(mesh_node_features, e, g2m.agg_map())
         mesh_node_features = mesh_node_features + n
-        grid_node_features = self.grid_node_mlp(grid_node_features, residual=grid_node_features)
-        return grid_node_features, mesh_node_features
+        return br.join(grid_out), mesh_node_features
 
 
 class GraphCastProcessor(nn.Module):
@@ -363,18 +409,33 @@ class DGraphCast(nn.Module):
         self.processor = GraphCastProcessor(cfg, comm)
         self.decoder = GraphCastDecoder(cfg, comm)
         self.final_prediction = MeshGraphMLP(self.hidden_dim, self.output_grid_dim)
+        # independent parts on a second stream (GPU): the mesh2grid edge embedding next to
+        # the encoder and the processor (whose mesh-sized kernels fill a fraction of the
+        # CUs), the encoder's grid node update next to its edge block
+        self.branch_streams = True
+        self._branch: Optional[_Branch] = None
 
     def forward(self, input_grid_features: torch.Tensor, static_graph) -> torch.Tensor:
         g = static_graph
         x = input_grid_features.reshape(-1, input_grid_features.shape[-1])
+        br = None
+        if self.branch_streams and x.is_cuda:
+            if self._branch is None or self._branch.stream.device != x.device:
+                self._branch = _Branch(x.device)
+            br = self._branch
+        emb = self.embedder
         with region("embedder"):
-            grid, mesh, e_m2m, e_g2m, e_m2g = self.embedder(
-                x, g.mesh_node_features.to(x.dtype), g.m2m.features.to(x.dtype),
-                g.g2m.features.to(x.dtype), g.m2g.features.to(x.dtype))
+            with _on_branch(br, x) as m2g_branch:
+                e_m2g = emb.mesh2grid_edge_embedder(g.m2g.features.to(x.dtype))
+            grid = emb.grid_feature_embedder(x)
+            mesh = emb.mesh_feature_embedder(g.mesh_node_features.to(x.dtype))
+            e_m2m = emb.mesh2mesh_edge_embedder(g.m2m.features.to(x.dtype))
+            e_g2m = emb.grid2mesh_edge_embedder(g.g2m.features.to(x.dtype))
         with region("encoder"):
-            grid, mesh = self.encoder(grid, mesh, e_g2m, g.g2m)
+            grid, mesh = self.encoder(grid, mesh, e_g2m, g.g2m, branch=br)
         with region("processor"):
             mesh, _ = self.processor(mesh, e_m2m, g.m2m)
+        e_m2g = m2g_branch.join(e_m2g)
         with region("decoder"):
             grid = self.decoder(e_m2g, grid, mesh, g.m2g)
         with region("final"):

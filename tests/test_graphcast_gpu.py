@@ -167,6 +167,7 @@ def test_graphcast_deferred_wgrad_bitwise():
             loss.backward()
         return loss
 
+    assert model.branch_streams  # (default) the reference step runs with the branch stream
     step(False)
     ref = [p.grad.clone() for p in model.parameters()]
     c0 = dense._DEFER.calls
@@ -180,5 +181,11 @@ def test_graphcast_deferred_wgrad_bitwise():
         run()
     torch.cuda.synchronize()
     assert run.captured
+    for (n, p), b in zip(model.named_parameters(), ref):
+        assert torch.equal(p.grad, b), n
+    # and without the branch stream (the m2g embedding / encoder grid update inline)
+    model.branch_streams = False
+    step(True)
+    torch.cuda.synchronize()
     for (n, p), b in zip(model.named_parameters(), ref):
         assert torch.equal(p.grad, b), n
