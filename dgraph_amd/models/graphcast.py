@@ -306,7 +306,8 @@ class _Branch:
 class _on_branch:
     """``with _on_branch(branch, x) as br: y = f(x)`` runs ``f`` on the branch stream (after
     everything already issued on the current one); ``br.join(y)`` makes the current stream
-    wait for it and returns ``y``. Without a branch both are no-ops."""
+    wait for that block only (an event recorded at its end: later blocks on the branch keep
+    running) and returns ``y``. Without a branch both are no-ops."""
 
     def __init__(self, branch: Optional[_Branch], ref: torch.Tensor, reads=()):
         self.branch = branch if branch is not None and ref.is_cuda else None
@@ -325,12 +326,14 @@ class _on_branch:
 
     def __exit__(self, *exc):
         if self._ctx is not None:
+            self.done = torch.cuda.Event()
+            self.done.record(self.branch.stream)
             self._ctx.__exit__(*exc)
         return False
 
     def join(self, *ts):
         if self.branch is not None:
-            self.cur.wait_stream(self.branch.stream)
+            self.cur.wait_event(self.done)
             for t in ts:
                 t.record_stream(self.cur)  # allocated on the branch, used on the current
         return ts[0] if len(ts) == 1 else ts
@@ -425,14 +428,19 @@ class DGraphCast(nn.Module):
             br = self._branch
         emb = self.embedder
         with region("embedder"):
+            # mesh-side embeddings on the branch, each joined just before its first use
+            with _on_branch(br, x) as mesh_branch:
+                mesh = emb.mesh_feature_embedder(g.mesh_node_features.to(x.dtype))
+            with _on_branch(br, x) as m2m_branch:
+                e_m2m = emb.mesh2mesh_edge_embedder(g.m2m.features.to(x.dtype))
             with _on_branch(br, x) as m2g_branch:
                 e_m2g = emb.mesh2grid_edge_embedder(g.m2g.features.to(x.dtype))
             grid = emb.grid_feature_embedder(x)
-            mesh = emb.mesh_feature_embedder(g.mesh_node_features.to(x.dtype))
-            e_m2m = emb.mesh2mesh_edge_embedder(g.m2m.features.to(x.dtype))
             e_g2m = emb.grid2mesh_edge_embedder(g.g2m.features.to(x.dtype))
+            mesh = mesh_branch.join(mesh)
         with region("encoder"):
             grid, mesh = self.encoder(grid, mesh, e_g2m, g.g2m, branch=br)
+        e_m2m = m2m_branch.join(e_m2m)
         with region("processor"):
             mesh, _ = self.processor(mesh, e_m2m, g.m2m)
         e_m2g = m2g_branch.join(e_m2g)
