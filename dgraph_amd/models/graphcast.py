@@ -157,18 +157,24 @@ class MeshEdgeBlock(nn.Module):
         return W[:, :a], W[:, a:a + b], W[:, a + b:], lin.bias
 
     def fused(self, src_feats: torch.Tensor, dst_feats: torch.Tensor, edge_feats: torch.Tensor,
-              src_map: IndexMap, dst_map: IndexMap) -> torch.Tensor:
-        """Edge update with index maps over the rows of ``src_feats`` / ``dst_feats``."""
+              src_map: IndexMap, dst_map: IndexMap, pre=None) -> torch.Tensor:
+        """Edge update with index maps over the rows of ``src_feats`` / ``dst_feats``.
+        ``pre``: ``(Y, Q)`` from :meth:`pre_dst`, computed earlier (e.g. on a branch)."""
         Ws, Wd, We, b = self._split_first()
         P = linear(src_feats, Ws)
-        Q = linear(dst_feats, Wd)
-        Y = linear(edge_feats, We, b)
+        Y, Q = pre if pre is not None else self.pre_dst(edge_feats, dst_feats)
         h = edge_pre_activation(Y, P, Q, src_map, dst_map, self.mesh_mlp.first_act_name())
         return self.mesh_mlp.tail(h, residual=edge_feats)
 
+    def pre_dst(self, edge_feats: torch.Tensor, dst_feats: torch.Tensor):
+        """The first Linear's edge term (with the bias) and destination-side projection:
+        ``(edge W_e^T + b, dst W_d^T)``, which need neither the sources nor their halo."""
+        _, Wd, We, b = self._split_first()
+        return linear(edge_feats, We, b), linear(dst_feats, Wd)
+
     def fused_halo(self, src_local: torch.Tensor, dst_local: torch.Tensor,
                    edge_feats: torch.Tensor, src_map: IndexMap, dst_map: IndexMap,
-                   halo, side: str) -> torch.Tensor:
+                   halo, side: str, pre=None) -> torch.Tensor:
         """:meth:`fused` with one endpoint's rows ``[local | halo]`` where the halo rows are
         still on the links (``halo``: an :class:`~dgraph_amd.parallel.halo.AsyncHalo`, or
         None when the edge set has no remote endpoint): the edge GEMM, the other endpoint's
@@ -176,16 +182,17 @@ class MeshEdgeBlock(nn.Module):
         only before its rows are projected (``side`` = "src" or "dst": the halo side). The
         index maps address the projected rows ``[local | halo]`` as before."""
         if halo is None:
-            return self.fused(src_local, dst_local, edge_feats, src_map, dst_map)
+            return self.fused(src_local, dst_local, edge_feats, src_map, dst_map, pre)
         Ws, Wd, We, b = self._split_first()
-        Y = linear(edge_feats, We, b)
         if side == "src":
-            Q = linear(dst_local, Wd)
+            Y, Q = pre if pre is not None else self.pre_dst(edge_feats, dst_local)
             P_loc = linear(src_local, Ws)
             with region("exchange-wait"):  # exposed exchange time (device)
                 hw = halo.wait()
             P = torch.cat([P_loc, linear(hw, Ws)], dim=0)
         else:
+            assert pre is None, "pre_dst applies to a source-side halo"
+            Y = linear(edge_feats, We, b)
             P = linear(src_local, Ws)
             Q_loc = linear(dst_local, Wd)
             with region("exchange-wait"):
@@ -392,11 +399,14 @@ class GraphCastDecoder(nn.Module):
         self.node_mlp = MeshNodeBlock(H, H, H, comm, H, 1)
         self.halo = _Halo(comm)
 
-    def forward(self, m2g_edge_features, grid_node_features, mesh_node_features, m2g):
+    def forward(self, m2g_edge_features, grid_node_features, mesh_node_features, m2g,
+                pre=None):
+        """``pre``: the edge block's ``pre_dst(m2g_edge_features, grid_node_features)``,
+        computed ahead (DGraphCast runs it on the branch stream during the processor)."""
         mesh_h = self.halo.start(mesh_node_features, m2g)  # senders: mesh (local|halo)
         e = self.edge_mlp.fused_halo(mesh_node_features, grid_node_features,
                                      m2g_edge_features, m2g.other_map(), m2g.agg_map(),
-                                     mesh_h, "src")
+                                     mesh_h, "src", pre=pre)
         n = self.node_mlp.fused(grid_node_features, e, m2g.agg_map())
         return grid_node_features + n
 
@@ -441,10 +451,18 @@ class DGraphCast(nn.Module):
         with region("encoder"):
             grid, mesh = self.encoder(grid, mesh, e_g2m, g.g2m, branch=br)
         e_m2m = m2m_branch.join(e_m2m)
+        # the decoder's edge and grid-side projections need only the m2g embedding and the
+        # encoder's grid: on the branch, beside the processor's mesh-sized kernels
+        pre = None
+        if br is not None:
+            with _on_branch(br, grid, reads=(grid,)) as dec_branch:
+                pre = self.decoder.edge_mlp.pre_dst(e_m2g, grid)
         with region("processor"):
             mesh, _ = self.processor(mesh, e_m2m, g.m2m)
         e_m2g = m2g_branch.join(e_m2g)
+        if pre is not None:
+            pre = dec_branch.join(*pre)
         with region("decoder"):
-            grid = self.decoder(e_m2g, grid, mesh, g.m2g)
+            grid = self.decoder(e_m2g, grid, mesh, g.m2g, pre=pre)
         with region("final"):
             return self.final_prediction(grid)
