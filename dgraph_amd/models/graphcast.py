@@ -399,14 +399,11 @@ class GraphCastDecoder(nn.Module):
         self.node_mlp = MeshNodeBlock(H, H, H, comm, H, 1)
         self.halo = _Halo(comm)
 
-    def forward(self, m2g_edge_features, grid_node_features, mesh_node_features, m2g,
-                pre=None):
-        """``pre``: the edge block's ``pre_dst(m2g_edge_features, grid_node_features)``,
-        computed ahead (DGraphCast runs it on the branch stream during the processor)."""
+    def forward(self, m2g_edge_features, grid_node_features, mesh_node_features, m2g):
         mesh_h = self.halo.start(mesh_node_features, m2g)  # senders: mesh (local|halo)
         e = self.edge_mlp.fused_halo(mesh_node_features, grid_node_features,
                                      m2g_edge_features, m2g.other_map(), m2g.agg_map(),
-                                     mesh_h, "src", pre=pre)
+                                     mesh_h, "src")
         n = self.node_mlp.fused(grid_node_features, e, m2g.agg_map())
         return grid_node_features + n
 
@@ -450,18 +447,12 @@ class DGraphCast(nn.Module):
             e_g2m = emb.grid2mesh_edge_embedder(g.g2m.features.to(x.dtype))
         with region("encoder"):
             grid, mesh = self.encoder(grid, mesh, e_g2m, g.g2m, branch=br)
-        # the decoder's edge and grid-side projections need only the m2g embedding and the
-        # encoder's grid: on the branch, beside the processor's mesh-sized kernels
-        pre = None
-        if br is not None:
-            with _on_branch(br, grid, reads=(grid,)) as dec_branch:
-                pre = self.decoder.edge_mlp.pre_dst(e_m2g, grid)
+        # (the decoder's edge / grid projections, MeshEdgeBlock.pre_dst, were also tried on
+        # the branch beside the processor: slower, W=8 rank 0 15.96 -> 16.34 ms)
         with region("processor"):
             mesh, _ = self.processor(mesh, e_m2m, g.m2m)
         e_m2g = m2g_branch.join(e_m2g)
-        if pre is not None:
-            pre = dec_branch.join(*pre)
         with region("decoder"):
-            grid = self.decoder(e_m2g, grid, mesh, g.m2g, pre=pre)
+            grid = self.decoder(e_m2g, grid, mesh, g.m2g)
         with region("final"):
             return self.final_prediction(grid)

@@ -9,8 +9,8 @@ timeout -k 10 300 python -u -m pytest tests/test_graphcast_gpu.py -m gpu -q \
 rc=$?; echo "== tests rc=$rc"; tail -2 $O/v_tests.log
 case $rc in 0) ;; *) grep -E "Error|assert" $O/v_tests.log | head; exit $rc;; esac
 timeout -k 10 300 python -u benchmarks/bench_graphcast.py --mode step --steps 20 --warmup 3 \
-  --cuda-graph > $O/w1_bs2_graph.log 2>&1 || exit $?
-grep '^{' $O/w1_bs2_graph.log | python3 -c "
+  --cuda-graph > $O/w1_${WTAG:-bs2}_graph.log 2>&1 || exit $?
+grep '^{' $O/w1_${WTAG:-bs2}_graph.log | python3 -c "
 import json,sys
 for l in sys.stdin: d=json.loads(l); print('w1', round(d['ms_per_step'],2))"
-RANKS="0 1 2 3" TAG=8 bash scripts/gpu_r06_k.sh
+RANKS="0 1 2 3" TAG=${TAG:-8} bash scripts/gpu_r06_k.sh
