@@ -132,8 +132,11 @@ def defer_param_grads(params: Sequence[torch.Tensor], compute: Callable[[], Sequ
     cur = torch.cuda.current_stream()
     side = _side_stream(params[0].device)
     dsts = []
+    uses: dict = {}
+    for leaf, _ in targets:
+        uses[id(leaf)] = uses.get(id(leaf), 0) + 1
     for leaf, view in targets:
-        if leaf.grad is None and view is None:
+        if leaf.grad is None and view is None and uses[id(leaf)] == 1:
             dsts.append(leaf)  # the gradient itself becomes .grad (no zero fill + add)
             continue
         if leaf.grad is None:
