@@ -59,6 +59,7 @@ def release_workspace() -> None:
 class _Deferral:  # process-wide: the autograd engine runs GPU backward on its own thread
     active = False
     calls = 0  # backward calls whose parameter gradients went to the side stream
+    pending: dict = {}  # id(leaf) -> [leaf, buffer]: this block's side-stream gradients
 
 
 _DEFER = _Deferral()
@@ -76,42 +77,50 @@ def _side_stream(dev: torch.device) -> torch.cuda.Stream:
 def deferred_wgrad(enabled: bool = True):
     """Inside the block, the backward of :func:`linear`, :func:`linear_sum` and
     ``ops.act.linear_act`` computes each weight (and bias) gradient on ONE side stream
-    and adds it into the parameter's ``.grad`` there, while the data-gradient chain goes
-    on on the current stream; leaving the block joins the side stream into the current
-    one, so the gradients are complete for what follows (gradient sync, optimizer).
+    into a per-parameter buffer, while the data-gradient chain goes on on the current
+    stream. Leaving the block joins the side stream into the current one and adds each
+    buffer into the parameter's ``.grad`` there (or makes it the ``.grad``), so the
+    gradients are complete for what follows (gradient sync, optimizer). ``.grad`` itself is
+    only ever touched on the current stream: a parameter whose gradient also arrives
+    through autograd's own accumulation (another op, a non-slice view) stays correct.
 
     For steps of many small kernels (GraphCast's MLPs at 10^5 rows per rank, where one
     GEMM fills a fraction of the 256 CUs) the weight gradients then run in the data
-    chain's idle CUs instead of after each of its kernels. The order of the adds into one
-    ``.grad`` is the backward's issue order, so results are bitwise reproducible. Every
-    use of a parameter in the step must go through these ops (a parameter whose gradient
-    also arrives through autograd's own accumulation would be added to from two streams);
-    parameters reached through another view than a plain slice of a contiguous leaf keep
-    the normal path. Capturable (the side stream forks from and joins the capturing
-    stream)."""
+    chain's idle CUs instead of after each of its kernels. A buffer sums its terms in the
+    backward's issue order, so a parameter whose every gradient is deferred gets exactly
+    the inline result (bitwise). For ``.backward()``: the deferred inputs get no gradient
+    through autograd (``torch.autograd.grad`` would not see them). Capturable (the side
+    stream forks from and joins the capturing stream)."""
     if not enabled or not torch.cuda.is_available():
         yield
         return
-    prev = _DEFER.active
-    _DEFER.active = True
+    prev, prev_pending = _DEFER.active, _DEFER.pending
+    _DEFER.active, _DEFER.pending = True, {}
     cur = torch.cuda.current_stream()
     try:
         yield
     finally:
-        _DEFER.active = prev
+        pending = _DEFER.pending
+        _DEFER.active, _DEFER.pending = prev, prev_pending
         s = _SIDE.get(cur.device.index)
         if s is not None:
             cur.wait_stream(s)
+        for leaf, buf in pending.values():
+            buf.record_stream(cur)  # (made on the side stream, read and freed here)
+            if leaf.grad is None:
+                leaf.grad = buf
+            else:
+                leaf.grad.add_(buf)
 
 
 def _leaf_target(p: torch.Tensor):
-    """(leaf parameter, view of its ``.grad`` that ``p``'s gradient adds into) or None."""
+    """(leaf parameter, (size, stride, offset) of ``p`` inside it, or None for the leaf
+    itself) or None when ``p`` is neither a leaf nor a slice of a contiguous one."""
     if not p.requires_grad:
         return None
     b = p if p.is_leaf else p._base
-    if b is None or not b.is_leaf or not b.requires_grad or not b.is_contiguous() or (
-            b.grad is not None and not b.grad.is_contiguous()):
-        return None  # (a view's strides address the grad only when both are contiguous)
+    if b is None or not b.is_leaf or not b.requires_grad or not b.is_contiguous():
+        return None
     if b is p:
         return p, None
     return b, (p.size(), p.stride(), p.storage_offset() - b.storage_offset())
@@ -120,7 +129,7 @@ def _leaf_target(p: torch.Tensor):
 def defer_param_grads(params: Sequence[torch.Tensor], compute: Callable[[], Sequence],
                       keep_alive: Sequence[torch.Tensor] = ()) -> bool:
     """Under :func:`deferred_wgrad`: run ``compute()`` (returning one gradient per entry
-    of ``params``) on the side stream and add each into its parameter's ``.grad``;
+    of ``params``) on the side stream and add each into its parameter's block buffer;
     returns True (the caller then returns None for those inputs). False, with nothing
     run, when deferral is off or a parameter is not a plain leaf / slice of one.
     ``keep_alive``: tensors ``compute`` reads (their memory is held for the side stream)."""
@@ -131,31 +140,29 @@ def defer_param_grads(params: Sequence[torch.Tensor], compute: Callable[[], Sequ
         return False
     cur = torch.cuda.current_stream()
     side = _side_stream(params[0].device)
-    dsts = []
-    uses: dict = {}
-    for leaf, _ in targets:
-        uses[id(leaf)] = uses.get(id(leaf), 0) + 1
+    pend = _DEFER.pending
+    slots = []  # per target: (pending entry, view) — entry [leaf, None] until first write
     for leaf, view in targets:
-        if leaf.grad is None and view is None and uses[id(leaf)] == 1:
-            dsts.append(leaf)  # the gradient itself becomes .grad (no zero fill + add)
-            continue
-        if leaf.grad is None:
-            leaf.grad = torch.zeros_like(leaf)  # on the current stream, before the fork
-        g = leaf.grad
-        dsts.append(g if view is None else g.as_strided(view[0], view[1],
-                                                       g.storage_offset() + view[2]))
+        e = pend.get(id(leaf))
+        if e is None:
+            e = pend[id(leaf)] = [leaf, None]
+        if e[1] is None and view is not None:
+            e[1] = torch.zeros_like(leaf)  # on the current stream, before the fork
+        slots.append((e, view))
     _DEFER.calls += 1
     side.wait_stream(cur)
     for t in keep_alive:
         t.record_stream(side)
     with torch.cuda.stream(side):
-        for d, o, p in zip(dsts, compute(), params):
-            if d is p:
-                o = o.to(p.dtype).contiguous()
-                o.record_stream(cur)  # read (and freed) on the current stream after the join
-                p.grad = o
+        for (e, view), o in zip(slots, compute()):
+            buf = e[1]
+            if buf is None:  # the parameter's first term: it becomes the buffer
+                e[1] = o.to(e[0].dtype).contiguous()
+            elif view is None:
+                buf.add_(o.to(buf.dtype))
             else:
-                d.add_(o.to(d.dtype))
+                buf.as_strided(view[0], view[1], buf.storage_offset() + view[2]).add_(
+                    o.to(buf.dtype))
     return True
 
 
