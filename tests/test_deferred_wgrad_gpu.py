@@ -27,7 +27,7 @@ def _run(defer: bool, existing: bool):
             p.grad = torch.full_like(p, 0.5)
     h = linear(x, W[:, :128], b)                       # slice of W
     h = linear_act([(h, W[:, 128:]), (y, V)], None, "silu")  # the other slice, and V
-    h = linear_sum([x, h], [V, V], None)               # V twice in one call
+    h = linear_sum([(x, V), (h, V)], None)              # V twice in one call
     h = linear(h, V.t().contiguous().t())              # V behind a non-slice view
     loss = (h * h).mean()
     with deferred_wgrad(defer):
