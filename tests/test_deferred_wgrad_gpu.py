@@ -16,8 +16,9 @@ def _run(defer: bool, existing: bool):
 
     dev = torch.device("cuda", 0)
     g = torch.Generator(device="cpu").manual_seed(3)
-    W = torch.randn(128, 256, generator=g).to(dev).requires_grad_(True)
-    V = torch.randn(128, 128, generator=g).to(dev).requires_grad_(True)
+    # (scaled like an initialised layer: the activations stay O(1) through the chain)
+    W = (torch.randn(128, 256, generator=g) / 16).to(dev).requires_grad_(True)
+    V = (torch.randn(128, 128, generator=g) / 11.3).to(dev).requires_grad_(True)
     b = torch.randn(128, generator=g).to(dev).requires_grad_(True)
     x = torch.randn(4096, 128, generator=g).to(dev)
     y = torch.randn(4096, 128, generator=g).to(dev)
@@ -47,5 +48,5 @@ def test_deferred_wgrad_cases_bitwise(existing):
     for a, r, n in zip(got, ref, ("W", "V", "b")):
         if n != "V" and not existing:
             assert torch.equal(a, r), n
-        else:
-            torch.testing.assert_close(a, r, atol=1e-6, rtol=1e-5)
+        else:  # the same terms in another association: fp32 rounding of the largest term
+            torch.testing.assert_close(a, r, atol=1e-5 * float(r.abs().max()), rtol=1e-5)
